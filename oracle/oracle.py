@@ -1,0 +1,168 @@
+"""ctypes front-end of the CPU oracle (oracle/sfm_oracle*.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, and only as the checker / timed CPU baseline — never by the product path under
+sfm-project_amd/.  Parity status: "parity unpinned" (see sfm_oracle.c header and DESIGN.md §5).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "lib", "liboracle.so")
+_lib = None
+
+XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
+INT64_MAX = np.iinfo(np.int64).max
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+        _bind(_lib)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _bind(L):
+    vp, i32, i64, u32, u64, f32, f64 = (C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64,
+                                        C.c_float, C.c_double)
+    L.oracle_match.argtypes = [vp, i32, vp, i32, i32, i32, i32, i32, i32, i64, vp, vp, vp]
+    L.oracle_match.restype = i32
+    L.oracle_nn_tables.argtypes = [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp]
+    L.oracle_philox4x32_10.argtypes = [vp, vp, vp]
+    L.oracle_sample8.argtypes = [u64, u32, u32, u32, i32, vp]
+    L.oracle_normalize.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.oracle_fit_f8.argtypes = [vp, vp, vp]
+    L.oracle_fit_f8.restype = i32
+    L.oracle_ransac_f.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp, vp, vp, vp]
+    L.oracle_ransac_f.restype = i32
+    L.oracle_ransac_counts.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp]
+    L.oracle_match_verify_batch.argtypes = [vp, vp, i32, i32, i32, vp, i32, i32, i32, i64, i32,
+                                            u64, f32, i32, vp, vp]
+    L.oracle_match_verify_batch.restype = C.c_longlong
+    L.oracle_ba_obs.argtypes = [vp, vp, vp, vp, f64, vp, vp, vp, vp, vp]
+    L.oracle_ba_jtj.argtypes = [i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp, vp, vp, vp, vp,
+                                vp]
+    L.oracle_ba_jtj.restype = f64
+
+
+def match(A, B, metric=0, cross_check=XC_MUTUAL, ratio=None, max_dist=-1):
+    """Returns (query_idx, train_idx, dist) arrays in ascending query order."""
+    A = np.ascontiguousarray(A, np.uint8)
+    B = np.ascontiguousarray(B, np.uint8)
+    num, den = (0, 0) if ratio is None else ratio
+    n = max(A.shape[0], 1)
+    q = np.zeros(n, np.int32)
+    t = np.zeros(n, np.int32)
+    d = np.zeros(n, np.int64)
+    k = lib().oracle_match(_p(A), A.shape[0], _p(B), B.shape[0], A.shape[1], metric, cross_check,
+                           num, den, max_dist, _p(q), _p(t), _p(d))
+    return q[:k], t[:k], d[:k]
+
+
+def nn_tables(A, B, metric=0):
+    A = np.ascontiguousarray(A, np.uint8)
+    B = np.ascontiguousarray(B, np.uint8)
+    Ka, Kb = A.shape[0], B.shape[0]
+    nn = np.zeros(Ka, np.int32); d1 = np.zeros(Ka, np.int64); d2 = np.zeros(Ka, np.int64)
+    rnn = np.zeros(Kb, np.int32); rd = np.zeros(Kb, np.int64)
+    lib().oracle_nn_tables(_p(A), Ka, _p(B), Kb, A.shape[1], metric, _p(nn), _p(d1), _p(d2),
+                           _p(rnn), _p(rd))
+    return nn, d1, d2, rnn, rd
+
+
+def philox(ctr, key):
+    c = np.asarray(ctr, np.uint32)
+    k = np.asarray(key, np.uint32)
+    o = np.zeros(4, np.uint32)
+    lib().oracle_philox4x32_10(_p(c), _p(k), _p(o))
+    return o
+
+
+def sample8(seed, pa, pb, h, M):
+    o = np.zeros(8, np.int32)
+    lib().oracle_sample8(seed, pa, pb, h, M, _p(o))
+    return o
+
+
+def normalize(xy):
+    xy = np.ascontiguousarray(xy, np.float32)
+    out = np.zeros_like(xy)
+    cx, cy, s = C.c_float(), C.c_float(), C.c_float()
+    lib().oracle_normalize(_p(xy), xy.shape[0], _p(out), C.byref(cx), C.byref(cy), C.byref(s))
+    return out, cx.value, cy.value, s.value
+
+
+def fit_f8(p1, p2):
+    p1 = np.ascontiguousarray(p1, np.float32)
+    p2 = np.ascontiguousarray(p2, np.float32)
+    F = np.zeros(9, np.float32)
+    ok = lib().oracle_fit_f8(_p(p1), _p(p2), _p(F))
+    return ok, F
+
+
+def ransac_f(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
+    """Returns dict(count, best_h, F (normalised, 9 f32), norm (6 f32), mask (u8 [M]))."""
+    xy1 = np.ascontiguousarray(xy1, np.float32)
+    xy2 = np.ascontiguousarray(xy2, np.float32)
+    M = xy1.shape[0]
+    bh = np.zeros(1, np.int32)
+    F = np.zeros(9, np.float32)
+    nrm = np.zeros(6, np.float32)
+    mask = np.zeros(max(M, 1), np.uint8)
+    c = lib().oracle_ransac_f(_p(xy1), _p(xy2), M, H, seed, pa, pb, thr, _p(bh), _p(F), _p(nrm),
+                              _p(mask))
+    return dict(count=c, best_h=int(bh[0]), F=F, norm=nrm, mask=mask[:M])
+
+
+def ransac_counts(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
+    xy1 = np.ascontiguousarray(xy1, np.float32)
+    xy2 = np.ascontiguousarray(xy2, np.float32)
+    counts = np.zeros(H, np.int32)
+    lib().oracle_ransac_counts(_p(xy1), _p(xy2), xy1.shape[0], H, seed, pa, pb, thr, _p(counts))
+    return counts
+
+
+def match_verify_batch(desc, kps, pairs, ratio=(4, 5), max_dist=-1, H=4096, seed=42, thr=1.0,
+                       min_inl=15):
+    desc = np.ascontiguousarray(desc, np.uint8)
+    kps = np.ascontiguousarray(kps, np.float32)
+    pairs = np.ascontiguousarray(pairs, np.int32)
+    P = pairs.shape[0]
+    nm = np.zeros(P, np.int32)
+    ni = np.zeros(P, np.int32)
+    tot = lib().oracle_match_verify_batch(_p(desc), _p(kps), desc.shape[0], desc.shape[1],
+                                          desc.shape[2], _p(pairs), P, ratio[0], ratio[1],
+                                          max_dist, H, seed, thr, min_inl, _p(nm), _p(ni))
+    return int(tot), nm, ni
+
+
+def ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0):
+    cams = np.ascontiguousarray(cams, np.float64)
+    pp = np.ascontiguousarray(pp, np.float64)
+    pts = np.ascontiguousarray(pts, np.float64)
+    cam_idx = np.ascontiguousarray(cam_idx, np.int32)
+    pt_idx = np.ascontiguousarray(pt_idx, np.int32)
+    uv = np.ascontiguousarray(uv, np.float64)
+    nc, npt, no = cams.shape[0], pts.shape[0], cam_idx.shape[0]
+    U = np.zeros((nc, 8, 8)); V = np.zeros((npt, 3, 3)); W = np.zeros((no, 8, 3))
+    gc = np.zeros((nc, 8)); gp = np.zeros((npt, 3)); res = np.zeros((no, 2))
+    cost = lib().oracle_ba_jtj(nc, _p(cams), _p(pp), npt, _p(pts), no, _p(cam_idx), _p(pt_idx),
+                               _p(uv), loss_s, _p(U), _p(V), _p(W), _p(gc), _p(gp), _p(res))
+    return dict(U=U, V=V, W=W, gc=gc, gp=gp, res=res, cost=cost)

@@ -1,0 +1,447 @@
+/*
+ * sfm_oracle.c — CPU restatement of the matching / geometric-verification / BA-J^TJ hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load this library, and only as the checker (or the timed CPU baseline).  The product path
+ * (sfm-project_amd/) never links, imports or falls back to it.
+ *
+ * PARITY STATUS: "parity unpinned" by the reference itself.  The reference
+ * (Justin-Huber/SfM-project) has no tests, no fixtures and cannot run here (no cv2);
+ * its arithmetic lives in OpenCV (third-party, un-vendored, unpinned version).  This file restates
+ *   - the reference's matching semantics, code/feature_matching.py:48-58 (BFMatcher NORM_HAMMING,
+ *     crossCheck=True, stable sort, keep distance < 26) with OpenCV's published batchDistance
+ *     cross-check rule, and
+ *   - the build spec for the empty modules code/geometric_verification.py (8-point RANSAC) and
+ *     code/3d_reconstruction.py (BA J^TJ), per SURVEY.md §8a rows a3', a6, a7 and DESIGN.md §3.
+ * It is cross-checked in-container against scikit-image 0.18.3 match_descriptors /
+ * FundamentalMatrixTransform and numpy (tests/golden/make_golden.py).
+ *
+ * Every floating-point expression is written op-by-op (explicit fmaf where fused), compiled with
+ * -ffp-contract=off, so that the HIP kernels — which follow the same op sequence — are bit-exact.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define SFM_XC_NONE 0
+#define SFM_XC_MUTUAL 1
+#define SFM_XC_OPENCV 2
+
+/* ------------------------------------------------------------------------------------------ */
+/* Matching (reference a1-a3: code/feature_matching.py:48-58; north_star a3' ratio test)        */
+/* ------------------------------------------------------------------------------------------ */
+
+static inline int64_t l2sq_u8(const uint8_t* a, const uint8_t* b, int D) {
+    int64_t s = 0;
+    for (int k = 0; k < D; ++k) { int d = (int)a[k] - (int)b[k]; s += d * d; }
+    return s;
+}
+
+static inline int64_t hamming_u8(const uint8_t* a, const uint8_t* b, int D) {
+    int64_t s = 0;
+    for (int k = 0; k < D; ++k) s += __builtin_popcount((unsigned)(a[k] ^ b[k]));
+    return s;
+}
+
+/*
+ * Brute-force match of query set A (Ka x D) against train set B (Kb x D).
+ * metric 0 = squared L2 over u8 (SIFT, D=128), 1 = Hamming over packed bits (ORB, D=32 bytes).
+ * Outputs, for every query i:  nn[i] (lowest-index argmin), d1[i], d2[i] (second smallest value
+ * of the distance multiset, INT64_MAX if Kb < 2); for every train j: rnn[j] (lowest-index argmin
+ * over queries), rd[j].
+ */
+static void nn_tables(const uint8_t* A, int Ka, const uint8_t* B, int Kb, int D, int metric,
+                      int32_t* nn, int64_t* d1, int64_t* d2, int32_t* rnn, int64_t* rd) {
+    for (int j = 0; j < Kb; ++j) { rnn[j] = -1; rd[j] = INT64_MAX; }
+    for (int i = 0; i < Ka; ++i) {
+        int64_t b1 = INT64_MAX, b2 = INT64_MAX;
+        int32_t j1 = -1;
+        for (int j = 0; j < Kb; ++j) {
+            int64_t d = metric ? hamming_u8(A + (size_t)i * D, B + (size_t)j * D, D)
+                               : l2sq_u8(A + (size_t)i * D, B + (size_t)j * D, D);
+            if (d < b1) { b2 = b1; b1 = d; j1 = j; }
+            else if (d < b2) { b2 = d; }
+            if (d < rd[j]) { rd[j] = d; rnn[j] = i; }  /* queries visited in ascending i */
+        }
+        nn[i] = j1; d1[i] = b1; d2[i] = b2;
+    }
+}
+
+/*
+ * Full match with the build spec:
+ *   cross_check 1 (mutual): keep query i iff rnn[nn[i]] == i.
+ *   cross_check 2 (OpenCV batchDistance crosscheck, the reference's BFMatcher(crossCheck=True)):
+ *     for each train j in ascending order with q = rnn[j]: if rd[j] < best[q] then best[q] = rd[j],
+ *     partner[q] = j.  Query q matches partner[q] if set.  (Ratio test not allowed in this mode.)
+ *   ratio (num/den, den > 0): keep iff den^2*d1^2 < num^2*d2^2 for L2 (squared domain);
+ *     den*d1 < num*d2 for Hamming.  d2 = INT64_MAX always passes.
+ *   max_dist >= 0: keep iff distance < max_dist (d^2 for L2, bits for Hamming).
+ * Matches are written in ascending query order.  Returns the count.
+ */
+int oracle_match(const uint8_t* A, int Ka, const uint8_t* B, int Kb, int D, int metric,
+                 int cross_check, int ratio_num, int ratio_den, int64_t max_dist,
+                 int32_t* out_q, int32_t* out_t, int64_t* out_d) {
+    if (Ka <= 0 || Kb <= 0) return 0;
+    int32_t* nn = (int32_t*)malloc(sizeof(int32_t) * Ka);
+    int64_t* d1 = (int64_t*)malloc(sizeof(int64_t) * Ka);
+    int64_t* d2 = (int64_t*)malloc(sizeof(int64_t) * Ka);
+    int32_t* rnn = (int32_t*)malloc(sizeof(int32_t) * Kb);
+    int64_t* rd = (int64_t*)malloc(sizeof(int64_t) * Kb);
+    nn_tables(A, Ka, B, Kb, D, metric, nn, d1, d2, rnn, rd);
+    int n = 0;
+    if (cross_check == SFM_XC_OPENCV) {
+        int64_t* best = (int64_t*)malloc(sizeof(int64_t) * Ka);
+        int32_t* part = (int32_t*)malloc(sizeof(int32_t) * Ka);
+        for (int i = 0; i < Ka; ++i) { best[i] = INT64_MAX; part[i] = -1; }
+        for (int j = 0; j < Kb; ++j) {
+            int q = rnn[j];
+            if (q >= 0 && rd[j] < best[q]) { best[q] = rd[j]; part[q] = j; }
+        }
+        for (int i = 0; i < Ka; ++i) {
+            if (part[i] < 0) continue;
+            if (max_dist >= 0 && !(best[i] < max_dist)) continue;
+            out_q[n] = i; out_t[n] = part[i]; out_d[n] = best[i]; ++n;
+        }
+        free(best); free(part);
+    } else {
+        for (int i = 0; i < Ka; ++i) {
+            int j = nn[i];
+            if (j < 0) continue;
+            if (cross_check == SFM_XC_MUTUAL && rnn[j] != i) continue;
+            if (ratio_den > 0 && d2[i] != INT64_MAX) {
+                if (metric == 0) {
+                    __int128 lhs = (__int128)ratio_den * ratio_den * d1[i];
+                    __int128 rhs = (__int128)ratio_num * ratio_num * d2[i];
+                    if (!(lhs < rhs)) continue;
+                } else {
+                    if (!((int64_t)ratio_den * d1[i] < (int64_t)ratio_num * d2[i])) continue;
+                }
+            }
+            if (max_dist >= 0 && !(d1[i] < max_dist)) continue;
+            out_q[n] = i; out_t[n] = j; out_d[n] = d1[i]; ++n;
+        }
+    }
+    free(nn); free(d1); free(d2); free(rnn); free(rd);
+    return n;
+}
+
+/* Per-query / per-train NN tables, exported for finer-grained tests. */
+void oracle_nn_tables(const uint8_t* A, int Ka, const uint8_t* B, int Kb, int D, int metric,
+                      int32_t* nn, int64_t* d1, int64_t* d2, int32_t* rnn, int64_t* rd) {
+    nn_tables(A, Ka, B, Kb, D, metric, nn, d1, d2, rnn, rd);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* RANSAC 8-point fundamental matrix (fills code/geometric_verification.py)   */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Philox4x32-10 (Salmon et al., SC'11; Random123).  ctr/key little-endian words. */
+void oracle_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Floyd sampling of 8 distinct indices in [0, M) from 8 uniform u32 words. */
+void oracle_sample8(uint64_t seed, uint32_t pa, uint32_t pb, uint32_t h, int M, int32_t out[8]) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t r[8];
+    uint32_t c0[4] = {h, 0u, pa, pb}, c1[4] = {h, 1u, pa, pb};
+    oracle_philox4x32_10(c0, key, r);
+    oracle_philox4x32_10(c1, key, r + 4);
+    for (int k = 0; k < 8; ++k) {
+        uint32_t jmax = (uint32_t)(M - 8 + k);
+        uint32_t t = (uint32_t)(((uint64_t)r[k] * (uint64_t)(jmax + 1u)) >> 32);
+        for (int q = 0; q < k; ++q)
+            if ((uint32_t)out[q] == t) { t = jmax; break; }
+        out[k] = (int32_t)t;
+    }
+}
+
+/* Fixed-order fp32 sum: 64 lane partials (lane l sums m = l, l+64, ... in order), then a
+ * halving tree (off = 32..1: p[l] += p[l+off]).  Mirrors the GPU wave reduction exactly. */
+static float fixed_sum(const float* v, int M) {
+    float p[64];
+    for (int l = 0; l < 64; ++l) {
+        float s = 0.0f;
+        for (int m = l; m < M; m += 64) s = s + v[m];
+        p[l] = s;
+    }
+    for (int off = 32; off >= 1; off >>= 1)
+        for (int l = 0; l < off; ++l) p[l] = p[l] + p[l + off];
+    return p[0];
+}
+
+/* Hartley isotropic normalisation of one image side: returns cx, cy, s and writes normalised xy. */
+void oracle_normalize(const float* xy, int M, float* nxy, float* cx, float* cy, float* s) {
+    float* tmp = (float*)malloc(sizeof(float) * (M > 0 ? M : 1));
+    for (int m = 0; m < M; ++m) tmp[m] = xy[2 * m];
+    float sx = fixed_sum(tmp, M);
+    for (int m = 0; m < M; ++m) tmp[m] = xy[2 * m + 1];
+    float sy = fixed_sum(tmp, M);
+    float mx = sx / (float)M, my = sy / (float)M;
+    for (int m = 0; m < M; ++m) {
+        float dx = xy[2 * m] - mx, dy = xy[2 * m + 1] - my;
+        float q = dx * dx;
+        q = fmaf(dy, dy, q);
+        tmp[m] = sqrtf(q);
+    }
+    float sd = fixed_sum(tmp, M);
+    float mean = sd / (float)M;
+    float sc = (mean > 0.0f) ? (1.41421356237309515f / mean) : 1.0f;
+    for (int m = 0; m < M; ++m) {
+        nxy[2 * m] = (xy[2 * m] - mx) * sc;
+        nxy[2 * m + 1] = (xy[2 * m + 1] - my) * sc;
+    }
+    *cx = mx; *cy = my; *s = sc;
+    free(tmp);
+}
+
+/*
+ * Fundamental matrix from 8 normalised correspondences (Householder QR null space of the 8x9
+ * epipolar system, then rank-2 by zeroing the smallest eigen-direction of F^T F, 5 Jacobi sweeps).
+ * p1/p2: [8][2] normalised points.  Returns 0 on success, -1 if degenerate.  F row-major.
+ */
+int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
+    float Mt[9][8]; /* Mt = A^T, column k = epipolar row of sample k */
+    for (int k = 0; k < 8; ++k) {
+        float x1 = p1[2 * k], y1 = p1[2 * k + 1], x2 = p2[2 * k], y2 = p2[2 * k + 1];
+        Mt[0][k] = x2 * x1; Mt[1][k] = x2 * y1; Mt[2][k] = x2;
+        Mt[3][k] = y2 * x1; Mt[4][k] = y2 * y1; Mt[5][k] = y2;
+        Mt[6][k] = x1;      Mt[7][k] = y1;      Mt[8][k] = 1.0f;
+    }
+    float V[8][9];
+    float beta[8];
+    for (int k = 0; k < 8; ++k) {
+        float nrm2 = 0.0f;
+        for (int r = k; r < 9; ++r) nrm2 = fmaf(Mt[r][k], Mt[r][k], nrm2);
+        if (!(nrm2 > 0.0f)) return -1;
+        float nrm = sqrtf(nrm2);
+        float alpha = (Mt[k][k] > 0.0f) ? -nrm : nrm;
+        for (int r = k; r < 9; ++r) V[k][r] = Mt[r][k];
+        V[k][k] = Mt[k][k] - alpha;
+        float vn2 = 0.0f;
+        for (int r = k; r < 9; ++r) vn2 = fmaf(V[k][r], V[k][r], vn2);
+        if (!(vn2 > 0.0f)) return -1;
+        beta[k] = 2.0f / vn2;
+        Mt[k][k] = alpha;
+        for (int c = k + 1; c < 8; ++c) {
+            float dot = 0.0f;
+            for (int r = k; r < 9; ++r) dot = fmaf(V[k][r], Mt[r][c], dot);
+            float f = beta[k] * dot;
+            for (int r = k; r < 9; ++r) Mt[r][c] = fmaf(-f, V[k][r], Mt[r][c]);
+        }
+    }
+    float z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 1.0f};
+    for (int k = 7; k >= 0; --k) {
+        float dot = 0.0f;
+        for (int r = k; r < 9; ++r) dot = fmaf(V[k][r], z[r], dot);
+        float f = beta[k] * dot;
+        for (int r = k; r < 9; ++r) z[r] = fmaf(-f, V[k][r], z[r]);
+    }
+    /* rank 2: G = F^T F, Jacobi eigen-decomposition, remove the smallest eigen-direction */
+    float G[3][3], E[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            float g = 0.0f;
+            for (int r = 0; r < 3; ++r) g = fmaf(z[3 * r + i], z[3 * r + j], g);
+            G[i][j] = g;
+        }
+    static const int PQ[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    for (int sweep = 0; sweep < 5; ++sweep) {
+        for (int e = 0; e < 3; ++e) {
+            int p = PQ[e][0], q = PQ[e][1];
+            float gpq = G[p][q];
+            if (gpq == 0.0f) continue;
+            float theta = (G[q][q] - G[p][p]) / (2.0f * gpq);
+            float at = fabsf(theta);
+            float t = 1.0f / (at + sqrtf(fmaf(theta, theta, 1.0f)));
+            if (theta < 0.0f) t = -t;
+            float c = 1.0f / sqrtf(fmaf(t, t, 1.0f));
+            float s = t * c;
+            /* G <- J^T G J with J = rotation in (p,q): column then row update */
+            for (int r = 0; r < 3; ++r) {
+                float gp = G[r][p], gq = G[r][q];
+                G[r][p] = c * gp - s * gq;
+                G[r][q] = fmaf(s, gp, c * gq);
+            }
+            for (int r = 0; r < 3; ++r) {
+                float gp = G[p][r], gq = G[q][r];
+                G[p][r] = c * gp - s * gq;
+                G[q][r] = fmaf(s, gp, c * gq);
+            }
+            for (int r = 0; r < 3; ++r) {
+                float ep = E[r][p], eq = E[r][q];
+                E[r][p] = c * ep - s * eq;
+                E[r][q] = fmaf(s, ep, c * eq);
+            }
+        }
+    }
+    int kmin = 0;
+    if (G[1][1] < G[kmin][kmin]) kmin = 1;
+    if (G[2][2] < G[kmin][kmin]) kmin = 2;
+    float v0 = E[0][kmin], v1 = E[1][kmin], v2 = E[2][kmin];
+    for (int r = 0; r < 3; ++r) {
+        float w = fmaf(z[3 * r + 2], v2, fmaf(z[3 * r + 1], v1, z[3 * r] * v0));
+        F[3 * r + 0] = fmaf(-w, v0, z[3 * r + 0]);
+        F[3 * r + 1] = fmaf(-w, v1, z[3 * r + 1]);
+        F[3 * r + 2] = fmaf(-w, v2, z[3 * r + 2]);
+    }
+    return 0;
+}
+
+/* Sampson inlier test in pixel units, evaluated in normalised coordinates. */
+static inline int sampson_inlier(const float F[9], float x1, float y1, float x2, float y2,
+                                 float s1sq, float s2sq, float thr) {
+    float a0 = fmaf(F[0], x1, fmaf(F[1], y1, F[2]));
+    float a1 = fmaf(F[3], x1, fmaf(F[4], y1, F[5]));
+    float a2 = fmaf(F[6], x1, fmaf(F[7], y1, F[8]));
+    float b0 = fmaf(F[0], x2, fmaf(F[3], y2, F[6]));
+    float b1 = fmaf(F[1], x2, fmaf(F[4], y2, F[7]));
+    float r = fmaf(x2, a0, fmaf(y2, a1, a2));
+    float g1 = fmaf(a0, a0, a1 * a1);
+    float g2 = fmaf(b0, b0, b1 * b1);
+    float den = fmaf(s2sq, g1, s1sq * g2);
+    return (r * r) < (thr * den);
+}
+
+/*
+ * RANSAC over one pair.  xy1/xy2: [M][2] pixel coordinates of the tentative matches (in match
+ * order).  Returns the best inlier count (-1 if M < 8); writes best hypothesis id, the normalised
+ * F (row-major) and the normalisation (cx1, cy1, s1, cx2, cy2, s2), and the inlier mask.
+ */
+int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t seed,
+                    uint32_t pa, uint32_t pb, float thr, int32_t* best_h, float Fout[9],
+                    float norm[6], uint8_t* mask) {
+    if (M < 8) {
+        *best_h = -1;
+        for (int i = 0; i < 9; ++i) Fout[i] = 0.0f;
+        for (int i = 0; i < 6; ++i) norm[i] = 0.0f;
+        for (int m = 0; m < M; ++m) mask[m] = 0;
+        return -1;
+    }
+    float* n1 = (float*)malloc(sizeof(float) * 2 * M);
+    float* n2 = (float*)malloc(sizeof(float) * 2 * M);
+    float cx1, cy1, s1, cx2, cy2, s2;
+    oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
+    oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
+    float s1sq = s1 * s1, s2sq = s2 * s2;
+    int bestc = -2, besth = -1;
+    for (int h = 0; h < H; ++h) {
+        int32_t idx[8];
+        oracle_sample8(seed, pa, pb, (uint32_t)h, M, idx);
+        float p1[16], p2[16], F[9];
+        for (int k = 0; k < 8; ++k) {
+            p1[2 * k] = n1[2 * idx[k]]; p1[2 * k + 1] = n1[2 * idx[k] + 1];
+            p2[2 * k] = n2[2 * idx[k]]; p2[2 * k + 1] = n2[2 * idx[k] + 1];
+        }
+        int cnt = -1;
+        if (oracle_fit_f8(p1, p2, F) == 0) {
+            cnt = 0;
+            for (int m = 0; m < M; ++m)
+                cnt += sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m], n2[2 * m + 1],
+                                      s1sq, s2sq, thr);
+        }
+        if (cnt > bestc) { bestc = cnt; besth = h; }
+    }
+    int32_t idx[8];
+    oracle_sample8(seed, pa, pb, (uint32_t)besth, M, idx);
+    float p1[16], p2[16], F[9];
+    for (int k = 0; k < 8; ++k) {
+        p1[2 * k] = n1[2 * idx[k]]; p1[2 * k + 1] = n1[2 * idx[k] + 1];
+        p2[2 * k] = n2[2 * idx[k]]; p2[2 * k + 1] = n2[2 * idx[k] + 1];
+    }
+    int ok = oracle_fit_f8(p1, p2, F);
+    int cnt = 0;
+    for (int m = 0; m < M; ++m) {
+        int in = (ok == 0) ? sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m],
+                                            n2[2 * m + 1], s1sq, s2sq, thr) : 0;
+        mask[m] = (uint8_t)in;
+        cnt += in;
+    }
+    for (int i = 0; i < 9; ++i) Fout[i] = (ok == 0) ? F[i] : 0.0f;
+    norm[0] = cx1; norm[1] = cy1; norm[2] = s1; norm[3] = cx2; norm[4] = cy2; norm[5] = s2;
+    *best_h = besth;
+    free(n1); free(n2);
+    return cnt;
+}
+
+/* Inlier count of every hypothesis (for fine-grained parity tests). */
+void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint64_t seed,
+                          uint32_t pa, uint32_t pb, float thr, int32_t* counts) {
+    float* n1 = (float*)malloc(sizeof(float) * 2 * M);
+    float* n2 = (float*)malloc(sizeof(float) * 2 * M);
+    float cx1, cy1, s1, cx2, cy2, s2;
+    oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
+    oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
+    float s1sq = s1 * s1, s2sq = s2 * s2;
+    for (int h = 0; h < H; ++h) {
+        int32_t idx[8];
+        oracle_sample8(seed, pa, pb, (uint32_t)h, M, idx);
+        float p1[16], p2[16], F[9];
+        for (int k = 0; k < 8; ++k) {
+            p1[2 * k] = n1[2 * idx[k]]; p1[2 * k + 1] = n1[2 * idx[k] + 1];
+            p2[2 * k] = n2[2 * idx[k]]; p2[2 * k + 1] = n2[2 * idx[k] + 1];
+        }
+        int cnt = -1;
+        if (oracle_fit_f8(p1, p2, F) == 0) {
+            cnt = 0;
+            for (int m = 0; m < M; ++m)
+                cnt += sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m], n2[2 * m + 1],
+                                      s1sq, s2sq, thr);
+        }
+        counts[h] = cnt;
+    }
+    free(n1); free(n2);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Batched match + verify over a pair list (the CPU baseline bench.py times; OpenMP over pairs). */
+/* ------------------------------------------------------------------------------------------ */
+/* desc [n_img][K][D], kps [n_img][K][2]; pairs [P][2].  Per pair: L2 + mutual cross-check + ratio,
+ * then RANSAC on the tentative matches.  Writes n_match[P], n_inl[P]; returns the number of
+ * verified matches (sum of inlier counts over pairs with n_inl >= min_inl). */
+long long oracle_match_verify_batch(const uint8_t* desc, const float* kps, int n_img, int K,
+                                    int D, const int32_t* pairs, int P, int ratio_num,
+                                    int ratio_den, int64_t max_dist, int H, uint64_t seed,
+                                    float thr, int min_inl, int32_t* n_match, int32_t* n_inl) {
+    long long total = 0;
+    (void)n_img;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+    for (int p = 0; p < P; ++p) {
+        int a = pairs[2 * p], b = pairs[2 * p + 1];
+        int32_t* q = (int32_t*)malloc(sizeof(int32_t) * K);
+        int32_t* t = (int32_t*)malloc(sizeof(int32_t) * K);
+        int64_t* d = (int64_t*)malloc(sizeof(int64_t) * K);
+        float* x1 = (float*)malloc(sizeof(float) * 2 * K);
+        float* x2 = (float*)malloc(sizeof(float) * 2 * K);
+        uint8_t* mask = (uint8_t*)malloc((size_t)K);
+        int M = oracle_match(desc + (size_t)a * K * D, K, desc + (size_t)b * K * D, K, D, 0,
+                             SFM_XC_MUTUAL, ratio_num, ratio_den, max_dist, q, t, d);
+        for (int m = 0; m < M; ++m) {
+            x1[2 * m] = kps[((size_t)a * K + q[m]) * 2];
+            x1[2 * m + 1] = kps[((size_t)a * K + q[m]) * 2 + 1];
+            x2[2 * m] = kps[((size_t)b * K + t[m]) * 2];
+            x2[2 * m + 1] = kps[((size_t)b * K + t[m]) * 2 + 1];
+        }
+        int32_t bh;
+        float F[9], nrm[6];
+        int c = oracle_ransac_f(x1, x2, M, H, seed, (uint32_t)a, (uint32_t)b, thr, &bh, F, nrm,
+                                mask);
+        n_match[p] = M;
+        n_inl[p] = c < 0 ? 0 : c;
+        if (c >= min_inl) total += c;
+        free(q); free(t); free(d); free(x1); free(x2); free(mask);
+    }
+    return total;
+}

@@ -1,0 +1,116 @@
+// C-ABI entry points of libsfmcore: context management, error reporting, argument validation.
+// The per-stage kernels live in match_l2.hip, match_hamming.hip, ransac.hip and ba.hip.
+#include "sfm_internal.h"
+
+static thread_local std::string g_err;
+
+namespace sfm {
+void set_error(const std::string& msg) { g_err = msg; }
+
+void* workspace(sfm_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->ws_bytes) return ctx->ws;
+    if (ctx->ws) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ctx->ws);
+        ctx->ws = nullptr;
+        ctx->ws_bytes = 0;
+    }
+    size_t want = align_up(bytes + bytes / 4, 1 << 20);
+    if (hipMalloc(&ctx->ws, want) != hipSuccess) {
+        set_error("workspace allocation of " + std::to_string(want) + " bytes failed");
+        return nullptr;
+    }
+    ctx->ws_bytes = want;
+    return ctx->ws;
+}
+}  // namespace sfm
+
+extern "C" {
+
+const char* sfm_last_error(void) { return g_err.c_str(); }
+
+int32_t sfm_version(void) { return 1; }
+
+int sfm_ctx_create(int32_t device, sfm_ctx** out) {
+    SFM_REQUIRE(out != nullptr, "sfm_ctx_create: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    SFM_HIP_CHECK(hipGetDeviceCount(&n));
+    SFM_REQUIRE(device >= 0 && device < n, "sfm_ctx_create: device index out of range");
+    SFM_HIP_CHECK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    SFM_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0) {
+        sfm::set_error(std::string("sfm_ctx_create: libsfmcore is built for gfx950, device is ") +
+                       prop.gcnArchName);
+        return SFM_ERR_INVALID;
+    }
+    sfm_ctx* c = new sfm_ctx();
+    c->device = device;
+    c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        sfm::set_error("sfm_ctx_create: hipStreamCreate failed");
+        return SFM_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return SFM_OK;
+}
+
+int sfm_ctx_destroy(sfm_ctx* ctx) {
+    if (!ctx) return SFM_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return SFM_OK;
+}
+
+int sfm_ctx_set_stream(sfm_ctx* ctx, void* hip_stream) {
+    SFM_REQUIRE(ctx != nullptr, "sfm_ctx_set_stream: ctx is NULL");
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return SFM_OK;
+}
+
+int sfm_ctx_sync(sfm_ctx* ctx) {
+    SFM_REQUIRE(ctx != nullptr, "sfm_ctx_sync: ctx is NULL");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    SFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return SFM_OK;
+}
+
+int sfm_match_batch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
+                    int32_t k_max, int32_t dim, const int32_t* pairs, int32_t n_pairs,
+                    const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                    int32_t* out_dist) {
+    SFM_REQUIRE(ctx && prm, "sfm_match_batch: ctx/prm is NULL");
+    SFM_REQUIRE(n_pairs >= 0 && n_img >= 0 && k_max >= 0, "sfm_match_batch: negative size");
+    if (n_pairs == 0) return SFM_OK;
+    SFM_REQUIRE(desc && n_kp && pairs && out_count && out_match && out_dist,
+                "sfm_match_batch: NULL array");
+    SFM_REQUIRE(prm->cross_check >= 0 && prm->cross_check <= 2, "sfm_match_batch: bad cross_check");
+    SFM_REQUIRE(!(prm->cross_check == SFM_XC_OPENCV && prm->ratio_den > 0),
+                "sfm_match_batch: ratio test is not defined with the OpenCV cross-check rule");
+    SFM_REQUIRE(prm->ratio_den >= 0 && prm->ratio_num >= 0 && prm->ratio_num <= 65535 &&
+                    prm->ratio_den <= 65535,
+                "sfm_match_batch: ratio must be num/den with 0 <= num, den <= 65535");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    if (prm->metric == SFM_METRIC_L2) {
+        SFM_REQUIRE(dim == 128, "sfm_match_batch: L2 metric needs dim == 128");
+        SFM_REQUIRE(k_max <= 8192, "sfm_match_batch: k_max > 8192 not supported");
+        return sfm_match_l2_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm, out_count,
+                                   out_match, out_dist);
+    }
+    if (prm->metric == SFM_METRIC_HAMMING) {
+        SFM_REQUIRE(dim == 32, "sfm_match_batch: Hamming metric needs dim == 32 (256-bit ORB)");
+        SFM_REQUIRE(k_max <= 8192, "sfm_match_batch: k_max > 8192 not supported");
+        return sfm_match_hamming_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
+                                        out_count, out_match, out_dist);
+    }
+    sfm::set_error("sfm_match_batch: unknown metric");
+    return SFM_ERR_INVALID;
+}
+
+}  // extern "C"

@@ -1,0 +1,51 @@
+// Internal helpers shared by the HIP translation units of libsfmcore (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/sfmcore.h"
+
+struct sfm_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    void* ws = nullptr;          // growable device workspace
+    size_t ws_bytes = 0;
+    int n_cu = 256;
+};
+
+namespace sfm {
+
+void set_error(const std::string& msg);
+
+// Returns a device pointer with at least `bytes` of workspace (grows, never shrinks).
+void* workspace(sfm_ctx* ctx, size_t bytes);
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+#define SFM_HIP_CHECK(expr)                                                                   \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            sfm::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                \
+            return SFM_ERR_HIP;                                                               \
+        }                                                                                     \
+    } while (0)
+
+#define SFM_REQUIRE(cond, msg)                                                                \
+    do {                                                                                      \
+        if (!(cond)) { sfm::set_error(msg); return SFM_ERR_INVALID; }                          \
+    } while (0)
+
+}  // namespace sfm
+
+// Kernel-launch entry points implemented in the per-stage translation units.
+int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
+                        int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                        const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                        int32_t* out_dist);
+int sfm_match_hamming_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp,
+                             int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                             const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                             int32_t* out_dist);

@@ -1,0 +1,83 @@
+"""Fills the reference's empty code/geometric_verification.py (0 bytes; the pipeline's
+"Geometric Verification" section at code/pipeline.py:60 is a bare comment).
+
+`pipeline.py` star-imports this module (code/pipeline.py:3).  Verification is the build's spec
+(after papers/schoenberger2016sfm.pdf §4.1): 8-point fundamental-matrix RANSAC,
+`n_hyp` hypotheses per pair drawn by a counter-based RNG keyed (seed, a, b, h), Sampson error in
+squared pixels below `thr`, best = max inlier count (lowest hypothesis id on ties); a pair is
+verified when the count reaches `min_inliers`.  All arithmetic runs in libsfmcore (HIP).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import sfmcore
+
+DEFAULT_HYPOTHESES = 4096
+DEFAULT_SEED = 42
+DEFAULT_THRESHOLD = 1.0   # Sampson error, px^2
+DEFAULT_MIN_INLIERS = 15  # COLMAP's default N_F
+
+
+def denormalize_F(Fn, norm) -> np.ndarray:
+    """Pixel-space F = T2^T Fn T1 (fp64), unit Frobenius norm.  norm = (cx1,cy1,s1,cx2,cy2,s2)."""
+    Fn = np.asarray(Fn, np.float64).reshape(3, 3)
+    cx1, cy1, s1, cx2, cy2, s2 = [float(v) for v in norm]
+    T1 = np.array([[s1, 0, -s1 * cx1], [0, s1, -s1 * cy1], [0, 0, 1.0]])
+    T2 = np.array([[s2, 0, -s2 * cx2], [0, s2, -s2 * cy2], [0, 0, 1.0]])
+    F = T2.T @ Fn @ T1
+    n = np.linalg.norm(F)
+    return F / n if n > 0 else F
+
+
+def verify_pair(kp1, kp2, matches, pair=(0, 1), n_hyp=DEFAULT_HYPOTHESES, seed=DEFAULT_SEED,
+                thr=DEFAULT_THRESHOLD, min_inliers=DEFAULT_MIN_INLIERS, device=0):
+    """kp1/kp2: [K,2] pixel coordinates; matches: list of DMatch or [M,2] (query, train) array.
+
+    Returns dict(F [3,3] pixel F, inliers [n] match indices (ascending), count, verified,
+    best_h)."""
+    import torch
+    if len(matches) and hasattr(matches[0], "queryIdx"):
+        mt = np.array([[m.queryIdx, m.trainIdx] for m in matches], np.int32)
+    else:
+        mt = np.asarray(matches, np.int32).reshape(-1, 2)
+    k1, k2 = np.asarray(kp1, np.float32), np.asarray(kp2, np.float32)
+    k_max = max(len(k1), len(k2), len(mt), 1)
+    kps = np.zeros((2, k_max, 2), np.float32)
+    kps[0, :len(k1)] = k1
+    kps[1, :len(k2)] = k2
+    match = np.zeros((1, k_max, 2), np.int32)
+    match[0, :len(mt)] = mt
+    dev = torch.device("cuda", device)
+    ctx = sfmcore.context(device)
+    # the RNG is keyed by the pair's image ids; pass them through as a 1-pair batch
+    a, b = int(pair[0]), int(pair[1])
+    n_img = max(a, b) + 1
+    kps_full = np.zeros((n_img, k_max, 2), np.float32)
+    kps_full[a] = kps[0]
+    kps_full[b] = kps[1]
+    out = ctx.ransac_batch(torch.from_numpy(kps_full).to(dev),
+                           torch.tensor([[a, b]], dtype=torch.int32, device=dev),
+                           torch.tensor([len(mt)], dtype=torch.int32, device=dev),
+                           torch.from_numpy(match).to(dev), n_hyp=n_hyp, seed=seed, thr=thr,
+                           min_inliers=min_inliers)
+    cnt = int(out["inl_count"].cpu()[0])
+    mask = out["mask"][0, :len(mt)].cpu().numpy().astype(bool)
+    F = denormalize_F(out["F"][0].cpu().numpy(), out["norm"][0].cpu().numpy())
+    return dict(F=F, inliers=np.nonzero(mask)[0], count=max(cnt, 0),
+                verified=cnt >= min_inliers, best_h=int(out["best_h"].cpu()[0]))
+
+
+def verify_pairs(pair_matches, keypoints, **kw):
+    """Verifies the reference's pair list (code/pipeline.py:36-47: Pair objects with img_inx_1,
+    img_inx_2, matches); keypoints[i] = [K,2] coordinates of image i.  Returns the verified
+    subset with `.matches` reduced to the inliers and `.F` attached."""
+    verified = []
+    for pr in pair_matches:
+        r = verify_pair(keypoints[pr.img_inx_1], keypoints[pr.img_inx_2], pr.matches,
+                        pair=(pr.img_inx_1, pr.img_inx_2), **kw)
+        if r["verified"]:
+            pr.matches = [pr.matches[i] for i in r["inliers"]]
+            pr.F = r["F"]
+            verified.append(pr)
+    return verified

@@ -1,0 +1,141 @@
+"""Batched match + verify over an image-pair list, sharded across GPUs.
+
+This is the reference's pair loop (code/pipeline.py:36-49: for every image pair, extract_and_match,
+keep non-empty results as Pair(img_inx_1, img_inx_2, matches)) restated for one process per GPU:
+
+* the unordered pair list (a<b) is cut into contiguous shards balanced by cost Ka*Kb;
+* each rank runs K1 (MFMA matcher) and K2 (RANSAC) on its shard — no collective on the data path;
+  RANSAC is keyed by (seed, a, b, h), so every pair's result is independent of the sharding;
+* the verified match graph (the analogue of `pair_matches`) is exchanged once with two
+  all-gathers (per-rank row count, then the padded rows) over RCCL (`nccl` backend) — or gloo
+  for the CPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import sfmcore
+
+
+def shard_pairs(pairs: np.ndarray, rank: int, world: int, n_kp=None) -> np.ndarray:
+    """Contiguous shard `rank` of `pairs`, balanced by the per-pair cost n_kp[a]*n_kp[b]."""
+    pairs = np.asarray(pairs, np.int32)
+    if world <= 1:
+        return pairs
+    if n_kp is None:
+        cost = np.ones(len(pairs))
+    else:
+        n_kp = np.asarray(n_kp, np.float64)
+        cost = n_kp[pairs[:, 0]] * n_kp[pairs[:, 1]] + 1.0
+    cum = np.concatenate([[0.0], np.cumsum(cost)])
+    cuts = np.searchsorted(cum, cum[-1] * np.arange(world + 1) / world, side="left")
+    cuts[0], cuts[-1] = 0, len(pairs)
+    cuts = np.maximum.accumulate(cuts)
+    return pairs[cuts[rank]:cuts[rank + 1]]
+
+
+class GraphBuilder:
+    """Holds one image set on the device and verifies pair batches against it."""
+
+    def __init__(self, desc, kps, n_kp=None, device: int = 0, ratio=(4, 5),
+                 cross_check=sfmcore.XC_MUTUAL, max_dist=-1, n_hyp=4096, seed=42, thr=1.0,
+                 min_inliers=15):
+        import torch
+        self.torch = torch
+        self.dev = torch.device("cuda", device)
+        self.ctx = sfmcore.context(device)
+        desc = np.ascontiguousarray(desc, np.uint8)
+        self.n_img, self.k_max, self.dim = desc.shape
+        if n_kp is None:
+            n_kp = np.full(self.n_img, self.k_max, np.int32)
+        self.desc = torch.from_numpy(desc).to(self.dev)
+        self.kps = torch.from_numpy(np.ascontiguousarray(kps, np.float32)).to(self.dev)
+        self.n_kp = torch.from_numpy(np.ascontiguousarray(n_kp, np.int32)).to(self.dev)
+        self.metric = sfmcore.METRIC_L2 if self.dim == 128 else sfmcore.METRIC_HAMMING
+        self.match_kw = dict(metric=self.metric, cross_check=cross_check, ratio=ratio,
+                             max_dist=max_dist)
+        self.ransac_kw = dict(n_hyp=n_hyp, seed=seed, thr=thr, min_inliers=min_inliers)
+        self.min_inliers = min_inliers
+        self._bufs = {}
+
+    def _buffers(self, P):
+        b = self._bufs.get(P)
+        if b is None:
+            torch, dev, K = self.torch, self.dev, self.k_max
+            b = dict(match=(torch.empty(P, dtype=torch.int32, device=dev),
+                            torch.empty((P, K, 2), dtype=torch.int32, device=dev),
+                            torch.empty((P, K), dtype=torch.int32, device=dev)),
+                     ransac=dict(inl_count=torch.empty(P, dtype=torch.int32, device=dev),
+                                 best_h=torch.empty(P, dtype=torch.int32, device=dev),
+                                 mask=torch.empty((P, K), dtype=torch.uint8, device=dev),
+                                 F=torch.empty((P, 9), dtype=torch.float32, device=dev),
+                                 norm=torch.empty((P, 6), dtype=torch.float32, device=dev)))
+            self._bufs = {P: b}
+        return b
+
+    def match(self, pairs_t):
+        b = self._buffers(pairs_t.shape[0])
+        return self.ctx.match_batch(self.desc, self.n_kp, pairs_t, out=b["match"],
+                                    **self.match_kw)
+
+    def verify(self, pairs_t, count, match):
+        b = self._buffers(pairs_t.shape[0])
+        return self.ctx.ransac_batch(self.kps, pairs_t, count, match, out=b["ransac"],
+                                     **self.ransac_kw)
+
+    def run(self, pairs_t):
+        """K1 + K2 on one pair batch; returns (count, match, dist, ransac dict) device tensors."""
+        count, match, dist = self.match(pairs_t)
+        rs = self.verify(pairs_t, count, match)
+        return count, match, dist, rs
+
+    def graph_rows(self, pair_base: int, count, match, rs):
+        """Verified inlier rows [n,3] int32 (global pair index, queryIdx, trainIdx), on device."""
+        torch = self.torch
+        K = self.k_max
+        ok = rs["inl_count"] >= self.min_inliers
+        ar = torch.arange(K, device=self.dev)
+        sel = (rs["mask"] != 0) & ok[:, None] & (ar[None, :] < count[:, None])
+        pm = sel.nonzero()
+        rows = torch.empty((pm.shape[0], 3), dtype=torch.int32, device=self.dev)
+        rows[:, 0] = (pm[:, 0] + pair_base).to(torch.int32)
+        rows[:, 1:] = match[pm[:, 0], pm[:, 1]]
+        return rows
+
+
+def all_gather_rows(rows, group=None):
+    """All-gather variable-length [n,3] int32 row blocks from every rank (rank order).
+
+    Two collectives: the per-rank row count, then the rows padded to the maximum count (RCCL has
+    no all-gatherv)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return rows
+    world = dist.get_world_size(group)
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    counts = [int(x.item()) for x in ns]
+    m = max(max(counts), 1)
+    pad = torch.zeros((m, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    pad[:rows.shape[0]] = rows
+    out = torch.empty((world * m, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    dist.all_gather_into_tensor(out, pad, group=group)
+    return torch.cat([out[r * m:r * m + counts[r]] for r in range(world)])
+
+
+def rows_to_pairs(rows: np.ndarray, pairs: np.ndarray):
+    """Host view of a gathered graph: list of (a, b, [(queryIdx, trainIdx), ...]) like the
+    reference's pair_matches (code/pipeline.py:43-47)."""
+    out = []
+    if len(rows) == 0:
+        return out
+    order = np.argsort(rows[:, 0], kind="stable")
+    rows = rows[order]
+    starts = np.flatnonzero(np.r_[True, rows[1:, 0] != rows[:-1, 0]])
+    ends = np.r_[starts[1:], len(rows)]
+    for s, e in zip(starts, ends):
+        p = int(rows[s, 0])
+        out.append((int(pairs[p, 0]), int(pairs[p, 1]), rows[s:e, 1:].copy()))
+    return out

@@ -1,0 +1,208 @@
+"""ctypes binding of libsfmcore.so (include/sfmcore.h) — the only way Python reaches the kernels.
+
+Device memory and streams come from PyTorch-ROCm (plumbing only): arrays are passed as
+`tensor.data_ptr()` and every call is enqueued on torch's current HIP stream, so kernels order
+correctly with torch copies.  There is no CPU fallback: if the library is missing or the device is
+not gfx950 the calls raise `SfmCoreError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsfmcore.so")
+
+METRIC_L2, METRIC_HAMMING = 0, 1
+XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
+
+EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_sync",
+            "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
+            "sfm_ba_jtj"]
+
+
+class SfmCoreError(RuntimeError):
+    pass
+
+
+class MatchParams(C.Structure):
+    _fields_ = [("metric", C.c_int32), ("cross_check", C.c_int32), ("ratio_num", C.c_int32),
+                ("ratio_den", C.c_int32), ("max_dist", C.c_int64)]
+
+
+class RansacParams(C.Structure):
+    _fields_ = [("n_hyp", C.c_int32), ("min_inliers", C.c_int32), ("thr", C.c_float),
+                ("_pad", C.c_int32), ("seed", C.c_uint64)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Loads (building it first if hipcc is present and the .so is missing) libsfmcore.so."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            if os.path.exists("/opt/rocm/bin/hipcc"):
+                from build_lib import build
+                build()
+            if not os.path.exists(path):
+                raise SfmCoreError(f"libsfmcore.so not found at {path}; run __graft_entry__.build()")
+        L = C.CDLL(path)
+        vp, i32, i64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+        L.sfm_ctx_create.argtypes = [i32, C.POINTER(vp)]
+        L.sfm_ctx_destroy.argtypes = [vp]
+        L.sfm_ctx_set_stream.argtypes = [vp, vp]
+        L.sfm_ctx_sync.argtypes = [vp]
+        L.sfm_last_error.restype = C.c_char_p
+        L.sfm_version.restype = i32
+        L.sfm_match_batch.argtypes = [vp, vp, vp, i32, i32, i32, vp, i32, C.POINTER(MatchParams),
+                                      vp, vp, vp]
+        L.sfm_ransac_f_batch.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
+                                         C.POINTER(RansacParams), vp, vp, vp, vp, vp]
+        L.sfm_ba_jtj.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp,
+                                 vp, vp, vp, vp, vp, vp]
+        for name in EXPORTED:
+            getattr(L, name).restype = getattr(L, name).restype or C.c_int
+        _lib = L
+        return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load_library().sfm_last_error().decode(errors="replace")
+        raise SfmCoreError(f"libsfmcore error {rc}: {msg}")
+
+
+def _ptr(t) -> int:
+    return t.data_ptr()
+
+
+class Context:
+    """One per device (not thread-safe).  Calls run on torch's current stream of that device."""
+
+    def __init__(self, device: int = 0):
+        import torch
+        self.torch = torch
+        if not torch.cuda.is_available():
+            raise SfmCoreError("no HIP device visible: the sfm core has no CPU fallback")
+        self.lib = load_library()
+        self.device = device
+        h = C.c_void_p()
+        _check(self.lib.sfm_ctx_create(device, C.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.sfm_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _bind_stream(self):
+        s = self.torch.cuda.current_stream(self.device).cuda_stream
+        _check(self.lib.sfm_ctx_set_stream(self.handle, C.c_void_p(s)))
+
+    def sync(self):
+        _check(self.lib.sfm_ctx_sync(self.handle))
+
+    # ---- matching --------------------------------------------------------------------------
+    def match_batch(self, desc, n_kp, pairs, metric=METRIC_L2, cross_check=XC_MUTUAL,
+                    ratio=None, max_dist=-1, out=None):
+        """desc [n_img,k_max,dim] u8, n_kp [n_img] i32, pairs [P,2] i32 (device tensors).
+
+        Returns (count [P] i32, match [P,k_max,2] i32, dist [P,k_max] i32)."""
+        torch = self.torch
+        n_img, k_max, dim = desc.shape
+        P = pairs.shape[0]
+        for t, dt in ((desc, torch.uint8), (n_kp, torch.int32), (pairs, torch.int32)):
+            if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+                raise SfmCoreError("match_batch: expected contiguous device tensors "
+                                   "(desc u8, n_kp i32, pairs i32)")
+        dev = desc.device
+        if out is None:
+            out = (torch.empty(P, dtype=torch.int32, device=dev),
+                   torch.empty((P, k_max, 2), dtype=torch.int32, device=dev),
+                   torch.empty((P, k_max), dtype=torch.int32, device=dev))
+        num, den = (0, 0) if ratio is None else ratio
+        prm = MatchParams(metric, cross_check, int(num), int(den), int(max_dist))
+        self._bind_stream()
+        _check(self.lib.sfm_match_batch(self.handle, _ptr(desc), _ptr(n_kp), n_img, k_max, dim,
+                                        _ptr(pairs), P, C.byref(prm), _ptr(out[0]), _ptr(out[1]),
+                                        _ptr(out[2])))
+        return out
+
+    # ---- geometric verification ------------------------------------------------------------
+    def ransac_batch(self, kps, pairs, count, match, n_hyp=4096, seed=42, thr=1.0,
+                     min_inliers=15, out=None):
+        """kps [n_img,k_max,2] f32 + the outputs of match_batch.  Returns dict of device tensors:
+        inl_count [P] (-1: fewer than 8 matches), best_h [P], mask [P,k_max] u8,
+        F [P,9] f32 (normalised coordinates), norm [P,6] f32 (cx1,cy1,s1,cx2,cy2,s2)."""
+        torch = self.torch
+        n_img, k_max, _ = kps.shape
+        P = pairs.shape[0]
+        dev = kps.device
+        if kps.dtype != torch.float32 or not kps.is_contiguous():
+            raise SfmCoreError("ransac_batch: kps must be contiguous float32")
+        if out is None:
+            out = dict(inl_count=torch.empty(P, dtype=torch.int32, device=dev),
+                       best_h=torch.empty(P, dtype=torch.int32, device=dev),
+                       mask=torch.empty((P, k_max), dtype=torch.uint8, device=dev),
+                       F=torch.empty((P, 9), dtype=torch.float32, device=dev),
+                       norm=torch.empty((P, 6), dtype=torch.float32, device=dev))
+        prm = RansacParams(int(n_hyp), int(min_inliers), float(thr), 0, int(seed))
+        self._bind_stream()
+        _check(self.lib.sfm_ransac_f_batch(self.handle, _ptr(kps), n_img, k_max, _ptr(pairs), P,
+                                           _ptr(count), _ptr(match), C.byref(prm),
+                                           _ptr(out["inl_count"]), _ptr(out["best_h"]),
+                                           _ptr(out["mask"]), _ptr(out["F"]), _ptr(out["norm"])))
+        return out
+
+    # ---- bundle adjustment -----------------------------------------------------------------
+    def ba_jtj(self, cams, pp, pts, cam_idx, pt_idx, uv, pt_ptr, cam_ptr, cam_obs, loss_s=0.0):
+        torch = self.torch
+        dev = cams.device
+        nc, npt, no = cams.shape[0], pts.shape[0], cam_idx.shape[0]
+        f64 = torch.float64
+        U = torch.empty((nc, 8, 8), dtype=f64, device=dev)
+        V = torch.empty((npt, 3, 3), dtype=f64, device=dev)
+        W = torch.empty((no, 8, 3), dtype=f64, device=dev)
+        gc = torch.empty((nc, 8), dtype=f64, device=dev)
+        gp = torch.empty((npt, 3), dtype=f64, device=dev)
+        res = torch.empty((no, 2), dtype=f64, device=dev)
+        cost = torch.empty(1, dtype=f64, device=dev)
+        self._bind_stream()
+        _check(self.lib.sfm_ba_jtj(self.handle, nc, _ptr(cams), _ptr(pp), npt, _ptr(pts), no,
+                                   _ptr(cam_idx), _ptr(pt_idx), _ptr(uv), _ptr(pt_ptr),
+                                   _ptr(cam_ptr), _ptr(cam_obs), float(loss_s), _ptr(U), _ptr(V),
+                                   _ptr(W), _ptr(gc), _ptr(gp), _ptr(res), _ptr(cost)))
+        return dict(U=U, V=V, W=W, gc=gc, gp=gp, res=res, cost=cost)
+
+
+_ctx_cache: dict = {}
+
+
+def context(device: int = 0) -> Context:
+    ctx = _ctx_cache.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _ctx_cache[device] = ctx
+    return ctx
+
+
+def csr_by(index: np.ndarray, n: int):
+    """CSR (ptr [n+1], order) grouping positions of `index` by value, stable."""
+    order = np.argsort(index, kind="stable").astype(np.int32)
+    ptr = np.zeros(n + 1, np.int32)
+    np.cumsum(np.bincount(index, minlength=n), out=ptr[1:])
+    return ptr, order

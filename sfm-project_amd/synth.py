@@ -1,0 +1,175 @@
+"""Seeded synthetic SfM scenes: cameras, 3D points, keypoints and descriptors.
+
+The reference reads real photos (`code/pipeline.py:25`, `dataset/Bicycle/images`) and extracts ORB
+features with OpenCV (`code/feature_matching.py:42-45`).  Neither the dataset nor `cv2` exists here,
+so every benchmark and parity test starts at the descriptor level from this generator
+(SURVEY.md §8d "Concrete synthetic inputs").
+
+Scene model
+-----------
+* 3D points uniform in the box [-2, 2]^3 around the origin.
+* Cameras on a 120-degree arc of radius 8 around the y axis, all looking at the origin;
+  pinhole f = 1000 px, 1920x1080, principal point at the image centre, optional radial k1.
+* Each image observes a random subset of the points (projection + N(0, noise_px) pixel noise) and is
+  topped up to exactly K keypoints with uniform random outlier keypoints.  A `misplace_frac` share of
+  the observed points is put at a random position while keeping the point's descriptor (repeated
+  texture), so tentative matches contain geometric outliers for RANSAC to reject.  Keypoints are
+  shuffled.
+* SIFT-like descriptors: per point a base |N(0,1)|^128, L2-normalised, clipped at 0.2,
+  renormalised, scaled to 512 and rounded into [0, 255].  Each view adds N(0, desc_noise), rounds
+  and clips.  Outliers get independent bases.
+* ORB-like descriptors: per point a random 256-bit base; each view flips every bit with p = 0.05.
+
+Everything is drawn from numpy's PCG64 with the given seed, so scenes are reproducible on every
+machine (the GPU box regenerates them from the seed instead of shipping data).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+WIDTH, HEIGHT, FOCAL = 1920, 1080, 1000.0
+
+
+def _look_at(center: np.ndarray) -> np.ndarray:
+    """World->camera rotation for a camera at `center` looking at the origin (y up)."""
+    z = -center / np.linalg.norm(center)
+    up = np.array([0.0, 1.0, 0.0])
+    x = np.cross(up, z)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    return np.stack([x, y, z])  # rows = camera axes
+
+
+def rotmat_to_angle_axis(R: np.ndarray) -> np.ndarray:
+    cos = np.clip((np.trace(R) - 1.0) / 2.0, -1.0, 1.0)
+    theta = np.arccos(cos)
+    if theta < 1e-12:
+        return np.zeros(3)
+    w = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    return w * (theta / (2.0 * np.sin(theta)))
+
+
+def angle_axis_to_rotmat(r: np.ndarray) -> np.ndarray:
+    theta = np.linalg.norm(r)
+    if theta < 1e-12:
+        return np.eye(3)
+    k = r / theta
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(theta) * K + (1 - np.cos(theta)) * K @ K
+
+
+def project(R, t, f, k1, cx, cy, X):
+    """Pinhole + one radial term; returns (N, 2) pixels and camera-frame depth."""
+    P = X @ R.T + t
+    p = P[:, :2] / P[:, 2:3]
+    d = 1.0 + k1 * np.sum(p * p, axis=1, keepdims=True)
+    return f * d * p + np.array([cx, cy]), P[:, 2]
+
+
+def _sift_bases(rng, n):
+    b = np.abs(rng.standard_normal((n, 128)))
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    b = np.minimum(b, 0.2)
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    return b * 512.0
+
+
+def make_scene(n_img: int, n_kp: int, seed: int = 0, n_pts: int | None = None,
+               inlier_frac: float = 0.7, noise_px: float = 0.5, desc_noise: float = 6.0,
+               k1_range: float = 0.0, orb: bool = False, arc_deg: float = 120.0,
+               misplace_frac: float = 0.25) -> dict:
+    """Build a scene; returns a dict of numpy arrays (see module docstring)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n_in = int(round(inlier_frac * n_kp))
+    if n_pts is None:
+        n_pts = max(int(1.5 * n_in), 16)
+    pts = rng.uniform(-2.0, 2.0, size=(n_pts, 3))
+    cx, cy = WIDTH / 2.0, HEIGHT / 2.0
+
+    cams = np.zeros((n_img, 8))          # angle-axis(3), t(3), f, k1
+    pp = np.tile(np.array([cx, cy]), (n_img, 1))
+    Rs = []
+    for i in range(n_img):
+        ang = np.deg2rad(-arc_deg / 2 + arc_deg * (i + 0.5) / n_img)
+        C = 8.0 * np.array([np.sin(ang), 0.15 * np.cos(3 * ang), np.cos(ang)])
+        R = _look_at(C)
+        t = -R @ C
+        Rs.append(R)
+        cams[i, :3] = rotmat_to_angle_axis(R)
+        cams[i, 3:6] = t
+        cams[i, 6] = FOCAL
+        cams[i, 7] = rng.uniform(-k1_range, k1_range) if k1_range > 0 else 0.0
+
+    if orb:
+        pbase = rng.integers(0, 256, size=(n_pts, 32), dtype=np.uint8)
+    else:
+        pbase = _sift_bases(rng, n_pts)
+
+    kps = np.zeros((n_img, n_kp, 2), np.float32)
+    desc = np.zeros((n_img, n_kp, 32 if orb else 128), np.uint8)
+    pid = np.full((n_img, n_kp), -1, np.int32)
+    for i in range(n_img):
+        uv, z = project(Rs[i], cams[i, 3:6], cams[i, 6], cams[i, 7], cx, cy, pts)
+        vis = np.nonzero((z > 0) & (uv[:, 0] >= 0) & (uv[:, 0] < WIDTH)
+                         & (uv[:, 1] >= 0) & (uv[:, 1] < HEIGHT))[0]
+        sel = rng.choice(vis, size=min(n_in, vis.size), replace=False)
+        n_out = n_kp - sel.size
+        xy_in = uv[sel] + rng.normal(0.0, noise_px, size=(sel.size, 2))
+        # repeated-texture confusers: the descriptor is the point's, the position is elsewhere
+        mis = rng.random(sel.size) < misplace_frac
+        xy_in[mis] = rng.uniform([0, 0], [WIDTH, HEIGHT], size=(int(mis.sum()), 2))
+        xy = np.concatenate([xy_in, rng.uniform([0, 0], [WIDTH, HEIGHT], size=(n_out, 2))])
+        ids = np.concatenate([sel, np.full(n_out, -1)]).astype(np.int32)
+        if orb:
+            d_in = pbase[sel]
+            flips = rng.random((sel.size, 256)) < 0.05
+            d_in = d_in ^ np.packbits(flips, axis=1)
+            d_out = rng.integers(0, 256, size=(n_out, 32), dtype=np.uint8)
+        else:
+            d_in = pbase[sel] + rng.normal(0.0, desc_noise, size=(sel.size, 128))
+            d_out = _sift_bases(rng, n_out)
+        d = np.concatenate([d_in, d_out])
+        if not orb:
+            d = np.clip(np.rint(d), 0, 255).astype(np.uint8)
+        perm = rng.permutation(n_kp)
+        kps[i] = xy[perm].astype(np.float32)
+        desc[i] = d[perm]
+        pid[i] = ids[perm]
+    return dict(kps=kps, desc=desc, point_ids=pid, cams=cams, pp=pp, pts=pts,
+                n_kp=np.full(n_img, n_kp, np.int32))
+
+
+def unordered_pairs(n_img: int) -> np.ndarray:
+    """All a<b pairs in row-major order (the shard axis)."""
+    a, b = np.triu_indices(n_img, k=1)
+    return np.stack([a, b], axis=1).astype(np.int32)
+
+
+def make_ba_problem(n_cam: int, n_pt: int, obs_per_pt: int = 5, seed: int = 0,
+                    noise_px: float = 0.5, perturb: float = 1e-3) -> dict:
+    """Bundle-adjustment observations: each point seen by `obs_per_pt` cameras.
+
+    Observations are grouped by point (point-major), the layout the BA kernels shard on.
+    Camera/point parameters are perturbed from the truth so residuals are non-trivial.
+    """
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sc = make_scene(n_cam, 8, seed=seed, n_pts=8, k1_range=0.05)
+    cams_true = sc["cams"]
+    pp = sc["pp"]
+    pts_true = rng.uniform(-2.0, 2.0, size=(n_pt, 3))
+    cam_idx = np.empty((n_pt, obs_per_pt), np.int32)
+    for p in range(n_pt):
+        cam_idx[p] = rng.choice(n_cam, size=obs_per_pt, replace=False)
+    cam_idx = np.sort(cam_idx, axis=1).reshape(-1)
+    pt_idx = np.repeat(np.arange(n_pt, dtype=np.int32), obs_per_pt)
+    uv = np.empty((cam_idx.size, 2))
+    Rs = [angle_axis_to_rotmat(c[:3]) for c in cams_true]
+    for c in range(n_cam):
+        sel = np.nonzero(cam_idx == c)[0]
+        uv[sel], _ = project(Rs[c], cams_true[c, 3:6], cams_true[c, 6], cams_true[c, 7],
+                             pp[c, 0], pp[c, 1], pts_true[pt_idx[sel]])
+    uv += rng.normal(0.0, noise_px, size=uv.shape)
+    cams = cams_true.copy()
+    cams[:, :6] += rng.normal(0.0, perturb, size=(n_cam, 6))
+    pts = pts_true + rng.normal(0.0, 10 * perturb, size=pts_true.shape)
+    return dict(cams=cams, pp=pp, pts=pts, cam_idx=cam_idx, pt_idx=pt_idx, uv=uv)

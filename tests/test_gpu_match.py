@@ -1,0 +1,117 @@
+"""GPU parity: libsfmcore matching (K1 MFMA L2, Hamming) vs the CPU oracle, bit-exact.
+
+Calls go through the C-ABI (sfmcore.py -> libsfmcore.so).  The oracle (oracle/sfm_oracle.c) is the
+checker only.  Edge cases mirror what BFMatcher sees in the reference loop (code/pipeline.py:38-47):
+empty descriptor sets, a single train, ragged per-image counts, non-multiple-of-32 sizes.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import sfmcore
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_match(ctx, desc, n_kp, pairs, **kw):
+    import torch
+    d = torch.from_numpy(np.ascontiguousarray(desc)).cuda()
+    n = torch.from_numpy(np.ascontiguousarray(n_kp, np.int32)).cuda()
+    pr = torch.from_numpy(np.ascontiguousarray(pairs, np.int32)).cuda()
+    cnt, mt, dist = ctx.match_batch(d, n, pr, **kw)
+    torch.cuda.synchronize()
+    return cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+
+
+def _check_pairs(ctx, desc, n_kp, pairs, metric=0, cross_check=1, ratio=None, max_dist=-1):
+    cnt, mt, dist = _gpu_match(ctx, desc, n_kp, pairs, metric=metric, cross_check=cross_check,
+                               ratio=ratio, max_dist=max_dist)
+    for p, (a, b) in enumerate(pairs):
+        q, t, d = O.match(desc[a, :n_kp[a]], desc[b, :n_kp[b]], metric=metric,
+                          cross_check=cross_check, ratio=ratio, max_dist=max_dist)
+        k = cnt[p]
+        assert k == len(q), f"pair {p} ({a},{b}): count {k} != oracle {len(q)}"
+        np.testing.assert_array_equal(mt[p, :k, 0], q)
+        np.testing.assert_array_equal(mt[p, :k, 1], t)
+        np.testing.assert_array_equal(dist[p, :k], d)
+    return cnt
+
+
+def test_l2_small_pair_mutual_ratio(ctx):
+    s = synth.make_scene(2, 512, seed=3)
+    cnt = _check_pairs(ctx, s["desc"], s["n_kp"], np.array([[0, 1], [1, 0]], np.int32),
+                       ratio=(4, 5))
+    assert cnt[0] > 100
+
+
+@pytest.mark.parametrize("xc,ratio,maxd", [(0, None, -1), (1, None, -1), (2, None, -1),
+                                           (1, (4, 5), -1), (0, (3, 4), -1), (1, (4, 5), 40000),
+                                           (2, None, 30000)])
+def test_l2_modes(ctx, xc, ratio, maxd):
+    s = synth.make_scene(4, 1000, seed=5)
+    pairs = synth.unordered_pairs(4)
+    _check_pairs(ctx, s["desc"], s["n_kp"], pairs, cross_check=xc, ratio=ratio, max_dist=maxd)
+
+
+def test_l2_batch_2048(ctx):
+    s = synth.make_scene(6, 2048, seed=7)
+    pairs = synth.unordered_pairs(6)
+    cnt = _check_pairs(ctx, s["desc"], s["n_kp"], pairs, ratio=(4, 5))
+    assert (cnt > 300).all()
+
+
+def test_l2_ragged_and_edges(ctx):
+    rng = np.random.default_rng(11)
+    k_max = 1100
+    n_img = 6
+    desc = rng.integers(0, 256, size=(n_img, k_max, 128), dtype=np.uint8)
+    # duplicated descriptors force exact distance ties (lowest-index rules)
+    desc[1, 5] = desc[1, 7]
+    desc[2, 10:20] = desc[0, 30]
+    n_kp = np.array([1100, 37, 1, 0, 2, 1025], np.int32)
+    pairs = np.array([[a, b] for a in range(n_img) for b in range(n_img) if a != b], np.int32)
+    for xc, ratio in [(1, (4, 5)), (0, None), (2, None), (1, None)]:
+        _check_pairs(ctx, desc, n_kp, pairs, cross_check=xc, ratio=ratio)
+
+
+def test_l2_extreme_values(ctx):
+    # all-0 vs all-255 descriptors: the largest possible distances (exactness of the int path)
+    desc = np.zeros((2, 64, 128), np.uint8)
+    desc[1, :32] = 255
+    desc[0, 40:] = 255
+    desc[1, 50] = 0
+    n_kp = np.array([64, 64], np.int32)
+    for xc in (0, 1, 2):
+        _check_pairs(ctx, desc, n_kp, np.array([[0, 1], [1, 0]], np.int32), cross_check=xc)
+
+
+@pytest.mark.parametrize("xc,ratio,maxd", [(2, None, 26), (1, None, 26), (0, (4, 5), -1),
+                                           (2, None, -1)])
+def test_hamming_reference_semantics(ctx, xc, ratio, maxd):
+    s = synth.make_scene(3, 500, seed=13, orb=True)
+    pairs = np.array([[0, 1], [1, 0], [0, 2], [2, 1]], np.int32)
+    cnt = _check_pairs(ctx, s["desc"], s["n_kp"], pairs, metric=1, cross_check=xc, ratio=ratio,
+                       max_dist=maxd)
+    assert cnt.sum() > 0
+
+
+def test_hamming_ragged(ctx):
+    rng = np.random.default_rng(2)
+    desc = rng.integers(0, 256, size=(4, 300, 32), dtype=np.uint8)
+    desc[1, 3] = desc[1, 4]
+    n_kp = np.array([300, 1, 0, 17], np.int32)
+    pairs = np.array([[a, b] for a in range(4) for b in range(4) if a != b], np.int32)
+    _check_pairs(ctx, desc, n_kp, pairs, metric=1, cross_check=2, max_dist=26)
+    _check_pairs(ctx, desc, n_kp, pairs, metric=1, cross_check=1)
+
+
+def test_invalid_arguments_raise(ctx):
+    import torch
+    d = torch.zeros((2, 8, 128), dtype=torch.uint8, device="cuda")
+    n = torch.full((2,), 8, dtype=torch.int32, device="cuda")
+    pr = torch.tensor([[0, 1]], dtype=torch.int32, device="cuda")
+    with pytest.raises(sfmcore.SfmCoreError):
+        ctx.match_batch(d, n, pr, cross_check=2, ratio=(4, 5))
+    with pytest.raises(sfmcore.SfmCoreError):
+        ctx.match_batch(d, n, pr, metric=1)  # Hamming needs dim 32
