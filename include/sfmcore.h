@@ -10,8 +10,9 @@
  * Conventions
  *   - Plain pointers and sizes only.  Every array argument is a DEVICE pointer (hipMalloc'd or a
  *     torch.cuda tensor's data_ptr), C-contiguous, caller-owned.
- *   - Work is enqueued on the context's stream (sfm_ctx_set_stream; default: a stream the context
- *     creates).  Entry points return after enqueueing; sfm_ctx_sync waits.
+ *   - Work is enqueued on the context's stream: a non-blocking stream the context creates, until
+ *     sfm_ctx_set_stream selects another (NULL selects the legacy default stream, which is what
+ *     torch's default stream is).  Entry points return after enqueueing; sfm_ctx_sync waits.
  *   - Return 0 (SFM_OK) on success, < 0 on error; sfm_last_error() gives a thread-local message.
  *     No C++ exception crosses the ABI.  No callbacks.
  *   - A context is bound to one device and must not be used from two threads at once.
@@ -59,7 +60,7 @@ typedef struct sfm_ransac_params {
 /* ---- context ---------------------------------------------------------------------------- */
 int sfm_ctx_create(int32_t device, sfm_ctx** out);
 int sfm_ctx_destroy(sfm_ctx* ctx);
-int sfm_ctx_set_stream(sfm_ctx* ctx, void* hip_stream);   /* NULL: the context's own stream */
+int sfm_ctx_set_stream(sfm_ctx* ctx, void* hip_stream);   /* hipStream_t; NULL = default stream */
 int sfm_ctx_sync(sfm_ctx* ctx);
 const char* sfm_last_error(void);
 int32_t sfm_version(void);

@@ -56,6 +56,8 @@ def _bind(L):
     L.oracle_match_verify_batch.argtypes = [vp, vp, i32, i32, i32, vp, i32, i32, i32, i64, i32,
                                             u64, f32, i32, vp, vp]
     L.oracle_match_verify_batch.restype = C.c_longlong
+    L.oracle_set_threads.argtypes = [i32]
+    L.oracle_get_threads.restype = i32
     L.oracle_ba_obs.argtypes = [vp, vp, vp, vp, f64, vp, vp, vp, vp, vp]
     L.oracle_ba_jtj.argtypes = [i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp, vp, vp, vp, vp,
                                 vp]
@@ -151,6 +153,11 @@ def match_verify_batch(desc, kps, pairs, ratio=(4, 5), max_dist=-1, H=4096, seed
                                           desc.shape[2], _p(pairs), P, ratio[0], ratio[1],
                                           max_dist, H, seed, thr, min_inl, _p(nm), _p(ni))
     return int(tot), nm, ni
+
+
+def set_threads(n: int) -> int:
+    lib().oracle_set_threads(int(n))
+    return lib().oracle_get_threads()
 
 
 def ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0):

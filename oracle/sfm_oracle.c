@@ -445,3 +445,8 @@ long long oracle_match_verify_batch(const uint8_t* desc, const float* kps, int n
     }
     return total;
 }
+
+/* Thread control for the timed CPU baseline (bench.py reports the count it used). */
+#include <omp.h>
+void oracle_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
+int oracle_get_threads(void) { return omp_get_max_threads(); }

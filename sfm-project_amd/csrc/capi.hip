@@ -70,7 +70,7 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
 
 int sfm_ctx_set_stream(sfm_ctx* ctx, void* hip_stream) {
     SFM_REQUIRE(ctx != nullptr, "sfm_ctx_set_stream: ctx is NULL");
-    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    ctx->stream = (hipStream_t)hip_stream;  // NULL = the legacy default stream (torch's default)
     return SFM_OK;
 }
 

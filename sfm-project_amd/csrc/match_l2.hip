@@ -9,18 +9,24 @@
 // train maximises  vr = 2 dot - |y'_j|^2  (= |x'_i|^2 - d^2);  for a fixed train j the best
 // query maximises  vc = 2 dot - |x'_i|^2  (= |y'_j|^2 - d^2).
 //
-// Tile geometry: MFMA output tile D[32 trains][32 queries]; the column (query) is the lane, the
-// 16 accumulator registers of a lane are 16 of the 32 train rows (the other 16 are in lane^32).
-//  * row direction (per query, top-2 over trains): lane-local.  Each register becomes the packed
-//    key vr*32 + (31 - row) with ONE v_mad_i32_i24 (dot*64 + (31 - row - 32|y'|^2)); a
-//    max3/med3 network keeps the tile top-2; the running (best, argbest, second) per query is
-//    merged once per tile.
-//  * column direction (per train, best query): the key vc*128 + (127 - q) (q = query slot in the
-//    wave) is one more v_mad_i32_i24 and a v_max per element, reduced over the wave's 4 query
-//    tiles in registers, then across the 32 lanes of each half with DPP, then across waves with
-//    64-bit LDS atomics; one slab per workgroup is written to HBM and merged in the finalize.
-// Every wave holds 4 query tiles (128 queries, B operand, 64 VGPRs); a 512-thread workgroup
-// covers 1024 queries of one pair and streams all train tiles of the other image.
+// Geometry.  A 512-thread workgroup owns 1024 queries of one pair (8 waves x 4 query tiles of 32;
+// the query descriptors are the MFMA B operand, held in 64 VGPRs per wave for the whole kernel)
+// and streams every train of the other image through LDS in chunks of 256 rows (8 tiles), double
+// buffered with global_load_lds (LDS-DMA) and an XOR-swizzled row image (conflict-free
+// ds_read_b128; the swizzle is applied on the DMA source address).  MFMA output tile
+// D[32 trains][32 queries]: the query is the lane, the 16 accumulator registers of a lane are 16
+// of the 32 train rows (the other 16 live in lane ^ 32).
+//  * row direction (per query: best, argbest, second over trains) is lane-local: one
+//    v_mad_i32_i24 per element forms key = vr*256 + (255 - row_in_chunk); a max3/med3 network
+//    keeps the chunk top-2 over all 256 trains of the chunk; (best, argbest, second) is merged once
+//    per chunk.
+//  * column direction (per train: best query): key = vc*128 + (127 - query_in_wave), one mad
+//    per element, v_max3 over the wave's 4 query tiles, then a transpose-reduce across the 32 lanes
+//    of each half (permlane16_swap + DPP: 40 instructions for 16 registers) that leaves one train
+//    row per lane pair, and one 64-bit LDS atomic max per lane merges the 8 waves.  Each workgroup
+//    writes its column slab once; the finalize kernel merges the slabs of a pair.
+// Padded trains/queries read a constant row of 0x80 bytes (i8 zero: dot = 0), so their keys are
+// the table constants alone and can never win.
 #include <algorithm>
 #include <climits>
 
@@ -34,30 +40,25 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int QT = 4;                 // query tiles (32 each) per wave
 constexpr int WAVES = 8;              // waves per workgroup
 constexpr int QB = WAVES * QT * 32;   // queries per workgroup
-constexpr int SENT_ROW = -1073741824; // Crow of padded trains: never wins (DESIGN.md §4.1 ranges)
-constexpr int SENT_COL = -1476395008; // Ccol of padded queries
-constexpr int COL_VALID_MIN = -940000000;  // col keys below come from padded queries only
-constexpr int ROW_VALID_MIN = -(1 << 24);  // row values below come from padded trains only
+constexpr int CHUNK = 256;            // trains per LDS stage (8 tiles)
+constexpr int KALIGN = 256;           // tables are padded to a multiple of CHUNK
+constexpr int SENT_ROW = INT_MIN + 1024;  // crow of padded trains (dot is 0 there)
+constexpr int SENT_COL = INT_MIN + 1024;  // ccol of padded queries
+constexpr int ROW_VALID_MIN = -(1 << 24); // merged row values below this are padding
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
 
 __device__ __forceinline__ int imax3(int a, int b, int c) { return max(a, max(b, c)); }
-__device__ __forceinline__ int imed3(int a, int b, int c) {
-    return max(min(a, b), min(max(a, b), c));
-}
+__device__ __forceinline__ int imed3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 __device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
 
 template <int CTRL>
 __device__ __forceinline__ int dpp(int x) {
     return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
 }
-
-// max over the 32 lanes of each wave half (lanes 0-31 and 32-63 independently)
-__device__ __forceinline__ int half_max32(int x) {
-    x = max(x, dpp<0x121>(x));  // row_ror:1
-    x = max(x, dpp<0x122>(x));  // row_ror:2
-    x = max(x, dpp<0x124>(x));  // row_ror:4
-    x = max(x, dpp<0x128>(x));  // row_ror:8
-    int y = __builtin_amdgcn_ds_swizzle(x, 0x401F);  // lane ^ 16 within 32
-    return max(x, y);
+__device__ __forceinline__ int swz_xor4(int x) {
+    return __builtin_amdgcn_ds_swizzle(x, (4 << 10) | 0x1F);  // lane ^ 4 within 32
 }
 
 __device__ __forceinline__ v4i xor80(v4i v) {
@@ -65,12 +66,44 @@ __device__ __forceinline__ v4i xor80(v4i v) {
     return v4i{v.x ^ m, v.y ^ m, v.z ^ m, v.w ^ m};
 }
 
-// |x'|^2 and the row constant per descriptor, padded to k_pad (multiple of 32).
+// Max-reduce each of 16 registers over the 32 lanes of its wave half; on return lane l holds the
+// result for register r(l) = 8*b1 + 4*b2 + 2*b3 + b4 (b_k = bit k of l); lanes l and l^1 agree.
+__device__ __forceinline__ int transpose_max16(const int (&c)[16], int lane) {
+    int m[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // lane bit 4: rows (16 lanes) swapped pairwise
+        auto s = __builtin_amdgcn_permlane16_swap(c[2 * k], c[2 * k + 1], false, false);
+        m[k] = max((int)s[0], (int)s[1]);
+    }
+    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
+    int n[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // lane bit 3: xor 8 inside a 16-lane row = row_ror:8
+        const int t0 = max(m[2 * k], dpp<0x128>(m[2 * k]));
+        const int t1 = max(m[2 * k + 1], dpp<0x128>(m[2 * k + 1]));
+        n[k] = b3 ? t1 : t0;
+    }
+    int o[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // lane bit 2: xor 4 via ds_swizzle
+        const int send = b2 ? n[2 * k] : n[2 * k + 1];
+        const int keep = b2 ? n[2 * k + 1] : n[2 * k];
+        o[k] = max(keep, swz_xor4(send));
+    }
+    // lane bit 1: quad_perm [2,3,0,1]; lane bit 0: quad_perm [1,0,3,2]
+    const int p0 = max(o[0], dpp<0x4E>(o[0]));
+    const int p1 = max(o[1], dpp<0x4E>(o[1]));
+    const int q = b1 ? p1 : p0;
+    return max(q, dpp<0xB1>(q));
+}
+
+// |x'|^2 plus the row / column key constants per descriptor, padded to k_pad (multiple of 256).
 __global__ void l2_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
                                int k_max, int k_pad, int32_t* __restrict__ norm,
-                               int32_t* __restrict__ crow) {
+                               int32_t* __restrict__ crow, uint8_t* __restrict__ zero_row) {
     const int img = blockIdx.y;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (img == 0 && j < 128) zero_row[j] = 0x80;
     if (j >= k_pad) return;
     int nv = 0;
     if (j < k_max) {
@@ -90,101 +123,156 @@ __global__ void l2_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* 
     }
     const size_t o = (size_t)img * k_pad + j;
     norm[o] = nv;
-    crow[o] = (j < n_kp[img]) ? (-32 * nv + 31 - (j & 31)) : SENT_ROW;
+    // row key = vr*256 + (255 - row_in_chunk) = dot*512 + crow;  vr = 2 dot - |y'|^2
+    crow[o] = (j < n_kp[img]) ? (-256 * nv + 255 - (j & (CHUNK - 1))) : SENT_ROW;
 }
 
 __global__ __launch_bounds__(512, 2) void l2_match_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ crow_tab,
-    const int32_t* __restrict__ pairs, int n_qblk, int4* __restrict__ rowres,
-    unsigned long long* __restrict__ colpart) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_col[];
+    const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
+    int4* __restrict__ rowres, unsigned long long* __restrict__ colpart) {
+    // one dynamic LDS array: [2][CHUNK][128 B] train rows | [2][CHUNK] crow | [k_pad] col state
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    unsigned char* bufA = lds;
+    int* bufC = (int*)(lds + 2 * CHUNK * 128);
+    unsigned long long* lds_col = (unsigned long long*)(lds + 2 * CHUNK * 128 + 2 * CHUNK * 4);
+
     const int p = blockIdx.x / n_qblk, qb = blockIdx.x - p * n_qblk;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     for (int j = tid; j < k_pad; j += 512) lds_col[j] = 0ull;
-    __syncthreads();
+
+    const uint8_t* db = desc + (size_t)b * k_max * 128;
+    const int32_t* crb = crow_tab + (size_t)b * k_pad;
+    const int n_chunk = (nb + CHUNK - 1) / CHUNK;
+
+    // stage chunk ch into buffer sel: 4 x 1 KB LDS-DMA pieces per wave (+ the crow piece)
+    auto stage = [&](int ch, int sel) {
+        unsigned char* dst = bufA + sel * CHUNK * 128;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = wave * 4 + i;         // 1 KB = 8 rows
+            const int row = piece * 8 + (lane >> 3);
+            const int slot = (lane & 7) ^ ((row >> 1) & 7);
+            const int j = ch * CHUNK + row;
+            const uint8_t* src = (j < nb) ? db + (size_t)j * 128 + slot * 16 : zero_row + slot * 16;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
+        }
+        if (wave == 0) {
+            const int32_t* src = crb + ch * CHUNK + lane * 4;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(bufC + sel * CHUNK), 16, 0, 0);
+        }
+    };
 
     const int qbase = qb * QB + wave * QT * 32;
-    if (qbase < na) {
-        const uint8_t* da = desc + (size_t)a * k_max * 128;
-        const uint8_t* db = desc + (size_t)b * k_max * 128;
-        const int32_t* crb = crow_tab + (size_t)b * k_pad;
-        v4i bq[QT][4];
-        int ccol[QT], B1[QT], J1[QT], B2[QT];
+    const bool active = qbase < na;  // wave-uniform
+    v4i bq[QT][4];
+    int ccol[QT], B1[QT], J1[QT], B2[QT], tb[QT], ts[QT];
+    const uint8_t* da = desc + (size_t)a * k_max * 128;
 #pragma unroll
-        for (int c = 0; c < QT; ++c) {
-            const int q = qbase + c * 32 + r32;
-            const int qq = min(q, k_max - 1);
-            const v4i* src = (const v4i*)(da + (size_t)qq * 128 + 64 * h);
+    for (int c = 0; c < QT; ++c) {
+        const int q = qbase + c * 32 + r32;
+        const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * 128 + 64 * h : zero_row + 64 * h);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) bq[c][s] = xor80(src[s]);
-            ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32))
-                               : SENT_COL;
-            B1[c] = INT_MIN; J1[c] = -1; B2[c] = INT_MIN;
-        }
-        const int nt = (nb + 31) >> 5;
-        for (int t = 0; t < nt; ++t) {
-            const int jj = min(t * 32 + r32, k_max - 1);
-            const v4i* srcb = (const v4i*)(db + (size_t)jj * 128 + 64 * h);
-            v4i af[4];
+        for (int s = 0; s < 4; ++s) bq[c][s] = xor80(src[s]);
+        // col key = vc*128 + (127 - q_in_wave) = dot*256 + ccol;  vc = 2 dot - |x'|^2
+        ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32)) : SENT_COL;
+        B1[c] = INT_MIN; J1[c] = -1; B2[c] = INT_MIN;
+        tb[c] = INT_MIN; ts[c] = INT_MIN;
+    }
+    if (n_chunk > 0) stage(0, 0);
+    __syncthreads();
+
+    for (int ch = 0; ch < n_chunk; ++ch) {
+        const int sel = ch & 1;
+        if (ch + 1 < n_chunk) stage(ch + 1, sel ^ 1);
+        const int nt = min(8, (nb - ch * CHUNK + 31) >> 5);
+        if (active) {
+            const unsigned char* A = bufA + sel * CHUNK * 128;
+            const int* Cr = bufC + sel * CHUNK;
+            int ckey[8];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) af[s] = xor80(srcb[s]);
-            int crow[16];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                v4i cv = *(const v4i*)(crb + t * 32 + 8 * g + 4 * h);
-                crow[4 * g + 0] = cv.x; crow[4 * g + 1] = cv.y;
-                crow[4 * g + 2] = cv.z; crow[4 * g + 3] = cv.w;
-            }
-            int colacc[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) colacc[r] = INT_MIN;
-#pragma unroll
-            for (int c = 0; c < QT; ++c) {
-                v16i acc = {0};
+            for (int tt = 0; tt < 8; ++tt) {
+                ckey[tt] = INT_MIN;
+                if (tt >= nt) continue;
+                const int row = tt * 32 + r32;
+                const int swz = (row >> 1) & 7;
+                v4i af[4];
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
-                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc, 0, 0, 0);
-                // row direction: tile top-2 of packed keys
-                int k0 = mad24(acc[0], 64, crow[0]), k1 = mad24(acc[1], 64, crow[1]);
-                int tb = max(k0, k1), ts = min(k0, k1);
+                    af[s] = xor80(*(const v4i*)(A + row * 128 + (((4 * h + s) ^ swz) << 4)));
+                int crow[16];
 #pragma unroll
-                for (int r = 2; r < 16; r += 2) {
-                    int x = mad24(acc[r], 64, crow[r]);
-                    int y = mad24(acc[r + 1], 64, crow[r + 1]);
-                    ts = max(ts, imed3(tb, x, y));
-                    tb = imax3(tb, x, y);
+                for (int g = 0; g < 4; ++g) {
+                    const v4i cv = *(const v4i*)(Cr + tt * 32 + 8 * g + 4 * h);
+                    crow[4 * g + 0] = cv.x; crow[4 * g + 1] = cv.y;
+                    crow[4 * g + 2] = cv.z; crow[4 * g + 3] = cv.w;
                 }
-                const int v1 = tb >> 5, v2 = ts >> 5;
-                const int j1 = t * 32 + 31 - (tb & 31);
+                int colacc[16];
+#pragma unroll
+                for (int c = 0; c < QT; c += 2) {
+                    v16i acc0 = {0}, acc1 = {0};
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) {  // row direction: running chunk top-2
+                        const int x0 = mad24(acc0[r], 512, crow[r]);
+                        const int y0 = mad24(acc0[r + 1], 512, crow[r + 1]);
+                        ts[c] = max(ts[c], imed3(tb[c], x0, y0));
+                        tb[c] = imax3(tb[c], x0, y0);
+                        const int x1 = mad24(acc1[r], 512, crow[r]);
+                        const int y1 = mad24(acc1[r + 1], 512, crow[r + 1]);
+                        ts[c + 1] = max(ts[c + 1], imed3(tb[c + 1], x1, y1));
+                        tb[c + 1] = imax3(tb[c + 1], x1, y1);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {  // column direction
+                        const int k0 = mad24(acc0[r], 256, ccol[c]);
+                        const int k1 = mad24(acc1[r], 256, ccol[c + 1]);
+                        colacc[r] = (c == 0) ? max(k0, k1) : imax3(colacc[r], k0, k1);
+                    }
+                }
+                ckey[tt] = transpose_max16(colacc, lane);
+            }
+            // LDS atomics after the chunk's MFMAs: an LDS access here waits for the in-flight
+            // LDS-DMA of the next chunk (vmcnt), which has had the whole chunk to land.
+            if (!(lane & 1)) {
+                const int rr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 +
+                               ((lane >> 3) & 1) * 2 + ((lane >> 4) & 1);
+                const int rowoff = (rr & 3) + 8 * (rr >> 2) + 4 * h;
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) {
+                    const int key = ckey[tt];
+                    if (key > SENT_COL + (1 << 29)) {
+                        const unsigned vb = (unsigned)(key >> 7) ^ 0x80000000u;
+                        const unsigned gq = (unsigned)(qbase + 127 - (key & 127));
+                        atomicMax(&lds_col[ch * CHUNK + tt * 32 + rowoff],
+                                  ((unsigned long long)vb << 32) |
+                                      (unsigned long long)(0xFFFFFFFFu - gq));
+                    }
+                }
+            }
+            // merge the chunk's top-2 into the running (best, argbest, second)
+#pragma unroll
+            for (int c = 0; c < QT; ++c) {
+                const int v1 = tb[c] >> 8, v2 = ts[c] >> 8;
+                const int j1 = ch * CHUNK + 255 - (tb[c] & 255);
                 const bool up = v1 > B1[c];
                 B2[c] = up ? max(B1[c], v2) : max(B2[c], v1);
                 J1[c] = up ? j1 : J1[c];
                 B1[c] = max(B1[c], v1);
-                // column direction
-#pragma unroll
-                for (int r = 0; r < 16; ++r) colacc[r] = max(colacc[r], mad24(acc[r], 256, ccol[c]));
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) colacc[r] = half_max32(colacc[r]);
-            if (r32 == 0) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = colacc[r];
-                    if (key > COL_VALID_MIN) {
-                        const int row = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        const unsigned vb = (unsigned)(key >> 7) ^ 0x80000000u;
-                        const unsigned gq = (unsigned)(qbase + 127 - (key & 127));
-                        const unsigned long long k64 =
-                            ((unsigned long long)vb << 32) | (unsigned long long)(0xFFFFFFFFu - gq);
-                        atomicMax(&lds_col[row], k64);
-                    }
-                }
+                tb[c] = INT_MIN; ts[c] = INT_MIN;
             }
         }
-        // merge the two halves' row state (same queries, complementary train rows)
+        __syncthreads();  // chunk ch+1 landed (vmcnt drained); everyone is done with buffer sel
+    }
+
+    if (active) {
 #pragma unroll
         for (int c = 0; c < QT; ++c) {
             const int P1 = __shfl_xor(B1[c], 32), PJ = __shfl_xor(J1[c], 32),
@@ -197,7 +285,6 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
             if (h == 0 && q < na) rowres[(size_t)p * k_pad + q] = make_int4(B1[c], J1[c], B2[c], 0);
         }
     }
-    __syncthreads();
     unsigned long long* dst = colpart + ((size_t)p * n_qblk + qb) * k_pad;
     for (int j = tid; j < k_pad; j += 512) dst[j] = lds_col[j];
 }
@@ -259,7 +346,7 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
             if (i < na) {
                 const int4 rr = rowres[(size_t)p * k_pad + i];
                 j = rr.y;
-                if (j >= 0) {
+                if (j >= 0 && rr.x > ROW_VALID_MIN) {
                     const long long nx = norm[(size_t)a * k_pad + i];
                     d1 = nx - rr.x;
                     const long long d2 = (rr.z > ROW_VALID_MIN) ? nx - rr.z : sfm::DIST_INF;
@@ -285,28 +372,29 @@ int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, 
                         int32_t k_max, const int32_t* pairs, int32_t n_pairs,
                         const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
                         int32_t* out_dist) {
-    const int k_pad = (int)sfm::align_up((size_t)std::max(k_max, 1), 32);
-    const int n_qblk = (k_max + QB - 1) / QB;
-    const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
-    const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
-    const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
-    char* ws = (char*)sfm::workspace(ctx, 2 * tab + rowb + colb + 1024);
-    if (!ws) return SFM_ERR_NOMEM;
-    int32_t* norm = (int32_t*)ws;
-    int32_t* crow = (int32_t*)(ws + tab);
-    int4* rowres = (int4*)(ws + 2 * tab);
-    unsigned long long* colpart = (unsigned long long*)(ws + 2 * tab + rowb);
     hipStream_t st = ctx->stream;
     if (k_max == 0) {
         SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_pairs, st));
         return SFM_OK;
     }
-    hipLaunchKernelGGL(l2_prep_kernel, dim3((k_pad + 255) / 256, n_img), dim3(256), 0, st, desc,
-                       n_kp, k_max, k_pad, norm, crow);
+    const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
+    const int n_qblk = (k_max + QB - 1) / QB;
+    const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
+    const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
+    const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + 1024);
+    if (!ws) return SFM_ERR_NOMEM;
+    uint8_t* zero_row = (uint8_t*)ws;
+    int32_t* norm = (int32_t*)(ws + 256);
+    int32_t* crow = (int32_t*)(ws + 256 + tab);
+    int4* rowres = (int4*)(ws + 256 + 2 * tab);
+    unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
+    hipLaunchKernelGGL(l2_prep_kernel, dim3(k_pad / 256, n_img), dim3(256), 0, st, desc, n_kp,
+                       k_max, k_pad, norm, crow, zero_row);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(l2_match_kernel, dim3(n_pairs * n_qblk), dim3(512),
-                       (size_t)k_pad * sizeof(unsigned long long), st, desc, n_kp, k_max, k_pad,
-                       norm, crow, pairs, n_qblk, rowres, colpart);
+    const size_t lds = 2 * CHUNK * 128 + 2 * CHUNK * 4 + (size_t)k_pad * 8;
+    hipLaunchKernelGGL(l2_match_kernel, dim3(n_pairs * n_qblk), dim3(512), lds, st, desc, n_kp,
+                       k_max, k_pad, norm, crow, zero_row, pairs, n_qblk, rowres, colpart);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(l2_finalize_kernel, dim3(n_pairs), dim3(256),
                        prm->cross_check == SFM_XC_OPENCV ? (size_t)k_pad * 8 : 0, st, n_kp, k_max,

@@ -17,11 +17,11 @@ import numpy as np
 import sfmcore
 
 
-def shard_pairs(pairs: np.ndarray, rank: int, world: int, n_kp=None) -> np.ndarray:
-    """Contiguous shard `rank` of `pairs`, balanced by the per-pair cost n_kp[a]*n_kp[b]."""
+def shard_range(pairs: np.ndarray, rank: int, world: int, n_kp=None):
+    """[lo, hi) of the contiguous shard `rank`, balanced by the per-pair cost n_kp[a]*n_kp[b]."""
     pairs = np.asarray(pairs, np.int32)
     if world <= 1:
-        return pairs
+        return 0, len(pairs)
     if n_kp is None:
         cost = np.ones(len(pairs))
     else:
@@ -31,7 +31,12 @@ def shard_pairs(pairs: np.ndarray, rank: int, world: int, n_kp=None) -> np.ndarr
     cuts = np.searchsorted(cum, cum[-1] * np.arange(world + 1) / world, side="left")
     cuts[0], cuts[-1] = 0, len(pairs)
     cuts = np.maximum.accumulate(cuts)
-    return pairs[cuts[rank]:cuts[rank + 1]]
+    return int(cuts[rank]), int(cuts[rank + 1])
+
+
+def shard_pairs(pairs: np.ndarray, rank: int, world: int, n_kp=None) -> np.ndarray:
+    lo, hi = shard_range(pairs, rank, world, n_kp)
+    return np.asarray(pairs, np.int32)[lo:hi]
 
 
 class GraphBuilder:
@@ -120,9 +125,15 @@ def all_gather_rows(rows, group=None):
     m = max(max(counts), 1)
     pad = torch.zeros((m, rows.shape[1]), dtype=rows.dtype, device=rows.device)
     pad[:rows.shape[0]] = rows
-    out = torch.empty((world * m, rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    dist.all_gather_into_tensor(out, pad, group=group)
-    return torch.cat([out[r * m:r * m + counts[r]] for r in range(world)])
+    if dist.get_backend(group) == "nccl":  # RCCL: one contiguous all-gather
+        out = torch.empty((world * m, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+        dist.all_gather_into_tensor(out, pad, group=group)
+        parts = [out[r * m:r * m + counts[r]] for r in range(world)]
+    else:  # gloo (CPU tests)
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad, group=group)
+        parts = [bufs[r][:counts[r]] for r in range(world)]
+    return torch.cat(parts)
 
 
 def rows_to_pairs(rows: np.ndarray, pairs: np.ndarray):

@@ -48,6 +48,9 @@ def load_library(path: str = LIB_PATH):
     with _lock:
         if _lib is not None:
             return _lib
+        # torch-ROCm ships its own libamdhip64.so.7: load it first so the process has ONE HIP
+        # runtime (the dynamic loader then resolves libsfmcore's dependency to it).
+        import torch  # noqa: F401
         if not os.path.exists(path):
             if os.path.exists("/opt/rocm/bin/hipcc"):
                 from build_lib import build

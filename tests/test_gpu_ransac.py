@@ -90,4 +90,7 @@ def test_ransac_shard_invariance(ctx):
     cnt2, mt2, part = _run(ctx, s, sub, H=512)
     np.testing.assert_array_equal(full["inl_count"][5:11], part["inl_count"])
     np.testing.assert_array_equal(full["best_h"][5:11], part["best_h"])
-    np.testing.assert_array_equal(full["mask"][5:11], part["mask"])
+    np.testing.assert_array_equal(cnt[5:11], cnt2)
+    for k in range(6):
+        M = cnt2[k]
+        np.testing.assert_array_equal(full["mask"][5 + k, :M], part["mask"][k, :M])
