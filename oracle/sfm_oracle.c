@@ -300,9 +300,13 @@ int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
     return 0;
 }
 
-/* Sampson inlier test in pixel units, evaluated in normalised coordinates. */
+/* Sampson inlier test in pixel units, evaluated in normalised coordinates:
+ *   r = x2^T F x1,  g1 = |(F x1)_{0,1}|^2,  g2 = |(F^T x2)_{0,1}|^2,
+ *   den = t2*g1 + t1*g2 with t1 = thr*s1^2, t2 = thr*s2^2 (s = normalisation scales),
+ *   inlier  <=>  e = den - r*r > 0, e evaluated as one fma.
+ * (Equivalent to r^2 / (s2^2 g1 + s1^2 g2) < thr up to rounding; this op sequence is the spec.) */
 static inline int sampson_inlier(const float F[9], float x1, float y1, float x2, float y2,
-                                 float s1sq, float s2sq, float thr) {
+                                 float t1, float t2) {
     float a0 = fmaf(F[0], x1, fmaf(F[1], y1, F[2]));
     float a1 = fmaf(F[3], x1, fmaf(F[4], y1, F[5]));
     float a2 = fmaf(F[6], x1, fmaf(F[7], y1, F[8]));
@@ -311,8 +315,9 @@ static inline int sampson_inlier(const float F[9], float x1, float y1, float x2,
     float r = fmaf(x2, a0, fmaf(y2, a1, a2));
     float g1 = fmaf(a0, a0, a1 * a1);
     float g2 = fmaf(b0, b0, b1 * b1);
-    float den = fmaf(s2sq, g1, s1sq * g2);
-    return (r * r) < (thr * den);
+    float den = fmaf(t2, g1, t1 * g2);
+    float e = fmaf(-r, r, den);
+    return e > 0.0f;
 }
 
 /*
@@ -335,7 +340,7 @@ int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t s
     float cx1, cy1, s1, cx2, cy2, s2;
     oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
     oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
-    float s1sq = s1 * s1, s2sq = s2 * s2;
+    float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
     int bestc = -2, besth = -1;
     for (int h = 0; h < H; ++h) {
         int32_t idx[8];
@@ -350,7 +355,7 @@ int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t s
             cnt = 0;
             for (int m = 0; m < M; ++m)
                 cnt += sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m], n2[2 * m + 1],
-                                      s1sq, s2sq, thr);
+                                      t1, t2);
         }
         if (cnt > bestc) { bestc = cnt; besth = h; }
     }
@@ -365,7 +370,7 @@ int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t s
     int cnt = 0;
     for (int m = 0; m < M; ++m) {
         int in = (ok == 0) ? sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m],
-                                            n2[2 * m + 1], s1sq, s2sq, thr) : 0;
+                                            n2[2 * m + 1], t1, t2) : 0;
         mask[m] = (uint8_t)in;
         cnt += in;
     }
@@ -384,7 +389,7 @@ void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint
     float cx1, cy1, s1, cx2, cy2, s2;
     oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
     oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
-    float s1sq = s1 * s1, s2sq = s2 * s2;
+    float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
     for (int h = 0; h < H; ++h) {
         int32_t idx[8];
         oracle_sample8(seed, pa, pb, (uint32_t)h, M, idx);
@@ -398,7 +403,7 @@ void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint
             cnt = 0;
             for (int m = 0; m < M; ++m)
                 cnt += sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m], n2[2 * m + 1],
-                                      s1sq, s2sq, thr);
+                                      t1, t2);
         }
         counts[h] = cnt;
     }

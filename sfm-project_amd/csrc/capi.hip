@@ -99,7 +99,7 @@ int sfm_match_batch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int3
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     if (prm->metric == SFM_METRIC_L2) {
         SFM_REQUIRE(dim == 128, "sfm_match_batch: L2 metric needs dim == 128");
-        SFM_REQUIRE(k_max <= 8192, "sfm_match_batch: k_max > 8192 not supported");
+        SFM_REQUIRE(k_max <= 4096, "sfm_match_batch: L2 k_max > 4096 not supported");
         return sfm_match_l2_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm, out_count,
                                    out_match, out_dist);
     }

@@ -25,8 +25,8 @@
 //    of each half (permlane16_swap + DPP: 40 instructions for 16 registers) that leaves one train
 //    row per lane pair, and one 64-bit LDS atomic max per lane merges the 8 waves.  Each workgroup
 //    writes its column slab once; the finalize kernel merges the slabs of a pair.
-// Padded trains/queries read a constant row of 0x80 bytes (i8 zero: dot = 0), so their keys are
-// the table constants alone and can never win.
+// The prep kernel writes the descriptors once as i8 (x ^ 0x80); padded trains/queries read a
+// constant all-zero i8 row (dot = 0), so their keys are the table constants alone and never win.
 #include <algorithm>
 #include <climits>
 
@@ -42,6 +42,7 @@ constexpr int WAVES = 8;              // waves per workgroup
 constexpr int QB = WAVES * QT * 32;   // queries per workgroup
 constexpr int CHUNK = 256;            // trains per LDS stage (8 tiles)
 constexpr int KALIGN = 256;           // tables are padded to a multiple of CHUNK
+constexpr int KMAX_L2 = 4096;         // largest k_max handled by this kernel (LDS column state)
 constexpr int SENT_ROW = INT_MIN + 1024;  // crow of padded trains (dot is 0 there)
 constexpr int SENT_COL = INT_MIN + 1024;  // ccol of padded queries
 constexpr int ROW_VALID_MIN = -(1 << 24); // merged row values below this are padding
@@ -53,17 +54,24 @@ __device__ __forceinline__ int imax3(int a, int b, int c) { return max(a, max(b,
 __device__ __forceinline__ int imed3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 __device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
 
+// No-return 64-bit LDS atomic max.  Inline asm: the compiler's LDS-DMA alias tracking treats a
+// builtin atomic to the column-state object as possibly aliasing the in-flight staging DMA and
+// inserts vmcnt(0); this one is ordered only by the lgkmcnt(0) of the barrier that precedes
+// every read of the column state.
+__device__ __forceinline__ void lds_max_u64(unsigned long long* p, unsigned long long v) {
+    const unsigned addr = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned long long*)p;
+    asm volatile("ds_max_u64 %0, %1" : : "v"(addr), "v"(v) : "memory");
+}
+
 template <int CTRL>
 __device__ __forceinline__ int dpp(int x) {
     return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
 }
-__device__ __forceinline__ int swz_xor4(int x) {
-    return __builtin_amdgcn_ds_swizzle(x, (4 << 10) | 0x1F);  // lane ^ 4 within 32
-}
-
-__device__ __forceinline__ v4i xor80(v4i v) {
-    const int m = (int)0x80808080u;
-    return v4i{v.x ^ m, v.y ^ m, v.z ^ m, v.w ^ m};
+// lane ^ 4 inside a 16-lane row with two bank-masked DPP moves (banks = 4-lane groups):
+// banks 0,2 read lane+4 (row_shl:4), banks 1,3 read lane-4 (row_shr:4).  No LDS round trip.
+__device__ __forceinline__ int dpp_xor4(int x) {
+    int y = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0x5, false);
+    return __builtin_amdgcn_update_dpp(y, x, 0x114, 0xF, 0xA, false);
 }
 
 // Max-reduce each of 16 registers over the 32 lanes of its wave half; on return lane l holds the
@@ -85,10 +93,10 @@ __device__ __forceinline__ int transpose_max16(const int (&c)[16], int lane) {
     }
     int o[2];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {  // lane bit 2: xor 4 via ds_swizzle
+    for (int k = 0; k < 2; ++k) {  // lane bit 2: xor 4
         const int send = b2 ? n[2 * k] : n[2 * k + 1];
         const int keep = b2 ? n[2 * k + 1] : n[2 * k];
-        o[k] = max(keep, swz_xor4(send));
+        o[k] = max(keep, dpp_xor4(send));
     }
     // lane bit 1: quad_perm [2,3,0,1]; lane bit 0: quad_perm [1,0,3,2]
     const int p0 = max(o[0], dpp<0x4E>(o[0]));
@@ -100,17 +108,21 @@ __device__ __forceinline__ int transpose_max16(const int (&c)[16], int lane) {
 // |x'|^2 plus the row / column key constants per descriptor, padded to k_pad (multiple of 256).
 __global__ void l2_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
                                int k_max, int k_pad, int32_t* __restrict__ norm,
-                               int32_t* __restrict__ crow, uint8_t* __restrict__ zero_row) {
+                               int32_t* __restrict__ crow, uint8_t* __restrict__ zero_row,
+                               uint4* __restrict__ desc_i8) {
     const int img = blockIdx.y;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (img == 0 && j < 128) zero_row[j] = 0x80;
+    if (img == 0 && j < 128) zero_row[j] = 0;  // i8 zero row for padded trains / queries
     if (j >= k_pad) return;
     int nv = 0;
     if (j < k_max) {
         const uint4* p = (const uint4*)(desc + ((size_t)img * k_max + j) * 128);
+        uint4* o8 = desc_i8 + ((size_t)img * k_max + j) * 8;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             uint4 v = p[q];
+            o8[q] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u,
+                               v.w ^ 0x80808080u);
             unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e)
@@ -132,11 +144,13 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
     const int32_t* __restrict__ norm, const int32_t* __restrict__ crow_tab,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
     int4* __restrict__ rowres, unsigned long long* __restrict__ colpart) {
-    // one dynamic LDS array: [2][CHUNK][128 B] train rows | [2][CHUNK] crow | [k_pad] col state
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    unsigned char* bufA = lds;
-    int* bufC = (int*)(lds + 2 * CHUNK * 128);
-    unsigned long long* lds_col = (unsigned long long*)(lds + 2 * CHUNK * 128 + 2 * CHUNK * 4);
+    // LDS: two DMA staging objects ([CHUNK][128 B] train rows + [CHUNK] crow each) and the column
+    // state, all distinct __shared__ objects: with the chunk loop unrolled by two every access
+    // names its buffer statically, so the compiler's LDS-DMA alias tracking does not make reads
+    // of one buffer wait (vmcnt) for the DMA into the other.
+    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * 128 + CHUNK * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * 128 + CHUNK * 4];
+    __shared__ unsigned long long lds_col[KMAX_L2];
 
     const int p = blockIdx.x / n_qblk, qb = blockIdx.x - p * n_qblk;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
@@ -148,9 +162,8 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
     const int32_t* crb = crow_tab + (size_t)b * k_pad;
     const int n_chunk = (nb + CHUNK - 1) / CHUNK;
 
-    // stage chunk ch into buffer sel: 4 x 1 KB LDS-DMA pieces per wave (+ the crow piece)
-    auto stage = [&](int ch, int sel) {
-        unsigned char* dst = bufA + sel * CHUNK * 128;
+    // stage chunk ch into buffer dst: 4 x 1 KB LDS-DMA pieces per wave (+ the crow piece)
+    auto stage = [&](int ch, unsigned char* dst) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int piece = wave * 4 + i;         // 1 KB = 8 rows
@@ -162,7 +175,7 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
         }
         if (wave == 0) {
             const int32_t* src = crb + ch * CHUNK + lane * 4;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(bufC + sel * CHUNK), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * 128), 16, 0, 0);
         }
     };
 
@@ -176,100 +189,98 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
         const int q = qbase + c * 32 + r32;
         const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * 128 + 64 * h : zero_row + 64 * h);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) bq[c][s] = xor80(src[s]);
+        for (int s = 0; s < 4; ++s) bq[c][s] = src[s];
         // col key = vc*128 + (127 - q_in_wave) = dot*256 + ccol;  vc = 2 dot - |x'|^2
         ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32)) : SENT_COL;
         B1[c] = INT_MIN; J1[c] = -1; B2[c] = INT_MIN;
         tb[c] = INT_MIN; ts[c] = INT_MIN;
     }
-    if (n_chunk > 0) stage(0, 0);
-    __syncthreads();
-
-    for (int ch = 0; ch < n_chunk; ++ch) {
-        const int sel = ch & 1;
-        if (ch + 1 < n_chunk) stage(ch + 1, sel ^ 1);
-        const int nt = min(8, (nb - ch * CHUNK + 31) >> 5);
-        if (active) {
-            const unsigned char* A = bufA + sel * CHUNK * 128;
-            const int* Cr = bufC + sel * CHUNK;
-            int ckey[8];
+    // process chunk ch from buffer cur while chunk ch+1 streams into buffer nxt
+    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
+        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
+            const int nt = min(8, (nb - ch * CHUNK + 31) >> 5);
+            if (active) {
+                const unsigned char* A = cur;
+                const int* Cr = (const int*)(cur + CHUNK * 128);
+                // one 32-train tile: MFMAs for the 4 query tiles + both epilogues; returns the
+                // transposed column key of this lane's train row
+                auto tile = [&](int tt) -> int {
+                    const int row = tt * 32 + r32;
+                    const int swz = (row >> 1) & 7;
+                    v4i af[4];
 #pragma unroll
-            for (int tt = 0; tt < 8; ++tt) {
-                ckey[tt] = INT_MIN;
-                if (tt >= nt) continue;
-                const int row = tt * 32 + r32;
-                const int swz = (row >> 1) & 7;
-                v4i af[4];
+                    for (int s = 0; s < 4; ++s)
+                        af[s] = *(const v4i*)(A + row * 128 + (((4 * h + s) ^ swz) << 4));
+                    int crow[16];
 #pragma unroll
-                for (int s = 0; s < 4; ++s)
-                    af[s] = xor80(*(const v4i*)(A + row * 128 + (((4 * h + s) ^ swz) << 4)));
-                int crow[16];
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const v4i cv = *(const v4i*)(Cr + tt * 32 + 8 * g + 4 * h);
-                    crow[4 * g + 0] = cv.x; crow[4 * g + 1] = cv.y;
-                    crow[4 * g + 2] = cv.z; crow[4 * g + 3] = cv.w;
-                }
-                int colacc[16];
-#pragma unroll
-                for (int c = 0; c < QT; c += 2) {
-                    v16i acc0 = {0}, acc1 = {0};
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
-                        acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
+                    for (int g = 0; g < 4; ++g) {
+                        const v4i cv = *(const v4i*)(Cr + tt * 32 + 8 * g + 4 * h);
+                        crow[4 * g + 0] = cv.x; crow[4 * g + 1] = cv.y;
+                        crow[4 * g + 2] = cv.z; crow[4 * g + 3] = cv.w;
                     }
+                    int colacc[16];
 #pragma unroll
-                    for (int r = 0; r < 16; r += 2) {  // row direction: running chunk top-2
-                        const int x0 = mad24(acc0[r], 512, crow[r]);
-                        const int y0 = mad24(acc0[r + 1], 512, crow[r + 1]);
-                        ts[c] = max(ts[c], imed3(tb[c], x0, y0));
-                        tb[c] = imax3(tb[c], x0, y0);
-                        const int x1 = mad24(acc1[r], 512, crow[r]);
-                        const int y1 = mad24(acc1[r + 1], 512, crow[r + 1]);
-                        ts[c + 1] = max(ts[c + 1], imed3(tb[c + 1], x1, y1));
-                        tb[c + 1] = imax3(tb[c + 1], x1, y1);
-                    }
+                    for (int c = 0; c < QT; c += 2) {
+                        v16i acc0 = {0}, acc1 = {0};
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {  // column direction
-                        const int k0 = mad24(acc0[r], 256, ccol[c]);
-                        const int k1 = mad24(acc1[r], 256, ccol[c + 1]);
-                        colacc[r] = (c == 0) ? max(k0, k1) : imax3(colacc[r], k0, k1);
+                        for (int s = 0; s < 4; ++s) {
+                            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
+                            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 16; r += 2) {  // row direction: running chunk top-2
+                            const int x0 = mad24(acc0[r], 512, crow[r]);
+                            const int y0 = mad24(acc0[r + 1], 512, crow[r + 1]);
+                            ts[c] = max(ts[c], imed3(tb[c], x0, y0));
+                            tb[c] = imax3(tb[c], x0, y0);
+                            const int x1 = mad24(acc1[r], 512, crow[r]);
+                            const int y1 = mad24(acc1[r + 1], 512, crow[r + 1]);
+                            ts[c + 1] = max(ts[c + 1], imed3(tb[c + 1], x1, y1));
+                            tb[c + 1] = imax3(tb[c + 1], x1, y1);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {  // column direction
+                            const int k0 = mad24(acc0[r], 256, ccol[c]);
+                            const int k1 = mad24(acc1[r], 256, ccol[c + 1]);
+                            colacc[r] = (c == 0) ? max(k0, k1) : imax3(colacc[r], k0, k1);
+                        }
                     }
-                }
-                ckey[tt] = transpose_max16(colacc, lane);
-            }
-            // LDS atomics after the chunk's MFMAs: an LDS access here waits for the in-flight
-            // LDS-DMA of the next chunk (vmcnt), which has had the whole chunk to land.
-            if (!(lane & 1)) {
-                const int rr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 +
-                               ((lane >> 3) & 1) * 2 + ((lane >> 4) & 1);
+                    return transpose_max16(colacc, lane);
+                };
+                const int rr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 + ((lane >> 3) & 1) * 2 +
+                               ((lane >> 4) & 1);
                 const int rowoff = (rr & 3) + 8 * (rr >> 2) + 4 * h;
-#pragma unroll
-                for (int tt = 0; tt < 8; ++tt) {
-                    const int key = ckey[tt];
-                    if (key > SENT_COL + (1 << 29)) {
+                auto col_merge = [&](int tt, int key) {
+                    if (!(lane & 1) && key > SENT_COL + (1 << 29)) {
                         const unsigned vb = (unsigned)(key >> 7) ^ 0x80000000u;
                         const unsigned gq = (unsigned)(qbase + 127 - (key & 127));
-                        atomicMax(&lds_col[ch * CHUNK + tt * 32 + rowoff],
-                                  ((unsigned long long)vb << 32) |
-                                      (unsigned long long)(0xFFFFFFFFu - gq));
+                        lds_max_u64(&lds_col[ch * CHUNK + tt * 32 + rowoff],
+                                    ((unsigned long long)vb << 32) | (unsigned long long)(0xFFFFFFFFu - gq));
                     }
+                };
+                // lds_col is its own __shared__ object, disjoint from the LDS-DMA staging buffers, so
+                // these atomics need not wait for the in-flight DMA of the next chunk.
+                for (int tt = 0; tt < nt; ++tt) col_merge(tt, tile(tt));
+                // merge the chunk's top-2 into the running (best, argbest, second)
+#pragma unroll
+                for (int c = 0; c < QT; ++c) {
+                    const int v1 = tb[c] >> 8, v2 = ts[c] >> 8;
+                    const int j1 = ch * CHUNK + 255 - (tb[c] & 255);
+                    const bool up = v1 > B1[c];
+                    B2[c] = up ? max(B1[c], v2) : max(B2[c], v1);
+                    J1[c] = up ? j1 : J1[c];
+                    B1[c] = max(B1[c], v1);
+                    tb[c] = INT_MIN; ts[c] = INT_MIN;
                 }
             }
-            // merge the chunk's top-2 into the running (best, argbest, second)
-#pragma unroll
-            for (int c = 0; c < QT; ++c) {
-                const int v1 = tb[c] >> 8, v2 = ts[c] >> 8;
-                const int j1 = ch * CHUNK + 255 - (tb[c] & 255);
-                const bool up = v1 > B1[c];
-                B2[c] = up ? max(B1[c], v2) : max(B2[c], v1);
-                J1[c] = up ? j1 : J1[c];
-                B1[c] = max(B1[c], v1);
-                tb[c] = INT_MIN; ts[c] = INT_MIN;
-            }
-        }
-        __syncthreads();  // chunk ch+1 landed (vmcnt drained); everyone is done with buffer sel
+    };
+    if (n_chunk > 0) stage(0, lds0);
+    __syncthreads();
+    for (int ch = 0; ch < n_chunk; ch += 2) {
+        process(ch, lds0, lds1);
+        __syncthreads();  // chunk ch+1 landed (vmcnt drained); everyone is done with lds0
+        if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
+        __syncthreads();
     }
 
     if (active) {
@@ -382,18 +393,23 @@ int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, 
     const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
     const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
     const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
-    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + 1024);
+    const size_t descb = sfm::align_up((size_t)n_img * k_max * 128, 256);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     uint8_t* zero_row = (uint8_t*)ws;
     int32_t* norm = (int32_t*)(ws + 256);
     int32_t* crow = (int32_t*)(ws + 256 + tab);
     int4* rowres = (int4*)(ws + 256 + 2 * tab);
     unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
+    uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
     hipLaunchKernelGGL(l2_prep_kernel, dim3(k_pad / 256, n_img), dim3(256), 0, st, desc, n_kp,
-                       k_max, k_pad, norm, crow, zero_row);
+                       k_max, k_pad, norm, crow, zero_row, (uint4*)desc_i8);
     SFM_HIP_CHECK(hipGetLastError());
-    const size_t lds = 2 * CHUNK * 128 + 2 * CHUNK * 4 + (size_t)k_pad * 8;
-    hipLaunchKernelGGL(l2_match_kernel, dim3(n_pairs * n_qblk), dim3(512), lds, st, desc, n_kp,
+    if (k_pad > KMAX_L2) {
+        sfm::set_error("sfm_match_batch: L2 k_max > 4096 not supported");
+        return SFM_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(l2_match_kernel, dim3(n_pairs * n_qblk), dim3(512), 0, st, desc_i8, n_kp,
                        k_max, k_pad, norm, crow, zero_row, pairs, n_qblk, rowres, colpart);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(l2_finalize_kernel, dim3(n_pairs), dim3(256),

@@ -159,9 +159,9 @@ __device__ __forceinline__ bool fit_f8(const float4 s[8], float F[9]) {
     return ok;
 }
 
-__device__ __forceinline__ int sampson_inlier(const float F[9], float4 m, float s1sq, float s2sq,
-                                              float thr) {
-    const float x1 = m.x, y1 = m.y, x2 = m.z, y2 = m.w;
+// Sampson inlier test (oracle/sfm_oracle.c sampson_inlier): e = t2*g1 + t1*g2 - r^2 > 0.
+__device__ __forceinline__ int sampson_inlier(const float F[9], float x1, float y1, float x2,
+                                              float y2, float t1, float t2) {
     const float a0 = fmaf(F[0], x1, fmaf(F[1], y1, F[2]));
     const float a1 = fmaf(F[3], x1, fmaf(F[4], y1, F[5]));
     const float a2 = fmaf(F[6], x1, fmaf(F[7], y1, F[8]));
@@ -170,8 +170,30 @@ __device__ __forceinline__ int sampson_inlier(const float F[9], float4 m, float 
     const float r = fmaf(x2, a0, fmaf(y2, a1, a2));
     const float g1 = fmaf(a0, a0, a1 * a1);
     const float g2 = fmaf(b0, b0, b1 * b1);
-    const float den = fmaf(s2sq, g1, s1sq * g2);
-    return (r * r) < (thr * den) ? 1 : 0;
+    const float den = fmaf(t2, g1, t1 * g2);
+    const float e = fmaf(-r, r, den);
+    return e > 0.0f ? 1 : 0;
+}
+
+// The same test on two matches at once: every op is a v_pk_fma_f32 / v_pk_mul_f32 (gfx950 issues
+// one packed op per 4 cycles like a scalar one, so this halves the scoring cost).  Each half is an
+// IEEE fma/mul exactly like the scalar form, so results are bit-identical.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 sp(float x) { return f2{x, x}; }
+__device__ __forceinline__ int sampson_inlier2(const float F[9], f2 x1, f2 y1, f2 x2, f2 y2,
+                                               float t1, float t2) {
+    const f2 a0 = fma2(sp(F[0]), x1, fma2(sp(F[1]), y1, sp(F[2])));
+    const f2 a1 = fma2(sp(F[3]), x1, fma2(sp(F[4]), y1, sp(F[5])));
+    const f2 a2 = fma2(sp(F[6]), x1, fma2(sp(F[7]), y1, sp(F[8])));
+    const f2 b0 = fma2(sp(F[0]), x2, fma2(sp(F[3]), y2, sp(F[6])));
+    const f2 b1 = fma2(sp(F[1]), x2, fma2(sp(F[4]), y2, sp(F[7])));
+    const f2 r = fma2(x2, a0, fma2(y2, a1, a2));
+    const f2 g1 = fma2(a0, a0, a1 * a1);
+    const f2 g2 = fma2(b0, b0, b1 * b1);
+    const f2 den = fma2(sp(t2), g1, sp(t1) * g2);
+    const f2 e = fma2(-r, r, den);
+    return (e.x > 0.0f ? 1 : 0) + (e.y > 0.0f ? 1 : 0);
 }
 
 // fixed-order sum: lane l accumulates m = l, l+64, ... then a halving tree (oracle fixed_sum)
@@ -184,12 +206,16 @@ __device__ __forceinline__ float wave_fixed_sum(float partial) {
 __global__ __launch_bounds__(64) void ransac_prep_kernel(
     const float* __restrict__ kps, int k_max, const int32_t* __restrict__ pairs,
     const int32_t* __restrict__ match_count, const int32_t* __restrict__ matches,
-    float4* __restrict__ nrm_xy, float* __restrict__ out_norm) {
+    float* __restrict__ nrm_xy, float* __restrict__ out_norm) {
     const int p = blockIdx.x, l = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int M = match_count[p];
     const int32_t* mt = matches + (size_t)p * k_max * 2;
-    float4* dst = nrm_xy + (size_t)p * k_max;
+    // SoA planes x1 | y1 | x2 | y2, k_max floats each
+    float* X1 = nrm_xy + (size_t)p * 4 * k_max;
+    float* Y1 = X1 + k_max;
+    float* X2 = Y1 + k_max;
+    float* Y2 = X2 + k_max;
     if (M < 8) {
         if (l < 6) out_norm[p * 6 + l] = 0.0f;
         return;
@@ -199,14 +225,14 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
         const float2 u = *(const float2*)(kps + ((size_t)a * k_max + mt[2 * m]) * 2);
         const float2 v = *(const float2*)(kps + ((size_t)b * k_max + mt[2 * m + 1]) * 2);
         sx1 = sx1 + u.x; sy1 = sy1 + u.y; sx2 = sx2 + v.x; sy2 = sy2 + v.y;
-        dst[m] = make_float4(u.x, u.y, v.x, v.y);
+        X1[m] = u.x; Y1[m] = u.y; X2[m] = v.x; Y2[m] = v.y;
     }
     const float fM = (float)M;
     const float mx1 = wave_fixed_sum(sx1) / fM, my1 = wave_fixed_sum(sy1) / fM;
     const float mx2 = wave_fixed_sum(sx2) / fM, my2 = wave_fixed_sum(sy2) / fM;
     float sd1 = 0.f, sd2 = 0.f;
     for (int m = l; m < M; m += 64) {
-        const float4 w = dst[m];
+        const float4 w = make_float4(X1[m], Y1[m], X2[m], Y2[m]);
         float dx = w.x - mx1, dy = w.y - my1;
         float q = dx * dx;
         q = fmaf(dy, dy, q);
@@ -220,9 +246,10 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
     const float s1 = (mean1 > 0.0f) ? (1.41421356237309515f / mean1) : 1.0f;
     const float s2 = (mean2 > 0.0f) ? (1.41421356237309515f / mean2) : 1.0f;
     for (int m = l; m < M; m += 64) {
-        const float4 w = dst[m];
-        dst[m] = make_float4((w.x - mx1) * s1, (w.y - my1) * s1, (w.z - mx2) * s2,
-                             (w.w - my2) * s2);
+        X1[m] = (X1[m] - mx1) * s1;
+        Y1[m] = (Y1[m] - my1) * s1;
+        X2[m] = (X2[m] - mx2) * s2;
+        Y2[m] = (Y2[m] - my2) * s2;
     }
     if (l == 0) {
         float* o = out_norm + p * 6;
@@ -232,30 +259,57 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
 
 __global__ __launch_bounds__(256) void ransac_hyp_kernel(
     int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
-    const float4* __restrict__ nrm_xy, const float* __restrict__ norm, uint64_t seed, float thr,
+    const float* __restrict__ nrm_xy, const float* __restrict__ norm, uint64_t seed, float thr,
     unsigned long long* __restrict__ best) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds_m[];
+    // LDS: the pair's normalised matches as SoA planes x1 | y1 | x2 | y2 (k2 floats each), so a
+    // float2 read hands the packed Sampson test two matches in adjacent registers
+    extern __shared__ __attribute__((aligned(16))) float lds_m[];
     __shared__ unsigned long long wbest[4];
     const int p = blockIdx.y;
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int tid = threadIdx.x;
-    const float4* src = nrm_xy + (size_t)p * k_max;
-    for (int m = tid; m < M; m += 256) lds_m[m] = src[m];
+    const int k2 = (k_max + 3) & ~3;
+    float* LX1 = lds_m;
+    float* LY1 = LX1 + k2;
+    float* LX2 = LY1 + k2;
+    float* LY2 = LX2 + k2;
+    const float* src = nrm_xy + (size_t)p * 4 * k_max;
+    for (int m = tid; m < M; m += 256) {
+        LX1[m] = src[m];
+        LY1[m] = src[k_max + m];
+        LX2[m] = src[2 * k_max + m];
+        LY2[m] = src[3 * k_max + m];
+    }
     __syncthreads();
     const uint32_t pa = (uint32_t)pairs[2 * p], pb = (uint32_t)pairs[2 * p + 1];
     const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
-    const float s1sq = s1 * s1, s2sq = s2 * s2;
+    const float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
     const uint32_t h = blockIdx.x * 256 + tid;
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
     float4 smp[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) smp[k] = lds_m[idx[k]];
+    for (int k = 0; k < 8; ++k)
+        smp[k] = make_float4(LX1[idx[k]], LY1[idx[k]], LX2[idx[k]], LY2[idx[k]]);
     float F[9];
     const bool ok = fit_f8(smp, F);
-    int cnt = 0;
-    for (int m = 0; m < M; ++m) cnt += sampson_inlier(F, lds_m[m], s1sq, s2sq, thr);
+    // two packed chains (4 matches) per iteration; the count is an integer, so the order of the
+    // partial sums does not change the result
+    const f2* PX1 = (const f2*)LX1;
+    const f2* PY1 = (const f2*)LY1;
+    const f2* PX2 = (const f2*)LX2;
+    const f2* PY2 = (const f2*)LY2;
+    int c0 = 0, c1 = 0;
+    int q = 0;
+    const int half = M >> 1;
+    for (; q + 2 <= half; q += 2) {
+        c0 += sampson_inlier2(F, PX1[q], PY1[q], PX2[q], PY2[q], t1, t2);
+        c1 += sampson_inlier2(F, PX1[q + 1], PY1[q + 1], PX2[q + 1], PY2[q + 1], t1, t2);
+    }
+    if (q < half) c0 += sampson_inlier2(F, PX1[q], PY1[q], PX2[q], PY2[q], t1, t2);
+    if (M & 1) c1 += sampson_inlier(F, LX1[M - 1], LY1[M - 1], LX2[M - 1], LY2[M - 1], t1, t2);
+    int cnt = c0 + c1;
     if (!ok) cnt = -1;
     unsigned long long key = ((unsigned long long)(unsigned)(cnt + 1) << 32) | (0xFFFFFFFFu - h);
 #pragma unroll
@@ -274,7 +328,7 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
 
 __global__ __launch_bounds__(256) void ransac_final_kernel(
     int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
-    const float4* __restrict__ nrm_xy, const float* __restrict__ norm, uint64_t seed, float thr,
+    const float* __restrict__ nrm_xy, const float* __restrict__ norm, uint64_t seed, float thr,
     const unsigned long long* __restrict__ best, int32_t* __restrict__ out_inl_count,
     int32_t* __restrict__ out_best_h, uint8_t* __restrict__ out_mask, float* __restrict__ out_F) {
     __shared__ int wsum[4];
@@ -289,19 +343,22 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
     }
     const uint32_t pa = (uint32_t)pairs[2 * p], pb = (uint32_t)pairs[2 * p + 1];
     const uint32_t h = 0xFFFFFFFFu - (uint32_t)best[p];
-    const float4* src = nrm_xy + (size_t)p * k_max;
+    const float* X1 = nrm_xy + (size_t)p * 4 * k_max;
+    const float* Y1 = X1 + k_max;
+    const float* X2 = Y1 + k_max;
+    const float* Y2 = X2 + k_max;
     const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
-    const float s1sq = s1 * s1, s2sq = s2 * s2;
+    const float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
     float4 smp[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) smp[k] = src[idx[k]];
+    for (int k = 0; k < 8; ++k) smp[k] = make_float4(X1[idx[k]], Y1[idx[k]], X2[idx[k]], Y2[idx[k]]);
     float F[9];
     const bool ok = fit_f8(smp, F);
     int cnt = 0;
     for (int m = tid; m < M; m += 256) {
-        const int in = ok ? sampson_inlier(F, src[m], s1sq, s2sq, thr) : 0;
+        const int in = ok ? sampson_inlier(F, X1[m], Y1[m], X2[m], Y2[m], t1, t2) : 0;
         mask[m] = (uint8_t)in;
         cnt += in;
     }
@@ -335,18 +392,19 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
     SFM_REQUIRE(k_max <= 8192, "sfm_ransac_f_batch: k_max > 8192 not supported");
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    const size_t xyb = (size_t)n_pairs * std::max(k_max, 1) * sizeof(float4);
+    const size_t xyb = (size_t)n_pairs * 4 * std::max(k_max, 1) * sizeof(float);
     const size_t bb = (size_t)n_pairs * sizeof(unsigned long long);
     char* ws = (char*)sfm::workspace(ctx, xyb + bb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
-    float4* nrm_xy = (float4*)ws;
+    float* nrm_xy = (float*)ws;
     unsigned long long* best = (unsigned long long*)(ws + xyb);
     SFM_HIP_CHECK(hipMemsetAsync(best, 0, bb, st));
     hipLaunchKernelGGL(ransac_prep_kernel, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
                        match_count, matches, nrm_xy, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(ransac_hyp_kernel, dim3(prm->n_hyp / 256, n_pairs), dim3(256),
-                       (size_t)std::max(k_max, 1) * sizeof(float4), st, k_max, pairs, match_count,
+                       (size_t)4 * ((std::max(k_max, 1) + 3) & ~3) * sizeof(float), st, k_max, pairs,
+                       match_count,
                        nrm_xy, out_norm, prm->seed, prm->thr, best);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(ransac_final_kernel, dim3(n_pairs), dim3(256), 0, st, k_max, pairs,
