@@ -52,3 +52,63 @@ def reprojection_errors(cams, pp, pts, cam_idx, pt_idx, uv, device: int = 0) -> 
     """Per-observation reprojection error (px) from the GPU residuals."""
     r = build_jtj(cams, pp, pts, cam_idx, pt_idx, uv, device=device)["res"]
     return np.sqrt(np.sum(r * r, axis=1))
+
+
+# ---- multi-GPU: observations sharded by point, camera blocks all-reduced (SURVEY.md §8e) --------
+
+def shard_points(pt_ptr, rank: int, world: int):
+    """[lo, hi) point range of `rank`: contiguous points, balanced by observation count.
+
+    Sharding by point keeps V_p, W_cp, g_p and the residuals rank-local; only the camera blocks
+    U_c / g_c (and the cost) are partial sums that need a reduction."""
+    pt_ptr = np.asarray(pt_ptr, np.int64)
+    n_pt = len(pt_ptr) - 1
+    if world <= 1:
+        return 0, n_pt
+    n_obs = int(pt_ptr[-1])
+    cuts = np.searchsorted(pt_ptr, n_obs * np.arange(world + 1) / world, side="left")
+    cuts[0], cuts[-1] = 0, n_pt
+    cuts = np.minimum(np.maximum.accumulate(cuts), n_pt)
+    return int(cuts[rank]), int(cuts[rank + 1])
+
+
+def allreduce_camera_blocks(U, gc, cost, group=None):
+    """Sum the per-rank camera blocks with ONE all-reduce: U [n_cam,8,8], g_c [n_cam,8] and the
+    cost packed into a single fp64 buffer (~290 KB at n_cam = 500: latency-bound, so one
+    collective instead of three).  RCCL (`nccl`) for device tensors, gloo on the CPU.
+    In place; returns (U, gc, cost)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return U, gc, cost
+    nu, ng = U.numel(), gc.numel()
+    buf = torch.cat([U.reshape(-1), gc.reshape(-1), cost.reshape(-1).to(U.dtype)])
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    U.copy_(buf[:nu].view_as(U))
+    gc.copy_(buf[nu:nu + ng].view_as(gc))
+    cost.copy_(buf[nu + ng:].view_as(cost))
+    return U, gc, cost
+
+
+def build_jtj_sharded(cams, pp, pts, cam_idx, pt_idx, uv, rank: int, world: int,
+                      loss_s: float = 0.0, device: int = 0, group=None):
+    """One process per GPU: this rank linearises the observations of its point shard on the GPU,
+    then the camera blocks are all-reduced over RCCL.  Observations must be point-major.
+
+    Returns dict like build_jtj(as_numpy=False) for the local points [lo, hi) plus `pt_range`;
+    U / gc / cost are the global sums on every rank."""
+    import torch
+    pt_idx = np.asarray(pt_idx, np.int32)
+    if len(pt_idx) and np.any(np.diff(pt_idx) < 0):
+        raise ValueError("build_jtj_sharded: observations must be grouped by point")
+    n_pt = len(pts)
+    pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
+    lo, hi = shard_points(pt_ptr, rank, world)
+    o0, o1 = int(pt_ptr[lo]), int(pt_ptr[hi])
+    out = build_jtj(cams, pp, np.asarray(pts)[lo:hi], np.asarray(cam_idx)[o0:o1],
+                    pt_idx[o0:o1] - lo, np.asarray(uv)[o0:o1], loss_s=loss_s, device=device,
+                    as_numpy=False)
+    allreduce_camera_blocks(out["U"], out["gc"], out["cost"], group=group)
+    torch.cuda.synchronize(device)
+    out["pt_range"] = (lo, hi)
+    return out

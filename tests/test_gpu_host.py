@@ -1,0 +1,130 @@
+"""GPU parity of the reference-facing host layer (drop-in modules) and of the sizes the benchmark
+configs use: K = 4096 (cfg4), the full 4096-hypothesis RANSAC (cfg3), the batched pair-graph
+builder, and the BA J^TJ build through reconstruction.py (single rank of the sharded path).
+Everything is checked against the CPU oracle (test infrastructure)."""
+import numpy as np
+import pytest
+
+import feature_matching as fm
+import geometric_verification as gv
+import match_graph
+import oracle as O
+import reconstruction
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_reference_semantics(d1, d2):
+    """code/feature_matching.py:48-58 on the oracle: OpenCV cross-check rule, stable sort by
+    distance, prefix with distance < 26."""
+    q, t, d = O.match(d1, d2, metric=1, cross_check=O.XC_OPENCV, ratio=None, max_dist=-1)
+    order = np.argsort(d, kind="stable")
+    out = []
+    for i in order:
+        if d[i] >= 26:
+            break
+        out.append((int(q[i]), int(t[i]), float(d[i])))
+    return out
+
+
+def test_match_descriptors_reference_semantics():
+    s = synth.make_scene(2, 500, seed=11, orb=True)
+    d1, d2 = s["desc"][0][:480], s["desc"][1][:500]
+    got = fm.match_descriptors(d1, d2)  # defaults = the reference's matcher
+    want = _ref_reference_semantics(d1, d2)
+    assert len(want) > 50
+    assert [(m.queryIdx, m.trainIdx, m.distance) for m in got] == want
+    assert all(m.imgIdx == 0 for m in got)
+
+
+def test_match_descriptors_l2_ratio():
+    s = synth.make_scene(2, 700, seed=12)
+    got = fm.match_descriptors(s["desc"][0], s["desc"][1], norm="l2", cross_check="mutual",
+                               max_distance=None, ratio=0.8, sort=False)
+    q, t, d = O.match(s["desc"][0], s["desc"][1], 0, 1, (4, 5))
+    assert [(m.queryIdx, m.trainIdx) for m in got] == list(zip(q.tolist(), t.tolist()))
+    np.testing.assert_array_equal([m.distance for m in got],
+                                  np.sqrt(d).astype(np.float32).astype(np.float64))
+
+
+def test_l2_k4096_cfg4_size(ctx):
+    import torch
+    s = synth.make_scene(3, 4096, seed=13)
+    pairs = np.array([[0, 1], [2, 0]], np.int32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    cnt, mt, dist = ctx.match_batch(T(s["desc"]), T(s["n_kp"]), T(pairs), ratio=(4, 5))
+    torch.cuda.synchronize()
+    cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+    for p, (a, b) in enumerate(pairs):
+        q, t, d = O.match(s["desc"][a], s["desc"][b], 0, 1, (4, 5))
+        assert cnt[p] == len(q) > 500
+        np.testing.assert_array_equal(mt[p, :cnt[p], 0], q)
+        np.testing.assert_array_equal(mt[p, :cnt[p], 1], t)
+        np.testing.assert_array_equal(dist[p, :cnt[p]], d)
+
+
+def test_verify_pair_full_4096_hypotheses():
+    s = synth.make_scene(2, 2048, seed=14)
+    q, t, _ = O.match(s["desc"][0], s["desc"][1], 0, 1, (4, 5))
+    r = gv.verify_pair(s["kps"][0], s["kps"][1], np.c_[q, t], pair=(0, 1), n_hyp=4096)
+    o = O.ransac_f(s["kps"][0][q], s["kps"][1][t], H=4096, seed=42, pa=0, pb=1)
+    assert r["count"] == o["count"] and r["best_h"] == o["best_h"] and r["verified"]
+    np.testing.assert_array_equal(r["inliers"], np.nonzero(o["mask"])[0])
+    np.testing.assert_allclose(r["F"], gv.denormalize_F(o["F"], o["norm"]), rtol=0, atol=1e-6)
+
+
+def test_verify_pairs_on_reference_pair_objects():
+    class Pair:  # code/pipeline.py:6-9
+        def __init__(self, i, j, matches):
+            self.img_inx_1, self.img_inx_2, self.matches = i, j, matches
+
+    s = synth.make_scene(3, 1024, seed=15)
+    prs = []
+    for i, j in ((0, 1), (1, 2)):
+        ms = fm.match_descriptors(s["desc"][i], s["desc"][j], norm="l2", cross_check="mutual",
+                                  max_distance=None, ratio=(4, 5), sort=False)
+        prs.append(Pair(i, j, ms))
+    n_before = [len(p.matches) for p in prs]
+    out = gv.verify_pairs(prs, s["kps"], n_hyp=1024)
+    assert len(out) == 2
+    for p, nb in zip(out, n_before):
+        mt = np.array([[m.queryIdx, m.trainIdx] for m in p.matches])
+        assert 15 <= len(mt) < nb and p.F.shape == (3, 3)
+
+
+def test_graph_builder_matches_oracle():
+    import torch
+    s = synth.make_scene(6, 1024, seed=16)
+    pairs = synth.unordered_pairs(6)
+    gb = match_graph.GraphBuilder(s["desc"], s["kps"], s["n_kp"], ratio=(4, 5), n_hyp=512)
+    pt = torch.from_numpy(pairs).cuda()
+    count, match, dist, rs = gb.run(pt)
+    rows = gb.graph_rows(0, count, match, rs).cpu().numpy()
+    want = []
+    for p, (a, b) in enumerate(pairs):
+        q, t, _ = O.match(s["desc"][a], s["desc"][b], 0, 1, (4, 5))
+        r = O.ransac_f(s["kps"][a][q], s["kps"][b][t], H=512, seed=42, pa=int(a), pb=int(b))
+        if r["count"] >= 15:
+            want += [(p, int(q[i]), int(t[i])) for i in np.nonzero(r["mask"])[0]]
+    np.testing.assert_array_equal(rows, np.array(want, np.int32).reshape(-1, 3))
+
+
+def test_build_jtj_and_sharded_single_rank():
+    pr = synth.make_ba_problem(9, 300, obs_per_pt=4, seed=17)
+    o = O.ba_jtj(pr["cams"], pr["pp"], pr["pts"], pr["cam_idx"], pr["pt_idx"], pr["uv"],
+                 loss_s=1.5)
+    g = reconstruction.build_jtj(pr["cams"], pr["pp"], pr["pts"], pr["cam_idx"], pr["pt_idx"],
+                                 pr["uv"], loss_s=1.5)
+    np.testing.assert_allclose(g["U"], o["U"], rtol=1e-10, atol=1e-8)
+    assert np.abs(g["res"] - o["res"]).max() < 1e-4
+    sh = reconstruction.build_jtj_sharded(pr["cams"], pr["pp"], pr["pts"], pr["cam_idx"],
+                                          pr["pt_idx"], pr["uv"], 0, 1, loss_s=1.5)
+    assert sh["pt_range"] == (0, 300)
+    np.testing.assert_array_equal(sh["U"].cpu().numpy(), g["U"])
+    # shuffled observation order goes through the regrouping path of build_jtj
+    perm = np.random.default_rng(0).permutation(len(pr["pt_idx"]))
+    g2 = reconstruction.build_jtj(pr["cams"], pr["pp"], pr["pts"], pr["cam_idx"][perm],
+                                  pr["pt_idx"][perm], pr["uv"][perm], loss_s=1.5)
+    np.testing.assert_array_equal(g2["res"], g["res"][perm])
+    np.testing.assert_allclose(g2["U"], g["U"], rtol=1e-12, atol=1e-9)

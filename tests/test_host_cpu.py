@@ -1,0 +1,114 @@
+"""CPU: the reference-facing host modules (drop-ins for code/feature_matching.py,
+code/geometric_verification.py, code/3d_reconstruction.py) — names, records, argument handling,
+and that nothing falls back to a CPU implementation when no GPU is present."""
+import importlib
+
+import numpy as np
+import pytest
+
+import feature_matching as fm
+import geometric_verification as gv
+import match_graph
+import oracle as O
+import reconstruction
+import sfmcore
+import synth
+
+
+def test_star_export_names_of_reference_module():
+    # code/pipeline.py:14,15,19,41 use os, cv2, np and extract_and_match from the star import
+    for name in ("os", "np", "cv2", "extract_and_match", "extract_and_match_draw", "read_img"):
+        assert hasattr(fm, name), name
+    ns = {}
+    exec("from feature_matching import *", ns)
+    assert "extract_and_match" in ns and "np" in ns and "os" in ns
+
+
+def test_3d_reconstruction_module_loads_under_reference_name():
+    m = importlib.import_module("3d_reconstruction")
+    assert hasattr(m, "build_jtj") and hasattr(m, "reprojection_errors")
+
+
+def test_extract_and_match_without_cv2_raises_clearly():
+    if fm.cv2 is not None:
+        pytest.skip("cv2 present")
+    with pytest.raises(ImportError, match="OpenCV"):
+        fm.extract_and_match(np.zeros((8, 8), np.uint8), np.zeros((8, 8), np.uint8))
+
+
+def test_dmatch_record():
+    a = fm.DMatch(3, 7, 0, 12.0)
+    assert (a.queryIdx, a.trainIdx, a.imgIdx, a.distance) == (3, 7, 0, 12.0)
+    assert a == fm.DMatch(3, 7, 0, 12) and a != fm.DMatch(3, 8, 0, 12)
+    assert "queryIdx=3" in repr(a)
+    # the reference sorts with key=lambda x: x.distance (code/feature_matching.py:52), stably
+    ms = [fm.DMatch(i, i, 0, d) for i, d in enumerate([5, 3, 5, 1])]
+    assert [m.queryIdx for m in sorted(ms, key=lambda x: x.distance)] == [3, 1, 0, 2]
+
+
+def test_empty_descriptor_sets_return_empty_list_without_device():
+    # cv2 raises on None descriptors; the drop-in returns [] so pipeline.py drops the pair (:42)
+    assert fm.match_descriptors(None, np.zeros((4, 32), np.uint8)) == []
+    assert fm.match_descriptors(np.zeros((0, 32), np.uint8), np.zeros((4, 32), np.uint8)) == []
+
+
+def test_no_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    d = np.random.default_rng(0).integers(0, 256, (16, 32), dtype=np.uint8)
+    with pytest.raises(sfmcore.SfmCoreError, match="no CPU fallback"):
+        fm.match_descriptors(d, d)
+    with pytest.raises(sfmcore.SfmCoreError):
+        gv.verify_pair(np.zeros((8, 2)), np.zeros((8, 2)), np.zeros((8, 2), np.int32))
+    with pytest.raises(sfmcore.SfmCoreError):
+        match_graph.GraphBuilder(np.zeros((2, 8, 128), np.uint8), np.zeros((2, 8, 2), np.float32))
+
+
+def test_ratio_fraction():
+    assert fm._ratio_fraction(0.8) == (4, 5)
+    assert fm._ratio_fraction(0.75) == (3, 4)
+    n, d = fm._ratio_fraction(0.7)
+    assert n / d == pytest.approx(0.7)
+
+
+def test_denormalize_F_matches_pixel_epipolar_constraint():
+    s = synth.make_scene(2, 256, seed=5)
+    q, t, _ = O.match(s["desc"][0], s["desc"][1], 0, 1, (4, 5))
+    x1, x2 = s["kps"][0][q], s["kps"][1][t]
+    r = O.ransac_f(x1, x2, H=256, seed=42, pa=0, pb=1)
+    assert r["count"] >= 15
+    F = gv.denormalize_F(r["F"], r["norm"])
+    assert np.linalg.norm(F) == pytest.approx(1.0)
+    assert np.linalg.matrix_rank(F, tol=1e-6) == 2
+    inl = r["mask"].astype(bool)
+    h1 = np.c_[x1[inl], np.ones(inl.sum())].astype(np.float64)
+    h2 = np.c_[x2[inl], np.ones(inl.sum())].astype(np.float64)
+    a = h1 @ F.T
+    b = h2 @ F
+    alg = np.sum(h2 * a, axis=1)
+    samp = alg ** 2 / (a[:, 0] ** 2 + a[:, 1] ** 2 + b[:, 0] ** 2 + b[:, 1] ** 2)
+    assert np.median(samp) < 1.0
+
+
+def test_rows_to_pairs_groups_by_pair():
+    pairs = synth.unordered_pairs(4)
+    rows = np.array([[2, 5, 6], [0, 1, 1], [2, 7, 8], [0, 3, 4]], np.int32)
+    g = match_graph.rows_to_pairs(rows, pairs)
+    assert [(a, b) for a, b, _ in g] == [tuple(pairs[0]), tuple(pairs[2])]
+    np.testing.assert_array_equal(g[0][2], [[1, 1], [3, 4]])
+    np.testing.assert_array_equal(g[1][2], [[5, 6], [7, 8]])
+    assert match_graph.rows_to_pairs(np.zeros((0, 3), np.int32), pairs) == []
+
+
+def test_csr_by_is_stable_grouping():
+    idx = np.array([2, 0, 2, 1, 0], np.int32)
+    ptr, order = sfmcore.csr_by(idx, 4)
+    np.testing.assert_array_equal(ptr, [0, 2, 3, 5, 5])
+    np.testing.assert_array_equal(order, [1, 4, 3, 0, 2])
+
+
+def test_build_jtj_sharded_rejects_unsorted_observations():
+    with pytest.raises(ValueError):
+        reconstruction.build_jtj_sharded(np.zeros((1, 8)), np.zeros((1, 2)), np.zeros((2, 3)),
+                                         [0, 0], [1, 0], np.zeros((2, 2)), 0, 1)
