@@ -98,6 +98,22 @@ int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_
                        int32_t* out_inl_count, int32_t* out_best_h, uint8_t* out_mask,
                        float* out_F, float* out_norm);
 
+/* ---- verified match graph -------------------------------------------------------------------
+ * Replaces the pair_matches list of code/pipeline.py:42-47 (Pair(img_inx_1, img_inx_2, matches)
+ * for every non-empty pair) for a batch: rows (pair_base + pair, queryIdx, trainIdx) of the RANSAC
+ * inliers of every pair whose inl_count >= min_inliers, pair-major, ascending match index.
+ *   sfm_graph_offsets: out_offsets [n_pairs + 1] i64, exclusive scan of the verified counts
+ *                      (out_offsets[n_pairs] = total rows); size out_rows from it.
+ *   sfm_graph_rows:    out_rows [total][3] i32; match_count / matches / mask / inl_count as
+ *                      written by sfm_match_batch and sfm_ransac_f_batch.
+ */
+int sfm_graph_offsets(sfm_ctx* ctx, int32_t n_pairs, const int32_t* inl_count,
+                      int32_t min_inliers, int64_t* out_offsets);
+int sfm_graph_rows(sfm_ctx* ctx, int32_t n_pairs, int32_t k_max, int32_t pair_base,
+                   const int32_t* match_count, const int32_t* matches, const uint8_t* mask,
+                   const int32_t* inl_count, int32_t min_inliers, const int64_t* offsets,
+                   int32_t* out_rows);
+
 /* ---- bundle-adjustment linearisation ---------------------------------------------------------
  * Fills the empty code/3d_reconstruction.py (import commented out at code/pipeline.py:4) with the
  * J^TJ build of papers/schoenberger2016sfm.pdf eq. (1) / §4.4.  Observations must be grouped by

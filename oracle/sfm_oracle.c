@@ -300,24 +300,46 @@ int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
     return 0;
 }
 
-/* Sampson inlier test in pixel units, evaluated in normalised coordinates:
- *   r = x2^T F x1,  g1 = |(F x1)_{0,1}|^2,  g2 = |(F^T x2)_{0,1}|^2,
- *   den = t2*g1 + t1*g2 with t1 = thr*s1^2, t2 = thr*s2^2 (s = normalisation scales),
- *   inlier  <=>  e = den - r*r > 0, e evaluated as one fma.
- * (Equivalent to r^2 / (s2^2 g1 + s1^2 g2) < thr up to rounding; this op sequence is the spec.) */
-static inline int sampson_inlier(const float F[9], float x1, float y1, float x2, float y2,
-                                 float t1, float t2) {
-    float a0 = fmaf(F[0], x1, fmaf(F[1], y1, F[2]));
-    float a1 = fmaf(F[3], x1, fmaf(F[4], y1, F[5]));
-    float a2 = fmaf(F[6], x1, fmaf(F[7], y1, F[8]));
-    float b0 = fmaf(F[0], x2, fmaf(F[3], y2, F[6]));
-    float b1 = fmaf(F[1], x2, fmaf(F[4], y2, F[7]));
-    float r = fmaf(x2, a0, fmaf(y2, a1, a2));
-    float g1 = fmaf(a0, a0, a1 * a1);
-    float g2 = fmaf(b0, b0, b1 * b1);
-    float den = fmaf(t2, g1, t1 * g2);
+/* Sampson inlier test in pixel units.  With t1 = thr*s1^2, t2 = thr*s2^2
+ * (s = normalisation scales) the test is  t2*|(F x1)_{0,1}|^2 + t1*|(F^T x2)_{0,1}|^2 > (x2^T F x1)^2.
+ * Scaling the homogeneous points x1 -> k1*(x1, y1, 1), x2 -> k2*(x2, y2, 1) with
+ * k = 1/(s*sqrt(thr)) turns both weights into 1, so the test becomes
+ *   |a|^2 + |b|^2 - r^2 > 0,  a = (G X1)_{0,1}, b = (G^T X2)_{0,1}, r = X2^T G X1
+ * on pre-scaled coordinates X = k * x_normalised and the per-hypothesis matrix G = F with the
+ * homogeneous column / row folded in (sampson_prep).  This op sequence is the spec. */
+static inline void sampson_scales(float s1, float s2, float thr, float* k1, float* k2) {
+    const float rt = sqrtf(thr);
+    *k1 = 1.0f / (s1 * rt);
+    *k2 = 1.0f / (s2 * rt);
+}
+
+static inline void sampson_prep(const float F[9], float k1, float k2, float G[9]) {
+    for (int i = 0; i < 9; ++i) G[i] = F[i];
+    G[2] = F[2] * k1;
+    G[5] = F[5] * k1;
+    G[6] = F[6] * k2;
+    G[7] = F[7] * k2;
+    G[8] = (F[8] * k1) * k2;
+}
+
+static inline int sampson_inlier(const float G[9], float x1, float y1, float x2, float y2) {
+    float a0 = fmaf(G[0], x1, fmaf(G[1], y1, G[2]));
+    float a1 = fmaf(G[3], x1, fmaf(G[4], y1, G[5]));
+    float c2 = fmaf(G[6], x1, fmaf(G[7], y1, G[8]));
+    float b0 = fmaf(G[0], x2, fmaf(G[3], y2, G[6]));
+    float b1 = fmaf(G[1], x2, fmaf(G[4], y2, G[7]));
+    float r = fmaf(x2, a0, fmaf(y2, a1, c2));
+    float den = fmaf(a0, a0, fmaf(a1, a1, fmaf(b0, b0, b1 * b1)));
     float e = fmaf(-r, r, den);
     return e > 0.0f;
+}
+
+/* scoring coordinates: X = k * x_normalised, planar per side */
+static void sampson_coords(const float* n, int M, float k, float* X) {
+    for (int m = 0; m < M; ++m) {
+        X[2 * m] = n[2 * m] * k;
+        X[2 * m + 1] = n[2 * m + 1] * k;
+    }
 }
 
 /*
@@ -340,7 +362,12 @@ int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t s
     float cx1, cy1, s1, cx2, cy2, s2;
     oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
     oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
-    float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
+    float k1, k2;
+    sampson_scales(s1, s2, thr, &k1, &k2);
+    float* X1 = (float*)malloc(sizeof(float) * 2 * M);
+    float* X2 = (float*)malloc(sizeof(float) * 2 * M);
+    sampson_coords(n1, M, k1, X1);
+    sampson_coords(n2, M, k2, X2);
     int bestc = -2, besth = -1;
     for (int h = 0; h < H; ++h) {
         int32_t idx[8];
@@ -352,10 +379,11 @@ int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t s
         }
         int cnt = -1;
         if (oracle_fit_f8(p1, p2, F) == 0) {
+            float G[9];
+            sampson_prep(F, k1, k2, G);
             cnt = 0;
             for (int m = 0; m < M; ++m)
-                cnt += sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m], n2[2 * m + 1],
-                                      t1, t2);
+                cnt += sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m], X2[2 * m + 1]);
         }
         if (cnt > bestc) { bestc = cnt; besth = h; }
     }
@@ -367,17 +395,19 @@ int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t s
         p2[2 * k] = n2[2 * idx[k]]; p2[2 * k + 1] = n2[2 * idx[k] + 1];
     }
     int ok = oracle_fit_f8(p1, p2, F);
+    float G[9];
+    sampson_prep(F, k1, k2, G);
     int cnt = 0;
     for (int m = 0; m < M; ++m) {
-        int in = (ok == 0) ? sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m],
-                                            n2[2 * m + 1], t1, t2) : 0;
+        int in = (ok == 0) ? sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m],
+                                            X2[2 * m + 1]) : 0;
         mask[m] = (uint8_t)in;
         cnt += in;
     }
     for (int i = 0; i < 9; ++i) Fout[i] = (ok == 0) ? F[i] : 0.0f;
     norm[0] = cx1; norm[1] = cy1; norm[2] = s1; norm[3] = cx2; norm[4] = cy2; norm[5] = s2;
     *best_h = besth;
-    free(n1); free(n2);
+    free(n1); free(n2); free(X1); free(X2);
     return cnt;
 }
 
@@ -389,7 +419,12 @@ void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint
     float cx1, cy1, s1, cx2, cy2, s2;
     oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
     oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
-    float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
+    float k1, k2;
+    sampson_scales(s1, s2, thr, &k1, &k2);
+    float* X1 = (float*)malloc(sizeof(float) * 2 * M);
+    float* X2 = (float*)malloc(sizeof(float) * 2 * M);
+    sampson_coords(n1, M, k1, X1);
+    sampson_coords(n2, M, k2, X2);
     for (int h = 0; h < H; ++h) {
         int32_t idx[8];
         oracle_sample8(seed, pa, pb, (uint32_t)h, M, idx);
@@ -400,14 +435,15 @@ void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint
         }
         int cnt = -1;
         if (oracle_fit_f8(p1, p2, F) == 0) {
+            float G[9];
+            sampson_prep(F, k1, k2, G);
             cnt = 0;
             for (int m = 0; m < M; ++m)
-                cnt += sampson_inlier(F, n1[2 * m], n1[2 * m + 1], n2[2 * m], n2[2 * m + 1],
-                                      t1, t2);
+                cnt += sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m], X2[2 * m + 1]);
         }
         counts[h] = cnt;
     }
-    free(n1); free(n2);
+    free(n1); free(n2); free(X1); free(X2);
 }
 
 /* ------------------------------------------------------------------------------------------ */

@@ -1,0 +1,112 @@
+// Verified match graph compaction (the reference's pair_matches list, code/pipeline.py:42-47:
+// keep non-empty pairs as Pair(img_inx_1, img_inx_2, matches)), restated for a pair batch on the
+// GPU: rows (global pair index, queryIdx, trainIdx) of the RANSAC inliers of every verified pair,
+// pair-major and ascending match index within a pair — the order the multi-GPU all-gather keeps.
+//
+// Two entry points so the caller can size the output between them:
+//   sfm_graph_offsets: one block, exclusive scan of the per-pair verified inlier counts -> [P+1]
+//   sfm_graph_rows:    one block per pair, ordered ballot compaction of the inlier mask.
+#include "match_common.h"
+#include "sfm_internal.h"
+
+namespace {
+
+constexpr int SCAN_T = 1024;
+
+__global__ __launch_bounds__(SCAN_T) void graph_offsets_kernel(int n_pairs,
+                                                               const int32_t* __restrict__ inl,
+                                                               int min_inl,
+                                                               int64_t* __restrict__ offsets) {
+    __shared__ int64_t wsum[SCAN_T / 64];
+    __shared__ int64_t carry;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n_pairs; base += SCAN_T) {
+        const int p = base + tid;
+        const int c = (p < n_pairs && inl[p] >= min_inl) ? inl[p] : 0;
+        // inclusive wave scan
+        int64_t v = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t o = __shfl_up(v, off, 64);
+            if (lane >= off) v += o;
+        }
+        if (lane == 63) wsum[wave] = v;
+        __syncthreads();
+        int64_t pre = carry;
+        for (int w = 0; w < wave; ++w) pre += wsum[w];
+        if (p < n_pairs) offsets[p] = pre + v - c;
+        __syncthreads();
+        if (tid == SCAN_T - 1) carry = pre + v;
+        __syncthreads();
+    }
+    if (tid == 0) offsets[n_pairs] = carry;
+}
+
+__global__ __launch_bounds__(256) void graph_rows_kernel(
+    int k_max, int pair_base, const int32_t* __restrict__ match_count,
+    const int32_t* __restrict__ matches, const uint8_t* __restrict__ mask,
+    const int32_t* __restrict__ inl, int min_inl, const int64_t* __restrict__ offsets,
+    int32_t* __restrict__ rows) {
+    __shared__ int wsum[4];
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (inl[p] < min_inl) return;  // block-uniform
+    const int M = match_count[p];
+    const uint8_t* mk = mask + (size_t)p * k_max;
+    const int32_t* mt = matches + (size_t)p * k_max * 2;
+    int64_t base = offsets[p];
+    for (int m0 = 0; m0 < M; m0 += 256) {
+        const int m = m0 + tid;
+        const bool keep = m < M && mk[m] != 0;
+        const unsigned long long bal = __ballot(keep);
+        const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = __popcll(bal);
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            off += (w < wave) ? wsum[w] : 0;
+            tot += wsum[w];
+        }
+        if (keep) {
+            int32_t* o = rows + (base + off + pre) * 3;
+            o[0] = pair_base + p;
+            o[1] = mt[2 * m];
+            o[2] = mt[2 * m + 1];
+        }
+        base += tot;
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+extern "C" int sfm_graph_offsets(sfm_ctx* ctx, int32_t n_pairs, const int32_t* inl_count,
+                                 int32_t min_inliers, int64_t* out_offsets) {
+    SFM_REQUIRE(ctx && out_offsets, "sfm_graph_offsets: NULL argument");
+    SFM_REQUIRE(n_pairs >= 0, "sfm_graph_offsets: negative size");
+    SFM_REQUIRE(n_pairs == 0 || inl_count, "sfm_graph_offsets: NULL inl_count");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(graph_offsets_kernel, dim3(1), dim3(SCAN_T), 0, ctx->stream, n_pairs,
+                       inl_count, min_inliers, out_offsets);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
+extern "C" int sfm_graph_rows(sfm_ctx* ctx, int32_t n_pairs, int32_t k_max, int32_t pair_base,
+                              const int32_t* match_count, const int32_t* matches,
+                              const uint8_t* mask, const int32_t* inl_count,
+                              int32_t min_inliers, const int64_t* offsets, int32_t* out_rows) {
+    SFM_REQUIRE(ctx, "sfm_graph_rows: ctx is NULL");
+    SFM_REQUIRE(n_pairs >= 0 && k_max >= 0 && pair_base >= 0, "sfm_graph_rows: negative size");
+    if (n_pairs == 0 || k_max == 0) return SFM_OK;
+    SFM_REQUIRE(match_count && matches && mask && inl_count && offsets && out_rows,
+                "sfm_graph_rows: NULL array");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(graph_rows_kernel, dim3(n_pairs), dim3(256), 0, ctx->stream, k_max,
+                       pair_base, match_count, matches, mask, inl_count, min_inliers, offsets,
+                       out_rows);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}

@@ -3,14 +3,20 @@
 // Fills the empty reference module code/geometric_verification.py (placeholder at
 // code/pipeline.py:60).  Three kernels per batch of pairs:
 //   ransac_prep   one wave per pair: gathers the tentative-match pixel coordinates, Hartley-
-//                 normalises each side with a fixed-order wave reduction, writes float4
-//                 (x1,y1,x2,y2) normalised per match and the (cx,cy,s) of both sides.
+//                 normalises each side with a fixed-order wave reduction and writes 8 planes per
+//                 pair: the normalised x1|y1|x2|y2 (fits) and the Sampson-scaled X1|Y1|X2|Y2
+//                 (scoring, X = k * x_normalised, k = 1/(s*sqrt(thr))), plus (cx,cy,s) per side.
 //   ransac_hyp    one LANE per hypothesis (256 per block): counter-based Philox sample of 8 distinct
 //                 matches (Floyd), Householder-QR null space of the 8x9 epipolar system, rank-2
-//                 projection (5 Jacobi sweeps on F^T F), then a sweep over all M matches held in LDS
-//                 (every lane reads the same float4: LDS broadcast) counting Sampson inliers.  The
-//                 block argmax (max count, lowest h) is a wave shuffle reduction, then one 64-bit
-//                 atomicMax per block into the pair's slot.
+//                 projection (5 Jacobi sweeps on F^T F), then a sweep over all M matches counting
+//                 Sampson inliers (17 flops + compare per match).  The match coordinates are
+//                 wave-uniform, so they are read with scalar loads into SGPRs and fed to packed
+//                 FMAs as SGPR-pair operands.  Exact pruning: every 64 matches a wave reads
+//                 the pair's best count so far (published by finished waves) and stops when no lane
+//                 can still reach it (count + remaining < best: strictly cannot win, so the result
+//                 is unchanged).  Each wave publishes its argmax (max count, lowest h) with one
+//                 64-bit atomicMax.  Grid x = pair, so the first hypothesis block of every pair runs
+//                 first and later blocks start with a bound.
 //   ransac_final  one block per pair: recomputes the winner, writes the inlier mask, F and count.
 // Every float expression follows oracle/sfm_oracle.c op for op (explicit fmaf, -ffp-contract=off),
 // so inlier sets are bit-identical to the CPU path at a fixed seed.
@@ -159,41 +165,37 @@ __device__ __forceinline__ bool fit_f8(const float4 s[8], float F[9]) {
     return ok;
 }
 
-// Sampson inlier test (oracle/sfm_oracle.c sampson_inlier): e = t2*g1 + t1*g2 - r^2 > 0.
-__device__ __forceinline__ int sampson_inlier(const float F[9], float x1, float y1, float x2,
-                                              float y2, float t1, float t2) {
-    const float a0 = fmaf(F[0], x1, fmaf(F[1], y1, F[2]));
-    const float a1 = fmaf(F[3], x1, fmaf(F[4], y1, F[5]));
-    const float a2 = fmaf(F[6], x1, fmaf(F[7], y1, F[8]));
-    const float b0 = fmaf(F[0], x2, fmaf(F[3], y2, F[6]));
-    const float b1 = fmaf(F[1], x2, fmaf(F[4], y2, F[7]));
-    const float r = fmaf(x2, a0, fmaf(y2, a1, a2));
-    const float g1 = fmaf(a0, a0, a1 * a1);
-    const float g2 = fmaf(b0, b0, b1 * b1);
-    const float den = fmaf(t2, g1, t1 * g2);
+// Sampson inlier test, oracle/sfm_oracle.c sampson_prep / sampson_inlier: G = F with the
+// homogeneous scales folded in, coordinates pre-scaled; inlier iff |a|^2 + |b|^2 - r^2 > 0.
+__device__ __forceinline__ void sampson_prep(const float F[9], float k1, float k2, float G[9]) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) G[i] = F[i];
+    G[2] = F[2] * k1;
+    G[5] = F[5] * k1;
+    G[6] = F[6] * k2;
+    G[7] = F[7] * k2;
+    G[8] = (F[8] * k1) * k2;
+}
+
+__device__ __forceinline__ int sampson_inlier(const float G[9], float x1, float y1, float x2,
+                                              float y2) {
+    const float a0 = fmaf(G[0], x1, fmaf(G[1], y1, G[2]));
+    const float a1 = fmaf(G[3], x1, fmaf(G[4], y1, G[5]));
+    const float c2 = fmaf(G[6], x1, fmaf(G[7], y1, G[8]));
+    const float b0 = fmaf(G[0], x2, fmaf(G[3], y2, G[6]));
+    const float b1 = fmaf(G[1], x2, fmaf(G[4], y2, G[7]));
+    const float r = fmaf(x2, a0, fmaf(y2, a1, c2));
+    const float den = fmaf(a0, a0, fmaf(a1, a1, fmaf(b0, b0, b1 * b1)));
     const float e = fmaf(-r, r, den);
     return e > 0.0f ? 1 : 0;
 }
 
-// The same test on two matches at once: every op is a v_pk_fma_f32 / v_pk_mul_f32 (gfx950 issues
-// one packed op per 4 cycles like a scalar one, so this halves the scoring cost).  Each half is an
-// IEEE fma/mul exactly like the scalar form, so results are bit-identical.
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 sp(float x) { return f2{x, x}; }
-__device__ __forceinline__ int sampson_inlier2(const float F[9], f2 x1, f2 y1, f2 x2, f2 y2,
-                                               float t1, float t2) {
-    const f2 a0 = fma2(sp(F[0]), x1, fma2(sp(F[1]), y1, sp(F[2])));
-    const f2 a1 = fma2(sp(F[3]), x1, fma2(sp(F[4]), y1, sp(F[5])));
-    const f2 a2 = fma2(sp(F[6]), x1, fma2(sp(F[7]), y1, sp(F[8])));
-    const f2 b0 = fma2(sp(F[0]), x2, fma2(sp(F[3]), y2, sp(F[6])));
-    const f2 b1 = fma2(sp(F[1]), x2, fma2(sp(F[4]), y2, sp(F[7])));
-    const f2 r = fma2(x2, a0, fma2(y2, a1, a2));
-    const f2 g1 = fma2(a0, a0, a1 * a1);
-    const f2 g2 = fma2(b0, b0, b1 * b1);
-    const f2 den = fma2(sp(t2), g1, sp(t1) * g2);
-    const f2 e = fma2(-r, r, den);
-    return (e.x > 0.0f ? 1 : 0) + (e.y > 0.0f ? 1 : 0);
+// per-pair scales of the scoring coordinates (oracle sampson_scales)
+__device__ __forceinline__ void sampson_scales(float s1, float s2, float thr, float& k1,
+                                               float& k2) {
+    const float rt = sqrtf(thr);
+    k1 = 1.0f / (s1 * rt);
+    k2 = 1.0f / (s2 * rt);
 }
 
 // fixed-order sum: lane l accumulates m = l, l+64, ... then a halving tree (oracle fixed_sum)
@@ -203,19 +205,23 @@ __device__ __forceinline__ float wave_fixed_sum(float partial) {
     return __shfl(partial, 0, 64);
 }
 
+// plane stride per pair: 8 planes of k_pl floats (k_pl multiple of 16: 64-B aligned planes)
+__host__ __device__ __forceinline__ int plane_len(int k_max) { return (k_max + 15) & ~15; }
+
 __global__ __launch_bounds__(64) void ransac_prep_kernel(
     const float* __restrict__ kps, int k_max, const int32_t* __restrict__ pairs,
-    const int32_t* __restrict__ match_count, const int32_t* __restrict__ matches,
-    float* __restrict__ nrm_xy, float* __restrict__ out_norm) {
+    const int32_t* __restrict__ match_count, const int32_t* __restrict__ matches, float thr,
+    float* __restrict__ planes, float* __restrict__ out_norm) {
     const int p = blockIdx.x, l = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int M = match_count[p];
     const int32_t* mt = matches + (size_t)p * k_max * 2;
-    // SoA planes x1 | y1 | x2 | y2, k_max floats each
-    float* X1 = nrm_xy + (size_t)p * 4 * k_max;
-    float* Y1 = X1 + k_max;
-    float* X2 = Y1 + k_max;
-    float* Y2 = X2 + k_max;
+    const int kp = plane_len(k_max);
+    float* X1 = planes + (size_t)p * 8 * kp;  // normalised x1 | y1 | x2 | y2
+    float* Y1 = X1 + kp;
+    float* X2 = Y1 + kp;
+    float* Y2 = X2 + kp;
+    float* S = Y2 + kp;                        // scaled X1 | Y1 | X2 | Y2
     if (M < 8) {
         if (l < 6) out_norm[p * 6 + l] = 0.0f;
         return;
@@ -245,11 +251,16 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
     const float mean1 = wave_fixed_sum(sd1) / fM, mean2 = wave_fixed_sum(sd2) / fM;
     const float s1 = (mean1 > 0.0f) ? (1.41421356237309515f / mean1) : 1.0f;
     const float s2 = (mean2 > 0.0f) ? (1.41421356237309515f / mean2) : 1.0f;
+    float k1, k2;
+    sampson_scales(s1, s2, thr, k1, k2);
     for (int m = l; m < M; m += 64) {
-        X1[m] = (X1[m] - mx1) * s1;
-        Y1[m] = (Y1[m] - my1) * s1;
-        X2[m] = (X2[m] - mx2) * s2;
-        Y2[m] = (Y2[m] - my2) * s2;
+        const float x1 = (X1[m] - mx1) * s1, y1 = (Y1[m] - my1) * s1;
+        const float x2 = (X2[m] - mx2) * s2, y2 = (Y2[m] - my2) * s2;
+        X1[m] = x1; Y1[m] = y1; X2[m] = x2; Y2[m] = y2;
+        S[m] = x1 * k1;
+        S[kp + m] = y1 * k1;
+        S[2 * kp + m] = x2 * k2;
+        S[3 * kp + m] = y2 * k2;
     }
     if (l == 0) {
         float* o = out_norm + p * 6;
@@ -257,59 +268,88 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
     }
 }
 
+typedef const __attribute__((address_space(4))) float* cfloat_p;  // scalar (constant) loads
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 sp(float x) { return f2{x, x}; }
+// two matches per call with v_pk_fma_f32 / v_pk_mul_f32; each half is the scalar op sequence
+__device__ __forceinline__ int sampson_inlier2(const float G[9], f2 x1, f2 y1, f2 x2, f2 y2) {
+    const f2 a0 = fma2(sp(G[0]), x1, fma2(sp(G[1]), y1, sp(G[2])));
+    const f2 a1 = fma2(sp(G[3]), x1, fma2(sp(G[4]), y1, sp(G[5])));
+    const f2 c2 = fma2(sp(G[6]), x1, fma2(sp(G[7]), y1, sp(G[8])));
+    const f2 b0 = fma2(sp(G[0]), x2, fma2(sp(G[3]), y2, sp(G[6])));
+    const f2 b1 = fma2(sp(G[1]), x2, fma2(sp(G[4]), y2, sp(G[7])));
+    const f2 r = fma2(x2, a0, fma2(y2, a1, c2));
+    const f2 den = fma2(a0, a0, fma2(a1, a1, fma2(b0, b0, b1 * b1)));
+    const f2 e = fma2(-r, r, den);
+    return (e.x > 0.0f ? 1 : 0) + (e.y > 0.0f ? 1 : 0);
+}
+
+constexpr int CH = 16;         // matches per scalar-load chunk (4 x s_load_dwordx16)
+constexpr int PRUNE_EVERY = 64;
+
+// One lane = one hypothesis; see the file comment.  The scoring coordinates are wave-uniform, so
+// they come through the scalar cache into SGPRs (no LDS traffic; the packed FMAs take them as
+// SGPR-pair operands).  Measured on cfg3 (tools/ransac_variants.py): LDS broadcast source
+// 1.93 ms, SGPR source 1.86 ms, SGPR + pruning 1.45 ms per 1225-pair launch.
+template <bool PRUNE>
 __global__ __launch_bounds__(256) void ransac_hyp_kernel(
     int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
-    const float* __restrict__ nrm_xy, const float* __restrict__ norm, uint64_t seed, float thr,
+    const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
     unsigned long long* __restrict__ best) {
-    // LDS: the pair's normalised matches as SoA planes x1 | y1 | x2 | y2 (k2 floats each), so a
-    // float2 read hands the packed Sampson test two matches in adjacent registers
-    extern __shared__ __attribute__((aligned(16))) float lds_m[];
-    __shared__ unsigned long long wbest[4];
-    const int p = blockIdx.y;
+    const int p = blockIdx.x;
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int tid = threadIdx.x;
-    const int k2 = (k_max + 3) & ~3;
-    float* LX1 = lds_m;
-    float* LY1 = LX1 + k2;
-    float* LX2 = LY1 + k2;
-    float* LY2 = LX2 + k2;
-    const float* src = nrm_xy + (size_t)p * 4 * k_max;
-    for (int m = tid; m < M; m += 256) {
-        LX1[m] = src[m];
-        LY1[m] = src[k_max + m];
-        LX2[m] = src[2 * k_max + m];
-        LY2[m] = src[3 * k_max + m];
-    }
-    __syncthreads();
+    const int kp = plane_len(k_max);
+    const float* pl = planes + (size_t)p * 8 * kp;
+    const cfloat_p S = (cfloat_p)(pl + 4 * kp);
     const uint32_t pa = (uint32_t)pairs[2 * p], pb = (uint32_t)pairs[2 * p + 1];
     const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
-    const float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
-    const uint32_t h = blockIdx.x * 256 + tid;
+    float k1, k2;
+    sampson_scales(s1, s2, thr, k1, k2);
+    const uint32_t h = blockIdx.y * 256 + tid;
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
     float4 smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        smp[k] = make_float4(LX1[idx[k]], LY1[idx[k]], LX2[idx[k]], LY2[idx[k]]);
-    float F[9];
+        smp[k] = make_float4(pl[idx[k]], pl[kp + idx[k]], pl[2 * kp + idx[k]],
+                             pl[3 * kp + idx[k]]);
+    float F[9], G[9];
     const bool ok = fit_f8(smp, F);
-    // two packed chains (4 matches) per iteration; the count is an integer, so the order of the
-    // partial sums does not change the result
-    const f2* PX1 = (const f2*)LX1;
-    const f2* PY1 = (const f2*)LY1;
-    const f2* PX2 = (const f2*)LX2;
-    const f2* PY2 = (const f2*)LY2;
-    int c0 = 0, c1 = 0;
-    int q = 0;
-    const int half = M >> 1;
-    for (; q + 2 <= half; q += 2) {
-        c0 += sampson_inlier2(F, PX1[q], PY1[q], PX2[q], PY2[q], t1, t2);
-        c1 += sampson_inlier2(F, PX1[q + 1], PY1[q + 1], PX2[q + 1], PY2[q + 1], t1, t2);
+    sampson_prep(F, k1, k2, G);
+
+    int cnt = 0;
+    const int Mc = M & ~(CH - 1);
+    int m = 0;
+#pragma unroll 1
+    for (; m < Mc; m += CH) {
+        float x1[CH], y1[CH], x2[CH], y2[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            x1[j] = S[m + j];
+            y1[j] = S[kp + m + j];
+            x2[j] = S[2 * kp + m + j];
+            y2[j] = S[3 * kp + m + j];
+        }
+#pragma unroll
+        for (int j = 0; j < CH; j += 2)
+            cnt += sampson_inlier2(G, f2{x1[j], x1[j + 1]}, f2{y1[j], y1[j + 1]},
+                                   f2{x2[j], x2[j + 1]}, f2{y2[j], y2[j + 1]});
+        if (PRUNE && ((m + CH) % PRUNE_EVERY) == 0) {
+            // Exact pruning: best[p] only grows and every published key is a real hypothesis's
+            // (count, id), so (key >> 32) - 1 is a lower bound on the winning count.  A wave
+            // whose lanes all satisfy count + remaining < bound holds no possible winner.
+            const unsigned long long bk =
+                __hip_atomic_load(&best[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int bound = (int)(bk >> 32) - 1;
+            if (__all(cnt + (M - m - CH) < bound)) return;  // wave-uniform exit
+        }
     }
-    if (q < half) c0 += sampson_inlier2(F, PX1[q], PY1[q], PX2[q], PY2[q], t1, t2);
-    if (M & 1) c1 += sampson_inlier(F, LX1[M - 1], LY1[M - 1], LX2[M - 1], LY2[M - 1], t1, t2);
-    int cnt = c0 + c1;
+#pragma unroll 1
+    for (; m < M; ++m) cnt += sampson_inlier(G, S[m], S[kp + m], S[2 * kp + m], S[3 * kp + m]);
     if (!ok) cnt = -1;
     unsigned long long key = ((unsigned long long)(unsigned)(cnt + 1) << 32) | (0xFFFFFFFFu - h);
 #pragma unroll
@@ -317,18 +357,12 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
         const unsigned long long o = __shfl_xor(key, off, 64);
         key = o > key ? o : key;
     }
-    if ((tid & 63) == 0) wbest[tid >> 6] = key;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long k = wbest[0];
-        for (int w = 1; w < 4; ++w) k = wbest[w] > k ? wbest[w] : k;
-        atomicMax(&best[p], k);
-    }
+    if ((tid & 63) == 0) atomicMax(&best[p], key);  // per wave: later waves prune sooner
 }
 
 __global__ __launch_bounds__(256) void ransac_final_kernel(
     int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
-    const float* __restrict__ nrm_xy, const float* __restrict__ norm, uint64_t seed, float thr,
+    const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
     const unsigned long long* __restrict__ best, int32_t* __restrict__ out_inl_count,
     int32_t* __restrict__ out_best_h, uint8_t* __restrict__ out_mask, float* __restrict__ out_F) {
     __shared__ int wsum[4];
@@ -343,22 +377,25 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
     }
     const uint32_t pa = (uint32_t)pairs[2 * p], pb = (uint32_t)pairs[2 * p + 1];
     const uint32_t h = 0xFFFFFFFFu - (uint32_t)best[p];
-    const float* X1 = nrm_xy + (size_t)p * 4 * k_max;
-    const float* Y1 = X1 + k_max;
-    const float* X2 = Y1 + k_max;
-    const float* Y2 = X2 + k_max;
+    const int kp = plane_len(k_max);
+    const float* pl = planes + (size_t)p * 8 * kp;
+    const float* S = pl + 4 * kp;
     const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
-    const float t1 = thr * (s1 * s1), t2 = thr * (s2 * s2);
+    float k1, k2;
+    sampson_scales(s1, s2, thr, k1, k2);
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
     float4 smp[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) smp[k] = make_float4(X1[idx[k]], Y1[idx[k]], X2[idx[k]], Y2[idx[k]]);
-    float F[9];
+    for (int k = 0; k < 8; ++k)
+        smp[k] = make_float4(pl[idx[k]], pl[kp + idx[k]], pl[2 * kp + idx[k]],
+                             pl[3 * kp + idx[k]]);
+    float F[9], G[9];
     const bool ok = fit_f8(smp, F);
+    sampson_prep(F, k1, k2, G);
     int cnt = 0;
     for (int m = tid; m < M; m += 256) {
-        const int in = ok ? sampson_inlier(F, X1[m], Y1[m], X2[m], Y2[m], t1, t2) : 0;
+        const int in = ok ? sampson_inlier(G, S[m], S[kp + m], S[2 * kp + m], S[3 * kp + m]) : 0;
         mask[m] = (uint8_t)in;
         cnt += in;
     }
@@ -375,6 +412,12 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
 
 }  // namespace
 
+// SFM_RANSAC_NOPRUNE=1 disables the exact pruning (same results; for measuring its effect).
+static bool ransac_prune() {
+    const char* e = getenv("SFM_RANSAC_NOPRUNE");
+    return !(e && atoi(e) != 0);
+}
+
 extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
                                   const int32_t* pairs, int32_t n_pairs,
                                   const int32_t* match_count, const int32_t* matches,
@@ -389,26 +432,32 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
                 "sfm_ransac_f_batch: NULL array");
     SFM_REQUIRE(prm->n_hyp > 0 && prm->n_hyp % 256 == 0,
                 "sfm_ransac_f_batch: n_hyp must be a positive multiple of 256");
+    SFM_REQUIRE(prm->thr > 0.0f, "sfm_ransac_f_batch: thr must be > 0");
     SFM_REQUIRE(k_max <= 8192, "sfm_ransac_f_batch: k_max > 8192 not supported");
+    SFM_REQUIRE(prm->n_hyp / 256 <= 65535, "sfm_ransac_f_batch: n_hyp too large");
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    const size_t xyb = (size_t)n_pairs * 4 * std::max(k_max, 1) * sizeof(float);
+    const int kp = plane_len(std::max(k_max, 1));
+    const size_t plb = (size_t)n_pairs * 8 * kp * sizeof(float);
     const size_t bb = (size_t)n_pairs * sizeof(unsigned long long);
-    char* ws = (char*)sfm::workspace(ctx, xyb + bb + 1024);
+    char* ws = (char*)sfm::workspace(ctx, plb + bb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
-    float* nrm_xy = (float*)ws;
-    unsigned long long* best = (unsigned long long*)(ws + xyb);
+    float* planes = (float*)ws;
+    unsigned long long* best = (unsigned long long*)(ws + plb);
     SFM_HIP_CHECK(hipMemsetAsync(best, 0, bb, st));
     hipLaunchKernelGGL(ransac_prep_kernel, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
-                       match_count, matches, nrm_xy, out_norm);
+                       match_count, matches, prm->thr, planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ransac_hyp_kernel, dim3(prm->n_hyp / 256, n_pairs), dim3(256),
-                       (size_t)4 * ((std::max(k_max, 1) + 3) & ~3) * sizeof(float), st, k_max, pairs,
-                       match_count,
-                       nrm_xy, out_norm, prm->seed, prm->thr, best);
+    const dim3 grid(n_pairs, prm->n_hyp / 256);
+    if (ransac_prune())
+        hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
+                           match_count, planes, out_norm, prm->seed, prm->thr, best);
+    else
+        hipLaunchKernelGGL(ransac_hyp_kernel<false>, grid, dim3(256), 0, st, k_max, pairs,
+                           match_count, planes, out_norm, prm->seed, prm->thr, best);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(ransac_final_kernel, dim3(n_pairs), dim3(256), 0, st, k_max, pairs,
-                       match_count, nrm_xy, out_norm, prm->seed, prm->thr, best, out_inl_count,
+                       match_count, planes, out_norm, prm->seed, prm->thr, best, out_inl_count,
                        out_best_h, out_mask, out_F);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;

@@ -95,17 +95,10 @@ class GraphBuilder:
         return count, match, dist, rs
 
     def graph_rows(self, pair_base: int, count, match, rs):
-        """Verified inlier rows [n,3] int32 (global pair index, queryIdx, trainIdx), on device."""
-        torch = self.torch
-        K = self.k_max
-        ok = rs["inl_count"] >= self.min_inliers
-        ar = torch.arange(K, device=self.dev)
-        sel = (rs["mask"] != 0) & ok[:, None] & (ar[None, :] < count[:, None])
-        pm = sel.nonzero()
-        rows = torch.empty((pm.shape[0], 3), dtype=torch.int32, device=self.dev)
-        rows[:, 0] = (pm[:, 0] + pair_base).to(torch.int32)
-        rows[:, 1:] = match[pm[:, 0], pm[:, 1]]
-        return rows
+        """Verified inlier rows [n,3] int32 (global pair index, queryIdx, trainIdx), on device
+        (sfm_graph_offsets + sfm_graph_rows)."""
+        return self.ctx.graph_rows(pair_base, count, match, rs["inl_count"], rs["mask"],
+                                   self.min_inliers)
 
 
 def all_gather_rows(rows, group=None):

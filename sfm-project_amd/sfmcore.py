@@ -21,7 +21,7 @@ XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
 
 EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_sync",
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
-            "sfm_ba_jtj"]
+            "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows"]
 
 
 class SfmCoreError(RuntimeError):
@@ -71,6 +71,8 @@ def load_library(path: str = LIB_PATH):
                                          C.POINTER(RansacParams), vp, vp, vp, vp, vp]
         L.sfm_ba_jtj.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp,
                                  vp, vp, vp, vp, vp, vp]
+        L.sfm_graph_offsets.argtypes = [vp, i32, vp, i32, vp]
+        L.sfm_graph_rows.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp]
         for name in EXPORTED:
             getattr(L, name).restype = getattr(L, name).restype or C.c_int
         _lib = L
@@ -170,6 +172,26 @@ class Context:
                                            _ptr(out["inl_count"]), _ptr(out["best_h"]),
                                            _ptr(out["mask"]), _ptr(out["F"]), _ptr(out["norm"])))
         return out
+
+    # ---- verified match graph --------------------------------------------------------------
+    def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15):
+        """Rows [n,3] i32 (pair_base + pair, queryIdx, trainIdx) of the inliers of every verified
+        pair (inl_count >= min_inliers), pair-major, ascending match index.  One device->host
+        read of the row total sizes the output."""
+        torch = self.torch
+        P, k_max = mask.shape
+        dev = mask.device
+        offs = torch.empty(P + 1, dtype=torch.int64, device=dev)
+        self._bind_stream()
+        _check(self.lib.sfm_graph_offsets(self.handle, P, _ptr(inl_count), int(min_inliers),
+                                          _ptr(offs)))
+        n = int(offs[P].item())
+        rows = torch.empty((n, 3), dtype=torch.int32, device=dev)
+        if n:
+            _check(self.lib.sfm_graph_rows(self.handle, P, k_max, int(pair_base), _ptr(count),
+                                           _ptr(match), _ptr(mask), _ptr(inl_count),
+                                           int(min_inliers), _ptr(offs), _ptr(rows)))
+        return rows
 
     # ---- bundle adjustment -----------------------------------------------------------------
     def ba_jtj(self, cams, pp, pts, cam_idx, pt_idx, uv, pt_ptr, cam_ptr, cam_obs, loss_s=0.0):

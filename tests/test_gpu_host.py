@@ -128,3 +128,22 @@ def test_build_jtj_and_sharded_single_rank():
                                   pr["pt_idx"][perm], pr["uv"][perm], loss_s=1.5)
     np.testing.assert_array_equal(g2["res"], g["res"][perm])
     np.testing.assert_allclose(g2["U"], g["U"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("P,K", [(1, 16), (37, 300), (2500, 64)])
+def test_graph_rows_compaction(ctx, P, K):
+    """sfm_graph_offsets / sfm_graph_rows against a numpy restatement on random masks: scan over
+    more than one 1024-pair tile, unverified / empty pairs, ragged match counts."""
+    import torch
+    rng = np.random.default_rng(P)
+    count = rng.integers(0, K + 1, P).astype(np.int32)
+    match = rng.integers(0, 5000, (P, K, 2)).astype(np.int32)
+    mask = (rng.random((P, K)) < 0.4).astype(np.uint8)
+    mask[:, :][np.arange(K)[None, :] >= count[:, None]] = 1  # stale entries beyond count
+    inl = np.array([mask[p, :count[p]].sum() for p in range(P)], np.int32)
+    inl[rng.random(P) < 0.2] = -1
+    want = [(7 + p, *match[p, m]) for p in range(P) if inl[p] >= 15
+            for m in range(count[p]) if mask[p, m]]
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    rows = ctx.graph_rows(7, T(count), T(match), T(inl), T(mask), 15).cpu().numpy()
+    np.testing.assert_array_equal(rows, np.array(want, np.int32).reshape(-1, 3))
