@@ -1,0 +1,50 @@
+"""Times K1 (sfm_match_batch, L2 mutual + ratio 4/5) on the cfg3 workload with HIP events and
+checks a sample of pairs bit-exactly against the CPU oracle.  Usage: python tools/k1_time.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracle")]
+
+import numpy as np
+import torch
+
+import oracle as O
+import sfmcore
+import synth
+
+
+def main():
+    n_img = int(os.environ.get("N_IMG", "50"))
+    K = int(os.environ.get("K", "2048"))
+    s = synth.make_scene(n_img, K, seed=0)
+    pairs = synth.unordered_pairs(n_img)
+    ctx = sfmcore.context(0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
+    for xc, ratio in ((1, (4, 5)), (2, None)):
+        out = ctx.match_batch(desc, n_kp, pr, cross_check=xc, ratio=ratio)
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        reps = 10
+        ev[0].record()
+        for _ in range(reps):
+            out = ctx.match_batch(desc, n_kp, pr, cross_check=xc, ratio=ratio, out=out)
+        ev[1].record()
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        cnt, mt, dist = (t.cpu().numpy() for t in out)
+        ok = True
+        for p in range(0, len(pairs), max(1, len(pairs) // 12)):
+            a, b = pairs[p]
+            q, t, d = O.match(s["desc"][a], s["desc"][b], 0, xc, ratio)
+            ok &= bool(cnt[p] == len(q) and (mt[p, :cnt[p], 0] == q).all()
+                       and (mt[p, :cnt[p], 1] == t).all() and (dist[p, :cnt[p]] == d).all())
+        ops = 2.0 * 128 * float(np.sum(s["n_kp"][pairs[:, 0]].astype(np.float64)
+                                       * s["n_kp"][pairs[:, 1]]))
+        print(f"xc={xc} ratio={ratio}: {ms:.3f} ms/launch  {ops / ms / 1e9:.0f} TOP/s  "
+              f"parity={ok}  matches={int(cnt.sum())}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
