@@ -34,6 +34,19 @@ RANSAC_FLOP_PER_EVAL = 33      # Sampson test: 16 fma + 1 mul (ransac.hip sampso
 RANSAC_FLOP_PER_FIT = 1900     # fit_f8: Householder QR 8x9 + Q e9 + Jacobi 3x3 + rank-2
 
 
+def pmc_traffic(kernel, n_img, k, world):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this exact workload
+    (tools/pmc_traffic.sh -> profiles/r01_traffic_cfg3.json: FETCH_SIZE x2 + WRITE_SIZE, separate
+    passes, MI355X_MICROARCH.md corrections), or None for any other workload."""
+    f = os.path.join(ROOT, "profiles", "r01_traffic_cfg3.json")
+    if not (os.path.exists(f) and n_img == 50 and k == 2048 and world == 1):
+        return None
+    try:
+        return float(json.load(open(f))["kernels"][kernel]["hbm_bytes"])
+    except (KeyError, ValueError):
+        return None
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -146,7 +159,9 @@ def main():
         "verified_matches_per_step": verified_per_step,
         "roofline": {"kernel": "l2_match (K1: prep + MFMA match + finalize, HIP events)",
                      "bound": "mfma", "achieved": k1_tops, "peak": PEAK_I8_TOPS,
-                     "unit": "TOP/s (i8)", "frac": k1_tops / PEAK_I8_TOPS, "traffic": None,
+                     "unit": "TOP/s (i8)", "frac": k1_tops / PEAK_I8_TOPS,
+                     "traffic": pmc_traffic("l2_match_kernel", n_img, args.k, world),
+                     "traffic_unit": "bytes per l2_match_kernel launch (PMC, profiles/r01_traffic_cfg3.json)",
                      "ms": match_ms, "ops_per_launch": k1_ops},
         "stages": {"match_ms": match_ms, "ransac_ms": ransac_ms,
                    "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,

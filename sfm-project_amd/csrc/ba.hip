@@ -2,15 +2,19 @@
 // DESIGN.md §4.3).  Fills the empty reference module code/3d_reconstruction.py.
 //
 // fp64 throughout.  Deterministic (no float atomics): every accumulation has a fixed order.
-//   ba_point_kernel   one thread per point, its observations are contiguous (pt_ptr CSR):
-//                     residual, J_c (2x8), J_p (2x3) per observation -> res, W = w J_c^T J_p,
-//                     V_p = sum w J_p^T J_p, g_p = sum w J_p^T r, the point's cost share.
-//   ba_camera_kernel  one 256-thread block per camera over its observation list (cam_ptr/cam_obs
-//                     CSR): recomputes J_c (cheaper than storing it: HBM is the bound) and reduces
-//                     U_c = sum w J_c^T J_c and g_c = sum w J_c^T r with a fixed lane-strided order
-//                     plus a fixed shuffle tree.
-//   ba_cost_kernel    one block: fixed-order sum of the per-point cost shares.
+//   ba_obs_kernel          one thread per observation (enough waves to stream HBM): residual,
+//                          J_c (2x8), J_p (2x3) -> res, W = w J_c^T J_p, and the observation's
+//                          point terms (w J_p^T J_p upper triangle, w J_p^T r, rho/2) to a scratch.
+//   ba_point_kernel        one thread per point: sums its observations' terms in order (pt_ptr
+//                          CSR) -> V_p, g_p; fixed-tree block sum of the cost shares.
+//   ba_camera_kernel       block (camera, split): recomputes J_c (cheaper than storing it: HBM is
+//                          the bound) over a contiguous share of the camera's observations
+//                          (cam_ptr/cam_obs CSR), fixed lane-strided order + shuffle tree.
+//   ba_camera_final_kernel sums the splits in order -> U_c = sum w J_c^T J_c, g_c = sum w J_c^T r.
+//   ba_cost_kernel         fixed-order sum of the block cost shares.
 // Algorithmic HBM traffic ~300 B/observation; this is an HBM-bound stage.
+#include <algorithm>
+
 #include "sfm_internal.h"
 
 namespace {
@@ -87,63 +91,97 @@ __device__ __forceinline__ void linearize(const double* __restrict__ cam, const 
     o.w = w; o.rho = rho;
 }
 
-__global__ __launch_bounds__(256) void ba_point_kernel(
-    int n_pt, const double* __restrict__ cams, const double* __restrict__ pp,
-    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
-    const double* __restrict__ uv, const int32_t* __restrict__ pt_ptr, double loss_s,
-    double* __restrict__ V, double* __restrict__ W, double* __restrict__ gp,
-    double* __restrict__ res, double* __restrict__ cost_pt) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_pt) return;
-    const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
-    double Vp[6] = {0, 0, 0, 0, 0, 0};  // upper triangle 00 01 02 11 12 22
-    double g[3] = {0, 0, 0};
-    double cost = 0.0;
-    const int o0 = pt_ptr[p], o1 = pt_ptr[p + 1];
-    for (int o = o0; o < o1; ++o) {
-        const int c = cam_idx[o];
-        ObsLin L;
-        linearize(cams + 8 * (size_t)c, pp + 2 * (size_t)c, X, uv[2 * (size_t)o],
-                  uv[2 * (size_t)o + 1], loss_s, true, L);
-        cost += 0.5 * L.rho;
-        res[2 * (size_t)o] = L.r[0];
-        res[2 * (size_t)o + 1] = L.r[1];
-        double* Wo = W + 24 * (size_t)o;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-                Wo[3 * i + j] = L.w * (L.Jc[i] * L.Jp[j] + L.Jc[8 + i] * L.Jp[3 + j]);
-        int t = 0;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-#pragma unroll
-            for (int j = i; j < 3; ++j) Vp[t++] += L.w * (L.Jp[i] * L.Jp[j] + L.Jp[3 + i] * L.Jp[3 + j]);
-            g[i] += L.w * (L.Jp[i] * L.r[0] + L.Jp[3 + i] * L.r[1]);
-        }
-    }
-    double* Vo = V + 9 * (size_t)p;
-    Vo[0] = Vp[0]; Vo[1] = Vp[1]; Vo[2] = Vp[2];
-    Vo[3] = Vp[1]; Vo[4] = Vp[3]; Vo[5] = Vp[4];
-    Vo[6] = Vp[2]; Vo[7] = Vp[4]; Vo[8] = Vp[5];
-    gp[3 * (size_t)p] = g[0]; gp[3 * (size_t)p + 1] = g[1]; gp[3 * (size_t)p + 2] = g[2];
-    cost_pt[p] = cost;
-}
-
+constexpr int NV = 10;      // per-observation point terms: V upper triangle (6), g_p (3), 0.5 rho
 constexpr int NU = 36 + 8;  // upper triangle of U_c (8x8) + g_c
 
+// One thread per observation: residual, W = w J_c^T J_p, and the observation's point terms.
+__global__ __launch_bounds__(256) void ba_obs_kernel(
+    int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
+    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
+    const int32_t* __restrict__ pt_idx, const double* __restrict__ uv, double loss_s,
+    double* __restrict__ W, double* __restrict__ res, double* __restrict__ terms) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n_obs) return;
+    const int c = cam_idx[o], p = pt_idx[o];
+    const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+    const double2 z = *(const double2*)(uv + 2 * (size_t)o);
+    ObsLin L;
+    linearize(cams + 8 * (size_t)c, pp + 2 * (size_t)c, X, z.x, z.y, loss_s, true, L);
+    *(double2*)(res + 2 * (size_t)o) = make_double2(L.r[0], L.r[1]);
+    double2* Wo = (double2*)(W + 24 * (size_t)o);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+        const int i0 = (2 * q) / 3, j0 = (2 * q) % 3, i1 = (2 * q + 1) / 3, j1 = (2 * q + 1) % 3;
+        Wo[q] = make_double2(L.w * (L.Jc[i0] * L.Jp[j0] + L.Jc[8 + i0] * L.Jp[3 + j0]),
+                             L.w * (L.Jc[i1] * L.Jp[j1] + L.Jc[8 + i1] * L.Jp[3 + j1]));
+    }
+    double t[NV];
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = i; j < 3; ++j) t[k++] = L.w * (L.Jp[i] * L.Jp[j] + L.Jp[3 + i] * L.Jp[3 + j]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[6 + i] = L.w * (L.Jp[i] * L.r[0] + L.Jp[3 + i] * L.r[1]);
+    t[9] = 0.5 * L.rho;
+    double2* To = (double2*)(terms + NV * (size_t)o);
+#pragma unroll
+    for (int q = 0; q < NV / 2; ++q) To[q] = make_double2(t[2 * q], t[2 * q + 1]);
+}
+
+// One thread per point: V_p, g_p and the cost share, summed over its observations in order; then a
+// fixed-order block reduction of the cost shares.
+__global__ __launch_bounds__(256) void ba_point_kernel(int n_pt, const int32_t* __restrict__ pt_ptr,
+                                                       const double* __restrict__ terms,
+                                                       double* __restrict__ V,
+                                                       double* __restrict__ gp,
+                                                       double* __restrict__ cost_blk) {
+    __shared__ double red[4];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x, tid = threadIdx.x;
+    double cost = 0.0;
+    if (p < n_pt) {
+        double a[NV - 1];
+#pragma unroll
+        for (int i = 0; i < NV - 1; ++i) a[i] = 0.0;
+        const int o0 = pt_ptr[p], o1 = pt_ptr[p + 1];
+        for (int o = o0; o < o1; ++o) {
+            const double2* T = (const double2*)(terms + NV * (size_t)o);
+#pragma unroll
+            for (int q = 0; q < NV / 2; ++q) {
+                const double2 v = T[q];
+                if (2 * q < NV - 1) a[2 * q] += v.x; else cost += v.x;
+                if (2 * q + 1 < NV - 1) a[2 * q + 1] += v.y; else cost += v.y;
+            }
+        }
+        double* Vo = V + 9 * (size_t)p;
+        Vo[0] = a[0]; Vo[1] = a[1]; Vo[2] = a[2];
+        Vo[3] = a[1]; Vo[4] = a[3]; Vo[5] = a[4];
+        Vo[6] = a[2]; Vo[7] = a[4]; Vo[8] = a[5];
+        gp[3 * (size_t)p] = a[6]; gp[3 * (size_t)p + 1] = a[7]; gp[3 * (size_t)p + 2] = a[8];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cost += __shfl_down(cost, off, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = cost;
+    __syncthreads();
+    if (tid == 0) cost_blk[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// Block (camera c, split s): fixed-order partial U_c / g_c over its share of the camera's
+// observations (J_c recomputed: cheaper than storing it, HBM is the bound).
 __global__ __launch_bounds__(256) void ba_camera_kernel(
     const double* __restrict__ cams, const double* __restrict__ pp, const double* __restrict__ pts,
     const int32_t* __restrict__ pt_idx, const double* __restrict__ uv,
     const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ cam_obs, double loss_s,
-    double* __restrict__ U, double* __restrict__ gc) {
+    int splits, double* __restrict__ part) {
     __shared__ double red[4][NU];
-    const int c = blockIdx.x, tid = threadIdx.x;
+    const int c = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     double acc[NU];
 #pragma unroll
     for (int i = 0; i < NU; ++i) acc[i] = 0.0;
     const double* cam = cams + 8 * (size_t)c;
-    const int e0 = cam_ptr[c], e1 = cam_ptr[c + 1];
+    const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
+    const int len = (c1 - c0 + splits - 1) / splits;
+    const int e0 = c0 + s * len, e1 = min(c1, e0 + len);
     for (int e = e0 + tid; e < e1; e += 256) {
         const int o = cam_obs[e];
         const int p = pt_idx[o];
@@ -171,27 +209,39 @@ __global__ __launch_bounds__(256) void ba_camera_kernel(
         for (int i = 0; i < NU; ++i) red[tid >> 6][i] = acc[i];
     }
     __syncthreads();
-    if (tid < NU) {
-        const double v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-        if (tid >= 36) {
-            gc[8 * (size_t)c + tid - 36] = v;
-        } else {
-            // map upper-triangle index -> (i, j)
-            int i = 0, t = tid;
-            while (t >= 8 - i) { t -= 8 - i; ++i; }
-            const int j = i + t;
-            U[64 * (size_t)c + 8 * i + j] = v;
-            U[64 * (size_t)c + 8 * j + i] = v;
-        }
+    if (tid < NU)
+        part[((size_t)c * splits + s) * NU + tid] =
+            ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+}
+
+// One thread per (camera, component): sum of the split partials in order -> U_c (both triangles),
+// g_c.
+__global__ __launch_bounds__(256) void ba_camera_final_kernel(int n_cam, int splits,
+                                                              const double* __restrict__ part,
+                                                              double* __restrict__ U,
+                                                              double* __restrict__ gc) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_cam * NU) return;
+    const int c = g / NU, k = g - c * NU;
+    double v = 0.0;
+    for (int s = 0; s < splits; ++s) v += part[((size_t)c * splits + s) * NU + k];
+    if (k >= 36) {
+        gc[8 * (size_t)c + k - 36] = v;
+    } else {
+        int i = 0, t = k;
+        while (t >= 8 - i) { t -= 8 - i; ++i; }
+        const int j = i + t;
+        U[64 * (size_t)c + 8 * i + j] = v;
+        U[64 * (size_t)c + 8 * j + i] = v;
     }
 }
 
-__global__ __launch_bounds__(256) void ba_cost_kernel(int n_pt, const double* __restrict__ cost_pt,
+__global__ __launch_bounds__(256) void ba_cost_kernel(int n, const double* __restrict__ cost_blk,
                                                       double* __restrict__ cost) {
     __shared__ double red[4];
     const int tid = threadIdx.x;
     double s = 0.0;
-    for (int p = tid; p < n_pt; p += 256) s += cost_pt[p];
+    for (int p = tid; p < n; p += 256) s += cost_blk[p];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) s += __shfl_down(s, off, 64);
     if ((tid & 63) == 0) red[tid >> 6] = s;
@@ -227,15 +277,42 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     SFM_REQUIRE(cams && pp && pts && cam_idx && pt_idx && uv && pt_ptr && cam_ptr && cam_obs && U &&
                     V && W && gc && gp && res,
                 "sfm_ba_jtj: NULL array");
-    double* cost_pt = (double*)sfm::workspace(ctx, sizeof(double) * (size_t)n_pt + 1024);
-    if (!cost_pt) return SFM_ERR_NOMEM;
-    hipLaunchKernelGGL(ba_point_kernel, dim3((n_pt + 255) / 256), dim3(256), 0, st, n_pt, cams, pp,
-                       pts, cam_idx, uv, pt_ptr, loss_s, V, W, gp, res, cost_pt);
+    // workspace: per-observation point terms | cost per point block | camera split partials
+    const int n_pblk = (n_pt + 255) / 256;
+    // few cameras: split each camera's observations so the grid still fills the chip
+    const int splits = std::max(1, std::min(16, (256 + n_cam - 1) / n_cam));
+    const size_t tb = sfm::align_up(sizeof(double) * NV * (size_t)n_obs, 256);
+    const size_t cb = sfm::align_up(sizeof(double) * (size_t)n_pblk, 256);
+    const size_t pb = sizeof(double) * NU * (size_t)n_cam * splits;
+    char* ws = (char*)sfm::workspace(ctx, tb + cb + pb + 1024);
+    if (!ws) return SFM_ERR_NOMEM;
+    double* terms = (double*)ws;
+    double* cost_blk = (double*)(ws + tb);
+    double* part = (double*)(ws + tb + cb);
+    // The observation kernel streams every input once (HBM-bound); afterwards the camera
+    // reduction (latency-bound gathers of points / uv, now L2-warm) and the point reduction are
+    // independent: they run concurrently on two streams.
+    if (n_obs > 0) {
+        hipLaunchKernelGGL(ba_obs_kernel, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs,
+                           cams, pp, pts, cam_idx, pt_idx, uv, loss_s, W, res, terms);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
+    hipStream_t aux = nullptr;
+    if (sfm::aux_stream(ctx, &aux) != SFM_OK) return SFM_ERR_HIP;
+    SFM_HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
+    SFM_HIP_CHECK(hipStreamWaitEvent(aux, ctx->ev_fork, 0));
+    hipLaunchKernelGGL(ba_camera_kernel, dim3(n_cam, splits), dim3(256), 0, aux, cams, pp, pts,
+                       pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ba_camera_kernel, dim3(n_cam), dim3(256), 0, st, cams, pp, pts, pt_idx, uv,
-                       cam_ptr, cam_obs, loss_s, U, gc);
+    hipLaunchKernelGGL(ba_camera_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, aux,
+                       n_cam, splits, part, U, gc);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ba_cost_kernel, dim3(1), dim3(256), 0, st, n_pt, cost_pt, cost);
+    SFM_HIP_CHECK(hipEventRecord(ctx->ev_join, aux));
+    hipLaunchKernelGGL(ba_point_kernel, dim3(n_pblk), dim3(256), 0, st, n_pt, pt_ptr, terms, V,
+                       gp, cost_blk);
+    SFM_HIP_CHECK(hipGetLastError());
+    SFM_HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_join, 0));
+    hipLaunchKernelGGL(ba_cost_kernel, dim3(1), dim3(256), 0, st, n_pblk, cost_blk, cost);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }

@@ -1,0 +1,16 @@
+#!/bin/bash
+# HBM traffic of the benchmark's kernels from rocprofv3 PMC, one counter per pass
+# (FETCH_SIZE and WRITE_SIZE cannot share a pass), then tools/traffic_summary.py.
+set -o pipefail
+TAG=${1:-traffic}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+RX="l2_prep_kernel|l2_match_kernel|l2_finalize_kernel|ransac_prep_kernel|ransac_hyp_kernel|ransac_final_kernel|graph_rows_kernel"
+i=0
+for c in FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $c GRBM_GUI_ACTIVE --kernel-include-regex "$RX" -d $OUT/p$i -o run --output-format csv -- $B > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python3 tools/traffic_summary.py $OUT > $OUT/traffic.json && cat $OUT/traffic.json
