@@ -59,7 +59,8 @@ def main():
     ap.add_argument("--n-img", type=int, default=0, help="override image count")
     ap.add_argument("--k", type=int, default=2048)
     ap.add_argument("--n-hyp", type=int, default=4096)
-    ap.add_argument("--cpu-pairs", type=int, default=96, help="CPU baseline sample (pairs)")
+    ap.add_argument("--cpu-pairs", type=int, default=384,
+                    help="CPU baseline sample (pairs; ~20 s of CPU work at cfg3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
