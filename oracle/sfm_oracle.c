@@ -209,9 +209,32 @@ void oracle_normalize(const float* xy, int M, float* nxy, float* cx, float* cy, 
 
 /*
  * Fundamental matrix from 8 normalised correspondences (Householder QR null space of the 8x9
- * epipolar system, then rank-2 by zeroing the smallest eigen-direction of F^T F, 5 Jacobi sweeps).
+ * epipolar system, then rank-2 by removing the smallest eigen-direction of F^T F, found by
+ * RANK2_ITERS power iterations on adj(F^T F)).
  * p1/p2: [8][2] normalised points.  Returns 0 on success, -1 if degenerate.  F row-major.
  */
+#define RANK2_ITERS 4
+
+/* adjugate of a symmetric 3x3 (itself symmetric) */
+static void adj3_sym(const float G[3][3], float A[3][3]) {
+    A[0][0] = fmaf(G[1][1], G[2][2], -(G[1][2] * G[1][2]));
+    A[1][1] = fmaf(G[0][0], G[2][2], -(G[0][2] * G[0][2]));
+    A[2][2] = fmaf(G[0][0], G[1][1], -(G[0][1] * G[0][1]));
+    A[0][1] = A[1][0] = fmaf(G[0][2], G[1][2], -(G[0][1] * G[2][2]));
+    A[0][2] = A[2][0] = fmaf(G[0][1], G[1][2], -(G[0][2] * G[1][1]));
+    A[1][2] = A[2][1] = fmaf(G[0][1], G[0][2], -(G[0][0] * G[1][2]));
+}
+
+/* v *= 2^-e with e the exponent of max|v_i| (exact; keeps the iteration away from under/overflow) */
+static void rescale3_pow2(float v[3]) {
+    const float m = fmaxf(fabsf(v[0]), fmaxf(fabsf(v[1]), fabsf(v[2])));
+    if (m > 0.0f && isfinite(m)) {
+        int e;
+        frexpf(m, &e);
+        for (int i = 0; i < 3; ++i) v[i] = ldexpf(v[i], -e);
+    }
+}
+
 int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
     float Mt[9][8]; /* Mt = A^T, column k = epipolar row of sample k */
     for (int k = 0; k < 8; ++k) {
@@ -249,53 +272,41 @@ int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
         float f = beta[k] * dot;
         for (int r = k; r < 9; ++r) z[r] = fmaf(-f, V[k][r], z[r]);
     }
-    /* rank 2: G = F^T F, Jacobi eigen-decomposition, remove the smallest eigen-direction */
-    float G[3][3], E[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    /* rank 2: smallest eigen-direction v of G = F^T F by power iteration on adj(G) (its dominant
+       eigenvector; ratio lambda_min/lambda_mid per step), exact power-of-two rescaling, then
+       F' = F - (F v) v^T */
+    float G[3][3];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
             float g = 0.0f;
             for (int r = 0; r < 3; ++r) g = fmaf(z[3 * r + i], z[3 * r + j], g);
             G[i][j] = g;
         }
-    static const int PQ[3][2] = {{0, 1}, {0, 2}, {1, 2}};
-    for (int sweep = 0; sweep < 5; ++sweep) {
-        for (int e = 0; e < 3; ++e) {
-            int p = PQ[e][0], q = PQ[e][1];
-            float gpq = G[p][q];
-            if (gpq == 0.0f) continue;
-            float theta = (G[q][q] - G[p][p]) / (2.0f * gpq);
-            float at = fabsf(theta);
-            float t = 1.0f / (at + sqrtf(fmaf(theta, theta, 1.0f)));
-            if (theta < 0.0f) t = -t;
-            float c = 1.0f / sqrtf(fmaf(t, t, 1.0f));
-            float s = t * c;
-            /* G <- J^T G J with J = rotation in (p,q): column then row update */
-            for (int r = 0; r < 3; ++r) {
-                float gp = G[r][p], gq = G[r][q];
-                G[r][p] = c * gp - s * gq;
-                G[r][q] = fmaf(s, gp, c * gq);
-            }
-            for (int r = 0; r < 3; ++r) {
-                float gp = G[p][r], gq = G[q][r];
-                G[p][r] = c * gp - s * gq;
-                G[q][r] = fmaf(s, gp, c * gq);
-            }
-            for (int r = 0; r < 3; ++r) {
-                float ep = E[r][p], eq = E[r][q];
-                E[r][p] = c * ep - s * eq;
-                E[r][q] = fmaf(s, ep, c * eq);
-            }
-        }
+    float A[3][3];
+    adj3_sym(G, A);
+    int kk = 0;
+    if (A[1][1] > A[kk][kk]) kk = 1;
+    if (A[2][2] > A[kk][kk]) kk = 2;
+    float v[3] = {A[0][kk], A[1][kk], A[2][kk]};
+    for (int it = 0; it < RANK2_ITERS; ++it) {
+        rescale3_pow2(v);
+        float w[3];
+        for (int i = 0; i < 3; ++i) w[i] = fmaf(A[i][2], v[2], fmaf(A[i][1], v[1], A[i][0] * v[0]));
+        v[0] = w[0]; v[1] = w[1]; v[2] = w[2];
     }
-    int kmin = 0;
-    if (G[1][1] < G[kmin][kmin]) kmin = 1;
-    if (G[2][2] < G[kmin][kmin]) kmin = 2;
-    float v0 = E[0][kmin], v1 = E[1][kmin], v2 = E[2][kmin];
-    for (int r = 0; r < 3; ++r) {
-        float w = fmaf(z[3 * r + 2], v2, fmaf(z[3 * r + 1], v1, z[3 * r] * v0));
-        F[3 * r + 0] = fmaf(-w, v0, z[3 * r + 0]);
-        F[3 * r + 1] = fmaf(-w, v1, z[3 * r + 1]);
-        F[3 * r + 2] = fmaf(-w, v2, z[3 * r + 2]);
+    rescale3_pow2(v);
+    const float n2 = fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0]));
+    if (n2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(n2);
+        const float v0 = v[0] * inv, v1 = v[1] * inv, v2 = v[2] * inv;
+        for (int r = 0; r < 3; ++r) {
+            float w = fmaf(z[3 * r + 2], v2, fmaf(z[3 * r + 1], v1, z[3 * r] * v0));
+            F[3 * r + 0] = fmaf(-w, v0, z[3 * r + 0]);
+            F[3 * r + 1] = fmaf(-w, v1, z[3 * r + 1]);
+            F[3 * r + 2] = fmaf(-w, v2, z[3 * r + 2]);
+        }
+    } else {
+        for (int i = 0; i < 9; ++i) F[i] = z[i];
     }
     return 0;
 }

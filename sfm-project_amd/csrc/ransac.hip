@@ -8,7 +8,7 @@
 //                 (scoring, X = k * x_normalised, k = 1/(s*sqrt(thr))), plus (cx,cy,s) per side.
 //   ransac_hyp    one LANE per hypothesis (256 per block): counter-based Philox sample of 8 distinct
 //                 matches (Floyd), Householder-QR null space of the 8x9 epipolar system, rank-2
-//                 projection (5 Jacobi sweeps on F^T F), then a sweep over all M matches counting
+//                 projection (power iteration on adj(F^T F)), then a sweep over all M matches counting
 //                 Sampson inliers (17 flops + compare per match).  The match coordinates are
 //                 wave-uniform, so they are read with scalar loads into SGPRs and fed to packed
 //                 FMAs as SGPR-pair operands.  Exact pruning: every 64 matches a wave reads
@@ -26,6 +26,8 @@
 #include "sfm_internal.h"
 
 namespace {
+
+constexpr int RANK2_ITERS = 4;  // oracle_fit_f8
 
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1, uint32_t out[4]) {
@@ -105,7 +107,8 @@ __device__ __forceinline__ bool fit_f8(const float4 s[8], float F[9]) {
 #pragma unroll
         for (int r = k + 1; r < 9; ++r) z[r] = fmaf(-f, Mt[r][k], z[r]);
     }
-    float G[3][3], E[3][3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
+    // rank 2 (oracle_fit_f8): smallest eigen-direction of G = F^T F by power iteration on adj(G)
+    float G[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -115,52 +118,49 @@ __device__ __forceinline__ bool fit_f8(const float4 s[8], float F[9]) {
             for (int r = 0; r < 3; ++r) g = fmaf(z[3 * r + i], z[3 * r + j], g);
             G[i][j] = g;
         }
+    float A[3][3];
+    A[0][0] = fmaf(G[1][1], G[2][2], -(G[1][2] * G[1][2]));
+    A[1][1] = fmaf(G[0][0], G[2][2], -(G[0][2] * G[0][2]));
+    A[2][2] = fmaf(G[0][0], G[1][1], -(G[0][1] * G[0][1]));
+    A[0][1] = A[1][0] = fmaf(G[0][2], G[1][2], -(G[0][1] * G[2][2]));
+    A[0][2] = A[2][0] = fmaf(G[0][1], G[1][2], -(G[0][2] * G[1][1]));
+    A[1][2] = A[2][1] = fmaf(G[0][1], G[0][2], -(G[0][0] * G[1][2]));
+    int kk = 0;
+    float amax = A[0][0];
+    if (A[1][1] > amax) { kk = 1; amax = A[1][1]; }
+    if (A[2][2] > amax) kk = 2;
+    float v0 = kk == 0 ? A[0][0] : (kk == 1 ? A[0][1] : A[0][2]);
+    float v1 = kk == 0 ? A[1][0] : (kk == 1 ? A[1][1] : A[1][2]);
+    float v2 = kk == 0 ? A[2][0] : (kk == 1 ? A[2][1] : A[2][2]);
 #pragma unroll
-    for (int sweep = 0; sweep < 5; ++sweep) {
-#pragma unroll
-        for (int e = 0; e < 3; ++e) {
-            const int p = (e == 2) ? 1 : 0, q = (e == 0) ? 1 : 2;
-            const float gpq = G[p][q];
-            const bool rot = (gpq != 0.0f);
-            const float theta = (G[q][q] - G[p][p]) / (2.0f * gpq);
-            const float at = fabsf(theta);
-            float t = 1.0f / (at + sqrtf(fmaf(theta, theta, 1.0f)));
-            if (theta < 0.0f) t = -t;
-            const float c = 1.0f / sqrtf(fmaf(t, t, 1.0f));
-            const float sn = t * c;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const float gp = G[r][p], gq = G[r][q];
-                G[r][p] = rot ? c * gp - sn * gq : gp;
-                G[r][q] = rot ? fmaf(sn, gp, c * gq) : gq;
-            }
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const float gp = G[p][r], gq = G[q][r];
-                G[p][r] = rot ? c * gp - sn * gq : gp;
-                G[q][r] = rot ? fmaf(sn, gp, c * gq) : gq;
-            }
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const float ep = E[r][p], eq = E[r][q];
-                E[r][p] = rot ? c * ep - sn * eq : ep;
-                E[r][q] = rot ? fmaf(sn, ep, c * eq) : eq;
-            }
+    for (int it = 0; it <= RANK2_ITERS; ++it) {
+        // exact power-of-two rescale by the exponent of max|v| (oracle rescale3_pow2)
+        const float m = fmaxf(fabsf(v0), fmaxf(fabsf(v1), fabsf(v2)));
+        if (m > 0.0f && isfinite(m)) {
+            int e;
+            frexpf(m, &e);
+            v0 = ldexpf(v0, -e); v1 = ldexpf(v1, -e); v2 = ldexpf(v2, -e);
         }
+        if (it == RANK2_ITERS) break;
+        const float w0 = fmaf(A[0][2], v2, fmaf(A[0][1], v1, A[0][0] * v0));
+        const float w1 = fmaf(A[1][2], v2, fmaf(A[1][1], v1, A[1][0] * v0));
+        const float w2 = fmaf(A[2][2], v2, fmaf(A[2][1], v1, A[2][0] * v0));
+        v0 = w0; v1 = w1; v2 = w2;
     }
-    int kmin = 0;
-    float gmin = G[0][0];
-    if (G[1][1] < gmin) { kmin = 1; gmin = G[1][1]; }
-    if (G[2][2] < gmin) { kmin = 2; }
-    const float v0 = kmin == 0 ? E[0][0] : (kmin == 1 ? E[0][1] : E[0][2]);
-    const float v1 = kmin == 0 ? E[1][0] : (kmin == 1 ? E[1][1] : E[1][2]);
-    const float v2 = kmin == 0 ? E[2][0] : (kmin == 1 ? E[2][1] : E[2][2]);
+    const float n2 = fmaf(v2, v2, fmaf(v1, v1, v0 * v0));
+    if (n2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(n2);
+        v0 = v0 * inv; v1 = v1 * inv; v2 = v2 * inv;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const float w = fmaf(z[3 * r + 2], v2, fmaf(z[3 * r + 1], v1, z[3 * r] * v0));
-        F[3 * r + 0] = fmaf(-w, v0, z[3 * r + 0]);
-        F[3 * r + 1] = fmaf(-w, v1, z[3 * r + 1]);
-        F[3 * r + 2] = fmaf(-w, v2, z[3 * r + 2]);
+        for (int r = 0; r < 3; ++r) {
+            const float w = fmaf(z[3 * r + 2], v2, fmaf(z[3 * r + 1], v1, z[3 * r] * v0));
+            F[3 * r + 0] = fmaf(-w, v0, z[3 * r + 0]);
+            F[3 * r + 1] = fmaf(-w, v1, z[3 * r + 1]);
+            F[3 * r + 2] = fmaf(-w, v2, z[3 * r + 2]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) F[i] = z[i];
     }
     return ok;
 }
@@ -360,6 +360,138 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
     if ((tid & 63) == 0) atomicMax(&best[p], key);  // per wave: later waves prune sooner
 }
 
+// ---- ordered variant: fit + preview, per-pair ordering, ordered scoring --------------------------
+//
+// Exact pruning only removes a wave once every lane is provably beaten, so it pays most when the
+// strong hypotheses are scored first and the weak ones end up together in the same waves.
+//   ransac_fit_kernel    lane per hypothesis: sample + fit, Sampson count over the first PV matches
+//                        (the "preview", same op sequence), G to a [pair][9][H] table.
+//   ransac_order_kernel  block per pair: counting sort of the hypotheses by preview count,
+//                        descending (order within a bucket is irrelevant: the winner key carries h).
+//   ransac_score_kernel  rank r of pair p scores hypothesis order[p][r] from match PV on, starting
+//                        from its preview count, with the same exact pruning; grid x = pair so the
+//                        best-previewed block of every pair runs first and publishes a strong bound.
+constexpr int PV = 64;  // preview matches (multiple of CH)
+
+// counts inliers of G over matches [m, mend) into cnt; with PRUNE checks the published bound every
+// PRUNE_EVERY matches and returns false (wave-uniform) when no lane can still win.
+template <bool PRUNE>
+__device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[9], int m, int mend,
+                                              int M, int& cnt,
+                                              const unsigned long long* __restrict__ bestp) {
+    const int mc = m + ((mend - m) & ~(CH - 1));
+#pragma unroll 1
+    for (; m < mc; m += CH) {
+        float x1[CH], y1[CH], x2[CH], y2[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            x1[j] = S[m + j];
+            y1[j] = S[kp + m + j];
+            x2[j] = S[2 * kp + m + j];
+            y2[j] = S[3 * kp + m + j];
+        }
+#pragma unroll
+        for (int j = 0; j < CH; j += 2)
+            cnt += sampson_inlier2(G, f2{x1[j], x1[j + 1]}, f2{y1[j], y1[j + 1]},
+                                   f2{x2[j], x2[j + 1]}, f2{y2[j], y2[j + 1]});
+        if (PRUNE && ((m + CH) % PRUNE_EVERY) == 0) {
+            const unsigned long long bk =
+                __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int bound = (int)(bk >> 32) - 1;
+            if (__all(cnt + (M - m - CH) < bound)) return false;
+        }
+    }
+#pragma unroll 1
+    for (; m < mend; ++m) cnt += sampson_inlier(G, S[m], S[kp + m], S[2 * kp + m], S[3 * kp + m]);
+    return true;
+}
+
+__global__ __launch_bounds__(256) void ransac_fit_kernel(
+    int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
+    const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
+    int n_hyp, float* __restrict__ hypG, int32_t* __restrict__ prev) {
+    const int p = blockIdx.x;
+    const int M = match_count[p];
+    if (M < 8) return;  // block-uniform
+    const int kp = plane_len(k_max);
+    const float* pl = planes + (size_t)p * 8 * kp;
+    const cfloat_p S = (cfloat_p)(pl + 4 * kp);
+    const uint32_t pa = (uint32_t)pairs[2 * p], pb = (uint32_t)pairs[2 * p + 1];
+    const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
+    float k1, k2;
+    sampson_scales(s1, s2, thr, k1, k2);
+    const uint32_t h = blockIdx.y * 256 + threadIdx.x;
+    int idx[8];
+    sample8(seed, pa, pb, h, M, idx);
+    float4 smp[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        smp[k] = make_float4(pl[idx[k]], pl[kp + idx[k]], pl[2 * kp + idx[k]],
+                             pl[3 * kp + idx[k]]);
+    float F[9], G[9];
+    const bool ok = fit_f8(smp, F);
+    sampson_prep(F, k1, k2, G);
+    int cnt = 0;
+    score_matches<false>(S, kp, G, 0, min(PV, M), M, cnt, nullptr);
+    float* gt = hypG + (size_t)p * 9 * n_hyp + h;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) gt[(size_t)i * n_hyp] = G[i];
+    prev[(size_t)p * n_hyp + h] = ok ? cnt : -1;
+}
+
+__global__ __launch_bounds__(1024) void ransac_order_kernel(int n_hyp,
+                                                            const int32_t* __restrict__ match_count,
+                                                            const int32_t* __restrict__ prev,
+                                                            uint16_t* __restrict__ order) {
+    __shared__ int hist[PV + 2];  // bucket = preview count + 1 (degenerate -1 -> 0)
+    const int p = blockIdx.x, tid = threadIdx.x;
+    if (match_count[p] < 8) return;
+    const int32_t* pv = prev + (size_t)p * n_hyp;
+    if (tid < PV + 2) hist[tid] = 0;
+    __syncthreads();
+    for (int h = tid; h < n_hyp; h += 1024) atomicAdd(&hist[pv[h] + 1], 1);
+    __syncthreads();
+    if (tid == 0) {  // descending exclusive offsets
+        int off = 0;
+        for (int b = PV + 1; b >= 0; --b) {
+            const int c = hist[b];
+            hist[b] = off;
+            off += c;
+        }
+    }
+    __syncthreads();
+    for (int h = tid; h < n_hyp; h += 1024)
+        order[(size_t)p * n_hyp + atomicAdd(&hist[pv[h] + 1], 1)] = (uint16_t)h;
+}
+
+template <bool PRUNE>
+__global__ __launch_bounds__(256) void ransac_score_kernel(
+    int k_max, const int32_t* __restrict__ match_count, const float* __restrict__ planes,
+    int n_hyp, const float* __restrict__ hypG, const int32_t* __restrict__ prev,
+    const uint16_t* __restrict__ order, unsigned long long* __restrict__ best) {
+    const int p = blockIdx.x;
+    const int M = match_count[p];
+    if (M < 8) return;  // block-uniform
+    const int kp = plane_len(k_max);
+    const cfloat_p S = (cfloat_p)(planes + (size_t)p * 8 * kp + 4 * kp);
+    const uint32_t h = order[(size_t)p * n_hyp + blockIdx.y * 256 + threadIdx.x];
+    const float* gt = hypG + (size_t)p * 9 * n_hyp + h;
+    float G[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) G[i] = gt[(size_t)i * n_hyp];
+    const int pc = prev[(size_t)p * n_hyp + h];
+    int cnt = max(pc, 0);
+    if (M > PV && !score_matches<PRUNE>(S, kp, G, PV, M, M, cnt, best + p)) return;
+    if (pc < 0) cnt = -1;
+    unsigned long long key = ((unsigned long long)(unsigned)(cnt + 1) << 32) | (0xFFFFFFFFu - h);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(key, off, 64);
+        key = o > key ? o : key;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(&best[p], key);
+}
+
 __global__ __launch_bounds__(256) void ransac_final_kernel(
     int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
     const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
@@ -412,10 +544,13 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
 
 }  // namespace
 
-// SFM_RANSAC_NOPRUNE=1 disables the exact pruning (same results; for measuring its effect).
-static bool ransac_prune() {
-    const char* e = getenv("SFM_RANSAC_NOPRUNE");
-    return !(e && atoi(e) != 0);
+// SFM_RANSAC_MODE (same results in every mode; for measuring the schedules):
+//   0 ordered (fit + preview, per-pair ordering, ordered pruned scoring) — default
+//   1 single pass with pruning, 2 single pass without pruning
+static int ransac_mode() {
+    const char* e = getenv("SFM_RANSAC_MODE");
+    const int v = e ? atoi(e) : 0;
+    return (v < 0 || v > 2) ? 0 : v;
 }
 
 extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
@@ -438,23 +573,42 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int kp = plane_len(std::max(k_max, 1));
-    const size_t plb = (size_t)n_pairs * 8 * kp * sizeof(float);
-    const size_t bb = (size_t)n_pairs * sizeof(unsigned long long);
-    char* ws = (char*)sfm::workspace(ctx, plb + bb + 1024);
+    const int H = prm->n_hyp;
+    const int mode = ransac_mode();
+    SFM_REQUIRE(mode != 0 || H <= 65536, "sfm_ransac_f_batch: n_hyp > 65536");
+    const size_t plb = sfm::align_up((size_t)n_pairs * 8 * kp * sizeof(float), 256);
+    const size_t bb = sfm::align_up((size_t)n_pairs * sizeof(unsigned long long), 256);
+    const size_t gb = mode == 0 ? sfm::align_up((size_t)n_pairs * 9 * H * sizeof(float), 256) : 0;
+    const size_t vb = mode == 0 ? sfm::align_up((size_t)n_pairs * H * sizeof(int32_t), 256) : 0;
+    const size_t ob = mode == 0 ? sfm::align_up((size_t)n_pairs * H * sizeof(uint16_t), 256) : 0;
+    char* ws = (char*)sfm::workspace(ctx, plb + bb + gb + vb + ob + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     float* planes = (float*)ws;
     unsigned long long* best = (unsigned long long*)(ws + plb);
+    float* hypG = (float*)(ws + plb + bb);
+    int32_t* prev = (int32_t*)(ws + plb + bb + gb);
+    uint16_t* order = (uint16_t*)(ws + plb + bb + gb + vb);
     SFM_HIP_CHECK(hipMemsetAsync(best, 0, bb, st));
     hipLaunchKernelGGL(ransac_prep_kernel, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
                        match_count, matches, prm->thr, planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
-    const dim3 grid(n_pairs, prm->n_hyp / 256);
-    if (ransac_prune())
+    const dim3 grid(n_pairs, H / 256);
+    if (mode == 0) {
+        hipLaunchKernelGGL(ransac_fit_kernel, grid, dim3(256), 0, st, k_max, pairs, match_count,
+                           planes, out_norm, prm->seed, prm->thr, H, hypG, prev);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(1024), 0, st, H, match_count,
+                           prev, order);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(ransac_score_kernel<true>, grid, dim3(256), 0, st, k_max, match_count,
+                           planes, H, hypG, prev, order, best);
+    } else if (mode == 1) {
         hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
                            match_count, planes, out_norm, prm->seed, prm->thr, best);
-    else
+    } else {
         hipLaunchKernelGGL(ransac_hyp_kernel<false>, grid, dim3(256), 0, st, k_max, pairs,
                            match_count, planes, out_norm, prm->seed, prm->thr, best);
+    }
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(ransac_final_kernel, dim3(n_pairs), dim3(256), 0, st, k_max, pairs,
                        match_count, planes, out_norm, prm->seed, prm->thr, best, out_inl_count,

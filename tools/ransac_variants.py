@@ -1,5 +1,6 @@
-"""Times K2 RANSAC with and without the exact pruning (SFM_RANSAC_NOPRUNE) on the cfg3 workload
-and checks each against the CPU oracle on a sample of pairs.  Usage: python tools/ransac_variants.py"""
+"""Times the K2 RANSAC schedules (SFM_RANSAC_MODE 0 ordered, 1 single-pass pruned, 2 unpruned) on
+the cfg3 workload and checks each against the CPU oracle on a sample of pairs.
+Usage: python tools/ransac_variants.py"""
 import os
 import sys
 import time
@@ -32,8 +33,8 @@ def main():
         M = cnt_np[p]
         ref[p] = O.ransac_f(s["kps"][a][mt_np[p, :M, 0]], s["kps"][b][mt_np[p, :M, 1]], H=4096,
                             seed=42, pa=int(a), pb=int(b))
-    for v in (0, 1):
-        os.environ["SFM_RANSAC_NOPRUNE"] = str(v)
+    for v in (0, 1, 2):
+        os.environ["SFM_RANSAC_MODE"] = str(v)
         for _ in range(2):
             out = ctx.ransac_batch(kps, pr, cnt, mt, n_hyp=4096)
         torch.cuda.synchronize()
@@ -50,7 +51,7 @@ def main():
         mask = out["mask"].cpu().numpy()
         ok = all(ic[p] == ref[p]["count"] and bh[p] == ref[p]["best_h"]
                  and (mask[p, :cnt_np[p]] == ref[p]["mask"]).all() for p in sample)
-        print(f"noprune={v}: {ms:.3f} ms/launch  parity({len(sample)} pairs)={ok}  "
+        print(f"mode={v}: {ms:.3f} ms/launch  parity({len(sample)} pairs)={ok}  "
               f"sum_inl={int(np.maximum(ic, 0).sum())}", flush=True)
 
 
