@@ -94,3 +94,55 @@ def test_ransac_shard_invariance(ctx):
     for k in range(6):
         M = cnt2[k]
         np.testing.assert_array_equal(full["mask"][5 + k, :M], part["mask"][k, :M])
+
+
+def _ransac_direct(ctx, kps, count, match, pairs, H):
+    import torch
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    out = ctx.ransac_batch(T(kps), T(pairs), T(count), T(match), n_hyp=H)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("M", [8, 9, 20, 63, 64, 65, 79, 80, 127, 130])
+def test_ransac_preview_boundaries(ctx, M):
+    """Match counts around the 64-match preview and the 16-match scoring chunks of the ordered
+    schedule (fit + preview / ordered scoring), on a real two-view geometry with outliers."""
+    s = synth.make_scene(2, 512, seed=30 + M)
+    q, t, _ = O.match(s["desc"][0], s["desc"][1], 0, 1, (4, 5))
+    assert len(q) >= M
+    k_max = 512
+    match = np.zeros((1, k_max, 2), np.int32)
+    match[0, :M, 0] = q[:M]
+    match[0, :M, 1] = t[:M]
+    out = _ransac_direct(ctx, s["kps"], np.array([M], np.int32), match,
+                         np.array([[0, 1]], np.int32), 512)
+    r = O.ransac_f(s["kps"][0][q[:M]], s["kps"][1][t[:M]], H=512, seed=42, pa=0, pb=1)
+    assert out["inl_count"][0] == r["count"] and out["best_h"][0] == r["best_h"]
+    np.testing.assert_array_equal(out["mask"][0, :M], r["mask"])
+    np.testing.assert_array_equal(out["F"][0].view(np.uint32), r["F"].view(np.uint32))
+
+
+def test_ransac_schedules_agree(ctx):
+    """The three K2 schedules (ordered, single-pass pruned, unpruned; SFM_RANSAC_MODE) differ only
+    in which work is skipped: every output must be identical."""
+    import os
+    s = synth.make_scene(8, 1024, seed=12)
+    pairs = synth.unordered_pairs(8)
+    outs = []
+    old = os.environ.get("SFM_RANSAC_MODE")
+    try:
+        for mode in ("0", "1", "2"):
+            os.environ["SFM_RANSAC_MODE"] = mode
+            outs.append(_run(ctx, s, pairs, H=1024))
+    finally:
+        if old is None:
+            os.environ.pop("SFM_RANSAC_MODE", None)
+        else:
+            os.environ["SFM_RANSAC_MODE"] = old
+    cnt = outs[0][0]
+    for _, _, o in outs[1:]:
+        for k in ("inl_count", "best_h", "F", "norm"):
+            np.testing.assert_array_equal(o[k], outs[0][2][k])
+        for p in range(len(pairs)):
+            np.testing.assert_array_equal(o["mask"][p, :cnt[p]], outs[0][2]["mask"][p, :cnt[p]])
