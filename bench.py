@@ -31,7 +31,7 @@ sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracl
 PEAK_I8_TOPS = 2048 * 4 * 256 * 2.4e9 / 1e12        # 5033 TOP/s
 PEAK_F32_VALU_TFLOPS = 157.3
 RANSAC_FLOP_PER_EVAL = 33      # Sampson test: 16 fma + 1 mul (ransac.hip sampson_inlier)
-RANSAC_FLOP_PER_FIT = 1900     # fit_f8: Householder QR 8x9 + Q e9 + Jacobi 3x3 + rank-2
+RANSAC_FLOP_PER_FIT = 1400     # sample + fit_f8: Householder QR 8x9 + Q e9 + adj(F^T F) power iteration
 
 
 def pmc_traffic(kernel, n_img, k, world):

@@ -3,13 +3,13 @@
 Inputs resident on the device; times sfm_ba_jtj with HIP events on torch's stream, reports the
 achieved algorithmic HBM bandwidth against the 8 TB/s peak, and checks U/V/W/g/residuals against
 the CPU oracle (fp64; U, g_c are reassociated sums: rel 1e-9; residuals 1e-4 px per north_star).
-Usage: python tools/ba_bench.py [n_cam n_pt obs_per_pt]"""
+Usage: python tests/perf/ba_bench.py [n_cam n_pt obs_per_pt]"""
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracle")]
 
 import numpy as np

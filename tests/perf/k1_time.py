@@ -1,9 +1,9 @@
 """Times K1 (sfm_match_batch, L2 mutual + ratio 4/5) on the cfg3 workload with HIP events and
-checks a sample of pairs bit-exactly against the CPU oracle.  Usage: python tools/k1_time.py"""
+checks a sample of pairs bit-exactly against the CPU oracle.  Usage: python tests/perf/k1_time.py"""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracle")]
 
 import numpy as np

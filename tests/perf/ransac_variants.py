@@ -1,11 +1,11 @@
 """Times the K2 RANSAC schedules (SFM_RANSAC_MODE 0 ordered, 1 single-pass pruned, 2 unpruned) on
 the cfg3 workload and checks each against the CPU oracle on a sample of pairs.
-Usage: python tools/ransac_variants.py"""
+Usage: python tests/perf/ransac_variants.py"""
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracle")]
 
 import numpy as np
