@@ -201,7 +201,7 @@ def cpu_baseline(scene, pairs, shard, pair_base, count, rs, n_sample, n_hyp):
     except Exception:
         model = "unknown"
     return {"value": tot / dt, "unit": "verified matches/s", "cores": threads, "kind": "port",
-            "sample": (f"{len(sample)} of {len(shard)} pairs (every {stride}th), full K1+K2 per "
+            "sample": (f"{len(sample)} of {len(shard)} pairs (stride {stride}), full K1+K2 per "
                        f"pair, OpenMP over pairs, {dt:.1f} s wall on {model}"),
             "per_pair_ms": dt * 1e3 * threads / len(sample),
             "inlier_parity_with_gpu": parity}
