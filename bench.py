@@ -5,7 +5,8 @@ Workload (BASELINE.json configs[2]): 50 synthetic images x 
 128-D u8 descriptors, all 1225 unordered pairs; per pair K1 (MFMA L2 match, mutual cross check +
 Lowe ratio 0.8) then K2 (8-point RANSAC, 4096 hypotheses, seed 42, Sampson 1 px^2, min 15 inliers).
 A step = one pass of match + verify over the pair list with descriptors/keypoints already resident
-in HBM, plus (N > 1) the RCCL all-gather of the verified match graph.
+in HBM, plus, for N > 1, the graph exchange: per-pair counts + 4-byte packed rows, RCCL
+all-gather, expanded to (pair, queryIdx, trainIdx) rows on every rank.
 
 Scaling is weak: at N GPUs the scene has n_img images with n_img(n_img-1)/2 ~= 1225*N pairs, cut
 into N contiguous cost-balanced shards (one process per GPU, no collective on the data path).
@@ -83,7 +84,8 @@ def main():
     t0 = time.time()
     scene = synth.make_scene(n_img, args.k, seed=0)
     pairs = synth.unordered_pairs(n_img)
-    pair_base, pair_end = match_graph.shard_range(pairs, rank, world, scene["n_kp"])
+    ranges = [match_graph.shard_range(pairs, r, world, scene["n_kp"]) for r in range(world)]
+    pair_base, pair_end = ranges[rank]
     shard = pairs[pair_base:pair_end]
     log(f"[rank {rank}] scene {n_img} imgs x {args.k} kps, {len(pairs)} pairs, shard "
         f"{len(shard)} (gen {time.time() - t0:.1f}s)")
@@ -102,8 +104,11 @@ def main():
         rs = gb.verify(pairs_t, count, match)
         if ev is not None:
             ev[2].record()
-        rows = gb.graph_rows(pair_base, count, match, rs)
-        graph = match_graph.all_gather_rows(rows)
+        if world == 1:  # the local rows are the whole graph: no exchange
+            return gb.graph_rows(pair_base, count, match, rs), count, rs
+        rows, offs = gb.graph_rows(pair_base, count, match, rs, return_offsets=True)
+        counts, packed = match_graph.pack_rows(rows, offs)
+        graph = match_graph.all_gather_graph(counts, packed, ranges)
         return graph, count, rs
 
     for _ in range(args.warmup):

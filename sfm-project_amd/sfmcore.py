@@ -174,10 +174,12 @@ class Context:
         return out
 
     # ---- verified match graph --------------------------------------------------------------
-    def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15):
+    def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15,
+                   return_offsets=False):
         """Rows [n,3] i32 (pair_base + pair, queryIdx, trainIdx) of the inliers of every verified
         pair (inl_count >= min_inliers), pair-major, ascending match index.  One device->host
-        read of the row total sizes the output."""
+        read of the row total sizes the output.  return_offsets: also the [P+1] i64 row offsets
+        per pair."""
         torch = self.torch
         P, k_max = mask.shape
         dev = mask.device
@@ -191,7 +193,7 @@ class Context:
             _check(self.lib.sfm_graph_rows(self.handle, P, k_max, int(pair_base), _ptr(count),
                                            _ptr(match), _ptr(mask), _ptr(inl_count),
                                            int(min_inliers), _ptr(offs), _ptr(rows)))
-        return rows
+        return (rows, offs) if return_offsets else rows
 
     # ---- bundle adjustment -----------------------------------------------------------------
     def ba_jtj(self, cams, pp, pts, cam_idx, pt_idx, uv, pt_ptr, cam_ptr, cam_obs, loss_s=0.0):

@@ -89,3 +89,45 @@ def test_all_gather_single_process_is_identity():
     import torch
     rows = torch.arange(12, dtype=torch.int32).reshape(4, 3)
     assert match_graph.all_gather_rows(rows) is rows
+
+
+def _worker_packed(rank, world, port, out_path):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scene = _scene()
+    pairs = synth.unordered_pairs(N_IMG)
+    ranges = [match_graph.shard_range(pairs, r, world, scene["n_kp"]) for r in range(world)]
+    lo, hi = ranges[rank]
+    rows = torch.from_numpy(_rows_for(scene, pairs[lo:hi], lo))
+    counts = torch.bincount(rows[:, 0].long() - lo, minlength=hi - lo)
+    offs = torch.zeros(hi - lo + 1, dtype=torch.int64)
+    offs[1:] = torch.cumsum(counts, 0)
+    c, pk = match_graph.pack_rows(rows, offs)
+    graph = match_graph.all_gather_graph(c, pk, ranges)
+    if rank == 0:
+        np.save(out_path, graph.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_gather_packed_graph_gloo_world2(tmp_path):
+    """Packed exchange (per-pair counts + 4 B rows) expands to exactly the single-process rows."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "graph.npy")
+    mp.spawn(_worker_packed, args=(2, _free_port(), out), nprocs=2, join=True)
+    scene = _scene()
+    full = _rows_for(scene, synth.unordered_pairs(N_IMG), 0)
+    np.testing.assert_array_equal(np.load(out), full)
+
+
+def test_packed_graph_single_process_roundtrip():
+    import torch
+    rows = torch.tensor([[3, 5, 7], [3, 4095, 0], [5, 1, 2]], dtype=torch.int32)
+    offs = torch.tensor([0, 0, 2, 2, 3], dtype=torch.int64)  # pairs 2..5 (base 2)
+    c, pk = match_graph.pack_rows(rows, offs)
+    assert c.tolist() == [0, 2, 0, 1]
+    g = match_graph.all_gather_graph(c, pk, [(2, 6)])
+    np.testing.assert_array_equal(g.numpy(), rows.numpy())

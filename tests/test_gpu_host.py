@@ -147,3 +147,18 @@ def test_graph_rows_compaction(ctx, P, K):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     rows = ctx.graph_rows(7, T(count), T(match), T(inl), T(mask), 15).cpu().numpy()
     np.testing.assert_array_equal(rows, np.array(want, np.int32).reshape(-1, 3))
+
+
+def test_graph_packed_roundtrip_on_device():
+    """Device path of the bench step: graph_rows + offsets -> pack_rows -> all_gather_graph
+    (world 1) reproduces the rows."""
+    import torch
+    s = synth.make_scene(5, 1024, seed=18)
+    pairs = synth.unordered_pairs(5)
+    gb = match_graph.GraphBuilder(s["desc"], s["kps"], s["n_kp"], ratio=(4, 5), n_hyp=512)
+    count, match, dist, rs = gb.run(torch.from_numpy(pairs).cuda())
+    rows, offs = gb.graph_rows(0, count, match, rs, return_offsets=True)
+    c, pk = match_graph.pack_rows(rows, offs)
+    g = match_graph.all_gather_graph(c, pk, [(0, len(pairs))])
+    np.testing.assert_array_equal(g.cpu().numpy(), rows.cpu().numpy())
+    assert int(offs[-1]) == rows.shape[0] > 0
