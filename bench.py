@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--cpu-pairs", type=int, default=384,
                     help="CPU baseline sample (pairs; ~20 s of CPU work at cfg3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="rehearsal only: 'gloo' lets N ranks share one GPU (RCCL cannot)")
+    ap.add_argument("--device", type=int, default=-1, help="rehearsal only: force this GPU")
     args = ap.parse_args()
 
     import numpy as np
@@ -75,9 +78,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.device >= 0:
+        local = args.device
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     n_img = args.n_img or (50 if world == 1 else
                            int(round((1 + math.sqrt(1 + 8 * 1225 * world)) / 2)))
@@ -125,7 +133,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64,
+                      device="cuda" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())

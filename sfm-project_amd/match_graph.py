@@ -181,9 +181,10 @@ def _gather(t, world, group):
         out = torch.empty((world, t.shape[0]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out.view(-1), t, group=group)
         return out
-    bufs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(bufs, t, group=group)
-    return torch.stack(bufs)
+    tc = t.cpu()  # gloo (CPU tests, same-GPU rehearsal): host buffers
+    bufs = [torch.empty_like(tc) for _ in range(world)]
+    dist.all_gather(bufs, tc, group=group)
+    return torch.stack(bufs).to(t.device)
 
 
 def rows_to_pairs(rows: np.ndarray, pairs: np.ndarray):
