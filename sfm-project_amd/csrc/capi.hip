@@ -123,6 +123,12 @@ int sfm_match_batch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int3
     if (prm->metric == SFM_METRIC_HAMMING) {
         SFM_REQUIRE(dim == 32, "sfm_match_batch: Hamming metric needs dim == 32 (256-bit ORB)");
         SFM_REQUIRE(k_max <= 8192, "sfm_match_batch: k_max > 8192 not supported");
+        // MFMA path (bits as 0/1 bytes, d = |a| + |b| - 2 a.b) up to 4096 descriptors; the VALU
+        // popcount kernel above that (or when SFM_HAMMING_VALU=1, for A/B measurements)
+        const char* e = getenv("SFM_HAMMING_VALU");
+        if (k_max <= 4096 && !(e && atoi(e) != 0))
+            return sfm_match_hamming_mfma_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs,
+                                                 prm, out_count, out_match, out_dist);
         return sfm_match_hamming_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
                                         out_count, out_match, out_dist);
     }

@@ -1,7 +1,11 @@
-// All-pairs L2 descriptor matching on MFMA (K1, SURVEY.md §8a a1/a3').
+// All-pairs descriptor matching on MFMA (K1, SURVEY.md §8a a1/a3').
 //
-// Replaces the arithmetic behind cv2.BFMatcher(...).match (code/feature_matching.py:48-50) for
-// 128-byte SIFT-like descriptors, fused with the Lowe ratio test and the cross check.
+// Replaces the arithmetic behind cv2.BFMatcher(...).match (code/feature_matching.py:48-50),
+// fused with the Lowe ratio test and the cross check, for both descriptor kinds:
+//   L2 (128-byte SIFT-like): features x' = x ^ 0x80 (D = 128), d^2 = |x'|^2 + |y'|^2 - 2 x'.y';
+//   Hamming (256-bit ORB, the reference's own NORM_HAMMING matcher): the bits as 0/1 bytes
+//   (D = 256), d = popc(x) + popc(y) - 2 x.y — the same contraction and the same epilogue.
+// (The L2 description below; the Hamming instantiation only changes D and the query tiles/wave.)
 //
 // Exact integer formulation.  With x' = x - 128 (u8 -> i8, a free XOR 0x80):
 //     d^2(i,j) = |x'_i|^2 + |y'_j|^2 - 2 x'_i.y'_j
@@ -37,12 +41,25 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int QT = 4;                 // query tiles (32 each) per wave
 constexpr int WAVES = 8;              // waves per workgroup
-constexpr int QB = WAVES * QT * 32;   // queries per workgroup
-constexpr int CHUNK = 256;            // trains per LDS stage (8 tiles)
-constexpr int KALIGN = 256;           // tables are padded to a multiple of CHUNK
+constexpr int STAGE_BYTES = 32768;    // train bytes per LDS stage (CHUNK = STAGE_BYTES / D rows)
+constexpr int KALIGN = 256;           // tables are padded to a multiple of 256 (row-key index field)
 constexpr int KMAX_L2 = 4096;         // largest k_max handled by this kernel (LDS column state)
+
+// Feature geometry per metric: D i8 features per row; QT query tiles (32 each) per wave.
+//   L2:      D = 128 (x ^ 0x80 = x - 128),              QT = 4 -> 1024 queries per workgroup
+//   Hamming: D = 256 (the 256 bits as 0/1 bytes),       QT = 2 ->  512 queries per workgroup
+// Both use d = n_i + n_j - 2 dot (n = |x'|^2 resp. popcount): one kernel, exact int32.
+template <int D> struct Geo {
+    static constexpr int QT = D == 128 ? 4 : 2;
+    static constexpr int QB = WAVES * QT * 32;
+    static constexpr int CHUNK = STAGE_BYTES / D;   // 256 resp. 128 trains per stage
+    static constexpr int NK = D / 32;               // MFMA k-steps per tile
+    static constexpr int SLOTS = D / 16;            // 16-B slots per row
+};
+template <int D> __device__ __forceinline__ int swz(int row) {
+    return D == 128 ? ((row >> 1) & 7) : (row & 15);  // conflict-free ds_read_b128
+}
 constexpr int SENT_ROW = INT_MIN + 1024;  // crow of padded trains (dot is 0 there)
 constexpr int SENT_COL = INT_MIN + 1024;  // ccol of padded queries
 constexpr int ROW_VALID_MIN = -(1 << 24); // merged row values below this are padding
@@ -105,41 +122,67 @@ __device__ __forceinline__ int transpose_max16(const int (&c)[16], int lane) {
     return max(q, dpp<0xB1>(q));
 }
 
-// |x'|^2 plus the row / column key constants per descriptor, padded to k_pad (multiple of 256).
-__global__ void l2_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
-                               int k_max, int k_pad, int32_t* __restrict__ norm,
-                               int32_t* __restrict__ crow, uint8_t* __restrict__ zero_row,
-                               uint4* __restrict__ desc_i8) {
+// Per descriptor: the i8 feature row (L2: x ^ 0x80; Hamming: bits -> 0/1 bytes), its norm
+// (|x'|^2 resp. popcount) and the row-key constant, padded to k_pad (multiple of 256).
+template <int METRIC>
+__global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
+                                 int k_max, int k_pad, int32_t* __restrict__ norm,
+                                 int32_t* __restrict__ crow, uint8_t* __restrict__ zero_row,
+                                 uint4* __restrict__ desc_i8) {
+    constexpr int DIN = METRIC == SFM_METRIC_L2 ? 128 : 32;   // input bytes per descriptor
+    constexpr int D = METRIC == SFM_METRIC_L2 ? 128 : 256;    // feature bytes per row
     const int img = blockIdx.y;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (img == 0 && j < 128) zero_row[j] = 0;  // i8 zero row for padded trains / queries
+    if (img == 0 && j < D) zero_row[j] = 0;  // i8 zero row for padded trains / queries
     if (j >= k_pad) return;
     int nv = 0;
     if (j < k_max) {
-        const uint4* p = (const uint4*)(desc + ((size_t)img * k_max + j) * 128);
-        uint4* o8 = desc_i8 + ((size_t)img * k_max + j) * 8;
+        const uint4* p = (const uint4*)(desc + ((size_t)img * k_max + j) * DIN);
+        uint4* o8 = desc_i8 + ((size_t)img * k_max + j) * (D / 16);
+        if (METRIC == SFM_METRIC_L2) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            uint4 v = p[q];
-            o8[q] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u,
-                               v.w ^ 0x80808080u);
-            unsigned w[4] = {v.x, v.y, v.z, v.w};
+            for (int q = 0; q < 8; ++q) {
+                uint4 v = p[q];
+                o8[q] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u,
+                                   v.w ^ 0x80808080u);
+                unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
+                for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    int x = (int)((w[e] >> (8 * b)) & 0xFF) - 128;
-                    nv += x * x;
+                    for (int b = 0; b < 4; ++b) {
+                        int x = (int)((w[e] >> (8 * b)) & 0xFF) - 128;
+                        nv += x * x;
+                    }
+            }
+        } else {
+            // bit b of byte k (OpenCV's bit order is irrelevant: the distance counts all bits)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint4 v = p[q];
+                const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    nv += __popc(w[e]);
+                    unsigned o[8];
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {  // 4 bits of word e -> one u32 of 0/1 bytes
+                        const unsigned nib = (w[e] >> (4 * t)) & 0xFu;
+                        o[t] = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+                    }
+                    o8[8 * q + 2 * e] = make_uint4(o[0], o[1], o[2], o[3]);
+                    o8[8 * q + 2 * e + 1] = make_uint4(o[4], o[5], o[6], o[7]);
                 }
+            }
         }
     }
     const size_t o = (size_t)img * k_pad + j;
     norm[o] = nv;
-    // row key = vr*256 + (255 - row_in_chunk) = dot*512 + crow;  vr = 2 dot - |y'|^2
-    crow[o] = (j < n_kp[img]) ? (-256 * nv + 255 - (j & (CHUNK - 1))) : SENT_ROW;
+    // row key = vr*256 + (255 - j mod 256) = dot*512 + crow;  vr = 2 dot - n_j
+    crow[o] = (j < n_kp[img]) ? (-256 * nv + 255 - (j & 255)) : SENT_ROW;
 }
 
-__global__ __launch_bounds__(512, 2) void l2_match_kernel(
+template <int D>
+__global__ __launch_bounds__(512, 2) void mfma_match_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ crow_tab,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
@@ -148,8 +191,12 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
     // state, all distinct __shared__ objects: with the chunk loop unrolled by two every access
     // names its buffer statically, so the compiler's LDS-DMA alias tracking does not make reads
     // of one buffer wait (vmcnt) for the DMA into the other.
-    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * 128 + CHUNK * 4];
-    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * 128 + CHUNK * 4];
+    constexpr int QT = Geo<D>::QT, QB = Geo<D>::QB, CHUNK = Geo<D>::CHUNK, NK = Geo<D>::NK;
+    constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32;
+    constexpr int PIECES = CHUNK * D / 1024 / WAVES;  // 1 KB LDS-DMA pieces per wave per chunk
+    constexpr int RPP = 1024 / D;                     // rows per 1 KB piece
+    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
     __shared__ unsigned long long lds_col[KMAX_L2];
 
     const int p = blockIdx.x / n_qblk, qb = blockIdx.x - p * n_qblk;
@@ -158,38 +205,39 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     for (int j = tid; j < k_pad; j += 512) lds_col[j] = 0ull;
 
-    const uint8_t* db = desc + (size_t)b * k_max * 128;
+    const uint8_t* db = desc + (size_t)b * k_max * D;
     const int32_t* crb = crow_tab + (size_t)b * k_pad;
     const int n_chunk = (nb + CHUNK - 1) / CHUNK;
 
-    // stage chunk ch into buffer dst: 4 x 1 KB LDS-DMA pieces per wave (+ the crow piece)
+    // stage chunk ch into buffer dst: PIECES x 1 KB LDS-DMA pieces per wave (+ the crow piece);
+    // lane L of a piece lands in slot L % SLOTS of row L / SLOTS and fetches the swizzled slot
     auto stage = [&](int ch, unsigned char* dst) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int piece = wave * 4 + i;         // 1 KB = 8 rows
-            const int row = piece * 8 + (lane >> 3);
-            const int slot = (lane & 7) ^ ((row >> 1) & 7);
+        for (int i = 0; i < PIECES; ++i) {
+            const int piece = wave * PIECES + i;
+            const int row = piece * RPP + lane / SLOTS;
+            const int slot = (lane % SLOTS) ^ swz<D>(row);
             const int j = ch * CHUNK + row;
-            const uint8_t* src = (j < nb) ? db + (size_t)j * 128 + slot * 16 : zero_row + slot * 16;
+            const uint8_t* src = (j < nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
             __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
         }
-        if (wave == 0) {
+        if (wave == 0 && lane < CHUNK / 4) {
             const int32_t* src = crb + ch * CHUNK + lane * 4;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * 128), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D), 16, 0, 0);
         }
     };
 
     const int qbase = qb * QB + wave * QT * 32;
     const bool active = qbase < na;  // wave-uniform
-    v4i bq[QT][4];
+    v4i bq[QT][NK];
     int ccol[QT], B1[QT], J1[QT], B2[QT], tb[QT], ts[QT];
-    const uint8_t* da = desc + (size_t)a * k_max * 128;
+    const uint8_t* da = desc + (size_t)a * k_max * D;
 #pragma unroll
     for (int c = 0; c < QT; ++c) {
         const int q = qbase + c * 32 + r32;
-        const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * 128 + 64 * h : zero_row + 64 * h);
+        const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * D + (D / 2) * h : zero_row + (D / 2) * h);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) bq[c][s] = src[s];
+        for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
         // col key = vc*128 + (127 - q_in_wave) = dot*256 + ccol;  vc = 2 dot - |x'|^2
         ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32)) : SENT_COL;
         B1[c] = INT_MIN; J1[c] = -1; B2[c] = INT_MIN;
@@ -198,19 +246,19 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
     // process chunk ch from buffer cur while chunk ch+1 streams into buffer nxt
     auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
         if (ch + 1 < n_chunk) stage(ch + 1, nxt);
-            const int nt = min(8, (nb - ch * CHUNK + 31) >> 5);
+            const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
             if (active) {
                 const unsigned char* A = cur;
-                const int* Cr = (const int*)(cur + CHUNK * 128);
+                const int* Cr = (const int*)(cur + CHUNK * D);
                 // one 32-train tile: MFMAs for the 4 query tiles + both epilogues; returns the
                 // transposed column key of this lane's train row
                 auto tile = [&](int tt) -> int {
                     const int row = tt * 32 + r32;
-                    const int swz = (row >> 1) & 7;
-                    v4i af[4];
+                    const int sw = swz<D>(row);
+                    v4i af[NK];
 #pragma unroll
-                    for (int s = 0; s < 4; ++s)
-                        af[s] = *(const v4i*)(A + row * 128 + (((4 * h + s) ^ swz) << 4));
+                    for (int s = 0; s < NK; ++s)
+                        af[s] = *(const v4i*)(A + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
                     int crow[16];
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
@@ -223,7 +271,7 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
                     for (int c = 0; c < QT; c += 2) {
                         v16i acc0 = {0}, acc1 = {0};
 #pragma unroll
-                        for (int s = 0; s < 4; ++s) {
+                        for (int s = 0; s < NK; ++s) {
                             acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
                             acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
                         }
@@ -265,7 +313,7 @@ __global__ __launch_bounds__(512, 2) void l2_match_kernel(
 #pragma unroll
                 for (int c = 0; c < QT; ++c) {
                     const int v1 = tb[c] >> 8, v2 = ts[c] >> 8;
-                    const int j1 = ch * CHUNK + 255 - (tb[c] & 255);
+                    const int j1 = ((ch * CHUNK) & ~255) + 255 - (tb[c] & 255);
                     const bool up = v1 > B1[c];
                     B2[c] = up ? max(B1[c], v2) : max(B2[c], v1);
                     J1[c] = up ? j1 : J1[c];
@@ -305,8 +353,8 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
     const int32_t* __restrict__ n_kp, int k_max, int k_pad, const int32_t* __restrict__ norm,
     const int32_t* __restrict__ pairs, int n_qblk, const int4* __restrict__ rowres,
     const unsigned long long* __restrict__ colpart, int xc, int rnum, int rden,
-    long long max_dist, int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
-    int32_t* __restrict__ out_dist) {
+    long long max_dist, int squared, int32_t* __restrict__ out_count,
+    int32_t* __restrict__ out_match, int32_t* __restrict__ out_dist) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
     __shared__ int wsum[8];
     const int p = blockIdx.x;
@@ -367,7 +415,7 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
                         for (int q = 0; q < n_qblk; ++q) best = max(best, cp[(size_t)q * k_pad + j]);
                         keep = (int)(0xFFFFFFFFu - (unsigned)best) == i;
                     }
-                    keep = keep && sfm::ratio_ok(d1, d2, rnum, rden, true);
+                    keep = keep && sfm::ratio_ok(d1, d2, rnum, rden, squared != 0);
                     keep = keep && (max_dist < 0 || d1 < max_dist);
                 }
             }
@@ -379,21 +427,29 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
 
 }  // namespace
 
-int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
-                        int32_t k_max, const int32_t* pairs, int32_t n_pairs,
-                        const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
-                        int32_t* out_dist) {
+// MFMA matcher for both metrics (L2: D = 128; Hamming: D = 256 bit-expanded).
+static int mfma_match_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const int32_t* n_kp,
+                             int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                             const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                             int32_t* out_dist) {
     hipStream_t st = ctx->stream;
     if (k_max == 0) {
         SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_pairs, st));
         return SFM_OK;
     }
+    const bool l2 = metric == SFM_METRIC_L2;
+    const int D = l2 ? 128 : 256;
+    const int QB = l2 ? Geo<128>::QB : Geo<256>::QB;
     const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
+    if (k_pad > KMAX_L2) {
+        sfm::set_error("sfm_match_batch: MFMA matcher needs k_max <= 4096");
+        return SFM_ERR_INVALID;
+    }
     const int n_qblk = (k_max + QB - 1) / QB;
     const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
     const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
     const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
-    const size_t descb = sfm::align_up((size_t)n_img * k_max * 128, 256);
+    const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
     char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     uint8_t* zero_row = (uint8_t*)ws;
@@ -402,21 +458,44 @@ int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, 
     int4* rowres = (int4*)(ws + 256 + 2 * tab);
     unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
     uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
-    hipLaunchKernelGGL(l2_prep_kernel, dim3(k_pad / 256, n_img), dim3(256), 0, st, desc, n_kp,
-                       k_max, k_pad, norm, crow, zero_row, (uint4*)desc_i8);
-    SFM_HIP_CHECK(hipGetLastError());
-    if (k_pad > KMAX_L2) {
-        sfm::set_error("sfm_match_batch: L2 k_max > 4096 not supported");
-        return SFM_ERR_INVALID;
+    if (l2) {
+        hipLaunchKernelGGL(mfma_prep_kernel<SFM_METRIC_L2>, dim3(k_pad / 256, n_img), dim3(256), 0,
+                           st, desc, n_kp, k_max, k_pad, norm, crow, zero_row, (uint4*)desc_i8);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(mfma_match_kernel<128>, dim3(n_pairs * n_qblk), dim3(512), 0, st,
+                           desc_i8, n_kp, k_max, k_pad, norm, crow, zero_row, pairs, n_qblk,
+                           rowres, colpart);
+    } else {
+        hipLaunchKernelGGL(mfma_prep_kernel<SFM_METRIC_HAMMING>, dim3(k_pad / 256, n_img),
+                           dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, crow, zero_row,
+                           (uint4*)desc_i8);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(mfma_match_kernel<256>, dim3(n_pairs * n_qblk), dim3(512), 0, st,
+                           desc_i8, n_kp, k_max, k_pad, norm, crow, zero_row, pairs, n_qblk,
+                           rowres, colpart);
     }
-    hipLaunchKernelGGL(l2_match_kernel, dim3(n_pairs * n_qblk), dim3(512), 0, st, desc_i8, n_kp,
-                       k_max, k_pad, norm, crow, zero_row, pairs, n_qblk, rowres, colpart);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(l2_finalize_kernel, dim3(n_pairs), dim3(256),
                        prm->cross_check == SFM_XC_OPENCV ? (size_t)k_pad * 8 : 0, st, n_kp, k_max,
                        k_pad, norm, pairs, n_qblk, rowres, colpart, prm->cross_check,
-                       prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, out_count,
-                       out_match, out_dist);
+                       prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, l2 ? 1 : 0,
+                       out_count, out_match, out_dist);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
+}
+
+int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
+                        int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                        const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                        int32_t* out_dist) {
+    return mfma_match_launch(ctx, SFM_METRIC_L2, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
+                             out_count, out_match, out_dist);
+}
+
+int sfm_match_hamming_mfma_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp,
+                                  int32_t n_img, int32_t k_max, const int32_t* pairs,
+                                  int32_t n_pairs, const sfm_match_params* prm,
+                                  int32_t* out_count, int32_t* out_match, int32_t* out_dist) {
+    return mfma_match_launch(ctx, SFM_METRIC_HAMMING, desc, n_kp, n_img, k_max, pairs, n_pairs,
+                             prm, out_count, out_match, out_dist);
 }

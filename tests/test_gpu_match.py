@@ -115,3 +115,28 @@ def test_invalid_arguments_raise(ctx):
         ctx.match_batch(d, n, pr, cross_check=2, ratio=(4, 5))
     with pytest.raises(sfmcore.SfmCoreError):
         ctx.match_batch(d, n, pr, metric=1)  # Hamming needs dim 32
+
+
+@pytest.mark.parametrize("K", [500, 1000, 4096])
+def test_hamming_mfma_and_valu_paths_agree(ctx, K):
+    """The MFMA Hamming path (bits expanded to 0/1 bytes) and the VALU popcount kernel are two
+    implementations of the same matcher: outputs must be identical in every mode."""
+    import os
+    s = synth.make_scene(3, K, seed=40 + K, orb=True)
+    n_kp = s["n_kp"].copy()
+    n_kp[1] = K - 37  # ragged
+    pairs = np.array([[0, 1], [1, 2], [2, 0]], np.int32)
+    for xc, ratio, md in ((2, None, 26), (1, None, -1), (1, (4, 5), 40), (0, None, -1)):
+        outs = []
+        for v in ("0", "1"):
+            os.environ["SFM_HAMMING_VALU"] = v
+            try:
+                outs.append(_gpu_match(ctx, s["desc"], n_kp, pairs, metric=1, cross_check=xc,
+                                       ratio=ratio, max_dist=md))
+            finally:
+                os.environ.pop("SFM_HAMMING_VALU", None)
+        (c0, m0, d0), (c1, m1, d1) = outs
+        np.testing.assert_array_equal(c0, c1)
+        for p in range(len(pairs)):
+            np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
+            np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
