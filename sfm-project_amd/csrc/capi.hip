@@ -1,5 +1,5 @@
 // C-ABI entry points of libsfmcore: context management, error reporting, argument validation.
-// The per-stage kernels live in match_l2.hip, match_hamming.hip, ransac.hip and ba.hip.
+// The per-stage kernels live in match_mfma.hip, match_hamming.hip, ransac.hip and ba.hip.
 #include "sfm_internal.h"
 
 static thread_local std::string g_err;
