@@ -80,12 +80,7 @@ def match_descriptors(des1, des2, norm: str = "hamming", cross_check: bool | str
           False: sfmcore.XC_NONE, None: sfmcore.XC_NONE}[cross_check]
     if ratio is not None and not isinstance(ratio, tuple):
         ratio = _ratio_fraction(float(ratio))
-    if max_distance is None:
-        md = -1
-    elif metric == sfmcore.METRIC_L2:
-        md = int(np.ceil(float(max_distance) ** 2))  # integer d^2: d < m  <=>  d^2 < ceil(m^2)
-    else:
-        md = int(np.ceil(float(max_distance)))
+    md = _max_dist(metric, max_distance)
     d1 = np.ascontiguousarray(des1, np.uint8)
     d2 = np.ascontiguousarray(des2, np.uint8)
     k_max = max(d1.shape[0], d2.shape[0])
@@ -114,6 +109,94 @@ def _ratio_fraction(r: float):
     from fractions import Fraction
     f = Fraction(r).limit_denominator(1000)
     return (f.numerator, f.denominator)
+
+
+class Pair:
+    """code/pipeline.py:6-9 record: img_inx_1, img_inx_2, matches."""
+
+    def __init__(self, img_inx_1=None, img_inx_2=None, matches=None):
+        self.img_inx_1 = img_inx_1
+        self.img_inx_2 = img_inx_2
+        self.matches = matches
+
+
+def match_all_pairs(descriptors, norm: str = "hamming", cross_check=True,
+                    max_distance=REFERENCE_MAX_HAMMING, ratio=None, ordered: bool = True,
+                    sort: bool = True, device: int = 0, keypoint_counts=None):
+    """The pair loop of code/pipeline.py:36-47 in one batched GPU call.
+
+    descriptors: list of u8 [K_i, 32] (ORB) or [K_i, 128] (SIFT-like) arrays, one per image (None
+    or empty for an image without keypoints).  For every ordered pair i != j (ordered=True, the
+    reference's enumeration) or every i < j (ordered=False) the matches of
+    match_descriptors(des_i, des_j, ...) are computed; pairs with no match are dropped, exactly
+    as `if match:` at code/pipeline.py:42.  Returns a list of Pair(i, j, [DMatch]) in the
+    reference's (i, j) order."""
+    import torch
+    n = len(descriptors)
+    dim = 32 if norm == "hamming" else 128
+    ks = [0 if d is None else len(d) for d in descriptors]
+    k_max = max(ks + [1])
+    desc = np.zeros((n, k_max, dim), np.uint8)
+    for i, d in enumerate(descriptors):
+        if ks[i]:
+            desc[i, :ks[i]] = np.asarray(d, np.uint8)
+    pairs = np.array([(i, j) for i in range(n) for j in range(n)
+                      if (i != j if ordered else i < j)], np.int32).reshape(-1, 2)
+    if len(pairs) == 0:
+        return []
+    metric = sfmcore.METRIC_HAMMING if norm == "hamming" else sfmcore.METRIC_L2
+    xc = {True: sfmcore.XC_OPENCV, "opencv": sfmcore.XC_OPENCV, "mutual": sfmcore.XC_MUTUAL,
+          False: sfmcore.XC_NONE, None: sfmcore.XC_NONE}[cross_check]
+    if ratio is not None and not isinstance(ratio, tuple):
+        ratio = _ratio_fraction(float(ratio))
+    md = _max_dist(metric, max_distance)
+    dev = torch.device("cuda", device)
+    cnt, mt, dist = sfmcore.context(device).match_batch(
+        torch.from_numpy(desc).to(dev), torch.tensor(ks, dtype=torch.int32, device=dev),
+        torch.from_numpy(pairs).to(dev), metric=metric, cross_check=xc, ratio=ratio, max_dist=md)
+    cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+    out = []
+    for p, (i, j) in enumerate(pairs.tolist()):
+        k = int(cnt[p])
+        if k == 0:
+            continue
+        d = dist[p, :k].astype(np.float64)
+        if metric == sfmcore.METRIC_L2:
+            d = np.sqrt(d).astype(np.float32).astype(np.float64)
+        ms = [DMatch(q, t, 0, dd) for (q, t), dd in zip(mt[p, :k].tolist(), d.tolist())]
+        if sort:
+            ms = sorted(ms, key=lambda x: x.distance)
+        out.append(Pair(i, j, ms))
+    return out
+
+
+def extract_all(images, nfeatures: int = 500):
+    """ORB once per image (code/feature_matching.py:42-45 extracts 2 x N(N-1) times): returns
+    (keypoints, descriptors) lists.  Needs cv2."""
+    _require_cv2("extract_all")
+    orb = cv2.ORB_create(nfeatures)
+    kps, des = [], []
+    for img in images:
+        k, d = orb.detectAndCompute(img, None)
+        kps.append(k)
+        des.append(d)
+    return kps, des
+
+
+def pipeline_pair_matches(images):
+    """Drop-in for the whole loop of code/pipeline.py:36-47: ORB once per image, then every
+    ordered pair matched with the reference's matcher (Hamming, crossCheck, distance < 26) in one
+    batched GPU call.  Returns the reference's pair_matches list."""
+    _, des = extract_all(images)
+    return match_all_pairs(des)
+
+
+def _max_dist(metric, max_distance):
+    if max_distance is None:
+        return -1
+    if metric == sfmcore.METRIC_L2:
+        return int(np.ceil(float(max_distance) ** 2))  # integer d^2: d < m  <=>  d^2 < ceil(m^2)
+    return int(np.ceil(float(max_distance)))
 
 
 def extract_and_match(gray1, gray2):

@@ -201,3 +201,33 @@ def rows_to_pairs(rows: np.ndarray, pairs: np.ndarray):
         p = int(rows[s, 0])
         out.append((int(pairs[p, 0]), int(pairs[p, 1]), rows[s:e, 1:].copy()))
     return out
+
+
+# ---- on-disk match graph ------------------------------------------------
+
+GRAPH_FORMAT = "sfm-core match graph v1"
+
+
+def save_graph(path: str, pairs: np.ndarray, rows: np.ndarray, n_kp=None, meta=None):
+    """Write a verified match graph as .npz (no pickles): pairs [P,2] i32 (image a, image b),
+    rows [n,3] i32 (pair index, queryIdx, trainIdx), optional per-image keypoint counts and a
+    JSON metadata string (e.g. RANSAC seed / threshold, descriptor kind)."""
+    import json
+    np.savez_compressed(path, format=np.array(GRAPH_FORMAT),
+                        pairs=np.ascontiguousarray(pairs, np.int32),
+                        rows=np.ascontiguousarray(rows, np.int32),
+                        n_kp=np.asarray([] if n_kp is None else n_kp, np.int32),
+                        meta=np.array(json.dumps(meta or {})))
+
+
+def load_graph(path: str):
+    """Inverse of save_graph (allow_pickle stays False).  Returns dict(pairs, rows, n_kp, meta)
+    and `pair_matches` = rows_to_pairs(rows, pairs)."""
+    import json
+    with np.load(path, allow_pickle=False) as z:
+        if str(z["format"]) != GRAPH_FORMAT:
+            raise ValueError(f"{path}: not a {GRAPH_FORMAT!r} file")
+        out = dict(pairs=z["pairs"], rows=z["rows"], n_kp=z["n_kp"],
+                   meta=json.loads(str(z["meta"])))
+    out["pair_matches"] = rows_to_pairs(out["rows"], out["pairs"])
+    return out

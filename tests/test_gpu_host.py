@@ -162,3 +162,22 @@ def test_graph_packed_roundtrip_on_device():
     g = match_graph.all_gather_graph(c, pk, [(0, len(pairs))])
     np.testing.assert_array_equal(g.cpu().numpy(), rows.cpu().numpy())
     assert int(offs[-1]) == rows.shape[0] > 0
+
+
+def test_match_all_pairs_equals_reference_loop():
+    """Batched all-pairs entry == the reference's per-ordered-pair loop (code/pipeline.py:38-47)
+    over match_descriptors, including the drop of empty results."""
+    s = synth.make_scene(4, 300, seed=19, orb=True)
+    des = [s["desc"][i][: 300 - 25 * i] for i in range(4)]
+    des.append(np.zeros((0, 32), np.uint8))  # an image without keypoints
+    got = fm.match_all_pairs(des)
+    want = []
+    for i in range(len(des)):
+        for j in range(len(des)):
+            if i != j:
+                m = fm.match_descriptors(des[i], des[j])
+                if m:
+                    want.append((i, j, [(x.queryIdx, x.trainIdx, x.distance) for x in m]))
+    assert [(p.img_inx_1, p.img_inx_2, [(x.queryIdx, x.trainIdx, x.distance) for x in p.matches])
+            for p in got] == want
+    assert all(p.img_inx_1 != 4 and p.img_inx_2 != 4 for p in got)

@@ -112,3 +112,23 @@ def test_build_jtj_sharded_rejects_unsorted_observations():
     with pytest.raises(ValueError):
         reconstruction.build_jtj_sharded(np.zeros((1, 8)), np.zeros((1, 2)), np.zeros((2, 3)),
                                          [0, 0], [1, 0], np.zeros((2, 2)), 0, 1)
+
+
+def test_graph_npz_roundtrip(tmp_path):
+    pairs = synth.unordered_pairs(4)
+    rows = np.array([[0, 1, 2], [0, 3, 4], [4, 5, 6]], np.int32)
+    f = str(tmp_path / "g.npz")
+    match_graph.save_graph(f, pairs, rows, n_kp=[10, 11, 12, 13], meta={"seed": 42})
+    g = match_graph.load_graph(f)
+    np.testing.assert_array_equal(g["rows"], rows)
+    np.testing.assert_array_equal(g["pairs"], pairs)
+    assert g["meta"] == {"seed": 42} and g["n_kp"].tolist() == [10, 11, 12, 13]
+    assert [(a, b) for a, b, _ in g["pair_matches"]] == [tuple(pairs[0]), tuple(pairs[4])]
+
+
+def test_pair_record_and_pipeline_entry_need_cv2():
+    p = fm.Pair(1, 2, [fm.DMatch(0, 1, 0, 3.0)])
+    assert (p.img_inx_1, p.img_inx_2, len(p.matches)) == (1, 2, 1)
+    if fm.cv2 is None:
+        with pytest.raises(ImportError):
+            fm.pipeline_pair_matches([np.zeros((8, 8), np.uint8)] * 2)
