@@ -375,30 +375,30 @@ constexpr int PV = 64;  // preview matches (multiple of CH)
 
 // counts inliers of G over matches [m, mend) into cnt; with PRUNE checks the published bound every
 // PRUNE_EVERY matches and returns false (wave-uniform) when no lane can still win.
-template <bool PRUNE>
+template <bool PRUNE, int C = CH>
 __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[9], int m, int mend,
                                               int M, int& cnt,
                                               const unsigned long long* __restrict__ bestp) {
-    const int mc = m + ((mend - m) & ~(CH - 1));
+    const int mc = m + ((mend - m) & ~(C - 1));
 #pragma unroll 1
-    for (; m < mc; m += CH) {
-        float x1[CH], y1[CH], x2[CH], y2[CH];
+    for (; m < mc; m += C) {
+        float x1[C], y1[C], x2[C], y2[C];
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
+        for (int j = 0; j < C; ++j) {
             x1[j] = S[m + j];
             y1[j] = S[kp + m + j];
             x2[j] = S[2 * kp + m + j];
             y2[j] = S[3 * kp + m + j];
         }
 #pragma unroll
-        for (int j = 0; j < CH; j += 2)
+        for (int j = 0; j < C; j += 2)
             cnt += sampson_inlier2(G, f2{x1[j], x1[j + 1]}, f2{y1[j], y1[j + 1]},
                                    f2{x2[j], x2[j + 1]}, f2{y2[j], y2[j + 1]});
-        if (PRUNE && ((m + CH) % PRUNE_EVERY) == 0) {
+        if (PRUNE && ((m + C) % PRUNE_EVERY) == 0) {
             const unsigned long long bk =
                 __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int bound = (int)(bk >> 32) - 1;
-            if (__all(cnt + (M - m - CH) < bound)) return false;
+            if (__all(cnt + (M - m - C) < bound)) return false;
         }
     }
 #pragma unroll 1
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256) void ransac_fit_kernel(
     const bool ok = fit_f8(smp, F);
     sampson_prep(F, k1, k2, G);
     int cnt = 0;
-    score_matches<false>(S, kp, G, 0, min(PV, M), M, cnt, nullptr);
+    score_matches<false, 8>(S, kp, G, 0, min(PV, M), M, cnt, nullptr);  // 8-match chunks: fewer VGPRs beside the fit
     float* gt = hypG + (size_t)p * 9 * n_hyp + h;
 #pragma unroll
     for (int i = 0; i < 9; ++i) gt[(size_t)i * n_hyp] = G[i];
