@@ -181,12 +181,31 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
     crow[o] = (j < n_kp[img]) ? (-256 * nv + 255 - (j & 255)) : SENT_ROW;
 }
 
+// Pair order by train image (counting sort; one block): consecutive entries share image b.
+__global__ __launch_bounds__(1024) void pair_order_kernel(const int32_t* __restrict__ pairs,
+                                                          int n_pairs, int n_img,
+                                                          int32_t* __restrict__ order,
+                                                          int32_t* __restrict__ hist) {
+    const int tid = threadIdx.x;
+    for (int i = tid; i < n_img; i += 1024) hist[i] = 0;
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += 1024) atomicAdd(&hist[pairs[2 * p + 1]], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int off = 0;
+        for (int i = 0; i < n_img; ++i) { const int c = hist[i]; hist[i] = off; off += c; }
+    }
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += 1024) order[atomicAdd(&hist[pairs[2 * p + 1]], 1)] = p;
+}
+
 template <int D>
 __global__ __launch_bounds__(512, 2) void mfma_match_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ crow_tab,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
-    int4* __restrict__ rowres, unsigned long long* __restrict__ colpart) {
+    const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
+    unsigned long long* __restrict__ colpart) {
     // LDS: two DMA staging objects ([CHUNK][128 B] train rows + [CHUNK] crow each) and the column
     // state, all distinct __shared__ objects: with the chunk loop unrolled by two every access
     // names its buffer statically, so the compiler's LDS-DMA alias tracking does not make reads
@@ -199,7 +218,14 @@ __global__ __launch_bounds__(512, 2) void mfma_match_kernel(
     __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
     __shared__ unsigned long long lds_col[KMAX_L2];
 
-    const int p = blockIdx.x / n_qblk, qb = blockIdx.x - p * n_qblk;
+    // XCD-aware block mapping: workgroups are dispatched round-robin over the 8 XCDs (L % 8), so
+    // XCD x takes the x-th contiguous run of the blocks ordered by train image (pair_order): the
+    // blocks an XCD runs together stream the same train descriptors through its own L2.  The
+    // grid is padded to 8 * per_xcd blocks (every XCD slot exists); slots past n_blk exit.
+    const int per_xcd = (int)(gridDim.x >> 3);
+    const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+    if (sblk >= n_blk) return;  // block-uniform, before any barrier
+    const int p = pair_order[sblk / n_qblk], qb = sblk % n_qblk;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
@@ -378,6 +404,7 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
             if (best == 0) continue;
             const int v = (int)((unsigned)(best >> 32) ^ 0x80000000u);
             const int gq = (int)(0xFFFFFFFFu - (unsigned)best);
+            if (gq < 0 || gq >= na) continue;  // defensive: a column winner is always a query
             const long long d = (long long)norm[(size_t)b * k_pad + j] - v;
             atomicMin(&lds_best[gq], ((unsigned long long)d << 32) | (unsigned)j);
         }
@@ -405,7 +432,7 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
             if (i < na) {
                 const int4 rr = rowres[(size_t)p * k_pad + i];
                 j = rr.y;
-                if (j >= 0 && rr.x > ROW_VALID_MIN) {
+                if (j >= 0 && j < nb && rr.x > ROW_VALID_MIN) {
                     const long long nx = norm[(size_t)a * k_pad + i];
                     d1 = nx - rr.x;
                     const long long d2 = (rr.z > ROW_VALID_MIN) ? nx - rr.z : sfm::DIST_INF;
@@ -450,7 +477,8 @@ static int mfma_match_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, cons
     const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
     const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
     const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
-    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + 1024);
+    const size_t ordb = sfm::align_up(sizeof(int32_t) * ((size_t)n_pairs + n_img), 256);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     uint8_t* zero_row = (uint8_t*)ws;
     int32_t* norm = (int32_t*)(ws + 256);
@@ -458,21 +486,27 @@ static int mfma_match_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, cons
     int4* rowres = (int4*)(ws + 256 + 2 * tab);
     unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
     uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
+    int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
+    const int n_blk = n_pairs * n_qblk;
+    const int grid = 8 * ((n_blk + 7) / 8);  // every XCD gets the same number of block slots
+    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), 0, st, pairs, n_pairs, n_img,
+                       pair_order, pair_order + n_pairs);
+    SFM_HIP_CHECK(hipGetLastError());
     if (l2) {
         hipLaunchKernelGGL(mfma_prep_kernel<SFM_METRIC_L2>, dim3(k_pad / 256, n_img), dim3(256), 0,
                            st, desc, n_kp, k_max, k_pad, norm, crow, zero_row, (uint4*)desc_i8);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(mfma_match_kernel<128>, dim3(n_pairs * n_qblk), dim3(512), 0, st,
+        hipLaunchKernelGGL(mfma_match_kernel<128>, dim3(grid), dim3(512), 0, st,
                            desc_i8, n_kp, k_max, k_pad, norm, crow, zero_row, pairs, n_qblk,
-                           rowres, colpart);
+                           pair_order, n_blk, rowres, colpart);
     } else {
         hipLaunchKernelGGL(mfma_prep_kernel<SFM_METRIC_HAMMING>, dim3(k_pad / 256, n_img),
                            dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, crow, zero_row,
                            (uint4*)desc_i8);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(mfma_match_kernel<256>, dim3(n_pairs * n_qblk), dim3(512), 0, st,
+        hipLaunchKernelGGL(mfma_match_kernel<256>, dim3(grid), dim3(512), 0, st,
                            desc_i8, n_kp, k_max, k_pad, norm, crow, zero_row, pairs, n_qblk,
-                           rowres, colpart);
+                           pair_order, n_blk, rowres, colpart);
     }
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(l2_finalize_kernel, dim3(n_pairs), dim3(256),
