@@ -3,15 +3,14 @@
 //
 // fp64 throughout.  Deterministic (no float atomics): every accumulation has a fixed order.
 //   ba_obs_kernel          one thread per observation (enough waves to stream HBM): residual,
-//                          J_c (2x8), J_p (2x3) -> res, W = w J_c^T J_p, and the observation's
-//                          point terms (w J_p^T J_p upper triangle, w J_p^T r, rho/2) to a scratch.
-//   ba_point_kernel        one thread per point: sums its observations' terms in order (pt_ptr
-//                          CSR) -> V_p, g_p; fixed-tree block sum of the cost shares.
+//                          J_c (2x8), J_p (2x3) -> res, W = w J_c^T J_p; V_p, g_p by a segmented
+//                          scan of the point terms across the wave (points are point-major
+//                          contiguous), boundary-cut segments to head/tail records.
+//   ba_camera_kernel finish blocks: points spanning waves, empty points, the cost;
+//   ba_final_kernel        camera split sums (only with fewer than 256 cameras).
 //   ba_camera_kernel       block (camera, split): recomputes J_c (cheaper than storing it: HBM is
 //                          the bound) over a contiguous share of the camera's observations
 //                          (cam_ptr/cam_obs CSR), fixed lane-strided order + shuffle tree.
-//   ba_camera_final_kernel sums the splits in order -> U_c = sum w J_c^T J_c, g_c = sum w J_c^T r.
-//   ba_cost_kernel         fixed-order sum of the block cost shares.
 // Algorithmic HBM traffic ~300 B/observation; this is an HBM-bound stage.
 #include <algorithm>
 
@@ -93,88 +92,125 @@ __device__ __forceinline__ void linearize(const double* __restrict__ cam, const 
 
 constexpr int NV = 10;      // per-observation point terms: V upper triangle (6), g_p (3), 0.5 rho
 constexpr int NU = 36 + 8;  // upper triangle of U_c (8x8) + g_c
+constexpr int SPLIT_TARGET = 256;  // camera blocks wanted (splits per camera = this / n_cam); more blocks only
+                                   // add reduction work (measured: 3 splits at 500 cameras 45 us vs 30 us)
 
-// One thread per observation: residual, W = w J_c^T J_p, and the observation's point terms.
+__device__ __forceinline__ void write_point(double* __restrict__ V, double* __restrict__ gp, int p,
+                                            const double (&a)[NV]) {
+    double* Vo = V + 9 * (size_t)p;
+    Vo[0] = a[0]; Vo[1] = a[1]; Vo[2] = a[2];
+    Vo[3] = a[1]; Vo[4] = a[3]; Vo[5] = a[4];
+    Vo[6] = a[2]; Vo[7] = a[4]; Vo[8] = a[5];
+    gp[3 * (size_t)p] = a[6]; gp[3 * (size_t)p + 1] = a[7]; gp[3 * (size_t)p + 2] = a[8];
+}
+
+// One thread per observation (enough waves to stream HBM): residual, W = w J_c^T J_p, and the
+// point terms (w J_p^T J_p upper triangle, w J_p^T r) summed per point by a segmented scan across
+// the wave — observations are point-major, so a point's observations are consecutive lanes.
+// Points whose observations lie inside one wave are written here; the segments cut by a wave
+// boundary go to head/tail records that the finish blocks combine.  The cost (sum of rho/2)
+// is reduced per wave.  All orders are fixed: deterministic.
 __global__ __launch_bounds__(256) void ba_obs_kernel(
     int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
     const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
-    const int32_t* __restrict__ pt_idx, const double* __restrict__ uv, double loss_s,
-    double* __restrict__ W, double* __restrict__ res, double* __restrict__ terms) {
+    const int32_t* __restrict__ pt_idx, const int32_t* __restrict__ pt_ptr,
+    const double* __restrict__ uv, double loss_s, double* __restrict__ W,
+    double* __restrict__ res, double* __restrict__ V, double* __restrict__ gp,
+    double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_wave) {
     const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= n_obs) return;
-    const int c = cam_idx[o], p = pt_idx[o];
-    const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
-    const double2 z = *(const double2*)(uv + 2 * (size_t)o);
-    ObsLin L;
-    linearize(cams + 8 * (size_t)c, pp + 2 * (size_t)c, X, z.x, z.y, loss_s, true, L);
-    *(double2*)(res + 2 * (size_t)o) = make_double2(L.r[0], L.r[1]);
-    double2* Wo = (double2*)(W + 24 * (size_t)o);
-#pragma unroll
-    for (int q = 0; q < 12; ++q) {
-        const int i0 = (2 * q) / 3, j0 = (2 * q) % 3, i1 = (2 * q + 1) / 3, j1 = (2 * q + 1) % 3;
-        Wo[q] = make_double2(L.w * (L.Jc[i0] * L.Jp[j0] + L.Jc[8 + i0] * L.Jp[3 + j0]),
-                             L.w * (L.Jc[i1] * L.Jp[j1] + L.Jc[8 + i1] * L.Jp[3 + j1]));
-    }
+    const int lane = threadIdx.x & 63;
+    const int wv = o >> 6;  // global wave index (blocks are whole waves)
+    const bool valid = o < n_obs;
+    int p = -1;
     double t[NV];
-    int k = 0;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < NV; ++k) t[k] = 0.0;
+    if (valid) {
+        const int c = cam_idx[o];
+        p = pt_idx[o];
+        const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+        const double2 z = *(const double2*)(uv + 2 * (size_t)o);
+        ObsLin L;
+        linearize(cams + 8 * (size_t)c, pp + 2 * (size_t)c, X, z.x, z.y, loss_s, true, L);
+        *(double2*)(res + 2 * (size_t)o) = make_double2(L.r[0], L.r[1]);
+        double2* Wo = (double2*)(W + 24 * (size_t)o);
 #pragma unroll
-        for (int j = i; j < 3; ++j) t[k++] = L.w * (L.Jp[i] * L.Jp[j] + L.Jp[3 + i] * L.Jp[3 + j]);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) t[6 + i] = L.w * (L.Jp[i] * L.r[0] + L.Jp[3 + i] * L.r[1]);
-    t[9] = 0.5 * L.rho;
-    double2* To = (double2*)(terms + NV * (size_t)o);
-#pragma unroll
-    for (int q = 0; q < NV / 2; ++q) To[q] = make_double2(t[2 * q], t[2 * q + 1]);
-}
-
-// One thread per point: V_p, g_p and the cost share, summed over its observations in order; then a
-// fixed-order block reduction of the cost shares.
-__global__ __launch_bounds__(256) void ba_point_kernel(int n_pt, const int32_t* __restrict__ pt_ptr,
-                                                       const double* __restrict__ terms,
-                                                       double* __restrict__ V,
-                                                       double* __restrict__ gp,
-                                                       double* __restrict__ cost_blk) {
-    __shared__ double red[4];
-    const int p = blockIdx.x * blockDim.x + threadIdx.x, tid = threadIdx.x;
-    double cost = 0.0;
-    if (p < n_pt) {
-        double a[NV - 1];
-#pragma unroll
-        for (int i = 0; i < NV - 1; ++i) a[i] = 0.0;
-        const int o0 = pt_ptr[p], o1 = pt_ptr[p + 1];
-        for (int o = o0; o < o1; ++o) {
-            const double2* T = (const double2*)(terms + NV * (size_t)o);
-#pragma unroll
-            for (int q = 0; q < NV / 2; ++q) {
-                const double2 v = T[q];
-                if (2 * q < NV - 1) a[2 * q] += v.x; else cost += v.x;
-                if (2 * q + 1 < NV - 1) a[2 * q + 1] += v.y; else cost += v.y;
-            }
+        for (int q = 0; q < 12; ++q) {
+            const int i0 = (2 * q) / 3, j0 = (2 * q) % 3, i1 = (2 * q + 1) / 3, j1 = (2 * q + 1) % 3;
+            Wo[q] = make_double2(L.w * (L.Jc[i0] * L.Jp[j0] + L.Jc[8 + i0] * L.Jp[3 + j0]),
+                                 L.w * (L.Jc[i1] * L.Jp[j1] + L.Jc[8 + i1] * L.Jp[3 + j1]));
         }
-        double* Vo = V + 9 * (size_t)p;
-        Vo[0] = a[0]; Vo[1] = a[1]; Vo[2] = a[2];
-        Vo[3] = a[1]; Vo[4] = a[3]; Vo[5] = a[4];
-        Vo[6] = a[2]; Vo[7] = a[4]; Vo[8] = a[5];
-        gp[3 * (size_t)p] = a[6]; gp[3 * (size_t)p + 1] = a[7]; gp[3 * (size_t)p + 2] = a[8];
-    }
+        int k = 0;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) cost += __shfl_down(cost, off, 64);
-    if ((tid & 63) == 0) red[tid >> 6] = cost;
-    __syncthreads();
-    if (tid == 0) cost_blk[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = i; j < 3; ++j) t[k++] = L.w * (L.Jp[i] * L.Jp[j] + L.Jp[3 + i] * L.Jp[3 + j]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) t[6 + i] = L.w * (L.Jp[i] * L.r[0] + L.Jp[3 + i] * L.r[1]);
+        t[9] = 0.5 * L.rho;
+    }
+    // cost: plain fixed-order wave sum, one entry per wave
+    double cw = t[9];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cw += __shfl_down(cw, off, 64);
+    if (lane == 0) cost_wave[wv] = cw;
+    // segmented inclusive scan over runs of equal point id (contiguous by construction)
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int pv = __shfl_up(p, off, 64);
+        const bool take = lane >= off && pv == p;
+#pragma unroll
+        for (int k = 0; k < NV - 1; ++k) {
+            const double v = __shfl_up(t[k], off, 64);
+            t[k] += take ? v : 0.0;
+        }
+    }
+    const int pn = __shfl_down(p, 1, 64);
+    const bool seg_end = valid && (lane == 63 || pn != p);
+    const int wbase = wv << 6;
+    int o_first = 0, o_last = 0;
+    if (seg_end) { o_first = pt_ptr[p]; o_last = pt_ptr[p + 1] - 1; }
+    const bool starts_here = o_first >= wbase, ends_here = o_last == o;
+    // the wave's tail record id (read by the fix-up) is always written: no memset needed
+    if (lane == 63) seg_pt[wv * 2 + 1] = (seg_end && starts_here && !ends_here) ? p : -1;
+    if (!seg_end) return;
+    if (starts_here && ends_here) {
+        write_point(V, gp, p, t);
+    } else {
+        const int side = starts_here ? 1 : 0;  // 1: tail (continues into later waves), 0: head
+        double* r = seg + ((size_t)wv * 2 + side) * NV;
+#pragma unroll
+        for (int k = 0; k < NV - 1; ++k) r[k] = t[k];
+    }
 }
 
 // Block (camera c, split s): fixed-order partial U_c / g_c over its share of the camera's
 // observations (J_c recomputed: cheaper than storing it, HBM is the bound).
+__device__ void finish_block(int fb, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
+                             const double* __restrict__ seg, const int32_t* __restrict__ seg_pt,
+                             double* __restrict__ V, double* __restrict__ gp,
+                             const double* __restrict__ cost_wave, double* __restrict__ cost);
+
+// Blocks [0, n_cam * splits): (camera c, split s) fixed-order U_c / g_c over a contiguous share of
+// the camera's observations — written directly when splits == 1, else as partials for
+// ba_final_kernel.  Blocks past that: finish_block (points spanning waves, empty points, cost),
+// which only needs the observation kernel's output.
 __global__ __launch_bounds__(256) void ba_camera_kernel(
     const double* __restrict__ cams, const double* __restrict__ pp, const double* __restrict__ pts,
     const int32_t* __restrict__ pt_idx, const double* __restrict__ uv,
     const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ cam_obs, double loss_s,
-    int splits, double* __restrict__ part) {
+    int n_cam, int splits, double* __restrict__ part, double* __restrict__ U,
+    double* __restrict__ gc, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
+    const double* __restrict__ seg, const int32_t* __restrict__ seg_pt, double* __restrict__ V,
+    double* __restrict__ gp, const double* __restrict__ cost_wave, double* __restrict__ cost) {
     __shared__ double red[4][NU];
-    const int c = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (b >= n_cam * splits) {
+        finish_block(b - n_cam * splits, n_wave, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_wave,
+                     cost);
+        return;
+    }
+    const int c = b / splits, s = b - c * splits;
     double acc[NU];
 #pragma unroll
     for (int i = 0; i < NU; ++i) acc[i] = 0.0;
@@ -182,20 +218,38 @@ __global__ __launch_bounds__(256) void ba_camera_kernel(
     const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
     const int len = (c1 - c0 + splits - 1) / splits;
     const int e0 = c0 + s * len, e1 = min(c1, e0 + len);
-    for (int e = e0 + tid; e < e1; e += 256) {
-        const int o = cam_obs[e];
-        const int p = pt_idx[o];
-        const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
-        ObsLin L;
-        linearize(cam, pp + 2 * (size_t)c, X, uv[2 * (size_t)o], uv[2 * (size_t)o + 1], loss_s,
-                  false, L);
-        int t = 0;
+    // four observations per step: the dependent gathers (cam_obs -> pt_idx -> point, uv) of all
+    // four are issued before any is used (memory-level parallelism; the kernel is latency-bound)
+    for (int e = e0 + tid; e < e1; e += 4 * 256) {
+        int o[4], pi[4];
+        double X[4][3], u[4], v[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int q = 0; q < 4; ++q) o[q] = (e + q * 256 < e1) ? cam_obs[e + q * 256] : -1;
 #pragma unroll
-            for (int j = i; j < 8; ++j) acc[t++] += L.w * (L.Jc[i] * L.Jc[j] + L.Jc[8 + i] * L.Jc[8 + j]);
+        for (int q = 0; q < 4; ++q) pi[q] = o[q] >= 0 ? pt_idx[o[q]] : 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[36 + i] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
+        for (int q = 0; q < 4; ++q) {
+            const int oo = o[q] >= 0 ? o[q] : 0;
+            X[q][0] = pts[3 * (size_t)pi[q]];
+            X[q][1] = pts[3 * (size_t)pi[q] + 1];
+            X[q][2] = pts[3 * (size_t)pi[q] + 2];
+            u[q] = uv[2 * (size_t)oo];
+            v[q] = uv[2 * (size_t)oo + 1];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (o[q] < 0) break;
+            ObsLin L;
+            linearize(cam, pp + 2 * (size_t)c, X[q], u[q], v[q], loss_s, false, L);
+            int t = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = i; j < 8; ++j)
+                    acc[t++] += L.w * (L.Jc[i] * L.Jc[j] + L.Jc[8 + i] * L.Jc[8 + j]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[36 + i] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
+        }
     }
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
@@ -209,22 +263,75 @@ __global__ __launch_bounds__(256) void ba_camera_kernel(
         for (int i = 0; i < NU; ++i) red[tid >> 6][i] = acc[i];
     }
     __syncthreads();
-    if (tid < NU)
-        part[((size_t)c * splits + s) * NU + tid] =
-            ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    if (tid < NU) {
+        const double v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+        if (splits > 1) {
+            part[((size_t)c * splits + s) * NU + tid] = v;
+        } else if (tid >= 36) {
+            gc[8 * (size_t)c + tid - 36] = v;
+        } else {
+            int i = 0, t = tid;
+            while (t >= 8 - i) { t -= 8 - i; ++i; }
+            const int j = i + t;
+            U[64 * (size_t)c + 8 * i + j] = v;
+            U[64 * (size_t)c + 8 * j + i] = v;
+        }
+    }
 }
 
-// One thread per (camera, component): sum of the split partials in order -> U_c (both triangles),
-// g_c.
-__global__ __launch_bounds__(256) void ba_camera_final_kernel(int n_cam, int splits,
-                                                              const double* __restrict__ part,
-                                                              double* __restrict__ U,
-                                                              double* __restrict__ gc) {
+// Finish work (256-thread block fb): points spanning waves (the point whose tail record wave g
+// wrote owns tail + the head records of the following waves up to its last observation, fixed
+// order), zero V_p / g_p for points without observations, and (block 0) the cost as a
+// fixed-order sum of the per-wave shares.
+__device__ void finish_block(int fb, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
+                             const double* __restrict__ seg, const int32_t* __restrict__ seg_pt,
+                             double* __restrict__ V, double* __restrict__ gp,
+                             const double* __restrict__ cost_wave, double* __restrict__ cost) {
+    const int tid = threadIdx.x;
+    const int g = fb * 256 + tid;
+    if (fb == 0) {
+        __shared__ double red[4];
+        double s = 0.0;
+        for (int w = tid; w < n_wave; w += 256) s += cost_wave[w];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_down(s, off, 64);
+        if ((tid & 63) == 0) red[tid >> 6] = s;
+        __syncthreads();
+        if (tid == 0) cost[0] = ((red[0] + red[1]) + red[2]) + red[3];
+    }
+    if (g < n_pt && pt_ptr[g] == pt_ptr[g + 1]) {
+        double z[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) z[k] = 0.0;
+        write_point(V, gp, g, z);
+    }
+    if (g < n_wave) {
+        const int p = seg_pt[g * 2 + 1];
+        if (p >= 0) {
+            double a[NV];
+#pragma unroll
+            for (int k = 0; k < NV - 1; ++k) a[k] = seg[((size_t)g * 2 + 1) * NV + k];
+            a[NV - 1] = 0.0;
+            const int w_last = (pt_ptr[p + 1] - 1) >> 6;
+            for (int w = g + 1; w <= w_last; ++w) {
+#pragma unroll
+                for (int k = 0; k < NV - 1; ++k) a[k] += seg[((size_t)w * 2) * NV + k];
+            }
+            write_point(V, gp, p, a);
+        }
+    }
+}
+
+// Few cameras (splits > 1): U_c / g_c component = the camera's split partials summed in order.
+__global__ __launch_bounds__(256) void ba_final_kernel(int n_cam, int splits,
+                                                       const double* __restrict__ part,
+                                                       double* __restrict__ U,
+                                                       double* __restrict__ gc) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_cam * NU) return;
     const int c = g / NU, k = g - c * NU;
     double v = 0.0;
-    for (int s = 0; s < splits; ++s) v += part[((size_t)c * splits + s) * NU + k];
+    for (int sp = 0; sp < splits; ++sp) v += part[((size_t)c * splits + sp) * NU + k];
     if (k >= 36) {
         gc[8 * (size_t)c + k - 36] = v;
     } else {
@@ -234,19 +341,6 @@ __global__ __launch_bounds__(256) void ba_camera_final_kernel(int n_cam, int spl
         U[64 * (size_t)c + 8 * i + j] = v;
         U[64 * (size_t)c + 8 * j + i] = v;
     }
-}
-
-__global__ __launch_bounds__(256) void ba_cost_kernel(int n, const double* __restrict__ cost_blk,
-                                                      double* __restrict__ cost) {
-    __shared__ double red[4];
-    const int tid = threadIdx.x;
-    double s = 0.0;
-    for (int p = tid; p < n; p += 256) s += cost_blk[p];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) s += __shfl_down(s, off, 64);
-    if ((tid & 63) == 0) red[tid >> 6] = s;
-    __syncthreads();
-    if (tid == 0) cost[0] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
 }  // namespace
@@ -277,42 +371,38 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     SFM_REQUIRE(cams && pp && pts && cam_idx && pt_idx && uv && pt_ptr && cam_ptr && cam_obs && U &&
                     V && W && gc && gp && res,
                 "sfm_ba_jtj: NULL array");
-    // workspace: per-observation point terms | cost per point block | camera split partials
-    const int n_pblk = (n_pt + 255) / 256;
+    // workspace: segment records (2 per wave) | their point ids | cost per wave | camera partials
+    const int n_wave = (n_obs + 63) / 64;
     // few cameras: split each camera's observations so the grid still fills the chip
-    const int splits = std::max(1, std::min(16, (256 + n_cam - 1) / n_cam));
-    const size_t tb = sfm::align_up(sizeof(double) * NV * (size_t)n_obs, 256);
-    const size_t cb = sfm::align_up(sizeof(double) * (size_t)n_pblk, 256);
+    const int splits = std::max(1, std::min(16, (SPLIT_TARGET + n_cam - 1) / n_cam));
+    const size_t sb = sfm::align_up(sizeof(double) * NV * 2 * (size_t)std::max(n_wave, 1), 256);
+    const size_t ib = sfm::align_up(sizeof(int32_t) * 2 * (size_t)std::max(n_wave, 1), 256);
+    const size_t cb = sfm::align_up(sizeof(double) * (size_t)std::max(n_wave, 1), 256);
     const size_t pb = sizeof(double) * NU * (size_t)n_cam * splits;
-    char* ws = (char*)sfm::workspace(ctx, tb + cb + pb + 1024);
+    char* ws = (char*)sfm::workspace(ctx, sb + ib + cb + pb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
-    double* terms = (double*)ws;
-    double* cost_blk = (double*)(ws + tb);
-    double* part = (double*)(ws + tb + cb);
-    // The observation kernel streams every input once (HBM-bound); afterwards the camera
-    // reduction (latency-bound gathers of points / uv, now L2-warm) and the point reduction are
-    // independent: they run concurrently on two streams.
+    double* seg = (double*)ws;
+    int32_t* seg_pt = (int32_t*)(ws + sb);
+    double* cost_wave = (double*)(ws + sb + ib);
+    double* part = (double*)(ws + sb + ib + cb);
+    // observation kernel (HBM streaming) -> camera reduction (gathers now L2-warm) plus, in the
+    // same launch, the finish blocks (points spanning waves, empty points, cost)
     if (n_obs > 0) {
         hipLaunchKernelGGL(ba_obs_kernel, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs,
-                           cams, pp, pts, cam_idx, pt_idx, uv, loss_s, W, res, terms);
+                           cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res, V, gp, seg,
+                           seg_pt, cost_wave);
         SFM_HIP_CHECK(hipGetLastError());
     }
-    hipStream_t aux = nullptr;
-    if (sfm::aux_stream(ctx, &aux) != SFM_OK) return SFM_ERR_HIP;
-    SFM_HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
-    SFM_HIP_CHECK(hipStreamWaitEvent(aux, ctx->ev_fork, 0));
-    hipLaunchKernelGGL(ba_camera_kernel, dim3(n_cam, splits), dim3(256), 0, aux, cams, pp, pts,
-                       pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part);
+    const int nw = n_obs > 0 ? n_wave : 0;
+    const int n_fin = std::max(std::max((nw + 255) / 256, (n_pt + 255) / 256), 1);
+    hipLaunchKernelGGL(ba_camera_kernel, dim3(n_cam * splits + n_fin), dim3(256), 0, st, cams, pp,
+                       pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, n_cam, splits, part, U, gc, nw,
+                       n_pt, pt_ptr, seg, seg_pt, V, gp, cost_wave, cost);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ba_camera_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, aux,
-                       n_cam, splits, part, U, gc);
-    SFM_HIP_CHECK(hipGetLastError());
-    SFM_HIP_CHECK(hipEventRecord(ctx->ev_join, aux));
-    hipLaunchKernelGGL(ba_point_kernel, dim3(n_pblk), dim3(256), 0, st, n_pt, pt_ptr, terms, V,
-                       gp, cost_blk);
-    SFM_HIP_CHECK(hipGetLastError());
-    SFM_HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_join, 0));
-    hipLaunchKernelGGL(ba_cost_kernel, dim3(1), dim3(256), 0, st, n_pblk, cost_blk, cost);
-    SFM_HIP_CHECK(hipGetLastError());
+    if (splits > 1) {
+        hipLaunchKernelGGL(ba_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, st,
+                           n_cam, splits, part, U, gc);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
     return SFM_OK;
 }

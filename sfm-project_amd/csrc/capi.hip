@@ -11,7 +11,6 @@ void* workspace(sfm_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return ctx->ws;
     if (ctx->ws) {
         (void)hipStreamSynchronize(ctx->stream);
-        if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
         (void)hipFree(ctx->ws);
         ctx->ws = nullptr;
         ctx->ws_bytes = 0;
@@ -23,18 +22,6 @@ void* workspace(sfm_ctx* ctx, size_t bytes) {
     }
     ctx->ws_bytes = want;
     return ctx->ws;
-}
-int aux_stream(sfm_ctx* ctx, hipStream_t* out) {
-    if (!ctx->aux) {
-        if (hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
-            set_error("aux stream / event creation failed");
-            return SFM_ERR_HIP;
-        }
-    }
-    *out = ctx->aux;
-    return SFM_OK;
 }
 }  // namespace sfm
 
@@ -75,11 +62,7 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
     if (!ctx) return SFM_OK;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
     if (ctx->ws) (void)hipFree(ctx->ws);
-    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-    if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return SFM_OK;

@@ -13,8 +13,6 @@ struct sfm_ctx {
     void* ws = nullptr;          // growable device workspace
     size_t ws_bytes = 0;
     int n_cu = 256;
-    hipStream_t aux = nullptr;   // second stream for independent kernels (created on first use)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace sfm {
@@ -23,9 +21,6 @@ void set_error(const std::string& msg);
 
 // Returns a device pointer with at least `bytes` of workspace (grows, never shrinks).
 void* workspace(sfm_ctx* ctx, size_t bytes);
-
-// The context's auxiliary non-blocking stream and its fork/join events (created on first use).
-int aux_stream(sfm_ctx* ctx, hipStream_t* out);
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
