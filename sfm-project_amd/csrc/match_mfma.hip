@@ -11,7 +11,14 @@
 //     d^2(i,j) = |x'_i|^2 + |y'_j|^2 - 2 x'_i.y'_j
 // The dot products run on v_mfma_i32_32x32x32_i8 (exact int32).  For a fixed query i the best
 // train maximises  vr = 2 dot - |y'_j|^2  (= |x'_i|^2 - d^2);  for a fixed train j the best
-// query maximises  vc = 2 dot - |x'_i|^2  (= |y'_j|^2 - d^2).
+// query maximises  -d^2.
+//
+// One key per element serves both directions:
+//     Kr = 256 dot + crow_j = 128 vr + (127 - j mod 128)          one v_lshl_add
+//     Kc = Kr + ccol_i      = -128 d^2 + (127 - j mod 128) + (127 - q_in_wave)   one v_add
+// For a fixed query, Kc - Kr is a constant, so the row top-2 runs on Kr; for a fixed train the
+// j term of Kc is a constant, so max Kc over queries is the (smallest d^2, lowest query) winner.
+// |128 d^2| < 2^30 for any u8 descriptors, so neither key overflows.
 //
 // Geometry.  A 512-thread workgroup owns 1024 queries of one pair (8 waves x 4 query tiles of 32;
 // the query descriptors are the MFMA B operand, held in 64 VGPRs per wave for the whole kernel)
@@ -20,12 +27,11 @@
 // ds_read_b128; the swizzle is applied on the DMA source address).  MFMA output tile
 // D[32 trains][32 queries]: the query is the lane, the 16 accumulator registers of a lane are 16
 // of the 32 train rows (the other 16 live in lane ^ 32).
-//  * row direction (per query: best, argbest, second over trains) is lane-local: one
-//    v_mad_i32_i24 per element forms key = vr*256 + (255 - row_in_chunk); a max3/med3 network
-//    keeps the chunk top-2 over all 256 trains of the chunk; (best, argbest, second) is merged once
-//    per chunk.
-//  * column direction (per train: best query): key = vc*128 + (127 - query_in_wave), one mad
-//    per element, v_max3 over the wave's 4 query tiles, then a transpose-reduce across the 32 lanes
+//  * row direction (per query: best, argbest, second over trains) is lane-local: a max3/med3
+//    network on Kr keeps the top-2 of each group of 128 trains; (best, argbest, second) is merged
+//    once per group.
+//  * column direction (per train: best query): Kc, v_max3 over the wave's 4 query tiles, then a
+//    transpose-reduce across the 32 lanes
 //    of each half (permlane16_swap + DPP: 40 instructions for 16 registers) that leaves one train
 //    row per lane pair, and one 64-bit LDS atomic max per lane merges the 8 waves.  Each workgroup
 //    writes its column slab once; the finalize kernel merges the slabs of a pair.
@@ -60,16 +66,29 @@ template <int D> struct Geo {
 template <int D> __device__ __forceinline__ int swz(int row) {
     return D == 128 ? ((row >> 1) & 7) : (row & 15);  // conflict-free ds_read_b128
 }
-constexpr int SENT_ROW = INT_MIN + 1024;  // crow of padded trains (dot is 0 there)
-constexpr int SENT_COL = INT_MIN + 1024;  // ccol of padded queries
-constexpr int ROW_VALID_MIN = -(1 << 24); // merged row values below this are padding
+// Padding constants (valid keys: Kr, Kc >= -128 * 128 * 255^2 > -2^30; |crow|, |ccol| < 2^28):
+// a padded train (dot = 0) has Kr = ROW_PAD, a padded query Kc < -2^30.  Only the (padded train,
+// padded query) sum wraps; padded train rows are never read.
+constexpr int ROW_PAD = -(3 << 29);       // crow of padded trains
+constexpr int COL_PAD = -(3 << 29);       // ccol of padded queries
+constexpr int VALID_MIN = -(1 << 23);     // decoded vr / -d^2 of real elements are > this
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-__device__ __forceinline__ int imax3(int a, int b, int c) { return max(a, max(b, c)); }
-__device__ __forceinline__ int imed3(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 __device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
+// 3-input max / median as single instructions.  Plain max/min expressions let the compiler share
+// max(tb, x) between the median and the max and emit two v_max_i32 instead of one v_max3_i32.
+__device__ __forceinline__ int vmax3(int a, int b, int c) {
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ int vmed3(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 // No-return 64-bit LDS atomic max.  Inline asm: the compiler's LDS-DMA alias tracking treats a
 // builtin atomic to the column-state object as possibly aliasing the in-flight staging DMA and
@@ -177,8 +196,8 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
     }
     const size_t o = (size_t)img * k_pad + j;
     norm[o] = nv;
-    // row key = vr*256 + (255 - j mod 256) = dot*512 + crow;  vr = 2 dot - n_j
-    crow[o] = (j < n_kp[img]) ? (-256 * nv + 255 - (j & 255)) : SENT_ROW;
+    // row key Kr = 128 vr + (127 - j mod 128) = 256 dot + crow;  vr = 2 dot - n_j
+    crow[o] = (j < n_kp[img]) ? (-128 * nv + 127 - (j & 127)) : ROW_PAD;
 }
 
 // Pair order by train image (counting sort; one block): consecutive entries share image b.
@@ -264,8 +283,8 @@ __global__ __launch_bounds__(512, 2) void mfma_match_kernel(
         const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * D + (D / 2) * h : zero_row + (D / 2) * h);
 #pragma unroll
         for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
-        // col key = vc*128 + (127 - q_in_wave) = dot*256 + ccol;  vc = 2 dot - |x'|^2
-        ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32)) : SENT_COL;
+        // Kc = Kr + ccol = -128 d^2 + (127 - j mod 128) + (127 - q_in_wave)
+        ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32)) : COL_PAD;
         B1[c] = INT_MIN; J1[c] = -1; B2[c] = INT_MIN;
         tb[c] = INT_MIN; ts[c] = INT_MIN;
     }
@@ -302,21 +321,21 @@ __global__ __launch_bounds__(512, 2) void mfma_match_kernel(
                             acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
                         }
 #pragma unroll
-                        for (int r = 0; r < 16; r += 2) {  // row direction: running chunk top-2
-                            const int x0 = mad24(acc0[r], 512, crow[r]);
-                            const int y0 = mad24(acc0[r + 1], 512, crow[r + 1]);
-                            ts[c] = max(ts[c], imed3(tb[c], x0, y0));
-                            tb[c] = imax3(tb[c], x0, y0);
-                            const int x1 = mad24(acc1[r], 512, crow[r]);
-                            const int y1 = mad24(acc1[r + 1], 512, crow[r + 1]);
-                            ts[c + 1] = max(ts[c + 1], imed3(tb[c + 1], x1, y1));
-                            tb[c + 1] = imax3(tb[c + 1], x1, y1);
-                        }
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {  // column direction
-                            const int k0 = mad24(acc0[r], 256, ccol[c]);
-                            const int k1 = mad24(acc1[r], 256, ccol[c + 1]);
-                            colacc[r] = (c == 0) ? max(k0, k1) : imax3(colacc[r], k0, k1);
+                        for (int r = 0; r < 16; r += 2) {
+                            // row direction on Kr: running top-2 of the 128-train group
+                            const int x0 = mad24(acc0[r], 256, crow[r]);
+                            const int y0 = mad24(acc0[r + 1], 256, crow[r + 1]);
+                            ts[c] = max(ts[c], vmed3(tb[c], x0, y0));
+                            tb[c] = vmax3(tb[c], x0, y0);
+                            const int x1 = mad24(acc1[r], 256, crow[r]);
+                            const int y1 = mad24(acc1[r + 1], 256, crow[r + 1]);
+                            ts[c + 1] = max(ts[c + 1], vmed3(tb[c + 1], x1, y1));
+                            tb[c + 1] = vmax3(tb[c + 1], x1, y1);
+                            // column direction on Kc = Kr + ccol (full-rate add)
+                            const int a0 = x0 + ccol[c], a1 = x1 + ccol[c + 1];
+                            const int b0 = y0 + ccol[c], b1 = y1 + ccol[c + 1];
+                            colacc[r] = (c == 0) ? max(a0, a1) : vmax3(colacc[r], a0, a1);
+                            colacc[r + 1] = (c == 0) ? max(b0, b1) : vmax3(colacc[r + 1], b0, b1);
                         }
                     }
                     return transpose_max16(colacc, lane);
@@ -324,27 +343,36 @@ __global__ __launch_bounds__(512, 2) void mfma_match_kernel(
                 const int rr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 + ((lane >> 3) & 1) * 2 +
                                ((lane >> 4) & 1);
                 const int rowoff = (rr & 3) + 8 * (rr >> 2) + 4 * h;
+                // lane pair's train row j: e = Kc - (127 - j mod 128) = -128 d^2 + (127 - q_in_wave)
                 auto col_merge = [&](int tt, int key) {
-                    if (!(lane & 1) && key > SENT_COL + (1 << 29)) {
-                        const unsigned vb = (unsigned)(key >> 7) ^ 0x80000000u;
-                        const unsigned gq = (unsigned)(qbase + 127 - (key & 127));
-                        lds_max_u64(&lds_col[ch * CHUNK + tt * 32 + rowoff],
+                    const int j = ch * CHUNK + tt * 32 + rowoff;
+                    const int e = key - (127 - (j & 127));
+                    const int nd = e >> 7;  // -d^2 (padding: out of range)
+                    if (!(lane & 1) && nd > VALID_MIN && nd <= 0) {
+                        const unsigned vb = (unsigned)nd ^ 0x80000000u;
+                        const unsigned gq = (unsigned)(qbase + 127 - (e & 127));
+                        lds_max_u64(&lds_col[j],
                                     ((unsigned long long)vb << 32) | (unsigned long long)(0xFFFFFFFFu - gq));
+                    }
+                };
+                // merge the 128-train group's top-2 into the running (best, argbest, second)
+                auto row_merge = [&](int gbase) {
+#pragma unroll
+                    for (int c = 0; c < QT; ++c) {
+                        const int v1 = tb[c] >> 7, v2 = ts[c] >> 7;
+                        const int j1 = gbase + 127 - (tb[c] & 127);
+                        const bool up = v1 > B1[c];
+                        B2[c] = up ? max(B1[c], v2) : max(B2[c], v1);
+                        J1[c] = up ? j1 : J1[c];
+                        B1[c] = max(B1[c], v1);
+                        tb[c] = INT_MIN; ts[c] = INT_MIN;
                     }
                 };
                 // lds_col is its own __shared__ object, disjoint from the LDS-DMA staging buffers, so
                 // these atomics need not wait for the in-flight DMA of the next chunk.
-                for (int tt = 0; tt < nt; ++tt) col_merge(tt, tile(tt));
-                // merge the chunk's top-2 into the running (best, argbest, second)
-#pragma unroll
-                for (int c = 0; c < QT; ++c) {
-                    const int v1 = tb[c] >> 8, v2 = ts[c] >> 8;
-                    const int j1 = ((ch * CHUNK) & ~255) + 255 - (tb[c] & 255);
-                    const bool up = v1 > B1[c];
-                    B2[c] = up ? max(B1[c], v2) : max(B2[c], v1);
-                    J1[c] = up ? j1 : J1[c];
-                    B1[c] = max(B1[c], v1);
-                    tb[c] = INT_MIN; ts[c] = INT_MIN;
+                for (int tt = 0; tt < nt; ++tt) {
+                    col_merge(tt, tile(tt));
+                    if ((tt & 3) == 3 || tt == nt - 1) row_merge(ch * CHUNK + (tt & ~3) * 32);
                 }
             }
     };
@@ -402,10 +430,10 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
             unsigned long long best = 0;
             for (int q = 0; q < n_qblk; ++q) best = max(best, cp[(size_t)q * k_pad + j]);
             if (best == 0) continue;
-            const int v = (int)((unsigned)(best >> 32) ^ 0x80000000u);
+            const int v = (int)((unsigned)(best >> 32) ^ 0x80000000u);  // -d^2
             const int gq = (int)(0xFFFFFFFFu - (unsigned)best);
             if (gq < 0 || gq >= na) continue;  // defensive: a column winner is always a query
-            const long long d = (long long)norm[(size_t)b * k_pad + j] - v;
+            const long long d = -(long long)v;
             atomicMin(&lds_best[gq], ((unsigned long long)d << 32) | (unsigned)j);
         }
         __syncthreads();
@@ -432,10 +460,10 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
             if (i < na) {
                 const int4 rr = rowres[(size_t)p * k_pad + i];
                 j = rr.y;
-                if (j >= 0 && j < nb && rr.x > ROW_VALID_MIN) {
+                if (j >= 0 && j < nb && rr.x > VALID_MIN) {
                     const long long nx = norm[(size_t)a * k_pad + i];
                     d1 = nx - rr.x;
-                    const long long d2 = (rr.z > ROW_VALID_MIN) ? nx - rr.z : sfm::DIST_INF;
+                    const long long d2 = (rr.z > VALID_MIN) ? nx - rr.z : sfm::DIST_INF;
                     keep = true;
                     if (xc == SFM_XC_MUTUAL) {
                         unsigned long long best = 0;

@@ -14,7 +14,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsfmcore.so")
+# SFMCORE_LIB: an alternative build of the same library (A/B timing of kernel variants only).
+LIB_PATH = os.environ.get("SFMCORE_LIB") or os.path.join(_HERE, "lib", "libsfmcore.so")
 
 METRIC_L2, METRIC_HAMMING = 0, 1
 XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
