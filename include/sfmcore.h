@@ -130,6 +130,41 @@ int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* pp
                const int32_t* cam_obs, double loss_s, double* U, double* V, double* W,
                double* gc, double* gp, double* res, double* cost);
 
+/* ---- bundle-adjustment step (LM with Schur complement + PCG) ----------------------------------
+ * SURVEY.md §8f item 3 ("rest of incremental SfM for cfg5"): the step of paper eq. (1) that the
+ * empty code/3d_reconstruction.py would take after the J^TJ build above.  Spec: DESIGN.md §4.5,
+ * restated by oracle/ba_lm.py.
+ *
+ * sfm_ba_solve: solves the Marquardt-damped normal equations of sfm_ba_jtj's blocks,
+ *     [U + λ D_U   W ; Wᵀ   V + λ D_V] [dc; dp] = -[gc; gp],  D = clamp(diag, 1e-6, 1e32),
+ *   by the Schur complement on the points and block-Jacobi preconditioned CG on the cameras
+ *   (S is never formed), then back-substitutes dp.  Same CSR inputs as sfm_ba_jtj
+ *   (observations point-major).  Stops when |r| <= tol |b| or after max_iter iterations.
+ *   out (device): dc [n_cam][8], dp [n_pt][3],
+ *   info [5] f64 = {CG iterations, |r|/|b|, gᵀδ, δᵀ JᵀJ δ (undamped), preconditioner fallback}
+ *   — the LM predicted decrease is -(gᵀδ + ½ δᵀ JᵀJ δ).
+ * sfm_ba_cost:   cost = 0.5 Σ ρ(|r|²) at the given parameters (no Jacobians).
+ * sfm_ba_update: cams_out = cams ⊕ dc (R <- exp([δr]x) R, the tangent space of the Jacobians;
+ *   t, f, k1 additive), pts_out = pts + dp.  Out-of-place.
+ */
+typedef struct sfm_ba_solve_params {
+    double lambda;    /* Marquardt damping λ (>= 0) */
+    double tol;       /* relative CG residual |r|/|b| */
+    int32_t max_iter; /* CG iteration cap */
+    int32_t _pad;
+} sfm_ba_solve_params;
+
+int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+                 const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
+                 const int32_t* cam_ptr, const int32_t* cam_obs, const double* U, const double* V,
+                 const double* W, const double* gc, const double* gp,
+                 const sfm_ba_solve_params* prm, double* dc, double* dp, double* info);
+int sfm_ba_cost(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* pp, int32_t n_pt,
+                const double* pts, int32_t n_obs, const int32_t* cam_idx, const int32_t* pt_idx,
+                const double* uv, double loss_s, double* cost);
+int sfm_ba_update(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* dc, int32_t n_pt,
+                  const double* pts, const double* dp, double* cams_out, double* pts_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -343,6 +343,138 @@ __global__ __launch_bounds__(256) void ba_final_kernel(int n_cam, int splits,
     }
 }
 
+// ---- LM support: cost at trial parameters, parameter update -----------------
+
+// Residual and rho only (linearize() without the Jacobians): same ops as linearize's residual.
+__device__ __forceinline__ void rotmat(double r0v, double r1v, double r2v, double (&R)[9]) {
+    const double th2 = r0v * r0v + r1v * r1v + r2v * r2v;
+    if (th2 > 1e-20) {
+        const double th = sqrt(th2);
+        double s, c;
+        sincos(th, &s, &c);
+        const double C = 1.0 - c;
+        const double kx = r0v / th, ky = r1v / th, kz = r2v / th;
+        R[0] = c + C * kx * kx;      R[1] = C * kx * ky - s * kz; R[2] = C * kx * kz + s * ky;
+        R[3] = C * ky * kx + s * kz; R[4] = c + C * ky * ky;      R[5] = C * ky * kz - s * kx;
+        R[6] = C * kz * kx - s * ky; R[7] = C * kz * ky + s * kx; R[8] = c + C * kz * kz;
+    } else {
+        R[0] = 1.0;  R[1] = -r2v; R[2] = r1v;
+        R[3] = r2v;  R[4] = 1.0;  R[5] = -r0v;
+        R[6] = -r1v; R[7] = r0v;  R[8] = 1.0;
+    }
+}
+
+// Thread per observation: 0.5 rho, summed per block in a fixed order; blocks summed by the
+// ba_cost_final kernel in a fixed order.
+__global__ __launch_bounds__(256) void ba_cost_kernel(
+    int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
+    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
+    const int32_t* __restrict__ pt_idx, const double* __restrict__ uv, double loss_s,
+    double* __restrict__ part) {
+    __shared__ double red[4];
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    double h = 0.0;
+    if (o < n_obs) {
+        const int c = cam_idx[o], p = pt_idx[o];
+        const double* cam = cams + 8 * (size_t)c;
+        double R[9];
+        rotmat(cam[0], cam[1], cam[2], R);
+        const double X0 = pts[3 * (size_t)p], X1 = pts[3 * (size_t)p + 1], X2 = pts[3 * (size_t)p + 2];
+        double P[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) P[i] = (R[3 * i] * X0 + R[3 * i + 1] * X1 + R[3 * i + 2] * X2) + cam[3 + i];
+        const double iz = 1.0 / P[2];
+        const double p0 = P[0] * iz, p1 = P[1] * iz;
+        const double f = cam[6], k1 = cam[7];
+        const double d = 1.0 + k1 * (p0 * p0 + p1 * p1);
+        const double e0 = f * d * p0 + pp[2 * (size_t)c] - uv[2 * (size_t)o];
+        const double e1 = f * d * p1 + pp[2 * (size_t)c + 1] - uv[2 * (size_t)o + 1];
+        const double e = e0 * e0 + e1 * e1;
+        double rho = e;
+        if (loss_s > 0.0) {
+            const double s2 = loss_s * loss_s;
+            rho = s2 * log1p(e / s2);
+        }
+        h = 0.5 * rho;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) h += __shfl_down(h, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ __launch_bounds__(1024) void ba_cost_final(int n_blk, const double* __restrict__ part,
+                                                      double* __restrict__ cost) {
+    __shared__ double red[16];
+    const int tid = threadIdx.x;
+    double a = 0.0;
+    for (int k = tid; k < n_blk; k += 1024) a += part[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) a += __shfl_down(a, off, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        double s = 0.0;
+        for (int w = 0; w < 16; ++w) s += red[w];
+        *cost = s;
+    }
+}
+
+// cams ⊕ dc: R <- exp([δr]x) R (the left increment the Jacobians are taken in), t, f, k1
+// additive; points additive.  Thread per camera / point.  Mirrors oracle/ba_lm.py update().
+__global__ __launch_bounds__(256) void ba_update_kernel(int n_cam, const double* __restrict__ cams,
+                                                        const double* __restrict__ dc, int n_pt,
+                                                        const double* __restrict__ pts,
+                                                        const double* __restrict__ dp,
+                                                        double* __restrict__ cams_out,
+                                                        double* __restrict__ pts_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_cam) {
+        const double* c = cams + 8 * (size_t)i;
+        const double* d = dc + 8 * (size_t)i;
+        double A[9], B[9], R[9];
+        rotmat(d[0], d[1], d[2], A);
+        rotmat(c[0], c[1], c[2], B);
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                R[3 * r + k] = A[3 * r] * B[k] + A[3 * r + 1] * B[3 + k] + A[3 * r + 2] * B[6 + k];
+        // log map, stable near 0 and pi
+        const double cs = fmin(fmax(0.5 * ((R[0] + R[4] + R[8]) - 1.0), -1.0), 1.0);
+        const double w0 = R[7] - R[5], w1 = R[2] - R[6], w2 = R[3] - R[1];
+        const double sn = 0.5 * sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+        const double th = atan2(sn, cs);
+        double o0, o1, o2;
+        if (sn > 1e-7) {
+            const double k = th / (2.0 * sn);
+            o0 = w0 * k; o1 = w1 * k; o2 = w2 * k;
+        } else if (cs > 0.0) {
+            o0 = 0.5 * w0; o1 = 0.5 * w1; o2 = 0.5 * w2;
+        } else {  // th ~ pi: axis from the largest diagonal column of (R + I) / 2
+            const double B0 = 0.5 * (R[0] + 1.0), B4 = 0.5 * (R[4] + 1.0), B8 = 0.5 * (R[8] + 1.0);
+            const int j = (B0 >= B4 && B0 >= B8) ? 0 : (B4 >= B8 ? 1 : 2);
+            const double bjj = j == 0 ? B0 : (j == 1 ? B4 : B8);
+            const double sq = sqrt(bjj);
+            double a0 = (j == 0 ? B0 : 0.5 * R[j]) / sq;          // column j of B = (R+I)/2
+            double a1 = (j == 1 ? B4 : 0.5 * R[3 + j]) / sq;
+            double a2 = (j == 2 ? B8 : 0.5 * R[6 + j]) / sq;
+            if (a0 * w0 + a1 * w1 + a2 * w2 < 0.0) { a0 = -a0; a1 = -a1; a2 = -a2; }
+            const double n = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
+            o0 = th * a0 / n; o1 = th * a1 / n; o2 = th * a2 / n;
+        }
+        double* out = cams_out + 8 * (size_t)i;
+        out[0] = o0; out[1] = o1; out[2] = o2;
+#pragma unroll
+        for (int k = 3; k < 8; ++k) out[k] = c[k] + d[k];
+    }
+    if (i < n_pt) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pts_out[3 * (size_t)i + k] = pts[3 * (size_t)i + k] + dp[3 * (size_t)i + k];
+    }
+}
+
 }  // namespace
 
 extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* pp,
@@ -404,5 +536,44 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
                            n_cam, splits, part, U, gc);
         SFM_HIP_CHECK(hipGetLastError());
     }
+    return SFM_OK;
+}
+
+extern "C" int sfm_ba_cost(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* pp,
+                           int32_t n_pt, const double* pts, int32_t n_obs, const int32_t* cam_idx,
+                           const int32_t* pt_idx, const double* uv, double loss_s, double* cost) {
+    SFM_REQUIRE(ctx != nullptr && cost != nullptr, "sfm_ba_cost: ctx/cost is NULL");
+    SFM_REQUIRE(n_cam >= 0 && n_pt >= 0 && n_obs >= 0, "sfm_ba_cost: negative size");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (n_obs == 0) {
+        SFM_HIP_CHECK(hipMemsetAsync(cost, 0, sizeof(double), st));
+        return SFM_OK;
+    }
+    SFM_REQUIRE(cams && pp && pts && cam_idx && pt_idx && uv, "sfm_ba_cost: NULL array");
+    const int nb = (n_obs + 255) / 256;
+    double* part = (double*)sfm::workspace(ctx, sizeof(double) * (size_t)nb + 256);
+    if (!part) return SFM_ERR_NOMEM;
+    hipLaunchKernelGGL(ba_cost_kernel, dim3(nb), dim3(256), 0, st, n_obs, cams, pp, pts, cam_idx,
+                       pt_idx, uv, loss_s, part);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(ba_cost_final, dim3(1), dim3(1024), 0, st, nb, part, cost);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
+extern "C" int sfm_ba_update(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* dc,
+                             int32_t n_pt, const double* pts, const double* dp, double* cams_out,
+                             double* pts_out) {
+    SFM_REQUIRE(ctx != nullptr, "sfm_ba_update: ctx is NULL");
+    SFM_REQUIRE(n_cam >= 0 && n_pt >= 0, "sfm_ba_update: negative size");
+    const int n = std::max(n_cam, n_pt);
+    if (n == 0) return SFM_OK;
+    SFM_REQUIRE((n_cam == 0 || (cams && dc && cams_out)) && (n_pt == 0 || (pts && dp && pts_out)),
+                "sfm_ba_update: NULL array");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(ba_update_kernel, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, n_cam,
+                       cams, dc, n_pt, pts, dp, cams_out, pts_out);
+    SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }

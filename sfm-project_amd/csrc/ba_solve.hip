@@ -1,0 +1,748 @@
+// Bundle-adjustment step solve (K4): the damped normal
+// equations of the J^TJ blocks that sfm_ba_jtj builds, reduced to the cameras by the Schur
+// complement and solved by block-Jacobi preconditioned CG without forming S (Ceres'
+// ITERATIVE_SCHUR + SCHUR_JACOBI):
+//     [U_d  W ; Wᵀ  V_d] [δc; δp] = -[g_c; g_p],   A_d = A + λ·clamp(diag A, 1e-6, 1e32)
+//     S δc = b,  S = U_d - Σ_o W_o V_d⁻¹ W_oᵀ,  b = -g_c + Σ_o W_o V_d⁻¹ g_p
+//     δp = V_d⁻¹ (-g_p - Σ_o W_oᵀ δc)
+// Restated on the CPU by oracle/ba_lm.py (schur_pcg), which the GPU tests compare against.
+//
+// fp64, deterministic (every sum has a fixed order; no float atomics).  Kernels:
+//   bas_point_setup     thread per point: V_d⁻¹ (3x3, adjugate), v_g = V_d⁻¹ g_p
+//   bas_camera_setup    block per camera: diagonal block of S (36 sums over the camera's
+//                       observations), its inverse (8x8 Cholesky) = the preconditioner, b, and
+//                       the CG start x = 0, r = b, z = M r, p = z
+//   CG iteration (3 launches, no host synchronisation; converged iterations exit at once):
+//     bas_pcg_point     8 lanes per point: t_p = V_d⁻¹ Σ_o W_oᵀ p_c     (SoA W, once)
+//     bas_pcg_camera    block per camera: q_c = U_d p_c - Σ_o W_o t_p   (SoA W, once)
+//     bas_pcg_vec       thread per camera component: α, x, r, z = M r, partial r·z, r·r
+//   bas_backsub         8 lanes per point: δp, and the point terms of gᵀδ and δᵀ(JᵀJ)δ
+//   bas_model           one block: gᵀδ, δᵀ(JᵀJ)δ (LM predicted decrease), iterations, |r|/|b|
+// HBM: a CG iteration reads W twice (2 x 192 B per observation) plus the camera/point vectors;
+// this stage is HBM-bound.
+#include <algorithm>
+
+#include "sfm_internal.h"
+
+namespace {
+
+constexpr double DIAG_MIN = 1e-6, DIAG_MAX = 1e32;
+constexpr int CT = 256;  // threads per camera block
+
+struct PcgState {
+    double beta;    // β_k of the current iteration (published by bas_pcg_point)
+    double rz;      // r·z of the current iterate
+    double bb;      // |b|^2
+    double rr;      // |r|^2 after the last step
+    int32_t iter;   // iterations done
+    int32_t done;   // converged (or max_iter reached)
+};
+
+__device__ __forceinline__ double dclamp(double d) { return fmin(fmax(d, DIAG_MIN), DIAG_MAX); }
+
+// Fixed-order block sum over CT threads of n values per thread (shuffle tree in each wave, then
+// the 4 wave partials in order).  Result valid in `red[i]` for i < n after the call.
+template <int N>
+__device__ __forceinline__ void block_sum(double (&a)[N], double (*red)[N], double* out) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double v = a[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
+        a[i] = v;
+    }
+    if ((tid & 63) == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) red[tid >> 6][i] = a[i];
+    }
+    __syncthreads();
+    if (tid < N) out[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    __syncthreads();
+}
+
+// ---- setup -------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void bas_point_setup(int n_pt, const int32_t* __restrict__ pt_ptr,
+                                                       const double* __restrict__ V,
+                                                       const double* __restrict__ gp, double lam,
+                                                       double* __restrict__ Vinv,
+                                                       double* __restrict__ vg) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pt) return;
+    double* Vi = Vinv + 9 * (size_t)p;
+    double* g = vg + 3 * (size_t)p;
+    if (pt_ptr[p + 1] == pt_ptr[p]) {  // unobserved point: δp = 0
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Vi[k] = 0.0;
+        g[0] = g[1] = g[2] = 0.0;
+        return;
+    }
+    const double* Vp = V + 9 * (size_t)p;
+    const double a = Vp[0] + lam * dclamp(Vp[0]), b = Vp[1], c = Vp[2];
+    const double d = Vp[4] + lam * dclamp(Vp[4]), e = Vp[5];
+    const double f = Vp[8] + lam * dclamp(Vp[8]);
+    // symmetric [[a b c][b d e][c e f]]: adjugate / determinant
+    const double A0 = d * f - e * e, A1 = c * e - b * f, A2 = b * e - c * d;
+    const double A4 = a * f - c * c, A5 = b * c - a * e, A8 = a * d - b * b;
+    const double inv = 1.0 / (a * A0 + b * A1 + c * A2);
+    const double m[9] = {A0 * inv, A1 * inv, A2 * inv, A1 * inv, A4 * inv,
+                         A5 * inv, A2 * inv, A5 * inv, A8 * inv};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Vi[k] = m[k];
+    const double* gg = gp + 3 * (size_t)p;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) g[i] = m[3 * i] * gg[0] + m[3 * i + 1] * gg[1] + m[3 * i + 2] * gg[2];
+}
+
+// Component-major (SoA) copies of W for the CG passes: Wp[24][n_obs] in observation (point-major)
+// order, Wc[24][n_obs] in camera-major order (cam_obs), ptc = pt_idx in camera-major order.  Each
+// pass then reads W with lane-contiguous 8-B loads instead of 192-B rows per lane; the copies
+// cost one read of W and two writes, once per solve.
+__global__ __launch_bounds__(256) void bas_soa(int n_obs, const int32_t* __restrict__ cam_obs,
+                                               const int32_t* __restrict__ pt_idx,
+                                               const double* __restrict__ W,
+                                               double* __restrict__ Wp, double* __restrict__ Wc,
+                                               int32_t* __restrict__ ptc) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_obs) return;
+    const size_t n = (size_t)n_obs;
+    const double2* a = (const double2*)(W + 24 * (size_t)e);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const double2 v = a[k];
+        Wp[(2 * k) * n + e] = v.x;
+        Wp[(2 * k + 1) * n + e] = v.y;
+    }
+    const int o = cam_obs[e];
+    ptc[e] = pt_idx[o];
+    const double2* b = (const double2*)(W + 24 * (size_t)o);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const double2 v = b[k];
+        Wc[(2 * k) * n + e] = v.x;
+        Wc[(2 * k + 1) * n + e] = v.y;
+    }
+}
+
+// 8x8 SPD inverse via Cholesky (one thread; 500-ish cameras).  Returns false if not SPD.
+__device__ bool inv8_spd(const double (&S)[64], double (&M)[64]) {
+    double L[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) L[k] = 0.0;
+    for (int j = 0; j < 8; ++j) {
+        double s = S[8 * j + j];
+        for (int k = 0; k < j; ++k) s -= L[8 * j + k] * L[8 * j + k];
+        if (!(s > 0.0)) return false;
+        const double ljj = sqrt(s);
+        L[8 * j + j] = ljj;
+        for (int i = j + 1; i < 8; ++i) {
+            double t = S[8 * i + j];
+            for (int k = 0; k < j; ++k) t -= L[8 * i + k] * L[8 * j + k];
+            L[8 * i + j] = t / ljj;
+        }
+    }
+    // M = L^-T L^-1, column by column: solve L y = e_c, then L^T m = y
+    for (int c = 0; c < 8; ++c) {
+        double y[8];
+        for (int i = 0; i < 8; ++i) {
+            double t = (i == c) ? 1.0 : 0.0;
+            for (int k = 0; k < i; ++k) t -= L[8 * i + k] * y[k];
+            y[i] = t / L[8 * i + i];
+        }
+        for (int i = 7; i >= 0; --i) {
+            double t = y[i];
+            for (int k = i + 1; k < 8; ++k) t -= L[8 * k + i] * M[8 * k + c];
+            M[8 * i + c] = t / L[8 * i + i];
+        }
+    }
+    return true;
+}
+
+// Block per camera: S_cc = U_d - Σ_o W_o V_d⁻¹ W_oᵀ (upper triangle, 36 sums) and
+// b_c = -g_c + Σ_o W_o v_g (8 sums) over the camera's observations (cam_obs order, lane-strided,
+// fixed tree); then the preconditioner block M_c = S_cc⁻¹ and the CG start.
+__global__ __launch_bounds__(CT) void bas_camera_setup(
+    int n_cam, int n_obs, const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ ptc,
+    const double* __restrict__ U, const double* __restrict__ Wc, const double* __restrict__ Vinv,
+    const double* __restrict__ vg, const double* __restrict__ gc, double lam,
+    double* __restrict__ Ud, double* __restrict__ Mc, double* __restrict__ x,
+    double* __restrict__ r, double* __restrict__ z, double* __restrict__ pv,
+    double* __restrict__ rz_c, double* __restrict__ bb_c, int32_t* __restrict__ bad) {
+    constexpr int N = 44;
+    __shared__ double red[4][N];
+    __shared__ double tot[N];
+    const int c = blockIdx.x, tid = threadIdx.x;
+    double acc[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc[i] = 0.0;
+    for (int e = cam_ptr[c] + tid; e < cam_ptr[c + 1]; e += CT) {
+        const int p = ptc[e];
+        const double* Vi = Vinv + 9 * (size_t)p;
+        const double* g = vg + 3 * (size_t)p;
+        double w[24], vi[9];
+#pragma unroll
+        for (int k = 0; k < 24; ++k) w[k] = Wc[k * (size_t)n_obs + e];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) vi[k] = Vi[k];
+        double wv[24];  // W_o V_d⁻¹ (8x3)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                wv[3 * i + j] = w[3 * i] * vi[j] + w[3 * i + 1] * vi[3 + j] + w[3 * i + 2] * vi[6 + j];
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = i; j < 8; ++j)
+                acc[t++] += wv[3 * i] * w[3 * j] + wv[3 * i + 1] * w[3 * j + 1] + wv[3 * i + 2] * w[3 * j + 2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[36 + i] += w[3 * i] * g[0] + w[3 * i + 1] * g[1] + w[3 * i + 2] * g[2];
+    }
+    block_sum<N>(acc, red, tot);
+    if (tid == 0) {
+        const double* Uc = U + 64 * (size_t)c;
+        double S[64], M[64], ud[64];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) ud[k] = Uc[k];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ud[9 * i] += lam * dclamp(Uc[9 * i]);
+        int t = 0;
+        for (int i = 0; i < 8; ++i)
+            for (int j = i; j < 8; ++j) {
+                S[8 * i + j] = ud[8 * i + j] - tot[t];
+                S[8 * j + i] = S[8 * i + j];
+                ++t;
+            }
+        if (!inv8_spd(S, M)) {
+            atomicOr(bad, 1);
+#pragma unroll
+            for (int k = 0; k < 64; ++k) M[k] = 0.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) M[9 * i] = 1.0 / fmax(S[9 * i], DIAG_MIN);
+        }
+        double* ud_o = Ud + 64 * (size_t)c;
+        double* m_o = Mc + 64 * (size_t)c;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) { ud_o[k] = ud[k]; m_o[k] = M[k]; }
+        double b[8], zz[8], rz = 0.0, bb = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) b[i] = tot[36 + i] - gc[8 * (size_t)c + i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += M[8 * i + j] * b[j];
+            zz[i] = s;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            x[8 * (size_t)c + i] = 0.0;
+            r[8 * (size_t)c + i] = b[i];
+            z[8 * (size_t)c + i] = zz[i];
+            pv[8 * (size_t)c + i] = 0.0;  // p_{-1}: p_0 = z_0 + 0 * p_{-1}
+            rz += b[i] * zz[i];
+            bb += b[i] * b[i];
+        }
+        rz_c[c] = rz;   // parity slot 0: rz_0
+        bb_c[c] = bb;   // |b|^2 share, also rr_0 (parity slot 0 of the rr partials)
+    }
+}
+
+// ---- CG iteration ------------------------------------------------------------------------------
+//
+// Three launches per iteration k and no communication between the blocks of a launch (kernel
+// boundaries are the only grid-wide synchronisation, so no fences or flags):
+//   bas_pcg_point(k)   t = V_d⁻¹ Wᵀ p_k,   p_k = z_k + β_k p_{k-1} formed on the fly
+//   bas_pcg_camera(k)  p_k stored; q = U_d p_k - W t; per-camera p·q
+//   bas_pcg_vec(k)     α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera r·z, r·r
+// The CG scalars are fixed-order sums of the per-camera partials that every block recomputes with
+// the same code (canon_sum), so every block of every kernel sees bit-identical α, β and the same
+// convergence decision.  Partials that a launch both reads and writes are double-buffered by the
+// parity of k; once converged, bas_pcg_vec carries the partials into the next slot, so the
+// decision sticks for the remaining (empty) launches.
+
+// Canonical fixed-order sum of a[0..n) by threads 0..255 of the block (any block size >= 256):
+// thread t sums a[t], a[t+256], ... in order; then a shuffle tree per wave and the 4 wave sums in
+// order.  Every caller gets the same bits for the same data.
+__device__ double canon_sum(const double* __restrict__ a, int n, double* red4) {
+    const int tid = threadIdx.x;
+    double v = 0.0;
+    if (tid < 256)
+        for (int i = tid; i < n; i += 256) v += a[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
+    __syncthreads();
+    if (tid < 256 && (tid & 63) == 0) red4[tid >> 6] = v;
+    __syncthreads();
+    const double s = ((red4[0] + red4[1]) + red4[2]) + red4[3];
+    __syncthreads();
+    return s;
+}
+
+struct Scalars {
+    double beta;  // β_k (0 at k = 0)
+    double rz;    // rz_k
+    bool done;    // converged before iteration k
+};
+
+// The CG scalars of iteration k from the per-camera partials, one pass over the three arrays
+// (rz partials: rzc[2][n_cam], slot k&1 = rz_k; rr partials rrc[2][n_cam] likewise): each sum has
+// canon_sum's association, so every block of every kernel gets the same bits.
+__device__ Scalars pcg_scalars(int k, int n_cam, const double* __restrict__ rzc,
+                               const double* __restrict__ rrc, double bb, double tol,
+                               double* red4x3) {
+    const int tid = threadIdx.x;
+    const double* a0 = rzc + (size_t)(k & 1) * n_cam;
+    const double* a1 = rrc + (size_t)(k & 1) * n_cam;
+    const double* a2 = rzc + (size_t)((k + 1) & 1) * n_cam;
+    const bool nb = k > 0;
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+    if (tid < 256)
+        for (int i = tid; i < n_cam; i += 256) {
+            v0 += a0[i];
+            v1 += a1[i];
+            if (nb) v2 += a2[i];
+        }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        v0 += __shfl_down(v0, off, 64);
+        v1 += __shfl_down(v1, off, 64);
+        v2 += __shfl_down(v2, off, 64);
+    }
+    __syncthreads();
+    if (tid < 256 && (tid & 63) == 0) {
+        red4x3[tid >> 6] = v0;
+        red4x3[4 + (tid >> 6)] = v1;
+        red4x3[8 + (tid >> 6)] = v2;
+    }
+    __syncthreads();
+    const double* r = red4x3;
+    Scalars sc;
+    sc.rz = ((r[0] + r[1]) + r[2]) + r[3];
+    const double rr = ((r[4] + r[5]) + r[6]) + r[7];
+    sc.beta = nb ? sc.rz / (((r[8] + r[9]) + r[10]) + r[11]) : 0.0;
+    sc.done = !(bb > 0.0) || rr <= tol * tol * bb;
+    __syncthreads();
+    return sc;
+}
+
+#ifndef SFM_BA_PG
+#define SFM_BA_PG 8
+#endif
+#ifndef SFM_BA_CC
+#define SFM_BA_CC 256
+#endif
+constexpr int PG = SFM_BA_PG;  // lanes per point in the point-major passes
+
+// PG lanes per point: t_p = V_d⁻¹ Σ_o W_oᵀ p_c.  Lane j of a point takes its observations
+// j, j+PG, ... in order; the PG partial sums are combined by a fixed shuffle tree.
+__global__ __launch_bounds__(256) void bas_pcg_point(
+    int k, int n_pt, int n_cam, int n_obs, const int32_t* __restrict__ pt_ptr,
+    const int32_t* __restrict__ cam_idx, const double* __restrict__ Wp,
+    const double* __restrict__ Vinv, const double* __restrict__ z, const double* __restrict__ pold,
+    const double* __restrict__ rzc, const double* __restrict__ rrc, double tol,
+    PcgState* __restrict__ st, double* __restrict__ t) {
+    __shared__ double red4[12];
+    const int g = blockIdx.x * (blockDim.x / PG) + threadIdx.x / PG;
+    const int j = threadIdx.x % PG;
+    const bool valid = g < n_pt;
+    const int o0 = (valid ? pt_ptr[g] : 0) + j;
+    const int o1 = valid ? pt_ptr[g + 1] : 0;
+    const size_t n = (size_t)n_obs;
+    // the lane's first observation is loaded before the CG scalars are reduced, so the two
+    // latencies overlap (the whole grid is resident at once: this pass is latency-bound)
+    double w[24], zc[8], pc[8];
+    const bool has = o0 < o1;
+    {
+        const int oo = has ? o0 : 0;
+        const int c = has ? cam_idx[oo] : 0;
+#pragma unroll
+        for (int m = 0; m < 24; ++m) w[m] = has ? Wp[m * n + oo] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            zc[i] = z[8 * (size_t)c + i];
+            pc[i] = pold[8 * (size_t)c + i];
+        }
+    }
+    const Scalars sc = pcg_scalars(k, n_cam, rzc, rrc, st->bb, tol, red4);
+    // every block computed the same scalars; block 0 publishes them for the camera and vector
+    // kernels of this iteration (the kernel boundary orders the store before their reads)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->beta = sc.beta;
+        st->rz = sc.rz;
+        st->done = sc.done ? 1 : 0;
+    }
+    if (sc.done) return;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    if (has) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double xi = zc[i] + sc.beta * pc[i];  // p_k, the same expression as bas_pcg_camera
+            s0 += w[3 * i] * xi;
+            s1 += w[3 * i + 1] * xi;
+            s2 += w[3 * i + 2] * xi;
+        }
+    }
+    for (int o = o0 + PG; o < o1; o += PG) {
+        const double* Wo = Wp + o;
+        const int c = cam_idx[o];
+        const double* zp = z + 8 * (size_t)c;
+        const double* pp = pold + 8 * (size_t)c;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double xi = zp[i] + sc.beta * pp[i];
+            s0 += Wo[(3 * i) * n] * xi;
+            s1 += Wo[(3 * i + 1) * n] * xi;
+            s2 += Wo[(3 * i + 2) * n] * xi;
+        }
+    }
+#pragma unroll
+    for (int off = PG / 2; off >= 1; off >>= 1) {
+        s0 += __shfl_down(s0, off, PG);
+        s1 += __shfl_down(s1, off, PG);
+        s2 += __shfl_down(s2, off, PG);
+    }
+    if (valid && j == 0) {
+        const double* Vi = Vinv + 9 * (size_t)g;
+        double* tp = t + 3 * (size_t)g;
+        tp[0] = Vi[0] * s0 + Vi[1] * s1 + Vi[2] * s2;
+        tp[1] = Vi[3] * s0 + Vi[4] * s1 + Vi[5] * s2;
+        tp[2] = Vi[6] * s0 + Vi[7] * s1 + Vi[8] * s2;
+    }
+}
+
+constexpr int CC = SFM_BA_CC;  // threads per camera block in the CG camera pass
+
+// Block per camera: p_k stored; q_c = U_d p_c - Σ_o W_o t_p; p_c·q_c.
+__global__ __launch_bounds__(CC) void bas_pcg_camera(
+    int k, int n_cam, int n_obs, const int32_t* __restrict__ cam_ptr,
+    const int32_t* __restrict__ ptc, const double* __restrict__ Wc, const double* __restrict__ t,
+    const double* __restrict__ Ud, const double* __restrict__ z, double* __restrict__ pv,
+    const PcgState* __restrict__ st, double* __restrict__ q, double* __restrict__ pq) {
+    __shared__ double red[CC / 64][8];
+    __shared__ double pc_s[8];
+    if (st->done) return;
+    const double beta = st->beta;
+    const int c = blockIdx.x, tid = threadIdx.x;
+    double acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.0;
+    const size_t n = (size_t)n_obs;
+    for (int e = cam_ptr[c] + tid; e < cam_ptr[c + 1]; e += CC) {
+        const double* Wo = Wc + e;
+        const double* tp = t + 3 * (size_t)ptc[e];
+        const double t0 = tp[0], t1 = tp[1], t2 = tp[2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            acc[i] += Wo[(3 * i) * n] * t0 + Wo[(3 * i + 1) * n] * t1 + Wo[(3 * i + 2) * n] * t2;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        double v = acc[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
+        acc[i] = v;
+    }
+    if ((tid & 63) == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[tid >> 6][i] = acc[i];
+    }
+    if (tid < 8) {
+        const size_t kk = 8 * (size_t)c + tid;
+        const double pk = z[kk] + beta * pv[kk];  // p_k, the same expression as bas_pcg_point
+        pc_s[tid] = pk;
+    }
+    __syncthreads();
+    if (tid < 8) {
+        double wt = 0.0;
+#pragma unroll
+        for (int w = 0; w < CC / 64; ++w) wt += red[w][tid];
+        const double* u = Ud + 64 * (size_t)c + 8 * tid;
+        double sU = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sU += u[j] * pc_s[j];
+        const double qi = sU - wt;
+        q[8 * (size_t)c + tid] = qi;
+        pv[8 * (size_t)c + tid] = pc_s[tid];
+        double v = pc_s[tid] * qi;
+        v += __shfl_down(v, 4, 8);
+        v += __shfl_down(v, 2, 8);
+        v += __shfl_down(v, 1, 8);
+        if (tid == 0) pq[c] = v;
+    }
+}
+
+// Thread per (camera, component): α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera
+// r·z (slot (k+1)&1) and r·r (slot (k+1)&1).  A breakdown (p·q <= 0) stops the iteration.
+__global__ __launch_bounds__(256) void bas_pcg_vec(
+    int k, int n_cam, const double* __restrict__ Mc, double* __restrict__ x,
+    double* __restrict__ r, double* __restrict__ z, const double* __restrict__ pv,
+    const double* __restrict__ q, const double* __restrict__ pq, double* __restrict__ rzc,
+    double* __restrict__ rrc, PcgState* __restrict__ st) {
+    __shared__ double red4[4];
+    const bool done = st->done != 0;
+    const double rz_k = st->rz;
+    const int gi = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = gi >> 3, i = gi & 7;
+    const bool valid = c < n_cam;
+    const int s0 = k & 1, s1 = (k + 1) & 1;
+    if (done) {
+        // converged earlier: carry the partials forward so iteration k+1 sees the same sums
+        if (valid && i == 0) {
+            rzc[(size_t)s1 * n_cam + c] = rzc[(size_t)s0 * n_cam + c];
+            rrc[(size_t)s1 * n_cam + c] = rrc[(size_t)s0 * n_cam + c];
+        }
+        return;
+    }
+    const double pqs = canon_sum(pq, n_cam, red4);
+    const bool breakdown = !(pqs > 0.0);
+    const double alpha = breakdown ? 0.0 : rz_k / pqs;
+    double ri = 0.0;
+    if (valid) {
+        const size_t kk = 8 * (size_t)c + i;
+        x[kk] += alpha * pv[kk];
+        ri = r[kk] - alpha * q[kk];
+        r[kk] = ri;
+    }
+    double zi = 0.0;
+    const double* M = Mc + 64 * (size_t)(valid ? c : 0) + 8 * i;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zi += M[j] * __shfl(ri, (threadIdx.x & ~7) + j, 64);
+    double rz = ri * zi, rr = ri * ri;
+    rz += __shfl_down(rz, 4, 8); rr += __shfl_down(rr, 4, 8);
+    rz += __shfl_down(rz, 2, 8); rr += __shfl_down(rr, 2, 8);
+    rz += __shfl_down(rz, 1, 8); rr += __shfl_down(rr, 1, 8);
+    if (valid) {
+        z[8 * (size_t)c + i] = zi;
+        if (i == 0) {
+            rzc[(size_t)s1 * n_cam + c] = rz;
+            rrc[(size_t)s1 * n_cam + c] = breakdown ? 0.0 : rr;
+        }
+    }
+    if (gi == 0) st->iter = k + 1;
+}
+
+// One block: |b|^2 (canonical sum of the setup's per-camera shares) and the iteration count.
+__global__ __launch_bounds__(256) void bas_pcg_init(int n_cam, const double* __restrict__ bb_c,
+                                                    PcgState* __restrict__ st) {
+    __shared__ double red4[4];
+    const double bb = canon_sum(bb_c, n_cam, red4);
+    if (threadIdx.x == 0) {
+        st->bb = bb;
+        st->rz = 0.0;
+        st->rr = bb;
+        st->iter = 0;
+        st->done = 0;
+    }
+}
+
+// Fixed-order sum over a 1024-thread block (16 waves); returns the total to every thread.
+__device__ __forceinline__ double block_sum1024(double v, double* red) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
+    const int tid = threadIdx.x;
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) s += red[w];
+    __syncthreads();
+    return s;
+}
+
+// ---- back-substitution and the LM model terms -------------------------------------------------
+
+// Thread per point: δp = -v_g - V_d⁻¹ Σ_o W_oᵀ δc; per-point share of gᵀδ + ... :
+//   mterm[p] = (g_p·δp,  δpᵀ V δp + 2 Σ_o δc_cᵀ W_o δp)   (the undamped JᵀJ)
+__global__ __launch_bounds__(256) void bas_backsub(int n_pt, int n_obs,
+                                                   const int32_t* __restrict__ pt_ptr,
+                                                   const int32_t* __restrict__ cam_idx,
+                                                   const double* __restrict__ Wp,
+                                                   const double* __restrict__ V,
+                                                   const double* __restrict__ Vinv,
+                                                   const double* __restrict__ vg,
+                                                   const double* __restrict__ gp,
+                                                   const double* __restrict__ dc,
+                                                   double* __restrict__ dp,
+                                                   double* __restrict__ mpart) {
+    // PG lanes per point (as bas_pcg_point): lane j sums observations j, j+PG, ...
+    __shared__ double red[2][4];
+    const int g = blockIdx.x * (blockDim.x / PG) + threadIdx.x / PG;
+    const int j = threadIdx.x % PG;
+    const bool valid = g < n_pt;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const size_t n = (size_t)n_obs;
+    const int o1 = valid ? pt_ptr[g + 1] : 0;
+    for (int o = (valid ? pt_ptr[g] : 0) + j; o < o1; o += PG) {
+        const double* Wo = Wp + o;
+        const double* x = dc + 8 * (size_t)cam_idx[o];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double xi = x[i];
+            s0 += Wo[(3 * i) * n] * xi;
+            s1 += Wo[(3 * i + 1) * n] * xi;
+            s2 += Wo[(3 * i + 2) * n] * xi;
+        }
+    }
+#pragma unroll
+    for (int off = PG / 2; off >= 1; off >>= 1) {
+        s0 += __shfl_down(s0, off, PG);
+        s1 += __shfl_down(s1, off, PG);
+        s2 += __shfl_down(s2, off, PG);
+    }
+    double m0 = 0.0, m1 = 0.0;
+    if (valid && j == 0) {
+        const double* Vi = Vinv + 9 * (size_t)g;
+        const double* gv = vg + 3 * (size_t)g;
+        const double d0 = -gv[0] - (Vi[0] * s0 + Vi[1] * s1 + Vi[2] * s2);
+        const double d1 = -gv[1] - (Vi[3] * s0 + Vi[4] * s1 + Vi[5] * s2);
+        const double d2 = -gv[2] - (Vi[6] * s0 + Vi[7] * s1 + Vi[8] * s2);
+        dp[3 * (size_t)g] = d0;
+        dp[3 * (size_t)g + 1] = d1;
+        dp[3 * (size_t)g + 2] = d2;
+        const double* gg = gp + 3 * (size_t)g;
+        const double* Vp = V + 9 * (size_t)g;
+        m0 = gg[0] * d0 + gg[1] * d1 + gg[2] * d2;
+        const double v0 = Vp[0] * d0 + Vp[1] * d1 + Vp[2] * d2;
+        const double v1 = Vp[3] * d0 + Vp[4] * d1 + Vp[5] * d2;
+        const double v2 = Vp[6] * d0 + Vp[7] * d1 + Vp[8] * d2;
+        // Σ_o δcᵀ W_o δp = (Σ_o W_oᵀ δc)·δp = s·δp
+        m1 = d0 * v0 + d1 * v1 + d2 * v2 + 2.0 * (s0 * d0 + s1 * d1 + s2 * d2);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        m0 += __shfl_down(m0, off, 64);
+        m1 += __shfl_down(m1, off, 64);
+    }
+    const int tid = threadIdx.x;
+    if ((tid & 63) == 0) { red[0][tid >> 6] = m0; red[1][tid >> 6] = m1; }
+    __syncthreads();
+    if (tid == 0) {
+        mpart[2 * (size_t)blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        mpart[2 * (size_t)blockIdx.x + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    }
+}
+
+// One block: camera terms (g_c·δc, δcᵀ U δc) + the point-block partials -> info.
+//   info = {iterations, |r|/|b|, gᵀδ, δᵀ JᵀJ δ, preconditioner fallback (0/1)}
+__global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const double* __restrict__ U,
+                                                  const double* __restrict__ gc,
+                                                  const double* __restrict__ dc,
+                                                  const double* __restrict__ mpart,
+                                                  const double* __restrict__ rrc,
+                                                  const PcgState* __restrict__ st,
+                                                  const int32_t* __restrict__ bad,
+                                                  double* __restrict__ info) {
+    __shared__ double red[16];
+    const int tid = threadIdx.x;
+    double a = 0.0, b = 0.0;
+    for (int c = tid; c < n_cam; c += 1024) {
+        const double* Uc = U + 64 * (size_t)c;
+        const double* d = dc + 8 * (size_t)c;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += Uc[8 * i + j] * d[j];
+            b += d[i] * s;
+            a += gc[8 * (size_t)c + i] * d[i];
+        }
+    }
+    for (int k = tid; k < n_pblk; k += 1024) { a += mpart[2 * (size_t)k]; b += mpart[2 * (size_t)k + 1]; }
+    const double ga = block_sum1024(a, red);
+    const double qb = block_sum1024(b, red);
+    const int it = st->iter;
+    const double rr = canon_sum(rrc + (size_t)(it & 1) * n_cam, n_cam, red);
+    if (tid == 0) {
+        info[0] = (double)it;
+        info[1] = st->bb > 0.0 ? sqrt(rr / st->bb) : 0.0;
+        info[2] = ga;
+        info[3] = qb;
+        info[4] = (double)*bad;
+    }
+}
+
+}  // namespace
+
+extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+                            const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
+                            const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
+                            const double* V, const double* W, const double* gc, const double* gp,
+                            const sfm_ba_solve_params* prm, double* dc, double* dp,
+                            double* info) {
+    SFM_REQUIRE(ctx != nullptr && prm != nullptr, "sfm_ba_solve: ctx/prm is NULL");
+    SFM_REQUIRE(n_cam > 0 && n_pt >= 0 && n_obs >= 0, "sfm_ba_solve: bad size");
+    SFM_REQUIRE(prm->max_iter >= 0 && prm->lambda >= 0.0 && prm->tol >= 0.0,
+                "sfm_ba_solve: max_iter, lambda and tol must be >= 0");
+    SFM_REQUIRE(cam_idx && pt_idx && pt_ptr && cam_ptr && cam_obs && U && V && W && gc && gp && dc &&
+                    dp && info,
+                "sfm_ba_solve: NULL array");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int pblk = std::max(1, (n_pt + 255) / 256);
+    // workspace: Vinv 9 | vg 3 | t 3 per point; Ud 64 | M 64 | r z p q 8 each | rz, rr partials
+    // (2 parity slots each) | p·q per camera; backsub partials; state; bad flag
+    const size_t np = (size_t)std::max(n_pt, 1), nc = (size_t)n_cam;
+    const size_t b_pt = sfm::align_up(sizeof(double) * 15 * np, 256);
+    const size_t b_cam = sfm::align_up(sizeof(double) * (128 + 32 + 5) * nc, 256);
+    const int gblk = std::max(1, (n_pt + 256 / PG - 1) / (256 / PG));  // PG lanes per point
+    const size_t b_part = sfm::align_up(sizeof(double) * 2 * (size_t)gblk, 256);
+    const size_t no = (size_t)std::max(n_obs, 1);
+    const size_t b_soa = sfm::align_up(sizeof(double) * 48 * no + sizeof(int32_t) * no, 256);
+    char* ws = (char*)sfm::workspace(ctx, b_pt + b_cam + b_part + 512 + b_soa);
+    if (!ws) return SFM_ERR_NOMEM;
+    double* Vinv = (double*)ws;
+    double* vg = Vinv + 9 * np;
+    double* t = vg + 3 * np;
+    double* Ud = (double*)(ws + b_pt);
+    double* Mc = Ud + 64 * nc;
+    double* r = Mc + 64 * nc;
+    double* z = r + 8 * nc;
+    double* pv = z + 8 * nc;
+    double* q = pv + 8 * nc;
+    double* rzc = q + 8 * nc;   // [2][n_cam]
+    double* rrc = rzc + 2 * nc; // [2][n_cam]
+    double* pq = rrc + 2 * nc;
+    double* mpart = (double*)(ws + b_pt + b_cam);
+    PcgState* state = (PcgState*)(ws + b_pt + b_cam + b_part);
+    int32_t* bad = (int32_t*)(ws + b_pt + b_cam + b_part + 256);
+    double* Wp = (double*)(ws + b_pt + b_cam + b_part + 512);
+    double* Wc = Wp + 24 * no;
+    int32_t* ptc = (int32_t*)(Wc + 24 * no);
+    const double lam = prm->lambda, tol = prm->tol;
+    SFM_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int32_t), st));
+    if (n_pt > 0) {
+        hipLaunchKernelGGL(bas_point_setup, dim3(pblk), dim3(256), 0, st, n_pt, pt_ptr, V, gp, lam,
+                           Vinv, vg);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
+    if (n_obs > 0) {
+        hipLaunchKernelGGL(bas_soa, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs, cam_obs,
+                           pt_idx, W, Wp, Wc, ptc);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr, ptc,
+                       U, Wc, Vinv, vg, gc, lam, Ud, Mc, dc, r, z, pv, rzc, rrc, bad);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, rrc, state);
+    SFM_HIP_CHECK(hipGetLastError());
+    const int vblk = (8 * n_cam + 255) / 256;
+    for (int k = 0; k < prm->max_iter; ++k) {
+        hipLaunchKernelGGL(bas_pcg_point, dim3(gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
+                           pt_ptr, cam_idx, Wp, Vinv, z, pv, rzc, rrc, tol, state, t);
+        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
+                           ptc, Wc, t, Ud, z, pv, state, q, pq);
+        hipLaunchKernelGGL(bas_pcg_vec, dim3(vblk), dim3(256), 0, st, k, n_cam, Mc, dc, r, z, pv, q,
+                           pq, rzc, rrc, state);
+    }
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bas_backsub, dim3(gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr, cam_idx, Wp, V,
+                       Vinv, vg, gp, dc, dp, mpart);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, gblk, U, gc, dc, mpart, rrc,
+                       state, bad, info);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}

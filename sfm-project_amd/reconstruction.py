@@ -3,8 +3,11 @@ code/pipeline.py:4 because a module name cannot start with a digit).  `3d_recons
 this directory re-exports this module under the reference's file name.
 
 Scope: the bundle-adjustment linearisation — residuals, Jacobians and the
-J^TJ blocks of papers/schoenberger2016sfm.pdf eq. (1)/§4.4 — on the GPU.  The LM solve,
-triangulation and registration are "next" (SURVEY.md §8f).
+J^TJ blocks of papers/schoenberger2016sfm.pdf eq. (1)/§4.4 — on the GPU; and (SURVEY.md §8f
+item 3) the Levenberg-Marquardt step on them: Schur complement on the points, block-Jacobi PCG on
+the reduced camera system, back-substitution, the SO(3)-aware parameter update and the trial
+cost — `bundle_adjust` (restated by oracle/ba_lm.py).  Triangulation and
+next-view registration remain "next".
 """
 from __future__ import annotations
 
@@ -112,3 +115,90 @@ def build_jtj_sharded(cams, pp, pts, cam_idx, pt_idx, uv, rank: int, world: int,
     torch.cuda.synchronize(device)
     out["pt_range"] = (lo, hi)
     return out
+
+
+# ---- Levenberg-Marquardt bundle adjustment ---------------
+
+class BAProblem:
+    """Device-resident observations + CSR indices for repeated linearisation / solves."""
+
+    def __init__(self, pp, cam_idx, pt_idx, uv, n_cam: int, n_pt: int, device: int = 0):
+        import torch
+        cam_idx = np.asarray(cam_idx, np.int32)
+        pt_idx = np.asarray(pt_idx, np.int32)
+        uv = np.asarray(uv, np.float64)
+        self.order = None
+        if len(pt_idx) and np.any(np.diff(pt_idx) < 0):
+            self.order = np.argsort(pt_idx, kind="stable")
+            cam_idx, pt_idx, uv = cam_idx[self.order], pt_idx[self.order], uv[self.order]
+        pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
+        cam_ptr, cam_obs = sfmcore.csr_by(cam_idx, n_cam)
+        self.dev = torch.device("cuda", device)
+        T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dt)).to(self.dev)
+        self.pp = T(pp, np.float64)
+        self.cam_idx, self.pt_idx, self.uv = T(cam_idx), T(pt_idx), T(uv)
+        self.pt_ptr, self.cam_ptr, self.cam_obs = T(pt_ptr), T(cam_ptr), T(cam_obs)
+        self.n_cam, self.n_pt = n_cam, n_pt
+        self.ctx = sfmcore.context(device)
+
+    def linearize(self, cams, pts, loss_s=0.0):
+        return self.ctx.ba_jtj(cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv,
+                               self.pt_ptr, self.cam_ptr, self.cam_obs, loss_s=loss_s)
+
+    def solve(self, lin, lam, max_iter=100, tol=1e-10):
+        return self.ctx.ba_solve(lin, self.cam_idx, self.pt_idx, self.pt_ptr, self.cam_ptr,
+                                 self.cam_obs, lam, max_iter=max_iter, tol=tol)
+
+    def cost(self, cams, pts, loss_s=0.0):
+        return self.ctx.ba_cost(cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv, loss_s)
+
+    def update(self, cams, dc, pts, dp):
+        return self.ctx.ba_update(cams, dc, pts, dp)
+
+
+def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
+                  lam0: float = 1e-4, ftol: float = 1e-12, max_cg: int = 200,
+                  cg_tol: float = 1e-10, device: int = 0):
+    """Levenberg-Marquardt on paper eq. (1): every step on the GPU
+    (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
+    accept / reject it.
+
+    Step rule (oracle/ba_lm.py, Nielsen): predicted decrease = -(gᵀδ + ½ δᵀJᵀJδ); accept iff
+    the cost decreases, then λ *= max(1/3, 1 - (2ρ-1)³); otherwise λ *= ν, ν *= 2.  Stops after
+    `max_iter` steps, when an accepted step lowers the cost by <= ftol·cost, or when λ > 1e16.
+
+    Returns (cams [n_cam,8], pts [n_pt,3], history [(cost, λ, accepted, cg_iterations)])."""
+    import torch
+    n_cam, n_pt = len(cams), len(pts)
+    prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(prob.dev)
+    cams_d, pts_d = T(cams), T(pts)
+    lam, nu = lam0, 2.0
+    hist = []
+    old = float(prob.cost(cams_d, pts_d, loss_s).item())
+    lin = prob.linearize(cams_d, pts_d, loss_s)
+    for _ in range(max_iter):
+        dc, dp, info = prob.solve(lin, lam, max_cg, cg_tol)
+        c2, p2 = prob.update(cams_d, dc, pts_d, dp)
+        new_t = prob.cost(c2, p2, loss_s)
+        vals = torch.cat([info, new_t]).cpu().numpy()       # the one host sync of the step
+        it, gd, q, new = int(vals[0]), float(vals[2]), float(vals[3]), float(vals[5])
+        pred = -(gd + 0.5 * q)
+        if new < old and pred > 0:
+            rho = (old - new) / pred
+            cams_d, pts_d = c2, p2
+            lam *= max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3)
+            nu = 2.0
+            hist.append((new, lam, True, it))
+            done = old - new <= ftol * old
+            old = new
+            if done:
+                break
+            lin = prob.linearize(cams_d, pts_d, loss_s)
+        else:
+            lam *= nu
+            nu *= 2.0
+            hist.append((old, lam, False, it))
+            if lam > 1e16:
+                break
+    return cams_d.cpu().numpy(), pts_d.cpu().numpy(), hist

@@ -22,7 +22,8 @@ XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
 
 EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_sync",
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
-            "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows"]
+            "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
+            "sfm_ba_update"]
 
 
 class SfmCoreError(RuntimeError):
@@ -32,6 +33,11 @@ class SfmCoreError(RuntimeError):
 class MatchParams(C.Structure):
     _fields_ = [("metric", C.c_int32), ("cross_check", C.c_int32), ("ratio_num", C.c_int32),
                 ("ratio_den", C.c_int32), ("max_dist", C.c_int64)]
+
+
+class BaSolveParams(C.Structure):
+    _fields_ = [("lam", C.c_double), ("tol", C.c_double), ("max_iter", C.c_int32),
+                ("_pad", C.c_int32)]
 
 
 class RansacParams(C.Structure):
@@ -72,6 +78,10 @@ def load_library(path: str = LIB_PATH):
                                          C.POINTER(RansacParams), vp, vp, vp, vp, vp]
         L.sfm_ba_jtj.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp,
                                  vp, vp, vp, vp, vp, vp]
+        L.sfm_ba_solve.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                   C.POINTER(BaSolveParams), vp, vp, vp]
+        L.sfm_ba_cost.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp]
+        L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
         L.sfm_graph_offsets.argtypes = [vp, i32, vp, i32, vp]
         L.sfm_graph_rows.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp]
         for name in EXPORTED:
@@ -215,6 +225,49 @@ class Context:
                                    _ptr(cam_ptr), _ptr(cam_obs), float(loss_s), _ptr(U), _ptr(V),
                                    _ptr(W), _ptr(gc), _ptr(gp), _ptr(res), _ptr(cost)))
         return dict(U=U, V=V, W=W, gc=gc, gp=gp, res=res, cost=cost)
+
+    def ba_solve(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, max_iter=100,
+                 tol=1e-10, out=None):
+        """Damped Schur-complement PCG step from the ba_jtj blocks `lin`; returns
+        (dc [n_cam,8], dp [n_pt,3], info [5] f64 device tensor)."""
+        torch = self.torch
+        U = lin["U"]
+        dev = U.device
+        nc, npt, no = U.shape[0], lin["V"].shape[0], cam_idx.shape[0]
+        if out is None:
+            f64 = torch.float64
+            out = (torch.empty((nc, 8), dtype=f64, device=dev),
+                   torch.empty((npt, 3), dtype=f64, device=dev),
+                   torch.empty(5, dtype=f64, device=dev))
+        dc, dp, info = out
+        prm = BaSolveParams(float(lam), float(tol), int(max_iter), 0)
+        self._bind_stream()
+        _check(self.lib.sfm_ba_solve(self.handle, nc, npt, no, _ptr(cam_idx), _ptr(pt_idx),
+                                     _ptr(pt_ptr), _ptr(cam_ptr), _ptr(cam_obs), _ptr(U),
+                                     _ptr(lin["V"]), _ptr(lin["W"]), _ptr(lin["gc"]),
+                                     _ptr(lin["gp"]), C.byref(prm), _ptr(dc), _ptr(dp),
+                                     _ptr(info)))
+        return dc, dp, info
+
+    def ba_cost(self, cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0, out=None):
+        torch = self.torch
+        cost = out if out is not None else torch.empty(1, dtype=torch.float64, device=cams.device)
+        self._bind_stream()
+        _check(self.lib.sfm_ba_cost(self.handle, cams.shape[0], _ptr(cams), _ptr(pp),
+                                    pts.shape[0], _ptr(pts), cam_idx.shape[0], _ptr(cam_idx),
+                                    _ptr(pt_idx), _ptr(uv), float(loss_s), _ptr(cost)))
+        return cost
+
+    def ba_update(self, cams, dc, pts, dp, out=None):
+        """(cams ⊕ dc, pts + dp), out of place."""
+        torch = self.torch
+        if out is None:
+            out = (torch.empty_like(cams), torch.empty_like(pts))
+        co, po = out
+        self._bind_stream()
+        _check(self.lib.sfm_ba_update(self.handle, cams.shape[0], _ptr(cams), _ptr(dc),
+                                      pts.shape[0], _ptr(pts), _ptr(dp), _ptr(co), _ptr(po)))
+        return co, po
 
 
 _ctx_cache: dict = {}

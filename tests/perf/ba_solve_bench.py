@@ -1,0 +1,73 @@
+"""Times the bundle-adjustment step solve (K4) and a full LM step at cfg5 scale on one GPU.
+
+Usage: python tests/perf/ba_solve_bench.py [n_cam n_pt obs_per_pt [cg_iters]]
+Prints one JSON line: per-CG-iteration time and its HBM roofline (algorithmic bytes: W read twice
+= 384 B/obs + indices 12 B/obs + per point V_d⁻¹ 72 B, t 24 B written and read, pt_ptr 4 B),
+setup / back-substitution time, and one LM step (J^TJ + solve + update + trial cost).
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd")]
+
+import numpy as np
+import torch
+
+import reconstruction as R
+import synth
+
+PEAK_HBM = 8.0e12
+
+
+def timed(fn, reps):
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    a = [int(x) for x in sys.argv[1:]]
+    n_cam, n_pt, k = (a + [500, 100_000, 5][len(a):])[:3]
+    cg = a[3] if len(a) > 3 else 50
+    prob = synth.make_ba_problem(n_cam, n_pt, obs_per_pt=k, seed=0)
+    n_obs = len(prob["cam_idx"])
+    P = R.BAProblem(prob["pp"], prob["cam_idx"], prob["pt_idx"], prob["uv"], n_cam, n_pt)
+    T = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float64)).cuda()
+    cams, pts = T(prob["cams"]), T(prob["pts"])
+    lin = P.linearize(cams, pts)
+    lam = 1e-3
+    # tol = 0: exactly `cg` iterations (the convergence flag never fires)
+    t0 = timed(lambda: P.solve(lin, lam, max_iter=0, tol=0.0), 20)
+    tn = timed(lambda: P.solve(lin, lam, max_iter=cg, tol=0.0), 10)
+    per_it = (tn - t0) / cg
+    _, _, info = P.solve(lin, lam, max_iter=500, tol=1e-6)
+    it6 = int(info[0].item())
+    bytes_it = n_obs * (384 + 12) + n_pt * (72 + 24 + 24 + 4) + n_cam * (64 * 8 + 4 * 8 * 8)
+
+    def lm_step():
+        ln = P.linearize(cams, pts)
+        dc, dp, _ = P.solve(ln, lam, max_iter=it6, tol=1e-6)
+        c2, p2 = P.update(cams, dc, pts, dp)
+        P.cost(c2, p2)
+    t_step = timed(lm_step, 5)
+    t_jtj = timed(lambda: P.linearize(cams, pts), 10)
+    out = {
+        "stage": "K4 BA step (Schur-complement PCG)", "n_cam": n_cam, "n_pt": n_pt, "n_obs": n_obs,
+        "cg_iter_ms": per_it, "setup_backsub_ms": t0,
+        "roofline": {"bound": "hbm", "bytes_per_iter": bytes_it,
+                     "achieved_GBs": bytes_it / (per_it * 1e-3) / 1e9, "peak_GBs": PEAK_HBM / 1e9,
+                     "frac": bytes_it / (per_it * 1e-3) / PEAK_HBM},
+        "cg_iters_to_1e-6": it6, "lm_step_ms": t_step, "jtj_ms": t_jtj,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
