@@ -165,6 +165,33 @@ int sfm_ba_cost(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* p
 int sfm_ba_update(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* dc, int32_t n_pt,
                   const double* pts, const double* dp, double* cams_out, double* pts_out);
 
+/* ---- feature tracks ----------------------------------------------------------------------------
+ * the verified match graph (sfm_graph_rows) -> tracks, the input of
+ * triangulation and bundle adjustment.  Nodes are (image, keypoint), node = img_base[image] +
+ * keypoint (img_base [n_img + 1] i32, exclusive scan of the keypoint counts); each graph row
+ * (pair, queryIdx, trainIdx) joins node(pairs[pair][0], q) and node(pairs[pair][1], t).
+ * A track is a connected component with >= min_len nodes and at most one node per image;
+ * tracks are ordered by their smallest node id, nodes ascending within a track (deterministic).
+ *   out (device): n_tracks [1], track_ptr [n_tracks + 1] (capacity n_nodes + 1),
+ *                 track_img, track_kp [track_ptr[n_tracks]] (capacity n_nodes).
+ * Synchronises the stream (the component rounds are host-driven). */
+int sfm_tracks(sfm_ctx* ctx, int32_t n_img, const int32_t* img_base, int32_t n_pairs,
+               const int32_t* pairs, int64_t n_rows, const int32_t* rows, int32_t min_len,
+               int32_t* out_n_tracks, int32_t* out_track_ptr, int32_t* out_track_img,
+               int32_t* out_track_kp);
+
+/* ---- triangulation ---------------------------------------------------------------------------
+ * the points of the tracks (sfm_tracks) from posed cameras, the start of
+ * bundle adjustment.  Multi-view DLT on undistorted normalised coordinates (spec in
+ * csrc/triangulate.hip; restated by oracle/recon.py).  Observations point-major: pt_ptr [n_pt+1]
+ * CSR, cam_idx [n_obs] i32, uv [n_obs][2] f64; cams [n_cam][8], pp [n_cam][2] as sfm_ba_jtj.
+ *   out (device): pts [n_pt][3] f64; stats [n_pt][4] f64 = {mean reprojection error (px), largest
+ *   ray angle (deg), smallest depth, status: 0 ok, 1 < 2 views, 2 at infinity, 3 behind a camera}.
+ */
+int sfm_triangulate(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* pp,
+                    int32_t n_pt, const int32_t* pt_ptr, const int32_t* cam_idx, const double* uv,
+                    double* out_pts, double* out_stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,126 @@
+"""CPU restatement of the incremental-SfM steps after the match graph: feature tracks and
+multi-view triangulation.
+
+TEST INFRASTRUCTURE ONLY (see oracle.py): imported by tests/ as the checker of
+sfm-project_amd/csrc/tracks.hip and triangulate.hip.  The reference has no code for these steps
+(code/3d_reconstruction.py is empty), so they follow the build's spec:
+
+* tracks: nodes (image, keypoint) numbered image-major, node = img_base[image] + keypoint; every
+  verified match joins two nodes; a track is a connected component with >= min_len nodes and at
+  most one node per image; tracks ordered by their smallest node id, nodes ascending;
+* triangulation: multi-view DLT on undistorted normalised coordinates (10 fixed-point
+  undistortion steps), X = eigenvector of the smallest eigenvalue of M = AᵀA (numpy eigh here,
+  Jacobi on the GPU), plus per-point statistics and status (csrc/triangulate.hip header).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def tracks(img_base, pairs, rows, min_len=2):
+    """Union-find restatement.  Returns (track_ptr, track_img, track_kp) int32 arrays."""
+    img_base = np.asarray(img_base, np.int64)
+    n = int(img_base[-1]) if len(img_base) else 0
+    parent = np.arange(n, dtype=np.int64)
+
+    def find(x):
+        r = x
+        while parent[r] != r:
+            r = parent[r]
+        while parent[x] != r:                      # path compression
+            parent[x], x = r, parent[x]
+        return r
+
+    pairs = np.asarray(pairs, np.int64)
+    rows = np.asarray(rows, np.int64).reshape(-1, 3)
+    for p, q, t in rows:
+        u = int(img_base[pairs[p, 0]] + q)
+        v = int(img_base[pairs[p, 1]] + t)
+        ru, rv = find(u), find(v)
+        if ru != rv:                               # union by smaller root id: root = min node
+            if ru < rv:
+                parent[rv] = ru
+            else:
+                parent[ru] = rv
+    label = np.array([find(v) for v in range(n)], np.int64)
+    node_img = np.searchsorted(img_base, np.arange(n), side="right") - 1
+    order = np.argsort(label, kind="stable")
+    ptr, imgs, kps = [0], [], []
+    i = 0
+    while i < n:
+        j = i
+        while j < n and label[order[j]] == label[order[i]]:
+            j += 1
+        nodes = order[i:j]                          # ascending node ids (stable sort)
+        im = node_img[nodes]
+        if len(nodes) >= min_len and len(np.unique(im)) == len(im):
+            imgs.extend(im.tolist())
+            kps.extend((nodes - img_base[im]).tolist())
+            ptr.append(len(imgs))
+        i = j
+    return (np.asarray(ptr, np.int32), np.asarray(imgs, np.int32), np.asarray(kps, np.int32))
+
+
+UNDISTORT_ITERS = 10
+
+
+def _rotmat(r):
+    th2 = float(np.dot(r, r))
+    if th2 <= 1e-20:
+        return np.array([[1.0, -r[2], r[1]], [r[2], 1.0, -r[0]], [-r[1], r[0], 1.0]])
+    th = np.sqrt(th2)
+    k = r / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def triangulate(cams, pp, pt_ptr, cam_idx, uv):
+    """Multi-view DLT (spec: csrc/triangulate.hip header).  Returns (pts [n,3], stats [n,4]):
+    stats = mean reprojection error (px), largest ray angle (deg), smallest depth, status."""
+    cams = np.asarray(cams, np.float64)
+    pp = np.asarray(pp, np.float64)
+    uv = np.asarray(uv, np.float64)
+    n = len(pt_ptr) - 1
+    pts = np.zeros((n, 3))
+    stats = np.zeros((n, 4))
+    Rs = [_rotmat(c[:3]) for c in cams]
+    for p in range(n):
+        o0, o1 = int(pt_ptr[p]), int(pt_ptr[p + 1])
+        if o1 - o0 < 2:
+            stats[p, 3] = 1
+            continue
+        M = np.zeros((4, 4))
+        for o in range(o0, o1):
+            c = int(cam_idx[o])
+            f, k1 = cams[c, 6], cams[c, 7]
+            xd = (uv[o] - pp[c]) / f
+            x = xd.copy()
+            for _ in range(UNDISTORT_ITERS):
+                x = xd / (1.0 + k1 * np.dot(x, x))
+            P = np.hstack([Rs[c], cams[c, 3:6, None]])
+            rows = np.stack([x[0] * P[2] - P[0], x[1] * P[2] - P[1]])
+            M += rows.T @ rows
+        w, V = np.linalg.eigh(M)
+        h = V[:, int(np.argmin(w))]
+        if not abs(h[3]) > 1e-12 * np.linalg.norm(h[:3]):
+            stats[p, 3] = 2
+            continue
+        X = h[:3] / h[3]
+        pts[p] = X
+        err, dmin, cmax = 0.0, np.inf, 1.0
+        rays = []
+        for o in range(o0, o1):
+            c = int(cam_idx[o])
+            Pc = Rs[c] @ X + cams[c, 3:6]
+            dmin = min(dmin, Pc[2])
+            q = Pc[:2] / Pc[2]
+            pred = cams[c, 6] * (1.0 + cams[c, 7] * np.dot(q, q)) * q + pp[c]
+            err += np.linalg.norm(pred - uv[o])
+            rays.append(X + Rs[c].T @ cams[c, 3:6])
+        for i in range(len(rays)):
+            for j in range(i + 1, len(rays)):
+                a, b = rays[i], rays[j]
+                cmax = min(cmax, np.dot(a, b) / (np.linalg.norm(a) * np.linalg.norm(b)))
+        stats[p] = (err / (o1 - o0), np.degrees(np.arccos(np.clip(cmax, -1, 1))), dmin,
+                    0 if dmin > 0 else 3)
+    return pts, stats

@@ -203,6 +203,37 @@ def rows_to_pairs(rows: np.ndarray, pairs: np.ndarray):
     return out
 
 
+# ---- tracks (graph -> tracks -> triangulation / BA) ---------------------
+
+def build_tracks(rows, pairs, n_kp, min_len: int = 2, device: int = 0):
+    """Feature tracks of a verified match graph on the GPU (`sfm_tracks`).
+
+    rows [n,3] (pair, queryIdx, trainIdx), pairs [P,2] (image a, image b), n_kp [n_img] keypoints
+    per image (numpy or device tensors).  Returns (track_ptr [T+1], track_img [m], track_kp [m])
+    int32 device tensors: track t observes keypoint track_kp[i] of image track_img[i] for
+    i in [track_ptr[t], track_ptr[t+1]); at most one keypoint per image."""
+    import torch
+    dev = torch.device("cuda", device)
+    T = lambda a: (a.to(dev, torch.int32).contiguous() if isinstance(a, torch.Tensor)
+                   else torch.from_numpy(np.ascontiguousarray(a, np.int32)).to(dev))
+    n_kp = T(n_kp)
+    img_base = torch.zeros(n_kp.shape[0] + 1, dtype=torch.int32, device=dev)
+    img_base[1:] = torch.cumsum(n_kp, 0)
+    return sfmcore.context(device).tracks(img_base, T(pairs).reshape(-1, 2),
+                                          T(rows).reshape(-1, 3), min_len)
+
+
+def tracks_to_observations(track_ptr, track_img, track_kp, kps):
+    """BA observations of the tracks: (cam_idx = image, pt_idx = track, uv [m,2] f64) in
+    point-major order, the layout sfm_ba_jtj / sfm_ba_solve take.  kps [n_img, K, 2] (device)."""
+    import torch
+    counts = track_ptr[1:] - track_ptr[:-1]
+    pt_idx = torch.repeat_interleave(torch.arange(counts.shape[0], device=counts.device,
+                                                  dtype=torch.int32), counts.long())
+    uv = kps[track_img.long(), track_kp.long()].to(torch.float64)
+    return track_img, pt_idx, uv
+
+
 # ---- on-disk match graph (SURVEY.md §8f item 4) ------------------------------------------------
 
 GRAPH_FORMAT = "sfm-core match graph v1"

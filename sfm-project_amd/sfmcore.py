@@ -23,7 +23,7 @@ XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
 EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_sync",
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
-            "sfm_ba_update"]
+            "sfm_ba_update", "sfm_tracks", "sfm_triangulate"]
 
 
 class SfmCoreError(RuntimeError):
@@ -82,6 +82,8 @@ def load_library(path: str = LIB_PATH):
                                    C.POINTER(BaSolveParams), vp, vp, vp]
         L.sfm_ba_cost.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp]
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
+        L.sfm_triangulate.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]
+        L.sfm_tracks.argtypes = [vp, i32, vp, i32, vp, i64, vp, i32, vp, vp, vp, vp]
         L.sfm_graph_offsets.argtypes = [vp, i32, vp, i32, vp]
         L.sfm_graph_rows.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp]
         for name in EXPORTED:
@@ -225,6 +227,40 @@ class Context:
                                    _ptr(cam_ptr), _ptr(cam_obs), float(loss_s), _ptr(U), _ptr(V),
                                    _ptr(W), _ptr(gc), _ptr(gp), _ptr(res), _ptr(cost)))
         return dict(U=U, V=V, W=W, gc=gc, gp=gp, res=res, cost=cost)
+
+    def tracks(self, img_base, pairs, rows, min_len=2):
+        """Tracks of a verified match graph (device tensors): img_base [n_img+1] i32,
+        pairs [P,2] i32, rows [n,3] i32.  Returns (track_ptr [T+1], track_img [n], track_kp [n])
+        device i32 tensors, trimmed to the T tracks."""
+        torch = self.torch
+        dev = img_base.device
+        n_img = img_base.shape[0] - 1
+        n_nodes = int(img_base[-1].item()) if n_img > 0 else 0
+        cap = max(n_nodes, 1)
+        nt = torch.zeros(1, dtype=torch.int32, device=dev)
+        ptr = torch.zeros(cap + 1, dtype=torch.int32, device=dev)
+        ti = torch.empty(cap, dtype=torch.int32, device=dev)
+        tk = torch.empty(cap, dtype=torch.int32, device=dev)
+        self._bind_stream()
+        _check(self.lib.sfm_tracks(self.handle, n_img, _ptr(img_base), pairs.shape[0],
+                                   _ptr(pairs) if pairs.numel() else None, rows.shape[0],
+                                   _ptr(rows) if rows.numel() else None, int(min_len), _ptr(nt),
+                                   _ptr(ptr), _ptr(ti), _ptr(tk)))
+        T = int(nt.item())
+        total = int(ptr[T].item())
+        return ptr[:T + 1], ti[:total], tk[:total]
+
+    def triangulate(self, cams, pp, pt_ptr, cam_idx, uv):
+        """(pts [n_pt,3], stats [n_pt,4]) f64 device tensors; see include/sfmcore.h."""
+        torch = self.torch
+        n_pt = pt_ptr.shape[0] - 1
+        pts = torch.empty((max(n_pt, 0), 3), dtype=torch.float64, device=cams.device)
+        stats = torch.empty((max(n_pt, 0), 4), dtype=torch.float64, device=cams.device)
+        self._bind_stream()
+        _check(self.lib.sfm_triangulate(self.handle, cams.shape[0], _ptr(cams), _ptr(pp), n_pt,
+                                        _ptr(pt_ptr), _ptr(cam_idx), _ptr(uv), _ptr(pts),
+                                        _ptr(stats)))
+        return pts, stats
 
     def ba_solve(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, max_iter=100,
                  tol=1e-10, out=None):

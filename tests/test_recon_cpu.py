@@ -1,0 +1,91 @@
+"""CPU: the track / triangulation restatement (oracle/recon.py) against independent checks.
+
+Tracks vs scipy.sparse.csgraph.connected_components (labels canonicalised to the smallest node id)
+plus the one-keypoint-per-image rule, on random graphs with chains, repeated edges and conflicts.
+"""
+import numpy as np
+import pytest
+
+import recon
+
+
+def random_graph(rng, n_img=6, k=40, n_rows=300):
+    n_kp = rng.integers(k // 2, k, size=n_img)
+    pairs = np.array([(a, b) for a in range(n_img) for b in range(a + 1, n_img)], np.int32)
+    p = rng.integers(0, len(pairs), size=n_rows)
+    q = rng.integers(0, n_kp[pairs[p, 0]])
+    t = rng.integers(0, n_kp[pairs[p, 1]])
+    rows = np.stack([p, q, t], 1).astype(np.int32)
+    return n_kp, pairs, rows
+
+
+def scipy_tracks(n_kp, pairs, rows, min_len):
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+    base = np.r_[0, np.cumsum(n_kp)]
+    n = int(base[-1])
+    u = base[pairs[rows[:, 0], 0]] + rows[:, 1]
+    v = base[pairs[rows[:, 0], 1]] + rows[:, 2]
+    _, lab = connected_components(coo_matrix((np.ones(len(u)), (u, v)), shape=(n, n)),
+                                  directed=False)
+    canon = {}
+    for node in range(n):                    # smallest node id of each component
+        canon.setdefault(lab[node], node)
+    tracks = {}
+    for node in range(n):
+        tracks.setdefault(canon[lab[node]], []).append(node)
+    img = np.searchsorted(base, np.arange(n), side="right") - 1
+    out = []
+    for key in sorted(tracks):
+        nodes = tracks[key]
+        im = img[nodes]
+        if len(nodes) >= min_len and len(set(im.tolist())) == len(im):
+            out.append([(int(img[x]), int(x - base[img[x]])) for x in nodes])
+    return out
+
+
+@pytest.mark.parametrize("seed,min_len", [(0, 2), (1, 2), (2, 3), (3, 2)])
+def test_tracks_match_scipy_components(seed, min_len):
+    rng = np.random.default_rng(seed)
+    n_kp, pairs, rows = random_graph(rng, n_rows=int(rng.integers(50, 400)))
+    base = np.r_[0, np.cumsum(n_kp)].astype(np.int32)
+    ptr, ti, tk = recon.tracks(base, pairs, rows, min_len)
+    got = [list(zip(ti[a:b].tolist(), tk[a:b].tolist())) for a, b in zip(ptr[:-1], ptr[1:])]
+    assert got == scipy_tracks(n_kp, pairs, rows, min_len)
+
+
+def test_tracks_drop_same_image_conflicts():
+    # image 0 kp 1 - image 1 kp 2 - image 2 kp 3 - image 0 kp 4: a component with image 0 twice
+    n_kp = np.array([10, 10, 10])
+    pairs = np.array([[0, 1], [1, 2], [0, 2]], np.int32)
+    rows = np.array([[0, 1, 2], [1, 2, 3], [2, 4, 3], [0, 7, 7]], np.int32)
+    base = np.r_[0, np.cumsum(n_kp)].astype(np.int32)
+    ptr, ti, tk = recon.tracks(base, pairs, rows, 2)
+    assert ptr.tolist() == [0, 2] and ti.tolist() == [0, 1] and tk.tolist() == [7, 7]
+
+
+def _noise_free_problem(seed=0, n_cam=8, n_pt=200, k=4):
+    import synth
+    prob = synth.make_ba_problem(n_cam, n_pt, obs_per_pt=k, seed=seed, noise_px=0.0, perturb=0.0)
+    ptr = np.r_[0, np.cumsum(np.bincount(prob["pt_idx"], minlength=n_pt))].astype(np.int32)
+    return prob, ptr
+
+
+def test_triangulation_recovers_exact_points():
+    prob, ptr = _noise_free_problem()
+    pts, st = recon.triangulate(prob["cams"], prob["pp"], ptr, prob["cam_idx"], prob["uv"])
+    assert np.all(st[:, 3] == 0)
+    np.testing.assert_allclose(pts, prob["pts"], rtol=0, atol=1e-7)
+    assert st[:, 0].max() < 1e-6                         # px
+    assert np.all(st[:, 1] > 0.1) and np.all(st[:, 2] > 0)
+
+
+def test_triangulation_status_codes():
+    prob, ptr = _noise_free_problem(seed=1, n_pt=20)
+    ptr = ptr.copy()
+    # point 0 keeps a single observation: status 1
+    cam_idx, uv = prob["cam_idx"].copy(), prob["uv"].copy()
+    ptr2 = np.r_[0, 1, ptr[2:] - 3].astype(np.int32)    # drop 3 of point 0's 4 observations
+    keep = np.r_[0, np.arange(4, len(cam_idx))]
+    pts, st = recon.triangulate(prob["cams"], prob["pp"], ptr2, cam_idx[keep], uv[keep])
+    assert st[0, 3] == 1 and np.all(st[1:, 3] == 0)
