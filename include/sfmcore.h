@@ -192,6 +192,26 @@ int sfm_triangulate(sfm_ctx* ctx, int32_t n_cam, const double* cams, const doubl
                     int32_t n_pt, const int32_t* pt_ptr, const int32_t* cam_idx, const double* uv,
                     double* out_pts, double* out_stats);
 
+/* ---- next-view registration ---------------------------------------------------------------
+ * registers a batch of images against triangulated points (P3P RANSAC +
+ * Gauss-Newton refinement; spec in oracle/sfm_oracle_reg.c / csrc/register.hip).  Per image i:
+ * correspondences corr_ptr[i]..corr_ptr[i+1] of xy [n][2] f64 (pixels) and X [n][3] f64 (world),
+ * intrinsics intr [n_img][4] = (f, k1, cx, cy), img_id [n_img] (keys the hypothesis RNG).
+ * Hypothesis h of image i depends only on (seed, img_id[i], h): batch-composition invariant.
+ *   out (device): cams [n_img][8] (angle-axis, t, f, k1; zeros on failure), count [n_img]
+ *   (RANSAC inliers, -1 = no pose), key [n_img] (4 h + root of the winner, -1), mask [n] u8. */
+typedef struct sfm_register_params {
+    int32_t n_hyp;   /* multiple of 256 */
+    int32_t refine;  /* 1: Gauss-Newton on the inliers (10 steps) */
+    double thr;      /* inlier threshold, pixels */
+    uint64_t seed;
+} sfm_register_params;
+
+int sfm_register_batch(sfm_ctx* ctx, int32_t n_img, const int32_t* corr_ptr, const double* xy,
+                       const double* X, const double* intr, const int32_t* img_id,
+                       const sfm_register_params* prm, double* out_cams, int32_t* out_count,
+                       int32_t* out_key, uint8_t* out_mask);
+
 #ifdef __cplusplus
 }
 #endif

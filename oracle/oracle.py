@@ -62,6 +62,12 @@ def _bind(L):
     L.oracle_ba_jtj.argtypes = [i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp, vp, vp, vp, vp,
                                 vp]
     L.oracle_ba_jtj.restype = f64
+    L.oracle_reg_bearing.argtypes = [f64, f64, vp, vp]
+    L.oracle_reg_sample3.argtypes = [u64, u32, u32, i32, vp]
+    L.oracle_reg_p3p.argtypes = [vp, vp, vp, vp, vp]
+    L.oracle_reg_p3p.restype = i32
+    L.oracle_reg_ransac.argtypes = [i32, vp, vp, vp, u32, i32, u64, f64, vp, vp, vp, vp]
+    L.oracle_reg_ransac.restype = i32
 
 
 def match(A, B, metric=0, cross_check=XC_MUTUAL, ratio=None, max_dist=-1):
@@ -173,3 +179,42 @@ def ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0):
     cost = lib().oracle_ba_jtj(nc, _p(cams), _p(pp), npt, _p(pts), no, _p(cam_idx), _p(pt_idx),
                                _p(uv), loss_s, _p(U), _p(V), _p(W), _p(gc), _p(gp), _p(res))
     return dict(U=U, V=V, W=W, gc=gc, gp=gp, res=res, cost=cost)
+
+
+# ---- next-view registration (oracle/sfm_oracle_reg.c) ---------------------------------------------
+
+def reg_bearing(xy, intr):
+    intr = np.ascontiguousarray(intr, np.float64)
+    out = np.zeros((len(xy), 3))
+    b = np.zeros(3)
+    for i, (x, y) in enumerate(np.asarray(xy, np.float64)):
+        lib().oracle_reg_bearing(float(x), float(y), _p(intr), _p(b))
+        out[i] = b
+    return out
+
+
+def reg_sample3(seed, img, h, n):
+    out = np.zeros(3, np.int32)
+    lib().oracle_reg_sample3(seed, img, h, n, _p(out))
+    return out
+
+
+def reg_p3p(b, X):
+    b = np.ascontiguousarray(b, np.float64)
+    X = np.ascontiguousarray(X, np.float64)
+    Rs = np.zeros((4, 9)); ts = np.zeros((4, 3)); ok = np.zeros(4, np.int32)
+    lib().oracle_reg_p3p(_p(b), _p(X), _p(Rs), _p(ts), _p(ok))
+    return [(Rs[k].reshape(3, 3), ts[k]) if ok[k] else None for k in range(4)]
+
+
+def reg_ransac(xy, X, intr, img=0, n_hyp=1024, seed=42, thr=4.0):
+    """Returns dict(count, key, R [3,3], t [3], mask [n])."""
+    xy = np.ascontiguousarray(xy, np.float64)
+    X = np.ascontiguousarray(X, np.float64)
+    intr = np.ascontiguousarray(intr, np.float64)
+    n = len(xy)
+    key = np.zeros(1, np.int32)
+    R = np.zeros(9); t = np.zeros(3); mask = np.zeros(max(n, 1), np.uint8)
+    cnt = lib().oracle_reg_ransac(n, _p(xy), _p(X), _p(intr), img, n_hyp, seed, thr, _p(key),
+                                  _p(R), _p(t), _p(mask))
+    return dict(count=int(cnt), key=int(key[0]), R=R.reshape(3, 3), t=t, mask=mask[:n])

@@ -124,3 +124,45 @@ def triangulate(cams, pp, pt_ptr, cam_idx, uv):
         stats[p] = (err / (o1 - o0), np.degrees(np.arccos(np.clip(cmax, -1, 1))), dmin,
                     0 if dmin > 0 else 3)
     return pts, stats
+
+
+def reg_refine(R, t, xy, X, intr, mask, iters=10):
+    """Gauss-Newton pose refinement on the inliers (left rotation increment R <- exp([δ]x) R,
+    additive t), the spec of csrc/register.hip's final kernel.  Returns (R, t)."""
+    R = np.array(R, np.float64)
+    t = np.array(t, np.float64)
+    f, k1, cx, cy = intr
+    sel = np.asarray(mask, bool)
+    xy = np.asarray(xy, np.float64)[sel]
+    X = np.asarray(X, np.float64)[sel]
+    for _ in range(iters):
+        Y = X @ R.T
+        P = Y + t
+        iz = 1.0 / P[:, 2]
+        p0, p1 = P[:, 0] * iz, P[:, 1] * iz
+        rho2 = p0 * p0 + p1 * p1
+        d = 1.0 + k1 * rho2
+        e = np.stack([f * d * p0 + cx - xy[:, 0], f * d * p1 + cy - xy[:, 1]], 1)
+        m00 = f * (d + 2 * k1 * p0 * p0)
+        m01 = f * (2 * k1 * p0 * p1)
+        m11 = f * (d + 2 * k1 * p1 * p1)
+        Dm = np.zeros((len(X), 2, 3))
+        Dm[:, 0, 0] = iz; Dm[:, 0, 2] = -p0 * iz
+        Dm[:, 1, 1] = iz; Dm[:, 1, 2] = -p1 * iz
+        M = np.stack([np.stack([m00, m01], 1), np.stack([m01, m11], 1)], 1)
+        A = M @ Dm                                           # [n, 2, 3]
+        S = np.zeros((len(X), 3, 3))
+        S[:, 0, 1], S[:, 0, 2] = Y[:, 2], -Y[:, 1]
+        S[:, 1, 0], S[:, 1, 2] = -Y[:, 2], Y[:, 0]
+        S[:, 2, 0], S[:, 2, 1] = Y[:, 1], -Y[:, 0]
+        J = np.concatenate([A @ S, A], 2)                    # [n, 2, 6]
+        H = np.einsum("nai,naj->ij", J, J)
+        g = np.einsum("nai,na->i", J, e)
+        try:
+            L = np.linalg.cholesky(H)
+        except np.linalg.LinAlgError:
+            break
+        dx = np.linalg.solve(H, -g)
+        R = _rotmat(dx[:3]) @ R
+        t = t + dx[3:]
+    return R, t

@@ -23,7 +23,7 @@ XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
 EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_sync",
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
-            "sfm_ba_update", "sfm_tracks", "sfm_triangulate"]
+            "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch"]
 
 
 class SfmCoreError(RuntimeError):
@@ -38,6 +38,11 @@ class MatchParams(C.Structure):
 class BaSolveParams(C.Structure):
     _fields_ = [("lam", C.c_double), ("tol", C.c_double), ("max_iter", C.c_int32),
                 ("_pad", C.c_int32)]
+
+
+class RegisterParams(C.Structure):
+    _fields_ = [("n_hyp", C.c_int32), ("refine", C.c_int32), ("thr", C.c_double),
+                ("seed", C.c_uint64)]
 
 
 class RansacParams(C.Structure):
@@ -82,6 +87,8 @@ def load_library(path: str = LIB_PATH):
                                    C.POINTER(BaSolveParams), vp, vp, vp]
         L.sfm_ba_cost.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp]
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
+        L.sfm_register_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(RegisterParams),
+                                         vp, vp, vp, vp]
         L.sfm_triangulate.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]
         L.sfm_tracks.argtypes = [vp, i32, vp, i32, vp, i64, vp, i32, vp, vp, vp, vp]
         L.sfm_graph_offsets.argtypes = [vp, i32, vp, i32, vp]
@@ -249,6 +256,25 @@ class Context:
         T = int(nt.item())
         total = int(ptr[T].item())
         return ptr[:T + 1], ti[:total], tk[:total]
+
+    def register_batch(self, corr_ptr, xy, X, intr, img_id, n_hyp=1024, thr=4.0, seed=42,
+                       refine=True):
+        """P3P RANSAC + refinement for a batch of images (device tensors, see
+        include/sfmcore.h).  Returns (cams [n_img,8] f64, count, key [n_img] i32, mask [n] u8)."""
+        torch = self.torch
+        dev = xy.device
+        n_img = corr_ptr.shape[0] - 1
+        n = xy.shape[0]
+        cams = torch.empty((max(n_img, 0), 8), dtype=torch.float64, device=dev)
+        count = torch.empty(max(n_img, 0), dtype=torch.int32, device=dev)
+        key = torch.empty(max(n_img, 0), dtype=torch.int32, device=dev)
+        mask = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        prm = RegisterParams(int(n_hyp), 1 if refine else 0, float(thr), int(seed))
+        self._bind_stream()
+        _check(self.lib.sfm_register_batch(self.handle, n_img, _ptr(corr_ptr), _ptr(xy), _ptr(X),
+                                           _ptr(intr), _ptr(img_id), C.byref(prm), _ptr(cams),
+                                           _ptr(count), _ptr(key), _ptr(mask)))
+        return cams, count, key, mask[:n]
 
     def triangulate(self, cams, pp, pt_ptr, cam_idx, uv):
         """(pts [n_pt,3], stats [n_pt,4]) f64 device tensors; see include/sfmcore.h."""

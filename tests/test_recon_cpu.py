@@ -89,3 +89,59 @@ def test_triangulation_status_codes():
     keep = np.r_[0, np.arange(4, len(cam_idx))]
     pts, st = recon.triangulate(prob["cams"], prob["pp"], ptr2, cam_idx[keep], uv[keep])
     assert st[0, 3] == 1 and np.all(st[1:, 3] == 0)
+
+
+# ---- next-view registration (oracle/sfm_oracle_reg.c) ---------------------------------------------
+
+def _rand_pose(rng):
+    from scipy.spatial.transform import Rotation
+    R = Rotation.random(random_state=int(rng.integers(1 << 30))).as_matrix()
+    return R, rng.normal(size=3)
+
+
+def test_reg_p3p_recovers_pose():
+    import oracle as O
+    rng = np.random.default_rng(0)
+    hits = 0
+    for _ in range(200):
+        R, t = _rand_pose(rng)
+        X = rng.normal(size=(3, 3))
+        t = t + np.array([0, 0, 5 - (X @ R.T + t)[:, 2].min()])
+        Pc = X @ R.T + t
+        b = Pc / np.linalg.norm(Pc, axis=1, keepdims=True)
+        sols = [s for s in O.reg_p3p(b, X) if s is not None]
+        err = min((np.abs(Rs - R).max() + np.abs(ts - t).max() for Rs, ts in sols), default=1e9)
+        hits += err < 1e-6
+    assert hits >= 198                       # (near-)degenerate triangles may lose the root
+
+
+def test_reg_bearing_inverts_projection():
+    import oracle as O
+    rng = np.random.default_rng(1)
+    intr = np.array([1000.0, 0.04, 960.0, 540.0])
+    q = rng.uniform(-0.8, 0.8, size=(50, 2))
+    xy = intr[0] * (1 + intr[1] * (q * q).sum(1, keepdims=True)) * q + intr[2:]
+    b = O.reg_bearing(xy, intr)
+    ref = np.c_[q, np.ones(50)]
+    ref /= np.linalg.norm(ref, axis=1, keepdims=True)
+    np.testing.assert_allclose(b, ref, atol=1e-9)
+
+
+def test_reg_ransac_finds_pose_with_outliers():
+    import oracle as O
+    rng = np.random.default_rng(2)
+    R, t = _rand_pose(rng)
+    X = rng.uniform(-2, 2, size=(300, 3))
+    t = t + np.array([0, 0, 8 - (X @ R.T + t)[:, 2].min()])
+    intr = np.array([1000.0, 0.02, 960.0, 540.0])
+    Pc = X @ R.T + t
+    q = Pc[:, :2] / Pc[:, 2:]
+    xy = intr[0] * (1 + intr[1] * (q * q).sum(1, keepdims=True)) * q + intr[2:]
+    xy += rng.normal(0, 0.5, size=xy.shape)
+    out = rng.random(300) < 0.4
+    xy[out] = rng.uniform([0, 0], [1920, 1080], size=(int(out.sum()), 2))
+    r = O.reg_ransac(xy, X, intr, img=5, n_hyp=512, seed=42, thr=3.0)
+    assert r["count"] >= 0.9 * (~out).sum()
+    np.testing.assert_allclose(r["R"], R, atol=5e-3)
+    assert np.abs(r["t"] - t).max() < 0.05 * np.linalg.norm(t)
+    assert r["mask"][~out].mean() > 0.95 and r["mask"][out].mean() < 0.05
