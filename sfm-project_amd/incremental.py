@@ -1,0 +1,211 @@
+"""Incremental structure from motion over the GPU core ("rest of incremental
+SfM for cfg5" — the pipeline papers/schoenberger2016sfm.pdf §2.1-2.2 describes and the reference's
+empty code/3d_reconstruction.py would hold).
+
+Every per-element stage runs on the GPU through the C-ABI: all-pairs matching (K1), F RANSAC (K2),
+verified-graph rows, tracks (`sfm_tracks`), triangulation (`sfm_triangulate`), batched next-view
+registration (`sfm_register_batch`, P3P RANSAC + refinement) and Levenberg-Marquardt bundle
+adjustment (`sfm_ba_jtj` / `sfm_ba_solve`).  The host does the orchestration: which images and
+tracks enter the model, and the one 3x3 essential-matrix decomposition of the initial pair (an
+8-point fit on that pair's inliers, O(1) work with no GPU counterpart).
+
+Cameras: angle-axis, t, f, k1 with known intrinsics (f, k1, principal point) per image.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import match_graph
+import reconstruction
+import sfmcore
+
+
+def _undistort(xy, intr, iters=10):
+    """Normalised, undistorted coordinates (the triangulation kernel's fixed-point spec)."""
+    f, k1, cx, cy = intr
+    xd = (np.asarray(xy, np.float64) - [cx, cy]) / f
+    x = xd.copy()
+    for _ in range(iters):
+        x = xd / (1.0 + k1 * np.sum(x * x, axis=1, keepdims=True))
+    return x
+
+
+def _angle_axis(R):
+    c = np.clip((np.trace(R) - 1.0) / 2.0, -1.0, 1.0)
+    w = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    s = 0.5 * np.linalg.norm(w)
+    th = np.arctan2(s, c)
+    return w * (th / (2.0 * s)) if s > 1e-12 else 0.5 * w
+
+
+def relative_pose(x1, x2):
+    """Pose (R, t), |t| = 1, of camera 2 w.r.t. camera 1 from normalised correspondences: linear
+    essential matrix on all pairs, projected to the essential manifold; the four decompositions
+    are returned for the cheirality vote."""
+    A = np.stack([x2[:, 0] * x1[:, 0], x2[:, 0] * x1[:, 1], x2[:, 0],
+                  x2[:, 1] * x1[:, 0], x2[:, 1] * x1[:, 1], x2[:, 1],
+                  x1[:, 0], x1[:, 1], np.ones(len(x1))], 1)
+    E = np.linalg.svd(A)[2][-1].reshape(3, 3)
+    U, _, Vt = np.linalg.svd(E)
+    if np.linalg.det(U) < 0:
+        U = -U
+    if np.linalg.det(Vt) < 0:
+        Vt = -Vt
+    W = np.array([[0.0, -1.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, 1.0]])
+    out = []
+    for R in (U @ W @ Vt, U @ W.T @ Vt):
+        for t in (U[:, 2], -U[:, 2]):
+            out.append((R, t / np.linalg.norm(t)))
+    return out
+
+
+class Reconstruction:
+    def __init__(self, n_img):
+        self.cams = np.zeros((n_img, 8))
+        self.registered = np.zeros(n_img, bool)
+        self.points = None
+        self.has_point = None
+        self.history = []
+
+
+def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
+                ba_iter=20, loss_s=2.0, device=0, log=None):
+    """desc [n_img,K,D] u8, kps [n_img,K,2] pixels, n_kp [n_img], intr [n_img,4] = (f, k1, cx, cy).
+    Returns a Reconstruction (cams [n_img,8], registered mask, points per track, track arrays)."""
+    import torch
+    dev = torch.device("cuda", device)
+    ctx = sfmcore.context(device)
+    say = log or (lambda *a: None)
+    n_img = len(desc)
+    intr = np.asarray(intr, np.float64)
+    pairs = np.array([(a, b) for a in range(n_img) for b in range(a + 1, n_img)], np.int32)
+    gb = match_graph.GraphBuilder(desc, kps, n_kp, device=device)
+    pairs_t = torch.from_numpy(pairs).to(dev)
+    count, match, _, rs = gb.run(pairs_t)
+    rows = gb.graph_rows(0, count, match, rs)
+    inl = rs["inl_count"].cpu().numpy()
+    ptr_t, timg_t, tkp_t = match_graph.build_tracks(rows, pairs_t, n_kp, min_track, device)
+    tptr, timg, tkp = (t.cpu().numpy() for t in (ptr_t, timg_t, tkp_t))
+    n_tr = len(tptr) - 1
+    kps_np = np.asarray(kps, np.float64)
+    obs_track = np.repeat(np.arange(n_tr), np.diff(tptr))
+    obs_xy = kps_np[timg, tkp]
+    say(f"graph: {len(rows)} verified matches, {n_tr} tracks")
+
+    rec = Reconstruction(n_img)
+    rec.points = np.zeros((n_tr, 3))
+    rec.has_point = np.zeros(n_tr, bool)
+    rec.tracks = (tptr, timg, tkp)
+    rec.cams[:, 6:8] = intr[:, :2]
+
+    # ---- initial pair: most verified inliers; relative pose from that pair's RANSAC-verified
+    # matches (tracks may still carry a wrong observation), then its tracks are triangulated
+    rows_np = rows.cpu().numpy()
+    order = np.argsort(-inl, kind="stable")
+    for p in order[:10]:
+        a, b = (int(v) for v in pairs[p])
+        r = rows_np[rows_np[:, 0] == p]
+        if len(r) < 50:
+            continue
+        xa = _undistort(kps_np[a, r[:, 1]], intr[a])
+        xb = _undistort(kps_np[b, r[:, 2]], intr[b])
+        common = np.intersect1d(obs_track[timg == a], obs_track[timg == b])
+        best = None
+        for R, t in relative_pose(xa, xb):
+            cams = rec.cams.copy()
+            cams[a, :6] = 0.0
+            cams[b, :3] = _angle_axis(R)
+            cams[b, 3:6] = t
+            pts, st = _triangulate(ctx, cams, intr, [a, b], common, tptr, timg, obs_xy, dev)
+            good = int(np.sum((st[:, 3] == 0) & (st[:, 0] < max_err)))
+            if best is None or good > best[0]:
+                best = (good, cams, pts, st)
+        if best[0] >= 30:
+            good, rec.cams, pts, st = best
+            ok = (st[:, 3] == 0) & (st[:, 0] < max_err) & (st[:, 1] > 1.0)
+            rec.points[common[ok]] = pts[ok]
+            rec.has_point[common[ok]] = True
+            rec.registered[[a, b]] = True
+            say(f"initial pair ({a}, {b}): {len(r)} verified matches, {int(ok.sum())} points")
+            break
+    if not rec.registered.any():
+        raise RuntimeError("reconstruct: no initial pair with enough well-conditioned matches")
+    _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device)
+
+    # ---- register, triangulate, adjust until no image can be added
+    while not rec.registered.all():
+        cand = [i for i in range(n_img) if not rec.registered[i]]
+        corr = [(i, np.nonzero((timg == i) & rec.has_point[obs_track])[0]) for i in cand]
+        corr = [(i, o) for i, o in corr if len(o) >= 30]
+        if not corr:
+            break
+        ids = np.array([i for i, _ in corr], np.int32)
+        cptr = np.r_[0, np.cumsum([len(o) for _, o in corr])].astype(np.int32)
+        sel = np.concatenate([o for _, o in corr])
+        T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
+        cams_r, cnt, _, _ = ctx.register_batch(T(cptr, np.int32), T(obs_xy[sel], np.float64),
+                                               T(rec.points[obs_track[sel]], np.float64),
+                                               T(intr[ids], np.float64), T(ids, np.int32),
+                                               n_hyp=n_hyp, thr=reg_thr)
+        cams_r, cnt = cams_r.cpu().numpy(), cnt.cpu().numpy()
+        added = 0
+        for j, i in enumerate(ids):
+            if cnt[j] >= 30:
+                rec.cams[i] = cams_r[j]
+                rec.registered[i] = True
+                added += 1
+        say(f"registered {added} of {len(ids)} candidates, total {int(rec.registered.sum())}")
+        if not added:
+            break
+        _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev)
+        _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device)
+    return rec
+
+
+def _triangulate(ctx, cams, intr, imgs, tracks, tptr, timg, obs_xy, dev):
+    """Triangulate `tracks` from their observations in the images `imgs` (GPU kernel)."""
+    import torch
+    imgs = np.asarray(imgs)
+    obs = [np.arange(tptr[t], tptr[t + 1]) for t in tracks]
+    obs = [o[np.isin(timg[o], imgs)] for o in obs]
+    ptr = np.r_[0, np.cumsum([len(o) for o in obs])].astype(np.int32)
+    o = np.concatenate(obs) if obs else np.zeros(0, np.int64)
+    T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
+    pts, st = ctx.triangulate(T(cams, np.float64), T(intr[:, 2:4], np.float64), T(ptr, np.int32),
+                              T(timg[o], np.int32), T(obs_xy[o], np.float64))
+    return pts.cpu().numpy(), st.cpu().numpy()
+
+
+def _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev):
+    reg_obs = rec.registered[timg]
+    n_reg = np.add.reduceat(reg_obs.astype(np.int64), tptr[:-1]) if len(timg) else np.zeros(0)
+    todo = np.nonzero(~rec.has_point & (n_reg >= 2))[0]
+    if len(todo) == 0:
+        return
+    pts, st = _triangulate(ctx, rec.cams, intr, np.nonzero(rec.registered)[0], todo, tptr, timg,
+                           obs_xy, dev)
+    ok = (st[:, 3] == 0) & (st[:, 0] < max_err) & (st[:, 1] > 1.0)
+    rec.points[todo[ok]] = pts[ok]
+    rec.has_point[todo[ok]] = True
+
+
+def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device):
+    """Global LM over the registered cameras and the triangulated points (GPU), then drop points
+    whose mean reprojection error stays above max_err."""
+    use = rec.registered[timg] & rec.has_point[obs_track]
+    tr = obs_track[use]
+    pts_ids, pt_idx = np.unique(tr, return_inverse=True)
+    cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
+                                                   timg[use], pt_idx.astype(np.int32),
+                                                   obs_xy[use], loss_s=loss_s, max_iter=ba_iter,
+                                                   device=device)
+    reg = rec.registered
+    rec.cams[reg] = cams[reg]
+    rec.points[pts_ids] = pts
+    err = reconstruction.reprojection_errors(rec.cams, intr[:, 2:4], pts, timg[use],
+                                             pt_idx.astype(np.int32), obs_xy[use], device=device)
+    mean = np.bincount(pt_idx, err, minlength=len(pts_ids)) / np.maximum(
+        np.bincount(pt_idx, minlength=len(pts_ids)), 1)
+    rec.has_point[pts_ids[mean > max_err]] = False
+    rec.history.append((int(reg.sum()), int(rec.has_point.sum()),
+                        float(hist[-1][0]) if hist else float("nan")))

@@ -1,0 +1,54 @@
+"""Incremental SfM on a synthetic cfg3-sized scene (50 images x 2048 keypoints, k1 in +-0.02):
+wall time and the reconstruction's quality against the scene's ground truth.
+
+Usage: python tests/perf/incremental_bench.py [n_img [n_kp]]   -> log lines + one JSON line.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "tests")]
+
+import numpy as np
+import torch
+
+import incremental
+import reconstruction as R
+import synth
+from test_gpu_incremental import _centres, _umeyama
+
+
+def main():
+    a = [int(x) for x in sys.argv[1:]]
+    n_img, n_kp = (a + [50, 2048][len(a):])[:2]
+    scene = synth.make_scene(n_img, n_kp, seed=21, k1_range=0.02)
+    intr = np.c_[scene["cams"][:, 6:8], scene["pp"]]
+    incremental.reconstruct(scene["desc"][:4], scene["kps"][:4], scene["n_kp"][:4], intr[:4])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rec = incremental.reconstruct(scene["desc"], scene["kps"], scene["n_kp"], intr,
+                                  log=lambda *m: print(*m, file=sys.stderr, flush=True))
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    tptr, timg, tkp = rec.tracks
+    obs_track = np.repeat(np.arange(len(tptr) - 1), np.diff(tptr))
+    use = rec.has_point[obs_track] & rec.registered[timg]
+    pts_ids, pt_idx = np.unique(obs_track[use], return_inverse=True)
+    err = R.reprojection_errors(rec.cams, scene["pp"], rec.points[pts_ids], timg[use],
+                                pt_idx.astype(np.int32), scene["kps"][timg[use], tkp[use]])
+    reg = rec.registered
+    s, Rm, t = _umeyama(_centres(rec.cams[reg]), _centres(scene["cams"][reg]))
+    al = (s * (Rm @ _centres(rec.cams[reg]).T)).T + t
+    print(json.dumps({
+        "stage": "incremental SfM (match + verify + tracks + register + triangulate + BA)",
+        "n_img": n_img, "n_kp": n_kp, "wall_s": wall, "registered": int(reg.sum()),
+        "points": int(rec.has_point.sum()), "observations": int(use.sum()),
+        "median_reproj_px": float(np.median(err)), "mean_reproj_px": float(err.mean()),
+        "max_centre_err_rel_radius": float(np.abs(al - _centres(scene["cams"][reg])).max() / 8.0),
+        "ba_history": rec.history}))
+
+
+if __name__ == "__main__":
+    main()
