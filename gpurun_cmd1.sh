@@ -2,7 +2,7 @@ set -o pipefail
 TAG=${1:-r1c}
 mkdir -p gpurun_out/prof_$TAG
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
 tail -30 gpurun_out/pytest_gpu_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && cat gpurun_out/bench_$TAG.json &&
