@@ -1,0 +1,736 @@
+// K1, ratio-test path: all-pairs 128-D L2 matching with the Lowe ratio test as a forward scan,
+// a recovery step and a reverse scan over the ratio survivors (DESIGN.md §4.1 "forward/reverse").
+//
+// Same results as the fused kernel in match_mfma.hip and the oracle (oracle/sfm_oracle.c
+// oracle_match: lowest-index nearest neighbour, second-smallest distance of the multiset, the
+// exact ratio test den^2 d1 < num^2 d2 on squared distances, mutual cross check
+// rnn[nn[q]] == q) — the rule restated from code/feature_matching.py:48-58 plus SURVEY.md §8a a3'.
+// Used when a ratio test is on and the cross check is mutual or off; the OpenCV cross-check rule
+// and ratio-free calls keep the fused kernel.
+//
+// Why a second path.  The fused kernel is VALU-issue-bound: every element of the
+// 2048 x 2048 distance tile pays a key build, the row top-2 and the column side (key, max over
+// query tiles, cross-lane transpose).  Here the hot loop keeps only the row top-2, on a value the
+// MFMA produces directly:
+//     e(q, j) = x'_q . y'_j - ceil(|y'_j|^2 / 2)        (accumulator initialised with -ceil(..))
+// vr = 2 x'.y' - |y'|^2 = |x'|^2 - d^2 orders the trains of a query exactly; vr = 2e + p_j with
+// p_j = |y'_j|^2 mod 2, so e orders them exactly up to ties in e.  Per query the scan keeps the top
+// two e values (e1 >= e2, multiset) and the 32-train tile where e1 first appeared.  Then:
+//   * d1 in [A - 2e1 - 1, A - 2e1], d2 in [A - 2e2 - 1, A - 2e2] (A = |x'_q|^2): a query that
+//     cannot pass the ratio test even at the favourable ends is dropped (about half of them);
+//   * recovery (block per pair): every other query recomputes the 32 dot products of its tile
+//     exactly; if e1 > e2 the unique train with e == e1 is the nearest neighbour j1 and d1 is
+//     exact; the ratio test is decided exactly unless d2's unit ambiguity straddles it; ties
+//     (e1 == e2) and straddles take an exact full-row scan (rare);
+//   * reverse scan (mutual only): the same MFMA scan with the survivors' j1 rows as queries and
+//     the other image streamed: top-2 of e'(j1, q') = x'_q'.y'_j1 - ceil(|x'_q'|^2 / 2) over q';
+//     q is j1's nearest query iff e'(j1, q) == E1 > E2 (E1 == E2 == e'(j1, q): exact column scan).
+// MFMA work: 1 + (survivor fraction) of the fused kernel; VALU per element: 1.5 instructions of
+// the top-2 network instead of about 4.5 + the transposes.
+#include <climits>
+#include <cstdlib>
+
+#include "match_common.h"
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+constexpr int D = 128;                       // i8 features per descriptor (x ^ 0x80)
+#ifndef L2FR_WAVES
+#define L2FR_WAVES 8
+#endif
+constexpr int WAVES = L2FR_WAVES;            // waves per scan workgroup (8, or 4)
+constexpr int SCAN_THREADS = 64 * WAVES;
+#ifndef L2FR_QT
+#define L2FR_QT 4
+#endif
+constexpr int QT = L2FR_QT;                  // query tiles (32 queries) per wave: 4, or 2
+constexpr int QB = WAVES * QT * 32;          // queries per workgroup (1024 resp. 512)
+constexpr int SCAN_MIN_WAVES = 8 / QT;       // waves per SIMD the scan kernel is built for (2 or 4)
+constexpr int CHUNK = 256;                   // train rows per LDS stage
+constexpr int NT = CHUNK / 32;               // tiles per stage
+constexpr int NK = D / 32;                   // MFMA k-steps per tile
+constexpr int SLOTS = D / 16;                // 16-B slots per row
+constexpr int PIECES = CHUNK * D / 1024 / WAVES;
+constexpr int RPP = 1024 / D;                // rows per 1 KB DMA piece
+constexpr int KALIGN = 256;
+constexpr int KMAX = 4096;
+constexpr int PAD_INIT = -(1 << 30);         // accumulator init of a padded train row
+constexpr int E_VALID = -(1 << 23);          // e of a real element is > -2^22
+
+enum : unsigned char { ST_DROP = 0, ST_CAND = 1, ST_SLOW = 2, ST_PASS = 3 };
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }  // conflict-free b128 reads
+
+// Top-2 insertion of two values: ts = max(ts, med3(tb, x, y)), tb = max3(tb, x, y).  The median
+// is written as max(min(tb,x), min(max(tb,x),y)), which the compiler emits as one v_med3_i32 and
+// pads against the MFMA that produced x and y (hipcc does not pad hazards into an asm statement,
+// so no asm may read an accumulator first).  The compiler turns max(ts, med) pairs into v_max3.
+// The new tb: one asm v_max3_i32 that takes the median as an extra operand, so it issues after
+// the compiler's padded read (L2FR_NO_ASM_MAX3: plain max(), which compiles to two v_max_i32).
+__device__ __forceinline__ void top2_insert(int& tb, int& ts, int x, int y) {
+    const int med = max(min(tb, x), min(max(tb, x), y));
+#ifndef L2FR_NO_ASM_MAX3
+    int top;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(top) : "v"(tb), "v"(x), "v"(y), "v"(med));
+#else
+    const int top = max(max(x, y), tb);
+#endif
+    ts = max(ts, med);
+    tb = top;
+}
+
+// Exact i8 dot product of two 128-byte feature rows (v_dot4_i32_i8).
+__device__ __forceinline__ int dot128(const uint4* x, const uint4* y) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint4 u = x[k], v = y[k];
+        s = __builtin_amdgcn_sdot4((int)u.x, (int)v.x, s, false);
+        s = __builtin_amdgcn_sdot4((int)u.y, (int)v.y, s, false);
+        s = __builtin_amdgcn_sdot4((int)u.z, (int)v.z, s, false);
+        s = __builtin_amdgcn_sdot4((int)u.w, (int)v.w, s, false);
+    }
+    return s;
+}
+
+// Per descriptor: the i8 row x ^ 0x80, A = |x'|^2 and the scan's accumulator init -ceil(A/2)
+// (PAD_INIT for the padding rows up to k_pad).
+__global__ void l2fr_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
+                                 int k_max, int k_pad, int32_t* __restrict__ norm,
+                                 int32_t* __restrict__ cinit, uint8_t* __restrict__ zero_row,
+                                 uint4* __restrict__ desc_i8) {
+    const int img = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (img == 0 && j < D) zero_row[j] = 0;
+    if (j >= k_pad) return;
+    int nv = 0;
+    if (j < k_max) {
+        const uint4* p = (const uint4*)(desc + ((size_t)img * k_max + j) * D);
+        uint4* o8 = desc_i8 + ((size_t)img * k_max + j) * SLOTS;
+#pragma unroll
+        for (int q = 0; q < SLOTS; ++q) {
+            const uint4 v = p[q];
+            o8[q] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u,
+                               v.w ^ 0x80808080u);
+            const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int x = (int)((w[e] >> (8 * b)) & 0xFF) - 128;
+                    nv += x * x;
+                }
+        }
+    }
+    const size_t o = (size_t)img * k_pad + j;
+    norm[o] = nv;
+    cinit[o] = (j < n_kp[img]) ? -((nv + 1) >> 1) : PAD_INIT;
+}
+
+// Pair orders by streamed image, counting sort in LDS: block 0 orders by pairs[p][1] (forward
+// scan) into order_f, block 1 by pairs[p][0] (reverse scan) into order_r.
+__global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restrict__ pairs,
+                                                          int n_pairs, int n_img,
+                                                          int32_t* __restrict__ order_f,
+                                                          int32_t* __restrict__ order_r) {
+    extern __shared__ int hist[];
+    const int tid = threadIdx.x, col = blockIdx.x == 0 ? 1 : 0;
+    int32_t* order = blockIdx.x == 0 ? order_f : order_r;
+    for (int i = tid; i < n_img; i += 1024) hist[i] = 0;
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += 1024) atomicAdd(&hist[pairs[2 * p + col]], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int off = 0;
+        for (int i = 0; i < n_img; ++i) { const int c = hist[i]; hist[i] = off; off += c; }
+    }
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += 1024) order[atomicAdd(&hist[pairs[2 * p + col]], 1)] = p;
+}
+
+// Ratio bounds of one forward record: DROP (cannot pass even at the favourable ends of the d1, d2
+// intervals), SLOW (e1 == e2: the nearest neighbour is not unique in e) or CAND.
+__device__ __forceinline__ unsigned char classify(int4 r, long long A, int rnum, int rden,
+                                                  long long max_dist) {
+    const long long d1lo = max(A - 2LL * r.x - 1, 0LL);
+    const long long d2hi = r.y > E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
+    if (!sfm::ratio_ok(d1lo, d2hi, rnum, rden, true) || (max_dist >= 0 && !(d1lo < max_dist)))
+        return ST_DROP;
+    return (r.y == r.x) ? ST_SLOW : ST_CAND;
+}
+
+// What the forward scan needs to classify its records (unused by the reverse scan).
+struct FwdCls {
+    const int32_t* norm;     // [n_img][k_pad] |x'|^2
+    int rnum, rden;          // ratio num/den
+    long long max_dist;
+    int4* qst;               // [P][k_pad] DROP / SLOW statuses
+    uint8_t* cls;            // [P][k_pad] tile group (e1 tile / 8) of a candidate, 0xFF otherwise
+};
+
+// The MFMA scan.  Forward (REV = false): queries = image pairs[p][0] rows 0..n-1, streamed trains =
+// image pairs[p][1].  Reverse (REV = true): queries = the survivor list's j1 rows of image
+// pairs[p][1] (entries 0..qcount[p]-1), streamed = image pairs[p][0].  Output per query entry:
+// (e1, e2, tile of e1, 0) at out[p][entry].
+//
+// Geometry as the fused kernel (match_mfma.hip): 512-thread workgroup = 8 waves x 4 query tiles,
+// query fragments in VGPRs for the whole kernel, trains through LDS in 256-row chunks,
+// double-buffered LDS-DMA with an XOR-swizzled row image, XCD-aware block order.  Per 32-train
+// tile and query tile: 4 MFMAs whose accumulator starts at the trains' -ceil(|y'|^2/2), then the
+// top-2 network ts = max(ts, med3(tb, x, y)), tb = max3(tb, x, y) — 1.5 VALU per element, no key
+// build, no column side.
+template <bool REV>
+__global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel(
+    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+    const int32_t* __restrict__ cinit, const uint8_t* __restrict__ zero_row,
+    const int32_t* __restrict__ pairs, int n_qblk, const int32_t* __restrict__ pair_order,
+    int n_blk, const int4* __restrict__ qlist, const int32_t* __restrict__ qcount,
+    int4* __restrict__ out, FwdCls fc) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
+
+    // XCD-aware block order: workgroups go round-robin over the 8 XCDs (blockIdx % 8); XCD x owns
+    // the x-th contiguous run of ppx pairs of pair_order (pairs sharing the streamed image are
+    // adjacent, so its L2 serves them) and runs all their query block 0s first, then block 1s
+    // (in the reverse scan most block 1s are empty and exit at once, after the real work).
+    const int ppx = (int)(gridDim.x >> 3) / n_qblk;
+    const int l = (int)(blockIdx.x >> 3);
+    const int pos = (int)(blockIdx.x & 7) * ppx + l % ppx, qb = l / ppx;
+    if (pos >= n_blk) return;  // block-uniform, before any barrier
+    const int p = pair_order[pos];
+    const int qi = pairs[2 * p + (REV ? 1 : 0)], ti = pairs[2 * p + (REV ? 0 : 1)];
+    const int nq = REV ? qcount[p] : n_kp[qi];
+    const int nb = n_kp[ti];
+    if (qb * QB >= nq || nb <= 0) return;  // block-uniform
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+
+    const uint8_t* db = desc + (size_t)ti * k_max * D;
+    const int32_t* cib = cinit + (size_t)ti * k_pad;
+    const int n_chunk = (nb + CHUNK - 1) / CHUNK;
+
+    auto stage = [&](int ch, unsigned char* dst) {
+#pragma unroll
+        for (int i = 0; i < PIECES; ++i) {
+            const int piece = wave * PIECES + i;
+            const int row = piece * RPP + lane / SLOTS;
+            const int slot = (lane % SLOTS) ^ swz(row);
+            const int j = ch * CHUNK + row;
+            const uint8_t* src = (j < nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
+        }
+        if (wave == 0 && lane < CHUNK / 4) {
+            const int32_t* src = cib + ch * CHUNK + lane * 4;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D), 16, 0, 0);
+        }
+    };
+
+    const int qbase = qb * QB + wave * QT * 32;
+    const bool active = qbase < nq;  // wave-uniform
+    v4i bq[QT][NK];
+    int tb[QT], ts[QT], t1[QT];
+    const uint8_t* da = desc + (size_t)qi * k_max * D;
+#pragma unroll
+    for (int c = 0; c < QT; ++c) {
+        const int e = qbase + c * 32 + r32;
+        int row = -1;
+        if (e < nq) row = REV ? qlist[(size_t)p * k_pad + e].y : e;
+        const v4i* src = (const v4i*)((row >= 0) ? da + (size_t)row * D + (D / 2) * h
+                                                 : zero_row + (D / 2) * h);
+#pragma unroll
+        for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
+        tb[c] = INT_MIN; ts[c] = INT_MIN; t1[c] = 0;
+    }
+
+    v16i acc[QT];
+    auto epi_all = [&](int gt) {  // top-2 of all query tiles of the tile in acc
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+            const int o = tb[u];
+#ifdef L2FR_ABL_NOEPI  // ablation: no top-2 network (MFMA + staging cost)
+            tb[u] = max(tb[u], acc[u][0] ^ acc[u][15]);
+#else
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) top2_insert(tb[u], ts[u], acc[u][r], acc[u][r + 1]);
+#endif
+            t1[u] = (tb[u] != o) ? gt : t1[u];
+        }
+    };
+
+    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
+        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
+        const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
+        if (active) {
+            const int* Ci = (const int*)(cur + CHUNK * D);
+            // A fragments (train rows) and the accumulator init of tile tt; accumulator register r
+            // of this lane is train row 8*(r/4) + 4*h + r%4
+            auto load_tile = [&](int tt, v4i (&af)[NK], v16i& init) {
+                const int row = tt * 32 + r32;
+                const int sw = swz(row);
+#pragma unroll
+                for (int s = 0; s < NK; ++s)
+                    af[s] = *(const v4i*)(cur + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
+                    init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
+                    init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
+                }
+            };
+            v4i af[NK];
+            v16i init;
+            load_tile(0, af, init);
+            for (int tt = 0; tt < nt; ++tt) {
+                const int gt = ch * NT + tt;
+#pragma unroll
+                for (int c = 0; c < QT; ++c) acc[c] = init;
+#pragma unroll
+                for (int s = 0; s < NK; ++s)
+#pragma unroll
+                    for (int c = 0; c < QT; ++c)
+                        acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc[c], 0, 0, 0);
+                if (tt + 1 < nt) load_tile(tt + 1, af, init);
+                epi_all(gt);
+            }
+        }
+    };
+    if (n_chunk > 0) stage(0, lds0);
+    __syncthreads();
+    for (int ch = 0; ch < n_chunk; ch += 2) {
+        process(ch, lds0, lds1);
+        __syncthreads();
+        if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
+        __syncthreads();
+    }
+    if (active) {
+#pragma unroll
+        for (int c = 0; c < QT; ++c) {
+            // lanes l and l^32 hold the two 16-row halves of every tile of the same query
+            const int P1 = __shfl_xor(tb[c], 32), P2 = __shfl_xor(ts[c], 32),
+                      PT = __shfl_xor(t1[c], 32);
+            const int e1 = max(tb[c], P1);
+            const int e2 = max(min(tb[c], P1), max(ts[c], P2));
+            const int t = tb[c] > P1 ? t1[c] : (P1 > tb[c] ? PT : min(t1[c], PT));
+            const int e = qbase + c * 32 + r32;
+            if (h == 0 && e < nq) {
+                const int4 rec = make_int4(e1, e2, t, 0);
+                out[(size_t)p * k_pad + e] = rec;
+                if (!REV) {  // ratio bounds: drop / slow now, candidates go to the recovery
+                    const unsigned char st =
+                        classify(rec, fc.norm[(size_t)qi * k_pad + e], fc.rnum, fc.rden, fc.max_dist);
+                    fc.cls[(size_t)p * k_pad + e] = st == ST_CAND ? (uint8_t)(t >> 3) : (uint8_t)0xFF;
+                    if (st != ST_CAND) fc.qst[(size_t)p * k_pad + e] = make_int4(st, 0, 0, 0);
+                }
+            }
+        }
+    }
+}
+
+// Exact (d1, j1, d2) of one query over all trains (multiset second, lowest-index j1), block-wide.
+// Returns through LDS slot `res` (valid for every thread after the call).
+struct Top2 { long long b1; int j1; long long b2; };
+
+__device__ __forceinline__ Top2 top2_merge(Top2 x, Top2 y) {
+    const bool xf = (x.b1 < y.b1) || (x.b1 == y.b1 && x.j1 < y.j1);
+    Top2 r;
+    r.b1 = xf ? x.b1 : y.b1;
+    r.j1 = xf ? x.j1 : y.j1;
+    r.b2 = min(min(x.b2, y.b2), xf ? y.b1 : x.b1);
+    return r;
+}
+
+__device__ Top2 exact_row_scan(const uint4* qrow, const uint8_t* db, const int32_t* normb, int nb,
+                               int qnorm, Top2* red) {
+    const int tid = threadIdx.x;
+    uint4 x[SLOTS];
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) x[s] = qrow[s];
+    Top2 m{sfm::DIST_INF, INT_MAX, sfm::DIST_INF};
+    for (int j = tid; j < nb; j += 256) {
+        const int dot = dot128(x, (const uint4*)(db + (size_t)j * D));
+        const long long d = (long long)qnorm + normb[j] - 2LL * dot;
+        m = top2_merge(m, Top2{d, j, sfm::DIST_INF});
+    }
+    red[tid] = m;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (tid < s) red[tid] = top2_merge(red[tid], red[tid + s]);
+        __syncthreads();
+    }
+    const Top2 r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// Ordered compaction of int4 records (block of 256), returns the new base.
+__device__ __forceinline__ int compact_rec(bool keep, int4 rec, int base, int* wsum, int4* dst) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long bal = __ballot(keep);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(bal);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int w = 0; w < 4; ++w) {
+        const int s = wsum[w];
+        off += (w < wave) ? s : 0;
+        tot += s;
+    }
+    if (keep) dst[base + off + pre] = rec;
+    __syncthreads();
+    return base + tot;
+}
+
+// Recovery (block of 256 per (pair, group of 8 train tiles)).  The group's 256 train rows (with
+// their accumulator init and |y'|^2) are staged in LDS, slot-swizzled for conflict-free
+// row-per-lane reads; the candidates of the group (cls == group, written by the forward scan) are
+// processed in batches of 64 whose query rows and records are staged too, so the only global
+// traffic is a few bulk loads per block.  Per candidate, 32 lanes (one train each) recompute the
+// tile's dot products exactly, the unique train with e == e1 is the nearest neighbour j1, and the
+// ratio test is decided exactly where d2's unit ambiguity allows: qst[p][q] = (status, j1, d1).
+__global__ __launch_bounds__(256) void l2fr_recover_kernel(
+    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+    const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
+    const int32_t* __restrict__ pairs, const int4* __restrict__ fwd,
+    const uint8_t* __restrict__ cls, int rnum, int rden, long long max_dist,
+    int4* __restrict__ qst) {
+    __shared__ uint4 tiles[CHUNK * SLOTS];   // 256 train rows, slot s of row r at s ^ (r & 7)
+    __shared__ int tci[CHUNK], tnb[CHUNK];   // their accumulator init and |y'|^2
+    __shared__ uint4 qrows[64 * SLOTS];      // a batch of 64 candidate query rows
+    __shared__ int4 crec[64];
+    __shared__ int cq[64], cA[64];
+    __shared__ short clist[KMAX];
+    __shared__ int ccount;
+    const int p = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    const int ntiles = (nb + 31) >> 5, tg = grp * 8;
+    if (na <= 0 || nb <= 0 || tg >= ntiles) return;  // block-uniform
+    const int4* fw = fwd + (size_t)p * k_pad;
+    int4* qs = qst + (size_t)p * k_pad;
+    const uint4* qa = (const uint4*)(desc + (size_t)a * k_max * D);
+    const uint4* db = (const uint4*)(desc + (size_t)b * k_max * D);
+
+    // bulk loads first (one round trip): train rows, their tables, the candidate classes
+    uint4 rv[SLOTS];
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) {
+        const int i = tid + 256 * k, j = tg * 32 + i / SLOTS;
+        rv[k] = (j < nb) ? db[(size_t)j * SLOTS + i % SLOTS] : make_uint4(0, 0, 0, 0);
+    }
+    const int tj = tg * 32 + tid;  // < k_pad: groups cover 256 rows, k_pad is a multiple of 256
+    const int ci = cinit[(size_t)b * k_pad + tj], nn = norm[(size_t)b * k_pad + tj];
+    uint4 cv = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (tid * 16 < na) cv = ((const uint4*)(cls + (size_t)p * k_pad))[tid];
+    if (tid == 0) ccount = 0;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) {
+        const int i = tid + 256 * k, r = i / SLOTS, sl = i % SLOTS;
+        tiles[r * SLOTS + (sl ^ (r & 7))] = rv[k];
+    }
+    tci[tid] = ci;
+    tnb[tid] = nn;
+    __syncthreads();
+    const unsigned cw[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int q = tid * 16 + k;
+        if (q < na && ((cw[k >> 2] >> (8 * (k & 3))) & 0xFF) == (unsigned)grp)
+            clist[atomicAdd(&ccount, 1)] = (short)q;
+    }
+    __syncthreads();
+    const int nc = ccount;
+    const int g = tid >> 5, t = tid & 31;
+    for (int c0 = 0; c0 < nc; c0 += 64) {
+        const int nbat = min(64, nc - c0);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int i = tid + 256 * k, c = i / SLOTS;
+            if (c < nbat) qrows[i] = qa[(size_t)clist[c0 + c] * SLOTS + i % SLOTS];
+        }
+        if (tid < nbat) {
+            const int q = clist[c0 + tid];
+            cq[tid] = q;
+            crec[tid] = fw[q];
+            cA[tid] = norm[(size_t)a * k_pad + q];
+        }
+        __syncthreads();
+        for (int c = g; c < nbat; c += 8) {
+            const int q = cq[c];
+            const int4 r = crec[c];
+            const int row = (r.z - tg) * 32 + t, j = r.z * 32 + t;
+            const uint4* x = &qrows[c * SLOTS];
+            const uint4* y = &tiles[row * SLOTS];
+            int dot = 0;
+#pragma unroll
+            for (int k = 0; k < SLOTS; ++k) {
+                const uint4 u = x[k], v = y[k ^ (row & 7)];
+                dot = __builtin_amdgcn_sdot4((int)u.x, (int)v.x, dot, false);
+                dot = __builtin_amdgcn_sdot4((int)u.y, (int)v.y, dot, false);
+                dot = __builtin_amdgcn_sdot4((int)u.z, (int)v.z, dot, false);
+                dot = __builtin_amdgcn_sdot4((int)u.w, (int)v.w, dot, false);
+            }
+            const bool hit = (j < nb) && (dot + tci[row] == r.x);
+            const unsigned long long bal = __ballot(hit);
+            const unsigned m = (unsigned)(bal >> (32 * (g & 1)));
+            if (t == 0 && m == 0) qs[q] = make_int4(ST_SLOW, 0, 0, 0);  // defensive
+            if (m != 0 && t == __builtin_ctz(m)) {
+                const long long A = cA[c];
+                const long long d1 = A - (2LL * dot - tnb[row]);
+                const long long d2lo = r.y > E_VALID ? A - 2LL * r.y - 1 : sfm::DIST_INF;
+                const long long d2hi = r.y > E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
+                int st;
+                if (max_dist >= 0 && !(d1 < max_dist)) st = ST_DROP;
+                else if (sfm::ratio_ok(d1, d2lo, rnum, rden, true)) st = ST_PASS;
+                else if (!sfm::ratio_ok(d1, d2hi, rnum, rden, true)) st = ST_DROP;
+                else st = ST_SLOW;
+                qs[q] = make_int4(st, j, (int)d1, 0);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Exact full-row scans for the SLOW queries (ties in e, straddled ratio decisions: rare), then the
+// ordered compaction of the survivors (q, j1, d1, 0) into surv[p][0..scount[p]-1] (block of 256
+// per pair).
+__global__ __launch_bounds__(256) void l2fr_compact_kernel(
+    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+    const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs,
+    const int4* __restrict__ qst, int rnum, int rden, long long max_dist,
+    int4* __restrict__ surv, int32_t* __restrict__ scount) {
+    __shared__ Top2 red[256];
+    __shared__ int slow[256];
+    __shared__ int nslow, wsum[8];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    if (na <= 0 || nb <= 0) {
+        if (tid == 0) scount[p] = 0;
+        return;
+    }
+    const int4* qs = qst + (size_t)p * k_pad;
+    const int32_t* na_norm = norm + (size_t)a * k_pad;
+    const int32_t* nb_norm = norm + (size_t)b * k_pad;
+    const uint4* qa = (const uint4*)(desc + (size_t)a * k_max * D);
+    const uint8_t* db = desc + (size_t)b * k_max * D;
+    int4* sv = surv + (size_t)p * k_pad;
+    int base = 0;
+    for (int q0 = 0; q0 < na; q0 += 256) {
+        const int q = q0 + tid;
+        int4 r = (q < na) ? qs[q] : make_int4(ST_DROP, 0, 0, 0);
+        if (tid == 0) nslow = 0;
+        __syncthreads();
+        if (r.x == ST_SLOW) slow[atomicAdd(&nslow, 1)] = tid;
+        __syncthreads();
+        const int ns = nslow;
+        for (int i = 0; i < ns; ++i) {
+            const int who = slow[i], qq = q0 + who;
+            const Top2 e = exact_row_scan(qa + (size_t)qq * SLOTS, db, nb_norm, nb, na_norm[qq], red);
+            if (tid == who) {
+                bool keep = sfm::ratio_ok(e.b1, e.b2, rnum, rden, true);
+                keep = keep && (max_dist < 0 || e.b1 < max_dist);
+                r = make_int4(keep ? ST_PASS : ST_DROP, e.j1, (int)e.b1, 0);
+            }
+        }
+        const bool keep = r.x == ST_PASS;
+        base = compact_rec(keep, make_int4(q, r.y, r.z, 0), base, wsum, sv);
+    }
+    if (tid == 0) scount[p] = base;
+}
+
+// Mutual decision from the reverse scan + ordered output (block of 256 per pair).
+__global__ __launch_bounds__(256) void l2fr_final_kernel(
+    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+    const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
+    const int32_t* __restrict__ pairs, const int4* __restrict__ surv,
+    const int32_t* __restrict__ scount, const int4* __restrict__ rev, int mutual,
+    int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
+    int32_t* __restrict__ out_dist) {
+    __shared__ int wsum[8];
+    __shared__ int amb[256];
+    __shared__ int namb;
+    __shared__ unsigned char keepx[256];
+    __shared__ long long redd[256];
+    __shared__ int redq[256];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    const int S = (na > 0 && nb > 0) ? scount[p] : 0;
+    const int4* sv = surv + (size_t)p * k_pad;
+    const int4* rv = rev + (size_t)p * k_pad;
+    const int32_t* na_norm = norm + (size_t)a * k_pad;
+    const int32_t* nb_norm = norm + (size_t)b * k_pad;
+    const int32_t* ca = cinit + (size_t)a * k_pad;
+    const uint8_t* da = desc + (size_t)a * k_max * D;
+    const uint4* dbv = (const uint4*)(desc + (size_t)b * k_max * D);
+    int32_t* om = out_match + (size_t)p * k_max * 2;
+    int32_t* od = out_dist + (size_t)p * k_max;
+    int base = 0;
+    for (int k0 = 0; k0 < S; k0 += 256) {
+        const int k = k0 + tid;
+        int4 s = make_int4(0, 0, 0, 0);
+        bool keep = false;
+        if (tid == 0) namb = 0;
+        __syncthreads();
+        if (k < S) {
+            s = sv[k];
+            keep = true;
+            if (mutual) {
+                const int4 r = rv[k];
+                const int dot = (int)(((long long)na_norm[s.x] + nb_norm[s.y] - s.z) >> 1);
+                const int ep = dot + ca[s.x];
+                keep = (ep == r.x) && (r.y < r.x);
+                if (ep == r.x && r.y == r.x) amb[atomicAdd(&namb, 1)] = tid;
+            }
+        }
+        keepx[tid] = keep;
+        __syncthreads();
+        const int nam = namb;
+        for (int i = 0; i < nam; ++i) {  // exact column scan: is q the lowest-index nearest query?
+            const int who = amb[i];
+            const int4 e = sv[k0 + who];
+            uint4 y[SLOTS];
+#pragma unroll
+            for (int u = 0; u < SLOTS; ++u) y[u] = dbv[(size_t)e.y * SLOTS + u];
+            long long bd = sfm::DIST_INF;
+            int bq = INT_MAX;
+            for (int q = tid; q < na; q += 256) {
+                const int dot = dot128((const uint4*)(da + (size_t)q * D), y);
+                const long long d = (long long)na_norm[q] + nb_norm[e.y] - 2LL * dot;
+                if (d < bd) { bd = d; bq = q; }
+            }
+            redd[tid] = bd; redq[tid] = bq;
+            __syncthreads();
+            for (int st = 128; st > 0; st >>= 1) {
+                if (tid < st) {
+                    const long long od2 = redd[tid + st];
+                    const int oq = redq[tid + st];
+                    if (od2 < redd[tid] || (od2 == redd[tid] && oq < redq[tid])) {
+                        redd[tid] = od2; redq[tid] = oq;
+                    }
+                }
+                __syncthreads();
+            }
+            if (tid == 0) keepx[who] = (redq[0] == e.x);
+            __syncthreads();
+        }
+        keep = keepx[tid] != 0 && k < S;
+        base = sfm::compact256(keep, s.x, s.y, s.z, base, wsum, om, od);
+    }
+    if (tid == 0) out_count[p] = base;
+}
+
+// Debug dump of an intermediate record table into the match outputs (SFM_L2FR_DEBUG=1/2/3).
+__global__ void l2fr_dump_kernel(const int32_t* __restrict__ n_kp, const int32_t* __restrict__ pairs,
+                                 int k_max, int k_pad, const int4* __restrict__ rec,
+                                 const int32_t* __restrict__ cnt, int32_t* __restrict__ out_count,
+                                 int32_t* __restrict__ out_match, int32_t* __restrict__ out_dist) {
+    const int p = blockIdx.x;
+    const int n = cnt ? cnt[p] : n_kp[pairs[2 * p]];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int4 r = rec[(size_t)p * k_pad + i];
+        out_match[((size_t)p * k_max + i) * 2] = r.x;
+        out_match[((size_t)p * k_max + i) * 2 + 1] = r.y;
+        out_dist[(size_t)p * k_max + i] = r.z;
+    }
+    if (threadIdx.x == 0) out_count[p] = n;
+}
+
+}  // namespace
+
+// Forward/reverse L2 matcher (ratio test on, cross check mutual or off).
+int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
+                          int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                          const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                          int32_t* out_dist) {
+    hipStream_t st = ctx->stream;
+    if (k_max == 0) {
+        SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_pairs, st));
+        return SFM_OK;
+    }
+    const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
+    SFM_REQUIRE(k_pad <= KMAX, "sfm_match_batch: L2 matcher needs k_max <= 4096");
+    const int n_qblk = (k_max + QB - 1) / QB;
+    const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
+    const size_t recb = (size_t)n_pairs * k_pad * sizeof(int4);
+    const size_t cntb = sfm::align_up(sizeof(int32_t) * (size_t)n_pairs, 256);
+    const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
+    const size_t ordb = sfm::align_up(sizeof(int32_t) * (size_t)n_pairs, 256);
+    const size_t clsb = (size_t)n_pairs * k_pad;
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + 3 * recb + cntb + descb + 2 * ordb + clsb);
+    if (!ws) return SFM_ERR_NOMEM;
+    char* w = ws;
+    uint8_t* zero_row = (uint8_t*)w; w += 256;
+    int32_t* norm = (int32_t*)w; w += tab;
+    int32_t* cinit = (int32_t*)w; w += tab;
+    int4* fwd = (int4*)w; w += recb;
+    int4* surv = (int4*)w; w += recb;
+    int4* rev = (int4*)w; w += recb;
+    int32_t* scount = (int32_t*)w; w += cntb;
+    uint8_t* desc_i8 = (uint8_t*)w; w += descb;
+    int32_t* ord_f = (int32_t*)w; w += ordb;
+    int32_t* ord_r = (int32_t*)w; w += ordb;
+    uint8_t* cls = (uint8_t*)w;
+    const int ppx = (n_pairs + 7) / 8;  // pairs per XCD run (scan kernel block order)
+    const int n_blk = n_pairs;
+    const int grid = 8 * ppx * n_qblk;
+    const bool mutual = prm->cross_check == SFM_XC_MUTUAL;
+
+    hipLaunchKernelGGL(l2fr_prep_kernel, dim3(k_pad / 256, n_img), dim3(256), 0, st, desc, n_kp,
+                       k_max, k_pad, norm, cinit, zero_row, (uint4*)desc_i8);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(l2fr_order_kernel, dim3(mutual ? 2 : 1), dim3(1024),
+                       sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img, ord_f, ord_r);
+    SFM_HIP_CHECK(hipGetLastError());
+    // qst (per-query status of the recovery) shares the reverse scan's output buffer: it is
+    // consumed by the compaction before the reverse scan writes there.
+    int4* qst = rev;
+    const FwdCls fc{norm, prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, qst, cls};
+    hipLaunchKernelGGL(l2fr_scan_kernel<false>, dim3(grid), dim3(SCAN_THREADS), 0, st, desc_i8, n_kp, k_max,
+                       k_pad, cinit, zero_row, pairs, n_qblk, ord_f, n_blk, (const int4*)nullptr,
+                       (const int32_t*)nullptr, fwd, fc);
+    SFM_HIP_CHECK(hipGetLastError());
+    const char* dbg = getenv("SFM_L2FR_DEBUG");
+    const int dmode = dbg ? atoi(dbg) : 0;
+    if (dmode == 1) {
+        hipLaunchKernelGGL(l2fr_dump_kernel, dim3(n_pairs), dim3(256), 0, st, n_kp, pairs, k_max,
+                           k_pad, (const int4*)fwd, (const int32_t*)nullptr, out_count, out_match,
+                           out_dist);
+        return SFM_OK;
+    }
+    hipLaunchKernelGGL(l2fr_recover_kernel, dim3(n_pairs, k_pad / CHUNK), dim3(256), 0, st, desc_i8,
+                       n_kp, k_max, k_pad, norm, cinit, pairs, fwd, (const uint8_t*)cls,
+                       prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, qst);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(l2fr_compact_kernel, dim3(n_pairs), dim3(256), 0, st, desc_i8, n_kp, k_max,
+                       k_pad, norm, pairs, (const int4*)qst, prm->ratio_num, prm->ratio_den,
+                       (long long)prm->max_dist, surv, scount);
+    SFM_HIP_CHECK(hipGetLastError());
+    if (dmode == 2) {
+        hipLaunchKernelGGL(l2fr_dump_kernel, dim3(n_pairs), dim3(256), 0, st, n_kp, pairs, k_max,
+                           k_pad, (const int4*)surv, (const int32_t*)scount, out_count, out_match,
+                           out_dist);
+        return SFM_OK;
+    }
+    if (mutual) {
+        hipLaunchKernelGGL(l2fr_scan_kernel<true>, dim3(grid), dim3(SCAN_THREADS), 0, st, desc_i8, n_kp,
+                           k_max, k_pad, cinit, zero_row, pairs, n_qblk, ord_r, n_blk,
+                           (const int4*)surv, (const int32_t*)scount, rev, fc);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
+    if (dmode == 3) {
+        hipLaunchKernelGGL(l2fr_dump_kernel, dim3(n_pairs), dim3(256), 0, st, n_kp, pairs, k_max,
+                           k_pad, (const int4*)rev, (const int32_t*)scount, out_count, out_match,
+                           out_dist);
+        return SFM_OK;
+    }
+    hipLaunchKernelGGL(l2fr_final_kernel, dim3(n_pairs), dim3(256), 0, st, desc_i8, n_kp, k_max,
+                       k_pad, norm, cinit, pairs, surv, scount, rev, mutual ? 1 : 0, out_count,
+                       out_match, out_dist);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}

@@ -45,6 +45,10 @@ int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, 
                         int32_t k_max, const int32_t* pairs, int32_t n_pairs,
                         const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
                         int32_t* out_dist);
+int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
+                          int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                          const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                          int32_t* out_dist);
 int sfm_match_hamming_mfma_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp,
                                   int32_t n_img, int32_t k_max, const int32_t* pairs,
                                   int32_t n_pairs, const sfm_match_params* prm,

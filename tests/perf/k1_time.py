@@ -22,7 +22,9 @@ def main():
     ctx = sfmcore.context(0)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
-    for xc, ratio in ((1, (4, 5)), (2, None)):
+    for xc, ratio, path in ((1, (4, 5), "fr"), (1, (4, 5), "fused"), (0, (4, 5), "fr"),
+                            (0, (4, 5), "fused"), (2, None, "fused")):
+        os.environ["SFM_L2_PATH"] = path
         out = ctx.match_batch(desc, n_kp, pr, cross_check=xc, ratio=ratio)
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -42,7 +44,7 @@ def main():
                        and (mt[p, :cnt[p], 1] == t).all() and (dist[p, :cnt[p]] == d).all())
         ops = 2.0 * 128 * float(np.sum(s["n_kp"][pairs[:, 0]].astype(np.float64)
                                        * s["n_kp"][pairs[:, 1]]))
-        print(f"xc={xc} ratio={ratio}: {ms:.3f} ms/launch  {ops / ms / 1e9:.0f} TOP/s  "
+        print(f"xc={xc} ratio={ratio} path={path}: {ms:.3f} ms/launch  {ops / ms / 1e9:.0f} TOP/s  "
               f"parity={ok}  matches={int(cnt.sum())}", flush=True)
 
 

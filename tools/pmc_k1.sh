@@ -3,6 +3,7 @@
 # Counters missing from `rocprofv3 -L` on the box are dropped from their pass.
 set -o pipefail
 TAG=${1:-pmc_k1}
+KRE=${2:-mfma_match}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -16,6 +17,6 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   keep=""
   for c in $set; do grep -qw "$c" $OUT/counters.txt && keep="$keep $c"; done
   echo "pass $i:$keep"
-  timeout -k 10 300 rocprofv3 --pmc $keep --kernel-include-regex "mfma_match" -d $OUT/p$i -o run --output-format csv -- python3 tests/perf/k1_time.py > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $keep --kernel-include-regex "$KRE" -d $OUT/p$i -o run --output-format csv -- python3 tests/perf/k1_time.py > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 tools/pmc_summary.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
