@@ -74,6 +74,10 @@ template <int D> __device__ __forceinline__ int swz(int row) {
 constexpr int ROW_PAD = -(3 << 29);       // crow of padded trains
 constexpr int COL_PAD = -(3 << 29);       // ccol of padded queries
 constexpr int VALID_MIN = -(1 << 23);     // decoded vr / -d^2 of real elements are > this
+// Mutual kernel (value-only row side): e = x'.y' - ceil(n_y/2) of a real element is > -2^22.
+constexpr int MU_PAD_ROW = -(1 << 23);    // accumulator init of padded trains: e below every real e
+constexpr int MU_E_VALID = -(1 << 22);
+constexpr int MU_COL_PAD = -(3 << 29);    // column constant of padded queries (zero rows: e <= 0)
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
@@ -145,7 +149,7 @@ __device__ __forceinline__ int transpose_max16(const int (&c)[16], int lane) {
 
 // Per descriptor: the i8 feature row (L2: x ^ 0x80; Hamming: bits -> 0/1 bytes), its norm
 // (|x'|^2 resp. popcount) and the row-key constant, padded to k_pad (multiple of 256).
-template <int METRIC>
+template <int METRIC, bool CINIT = false>
 __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
                                  int k_max, int k_pad, int32_t* __restrict__ norm,
                                  int32_t* __restrict__ crow, uint8_t* __restrict__ zero_row,
@@ -199,7 +203,10 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
     const size_t o = (size_t)img * k_pad + j;
     norm[o] = nv;
     // row key Kr = 128 vr + (127 - j mod 128) = 256 dot + crow;  vr = 2 dot - n_j
-    crow[o] = (j < n_kp[img]) ? (-128 * nv + 127 - (j & 127)) : ROW_PAD;
+    if (CINIT)  // mutual kernel: accumulator init -ceil(n/2) (its padding: MU_PAD_ROW)
+        crow[o] = (j < n_kp[img]) ? -((nv + 1) >> 1) : MU_PAD_ROW;
+    else
+        crow[o] = (j < n_kp[img]) ? (-128 * nv + 127 - (j & 127)) : ROW_PAD;
 }
 
 // Pair order by train image (counting sort; one block): consecutive entries share image b.
@@ -482,6 +489,296 @@ __global__ __launch_bounds__(256) void l2_finalize_kernel(
     if (tid == 0) out_count[p] = base;
 }
 
+
+// ---- Mutual cross check on a value-only row side (L2; DESIGN.md §4.1 "mutual kernel") ----------
+//
+// The row side needs no train index under the mutual rule: the column side already names, for
+// every train j, its nearest query (exact, lowest index).  So the row side keeps only the top-2
+// VALUES of e = x'.y' - ceil(|y'|^2/2) — produced by the MFMA itself (accumulator initialised from
+// the trains' -ceil(|y'|^2/2) table), no key build — and the column key is built from e:
+//     Kc = 256 e + (-128 |x'_q|^2 + 127 - q_in_wave) = 128 (2e - |x'_q|^2) + (127 - q_in_wave)
+// (one v_lshl_add_u32; 2e - |x'_q|^2 = -d^2 - p_j with p_j = |y'_j|^2 mod 2, constant per train).
+// Finalize: every train's column winner q proposes (d, j); a query keeps its smallest proposal
+// D*.  If e1 > e2, the only train with d <= |x'|^2 - 2 e1 is the query's unique nearest neighbour
+// j1 (d = |x'|^2 - 2e - p_j, so any other train is >= 1 farther), hence q is mutual iff D* <=
+// |x'|^2 - 2 e1, and then d1 = D* exactly; d2 lies in [|x'|^2 - 2e2 - 1, |x'|^2 - 2e2], which
+// decides the ratio test unless it straddles it.  e1 == e2 and straddles take an exact row scan.
+__device__ __forceinline__ void mu_top2(int& tb, int& ts, int x, int y) {
+    // compiler-emitted v_med3_i32 (the compiler pads the MFMA -> VALU hazard), then the asm
+    // v_max3_i32 ordered after it by the median operand (hipcc pads nothing into an asm statement)
+    const int med = max(min(tb, x), min(max(tb, x), y));
+    int top;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(top) : "v"(tb), "v"(x), "v"(y), "v"(med));
+    ts = max(ts, med);
+    tb = top;
+}
+
+__global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
+    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+    const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
+    const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
+    const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
+    unsigned long long* __restrict__ colpart) {
+    constexpr int D = 128, QT = Geo<D>::QT, QB = Geo<D>::QB, CHUNK = Geo<D>::CHUNK, NK = Geo<D>::NK;
+    constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32;
+    constexpr int PIECES = CHUNK * D / 1024 / WAVES, RPP = 1024 / D;
+    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
+    __shared__ unsigned long long lds_col[KMAX_L2];
+
+    const int per_xcd = (int)(gridDim.x >> 3);
+    const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+    if (sblk >= n_blk) return;  // block-uniform, before any barrier
+    const int p = pair_order[sblk / n_qblk], qb = sblk % n_qblk;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+    for (int j = tid; j < k_pad; j += 512) lds_col[j] = 0ull;
+
+    const uint8_t* db = desc + (size_t)b * k_max * D;
+    const int32_t* cib = cinit + (size_t)b * k_pad;
+    const int n_chunk = (nb + CHUNK - 1) / CHUNK;
+    auto stage = [&](int ch, unsigned char* dst) {
+#pragma unroll
+        for (int i = 0; i < PIECES; ++i) {
+            const int piece = wave * PIECES + i;
+            const int row = piece * RPP + lane / SLOTS;
+            const int slot = (lane % SLOTS) ^ swz<D>(row);
+            const int j = ch * CHUNK + row;
+            const uint8_t* src = (j < nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
+        }
+        if (wave == 0 && lane < CHUNK / 4) {
+            const int32_t* src = cib + ch * CHUNK + lane * 4;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D), 16, 0, 0);
+        }
+    };
+
+    const int qbase = qb * QB + wave * QT * 32;
+    const bool active = qbase < na;  // wave-uniform
+    v4i bq[QT][NK];
+    int ccol[QT], tb[QT], ts[QT];
+    const uint8_t* da = desc + (size_t)a * k_max * D;
+#pragma unroll
+    for (int c = 0; c < QT; ++c) {
+        const int q = qbase + c * 32 + r32;
+        const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * D + (D / 2) * h : zero_row + (D / 2) * h);
+#pragma unroll
+        for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
+        ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32)) : MU_COL_PAD;
+        tb[c] = INT_MIN; ts[c] = INT_MIN;
+    }
+    const int rr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 + ((lane >> 3) & 1) * 2 +
+                   ((lane >> 4) & 1);
+    const int rowoff = (rr & 3) + 8 * (rr >> 2) + 4 * h;
+
+    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
+        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
+        const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
+        if (active) {
+            const unsigned char* A = cur;
+            const int* Ci = (const int*)(cur + CHUNK * D);
+            for (int tt = 0; tt < nt; ++tt) {
+                const int row = tt * 32 + r32;
+                const int sw = swz<D>(row);
+                v4i af[NK];
+#pragma unroll
+                for (int s = 0; s < NK; ++s)
+                    af[s] = *(const v4i*)(A + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
+                v16i init;  // accumulator register r of this lane is train row 8*(r/4) + 4*h + r%4
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
+                    init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
+                    init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
+                }
+                int colacc[16];
+#pragma unroll
+                for (int c = 0; c < QT; c += 2) {
+                    v16i acc0 = init, acc1 = init;
+#pragma unroll
+                    for (int s = 0; s < NK; ++s) {
+                        acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) {
+                        mu_top2(tb[c], ts[c], acc0[r], acc0[r + 1]);
+                        mu_top2(tb[c + 1], ts[c + 1], acc1[r], acc1[r + 1]);
+                        // column keys: 256 e + ccol (wraps only for padded-train rows, never merged)
+                        const int a0 = (int)(((unsigned)acc0[r] << 8) + (unsigned)ccol[c]);
+                        const int a1 = (int)(((unsigned)acc1[r] << 8) + (unsigned)ccol[c + 1]);
+                        const int b0 = (int)(((unsigned)acc0[r + 1] << 8) + (unsigned)ccol[c]);
+                        const int b1 = (int)(((unsigned)acc1[r + 1] << 8) + (unsigned)ccol[c + 1]);
+                        colacc[r] = (c == 0) ? max(a0, a1) : vmax3(colacc[r], a0, a1);
+                        colacc[r + 1] = (c == 0) ? max(b0, b1) : vmax3(colacc[r + 1], b0, b1);
+                    }
+                }
+                const int key = transpose_max16(colacc, lane);
+                const int j = ch * CHUNK + tt * 32 + rowoff;
+                if (!(lane & 1) && j < nb) {
+                    const int nd = key >> 7;  // 2e - |x'_q|^2 = -d^2 - p_j
+                    const unsigned gq = (unsigned)(qbase + 127 - (key & 127));
+                    lds_max_u64(&lds_col[j], ((unsigned long long)((unsigned)nd ^ 0x80000000u) << 32) |
+                                                 (unsigned long long)(0xFFFFFFFFu - gq));
+                }
+            }
+        }
+    };
+    if (n_chunk > 0) stage(0, lds0);
+    __syncthreads();
+    for (int ch = 0; ch < n_chunk; ch += 2) {
+        process(ch, lds0, lds1);
+        __syncthreads();
+        if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
+        __syncthreads();
+    }
+    if (active) {
+#pragma unroll
+        for (int c = 0; c < QT; ++c) {
+            const int P1 = __shfl_xor(tb[c], 32), P2 = __shfl_xor(ts[c], 32);
+            const int e1 = max(tb[c], P1);
+            const int e2 = max(min(tb[c], P1), max(ts[c], P2));
+            const int q = qbase + c * 32 + r32;
+            if (h == 0 && q < na) rowres[(size_t)p * k_pad + q] = make_int4(e1, e2, 0, 0);
+        }
+    }
+    unsigned long long* dst = colpart + ((size_t)p * n_qblk + qb) * k_pad;
+    for (int j = tid; j < k_pad; j += 512) dst[j] = lds_col[j];
+}
+
+// Exact dot product of two 128-byte i8 rows (v_dot4_i32_i8).
+__device__ __forceinline__ int mu_dot128(const uint4* x, const uint4* y) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint4 u = x[k], v = y[k];
+        s = __builtin_amdgcn_sdot4((int)u.x, (int)v.x, s, false);
+        s = __builtin_amdgcn_sdot4((int)u.y, (int)v.y, s, false);
+        s = __builtin_amdgcn_sdot4((int)u.z, (int)v.z, s, false);
+        s = __builtin_amdgcn_sdot4((int)u.w, (int)v.w, s, false);
+    }
+    return s;
+}
+
+// Finalize of the mutual kernel (block of 256 per pair; dynamic LDS: k_pad u64).
+__global__ __launch_bounds__(256) void mutual_finalize_kernel(
+    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+    const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs, int n_qblk,
+    const int4* __restrict__ rowres, const unsigned long long* __restrict__ colpart, int rnum,
+    int rden, long long max_dist, int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
+    int32_t* __restrict__ out_dist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
+    __shared__ int wsum[8], slow[256], nslow;
+    __shared__ long long rb1[256], rb2[256];
+    __shared__ int rj1[256];
+    __shared__ unsigned char keepx[256];
+    __shared__ int jx[256], dx[256];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    if (na <= 0 || nb <= 0) {
+        if (tid == 0) out_count[p] = 0;
+        return;
+    }
+    const unsigned long long* cp = colpart + (size_t)p * n_qblk * k_pad;
+    const int32_t* na_norm = norm + (size_t)a * k_pad;
+    const int32_t* nb_norm = norm + (size_t)b * k_pad;
+    const uint4* qa = (const uint4*)(desc + (size_t)a * k_max * 128);
+    const uint4* dbv = (const uint4*)(desc + (size_t)b * k_max * 128);
+    int32_t* om = out_match + (size_t)p * k_max * 2;
+    int32_t* od = out_dist + (size_t)p * k_max;
+    auto col_winner = [&](int j) {  // train j's nearest query (lowest index), or -1
+        unsigned long long best = 0;
+        for (int q = 0; q < n_qblk; ++q) best = max(best, cp[(size_t)q * k_pad + j]);
+        return best == 0 ? -1 : (int)(0xFFFFFFFFu - (unsigned)best);
+    };
+    for (int i = tid; i < na; i += 256) lds_best[i] = ~0ull;
+    __syncthreads();
+    for (int j = tid; j < nb; j += 256) {
+        unsigned long long best = 0;
+        for (int q = 0; q < n_qblk; ++q) best = max(best, cp[(size_t)q * k_pad + j]);
+        if (best == 0) continue;
+        const int nd = (int)((unsigned)(best >> 32) ^ 0x80000000u);
+        const int gq = (int)(0xFFFFFFFFu - (unsigned)best);
+        if (gq < 0 || gq >= na) continue;  // defensive: a column winner is always a query
+        const long long d = -(long long)nd - (nb_norm[j] & 1);
+        atomicMin(&lds_best[gq], ((unsigned long long)d << 32) | (unsigned)j);
+    }
+    __syncthreads();
+    int base = 0;
+    for (int i0 = 0; i0 < na; i0 += 256) {
+        const int i = i0 + tid;
+        bool keep = false, sl = false;
+        int jj = 0;
+        long long d1 = 0;
+        if (tid == 0) nslow = 0;
+        if (i < na) {
+            const int4 r = rowres[(size_t)p * k_pad + i];
+            const long long A = na_norm[i];
+            if (r.x == r.y) {
+                sl = true;  // nearest neighbour not unique in e
+            } else {
+                const unsigned long long e = lds_best[i];
+                if (e != ~0ull && (long long)(e >> 32) <= A - 2LL * r.x) {  // mutual
+                    d1 = (long long)(e >> 32);
+                    jj = (int)(unsigned)e;
+                    const long long d2lo = r.y > MU_E_VALID ? A - 2LL * r.y - 1 : sfm::DIST_INF;
+                    const long long d2hi = r.y > MU_E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
+                    if (sfm::ratio_ok(d1, d2lo, rnum, rden, true)) keep = true;
+                    else if (sfm::ratio_ok(d1, d2hi, rnum, rden, true)) sl = true;
+                    keep = keep && (max_dist < 0 || d1 < max_dist);
+                }
+            }
+        }
+        keepx[tid] = keep;
+        jx[tid] = jj;
+        dx[tid] = (int)d1;
+        __syncthreads();
+        if (sl) slow[atomicAdd(&nslow, 1)] = tid;
+        __syncthreads();
+        const int ns = nslow;
+        for (int s = 0; s < ns; ++s) {  // exact row scan of query i0 + slow[s] (rare)
+            const int who = slow[s], q = i0 + who;
+            uint4 x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = qa[(size_t)q * 8 + u];
+            long long b1 = sfm::DIST_INF, b2 = sfm::DIST_INF;
+            int j1 = INT_MAX;
+            for (int j = tid; j < nb; j += 256) {
+                const long long d = (long long)na_norm[q] + nb_norm[j] - 2LL * mu_dot128(x, dbv + (size_t)j * 8);
+                if (d < b1) { b2 = b1; b1 = d; j1 = j; } else if (d < b2) { b2 = d; }
+            }
+            rb1[tid] = b1; rb2[tid] = b2; rj1[tid] = j1;
+            __syncthreads();
+            for (int st = 128; st > 0; st >>= 1) {
+                if (tid < st) {
+                    const long long ob1 = rb1[tid + st], ob2 = rb2[tid + st];
+                    const int oj = rj1[tid + st];
+                    const bool other = ob1 < rb1[tid] || (ob1 == rb1[tid] && oj < rj1[tid]);
+                    const long long m2 = min(min(rb2[tid], ob2), other ? rb1[tid] : ob1);
+                    if (other) { rb1[tid] = ob1; rj1[tid] = oj; }
+                    rb2[tid] = m2;
+                }
+                __syncthreads();
+            }
+            if (tid == 0) {
+                const int n1 = rj1[0];
+                bool k = n1 >= 0 && n1 < nb && col_winner(n1) == q;
+                k = k && sfm::ratio_ok(rb1[0], rb2[0], rnum, rden, true);
+                k = k && (max_dist < 0 || rb1[0] < max_dist);
+                keepx[who] = k;
+                jx[who] = n1;
+                dx[who] = (int)rb1[0];
+            }
+            __syncthreads();
+        }
+        const bool kk = i < na && keepx[tid];
+        base = sfm::compact256(kk, i, jx[tid], dx[tid], base, wsum, om, od);
+    }
+    if (tid == 0) out_count[p] = base;
+}
+
 }  // namespace
 
 // MFMA matcher for both metrics (L2: D = 128; Hamming: D = 256 bit-expanded).
@@ -548,20 +845,76 @@ static int mfma_match_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, cons
     return SFM_OK;
 }
 
+// L2 with the mutual cross check (any ratio): value-only row side + column winners.
+static int mfma_mutual_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp,
+                              int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                              const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                              int32_t* out_dist) {
+    hipStream_t st = ctx->stream;
+    if (k_max == 0) {
+        SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_pairs, st));
+        return SFM_OK;
+    }
+    constexpr int D = 128, QB = Geo<128>::QB;
+    const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
+    SFM_REQUIRE(k_pad <= KMAX_L2, "sfm_match_batch: MFMA matcher needs k_max <= 4096");
+    const int n_qblk = (k_max + QB - 1) / QB;
+    const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
+    const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
+    const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
+    const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
+    const size_t ordb = sfm::align_up(sizeof(int32_t) * ((size_t)n_pairs + n_img), 256);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + 1024);
+    if (!ws) return SFM_ERR_NOMEM;
+    uint8_t* zero_row = (uint8_t*)ws;
+    int32_t* norm = (int32_t*)(ws + 256);
+    int32_t* cinit = (int32_t*)(ws + 256 + tab);
+    int4* rowres = (int4*)(ws + 256 + 2 * tab);
+    unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
+    uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
+    int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
+    const int n_blk = n_pairs * n_qblk;
+    const int grid = 8 * ((n_blk + 7) / 8);
+    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), 0, st, pairs, n_pairs, n_img,
+                       pair_order, pair_order + n_pairs);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_L2, true>), dim3(k_pad / 256, n_img), dim3(256),
+                       0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row, (uint4*)desc_i8);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(mfma_mutual_kernel, dim3(grid), dim3(512), 0, st, desc_i8, n_kp, k_max, k_pad,
+                       norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk, rowres, colpart);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(mutual_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st,
+                       desc_i8, n_kp, k_max, k_pad, norm, pairs, n_qblk, rowres, colpart,
+                       prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, out_count,
+                       out_match, out_dist);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
 int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
                         int32_t k_max, const int32_t* pairs, int32_t n_pairs,
                         const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
                         int32_t* out_dist) {
-    // Ratio test on, cross check off or mutual: the forward/reverse path (match_l2fr.hip) or this
-    // fused kernel, whichever is faster for the rule (cfg3, 1225 pairs x 2048: without cross check
-    // 0.90 vs 1.19 ms; mutual 1.24 vs 1.19 ms).  SFM_L2_PATH=fr|fused overrides.
-    if (prm->ratio_den > 0 && prm->cross_check != SFM_XC_OPENCV) {
-        const char* pe = getenv("SFM_L2_PATH");
-        const bool fr = pe ? strcmp(pe, "fr") == 0 : prm->cross_check == SFM_XC_NONE;
-        if (fr)
-            return sfm_match_l2fr_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
-                                         out_count, out_match, out_dist);
-    }
+    // Path per rule (cfg3, 1225 pairs x 2048): mutual cross check -> the
+    // value-only-row mutual kernel; ratio test without cross check -> the forward/reverse path
+    // (match_l2fr.hip); everything else (OpenCV rule, no cross check and no ratio) -> the fused
+    // key kernel.  SFM_L2_PATH=mutual|fr|fused overrides where the rule allows it.
+    const char* pe = getenv("SFM_L2_PATH");
+    const bool xc_mutual = prm->cross_check == SFM_XC_MUTUAL;
+    const bool ratio = prm->ratio_den > 0;
+    if (pe && strcmp(pe, "fused") == 0)
+        return mfma_match_launch(ctx, SFM_METRIC_L2, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
+                                 out_count, out_match, out_dist);
+    if (pe && strcmp(pe, "fr") == 0 && ratio && prm->cross_check != SFM_XC_OPENCV)
+        return sfm_match_l2fr_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
+                                     out_count, out_match, out_dist);
+    if (xc_mutual)
+        return mfma_mutual_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm, out_count,
+                                  out_match, out_dist);
+    if (ratio && prm->cross_check == SFM_XC_NONE)
+        return sfm_match_l2fr_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
+                                     out_count, out_match, out_dist);
     return mfma_match_launch(ctx, SFM_METRIC_L2, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
                              out_count, out_match, out_dist);
 }

@@ -22,8 +22,9 @@ def main():
     ctx = sfmcore.context(0)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
-    for xc, ratio, path in ((1, (4, 5), "fr"), (1, (4, 5), "fused"), (0, (4, 5), "fr"),
-                            (0, (4, 5), "fused"), (2, None, "fused")):
+    for xc, ratio, path in ((1, (4, 5), "mutual"), (1, (4, 5), "fused"), (1, (4, 5), "fr"),
+                            (0, (4, 5), "fr"), (0, (4, 5), "fused"), (2, None, "fused"),
+                            (1, None, "mutual")):
         os.environ["SFM_L2_PATH"] = path
         out = ctx.match_batch(desc, n_kp, pr, cross_check=xc, ratio=ratio)
         torch.cuda.synchronize()

@@ -135,11 +135,12 @@ def test_hamming_mfma_and_valu_paths_agree(ctx, K):
                                        ratio=ratio, max_dist=md))
             finally:
                 os.environ.pop("SFM_HAMMING_VALU", None)
-        (c0, m0, d0), (c1, m1, d1) = outs
-        np.testing.assert_array_equal(c0, c1)
-        for p in range(len(pairs)):
-            np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
-            np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
+        c0, m0, d0 = outs[0]
+        for c1, m1, d1 in outs[1:]:
+            np.testing.assert_array_equal(c0, c1)
+            for p in range(len(pairs)):
+                np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
+                np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
 
 
 def _tie_heavy(rng, n_img, k, levels):
@@ -150,8 +151,9 @@ def _tie_heavy(rng, n_img, k, levels):
 @pytest.mark.parametrize("ratio", [(4, 5), (1, 1), (3, 2), (65535, 1)])
 @pytest.mark.parametrize("xc", [1, 0])
 def test_l2_ratio_path_ties_and_ragged(ctx, xc, ratio):
-    """The forward/reverse ratio path (match_l2fr.hip): exact tie handling (e1 == e2, the unit
-    ambiguity of d2, ambiguous column winners) against the oracle on tie-heavy, ragged sets."""
+    """The forward/reverse ratio path (match_l2fr.hip) and the value-only-row mutual kernel:
+    exact tie handling (e1 == e2, the unit ambiguity of d2, ambiguous column winners) against the
+    oracle on tie-heavy, ragged sets."""
     import os
     rng = np.random.default_rng(100 + xc)
     desc = np.concatenate([_tie_heavy(rng, 3, 600, 2), _tie_heavy(rng, 2, 600, 3),
@@ -160,12 +162,13 @@ def test_l2_ratio_path_ties_and_ragged(ctx, xc, ratio):
     desc[6, :50] = desc[5, :50]
     n_kp = np.array([600, 599, 33, 600, 1, 600, 257], np.int32)
     pairs = np.array([[a, b] for a in range(7) for b in range(7) if a != b], np.int32)
-    os.environ["SFM_L2_PATH"] = "fr"
-    try:
-        _check_pairs(ctx, desc, n_kp, pairs, cross_check=xc, ratio=ratio)
-        _check_pairs(ctx, desc, n_kp, pairs, cross_check=xc, ratio=ratio, max_dist=200000)
-    finally:
-        os.environ.pop("SFM_L2_PATH", None)
+    for path in (("fr", "mutual") if xc == 1 else ("fr",)):
+        os.environ["SFM_L2_PATH"] = path
+        try:
+            _check_pairs(ctx, desc, n_kp, pairs, cross_check=xc, ratio=ratio)
+            _check_pairs(ctx, desc, n_kp, pairs, cross_check=xc, ratio=ratio, max_dist=200000)
+        finally:
+            os.environ.pop("SFM_L2_PATH", None)
 
 
 @pytest.mark.parametrize("K", [2048, 4096])
@@ -177,16 +180,17 @@ def test_l2_ratio_path_and_fused_kernel_agree(ctx, K):
     n_kp = s["n_kp"].copy()
     n_kp[2] = K - 101
     pairs = synth.unordered_pairs(4)
-    for xc, ratio in ((1, (4, 5)), (0, (4, 5)), (1, (9, 10))):
+    for xc, ratio in ((1, (4, 5)), (0, (4, 5)), (1, (9, 10)), (1, None)):
         outs = []
-        for v in ("fr", "fused"):
+        for v in (("fr", "fused", "mutual") if ratio else ("mutual", "fused")):
             os.environ["SFM_L2_PATH"] = v
             try:
                 outs.append(_gpu_match(ctx, s["desc"], n_kp, pairs, cross_check=xc, ratio=ratio))
             finally:
                 os.environ.pop("SFM_L2_PATH", None)
-        (c0, m0, d0), (c1, m1, d1) = outs
-        np.testing.assert_array_equal(c0, c1)
-        for p in range(len(pairs)):
-            np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
-            np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
+        c0, m0, d0 = outs[0]
+        for c1, m1, d1 in outs[1:]:
+            np.testing.assert_array_equal(c0, c1)
+            for p in range(len(pairs)):
+                np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
+                np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
