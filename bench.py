@@ -172,11 +172,11 @@ def main():
             "k": args.k, "n_hyp": args.n_hyp, "parallelism": f"pair-sharded dp{world}",
         },
         "verified_matches_per_step": verified_per_step,
-        "roofline": {"kernel": "K1 L2 match (mfma_prep + mfma_match_kernel<128> + l2_finalize, HIP events)",
+        "roofline": {"kernel": "K1 L2 match, mutual rule (mfma_prep + mfma_mutual_kernel + mutual_finalize, HIP events)",
                      "bound": "mfma", "achieved": k1_tops, "peak": PEAK_I8_TOPS,
                      "unit": "TOP/s (i8)", "frac": k1_tops / PEAK_I8_TOPS,
-                     "traffic": pmc_traffic("mfma_match_kernel", n_img, args.k, world),
-                     "traffic_unit": "bytes per mfma_match_kernel<128> launch (PMC, profiles/r01_traffic_cfg3.json)",
+                     "traffic": pmc_traffic("mfma_mutual_kernel", n_img, args.k, world),
+                     "traffic_unit": "bytes per mfma_mutual_kernel launch (PMC, profiles/r01_traffic_cfg3.json)",
                      "ms": match_ms, "ops_per_launch": k1_ops},
         "stages": {"match_ms": match_ms, "ransac_ms": ransac_ms,
                    "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,

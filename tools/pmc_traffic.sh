@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
-RX="mfma_prep_kernel|mfma_match_kernel|l2_finalize_kernel|ransac_prep_kernel|ransac_fit_kernel|ransac_order_kernel|ransac_score_kernel|ransac_final_kernel|graph_rows_kernel"
+RX="mfma_prep_kernel|mfma_match_kernel|mfma_mutual_kernel|mutual_finalize_kernel|l2_finalize_kernel|ransac_prep_kernel|ransac_fit_kernel|ransac_order_kernel|ransac_score_kernel|ransac_final_kernel|graph_rows_kernel"
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
