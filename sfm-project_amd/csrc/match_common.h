@@ -40,4 +40,30 @@ __device__ inline int compact256(bool keep, int i, int j, int d, int base, int* 
     return base + tot;
 }
 
+// Block-wide ordered compaction for NT threads (NT/64 waves): as compact256, wsum holds NT/64 ints.
+template <int NT>
+__device__ inline int compact_n(bool keep, int i, int j, int d, int base, int* wsum,
+                                int32_t* out_match, int32_t* out_dist) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long bal = __ballot(keep);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(bal);
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const int s = wsum[w];
+        off += (w < wave) ? s : 0;
+        tot += s;
+    }
+    if (keep) {
+        const int o = base + off + pre;
+        out_match[2 * o] = i;
+        out_match[2 * o + 1] = j;
+        out_dist[o] = d;
+    }
+    __syncthreads();
+    return base + tot;
+}
+
 }  // namespace sfm

@@ -209,11 +209,12 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
         crow[o] = (j < n_kp[img]) ? (-128 * nv + 127 - (j & 127)) : ROW_PAD;
 }
 
-// Pair order by train image (counting sort; one block): consecutive entries share image b.
+// Pair order by train image (counting sort in LDS; one block): consecutive entries share image b.
 __global__ __launch_bounds__(1024) void pair_order_kernel(const int32_t* __restrict__ pairs,
                                                           int n_pairs, int n_img,
                                                           int32_t* __restrict__ order,
-                                                          int32_t* __restrict__ hist) {
+                                                          int32_t* __restrict__ unused) {
+    extern __shared__ int hist[];
     const int tid = threadIdx.x;
     for (int i = tid; i < n_img; i += 1024) hist[i] = 0;
     __syncthreads();
@@ -661,19 +662,25 @@ __device__ __forceinline__ int mu_dot128(const uint4* x, const uint4* y) {
     return s;
 }
 
-// Finalize of the mutual kernel (block of 256 per pair; dynamic LDS: k_pad u64).
-__global__ __launch_bounds__(256) void mutual_finalize_kernel(
+// Finalize of the mutual kernel (block of MU_FT threads per pair; dynamic LDS: k_pad u64).
+// A wide block: every pass over the trains / queries is one global round trip, so fewer passes
+// (2 at k = 2048) is what makes this latency-bound kernel fast.
+#ifndef MU_FT_THREADS
+#define MU_FT_THREADS 256
+#endif
+constexpr int MU_FT = MU_FT_THREADS;
+__global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs, int n_qblk,
     const int4* __restrict__ rowres, const unsigned long long* __restrict__ colpart, int rnum,
     int rden, long long max_dist, int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
     int32_t* __restrict__ out_dist) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
-    __shared__ int wsum[8], slow[256], nslow;
-    __shared__ long long rb1[256], rb2[256];
-    __shared__ int rj1[256];
-    __shared__ unsigned char keepx[256];
-    __shared__ int jx[256], dx[256];
+    __shared__ int wsum[MU_FT / 64], slow[MU_FT], nslow;
+    __shared__ long long rb1[MU_FT], rb2[MU_FT];
+    __shared__ int rj1[MU_FT];
+    __shared__ unsigned char keepx[MU_FT];
+    __shared__ int jx[MU_FT], dx[MU_FT];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
@@ -693,9 +700,9 @@ __global__ __launch_bounds__(256) void mutual_finalize_kernel(
         for (int q = 0; q < n_qblk; ++q) best = max(best, cp[(size_t)q * k_pad + j]);
         return best == 0 ? -1 : (int)(0xFFFFFFFFu - (unsigned)best);
     };
-    for (int i = tid; i < na; i += 256) lds_best[i] = ~0ull;
+    for (int i = tid; i < na; i += MU_FT) lds_best[i] = ~0ull;
     __syncthreads();
-    for (int j = tid; j < nb; j += 256) {
+    for (int j = tid; j < nb; j += MU_FT) {
         unsigned long long best = 0;
         for (int q = 0; q < n_qblk; ++q) best = max(best, cp[(size_t)q * k_pad + j]);
         if (best == 0) continue;
@@ -707,7 +714,7 @@ __global__ __launch_bounds__(256) void mutual_finalize_kernel(
     }
     __syncthreads();
     int base = 0;
-    for (int i0 = 0; i0 < na; i0 += 256) {
+    for (int i0 = 0; i0 < na; i0 += MU_FT) {
         const int i = i0 + tid;
         bool keep = false, sl = false;
         int jj = 0;
@@ -716,15 +723,21 @@ __global__ __launch_bounds__(256) void mutual_finalize_kernel(
         if (i < na) {
             const int4 r = rowres[(size_t)p * k_pad + i];
             const long long A = na_norm[i];
-            if (r.x == r.y) {
-                sl = true;  // nearest neighbour not unique in e
-            } else {
-                const unsigned long long e = lds_best[i];
-                if (e != ~0ull && (long long)(e >> 32) <= A - 2LL * r.x) {  // mutual
-                    d1 = (long long)(e >> 32);
+            const unsigned long long e = lds_best[i];
+            const long long D = e != ~0ull ? (long long)(e >> 32) : sfm::DIST_INF;
+            const long long d1lo = max(A - 2LL * r.x - 1, 0LL);
+            const long long d2lo = r.y > MU_E_VALID ? A - 2LL * r.y - 1 : sfm::DIST_INF;
+            const long long d2hi = r.y > MU_E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
+            // not mutual: no train whose nearest query is i lies within the nearest distance
+            // (if i were mutual with its nearest neighbour j1, j1 would propose d1 <= A - 2e1);
+            // then the bounds: the ratio test / max_dist cannot pass even at the favourable ends
+            if (D <= A - 2LL * r.x && sfm::ratio_ok(d1lo, d2hi, rnum, rden, true) &&
+                (max_dist < 0 || d1lo < max_dist)) {
+                if (r.x == r.y) {
+                    sl = true;  // nearest neighbour not unique in e: exact row scan
+                } else {        // unique nearest neighbour = the proposing train, d1 = D exactly
+                    d1 = D;
                     jj = (int)(unsigned)e;
-                    const long long d2lo = r.y > MU_E_VALID ? A - 2LL * r.y - 1 : sfm::DIST_INF;
-                    const long long d2hi = r.y > MU_E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
                     if (sfm::ratio_ok(d1, d2lo, rnum, rden, true)) keep = true;
                     else if (sfm::ratio_ok(d1, d2hi, rnum, rden, true)) sl = true;
                     keep = keep && (max_dist < 0 || d1 < max_dist);
@@ -745,13 +758,13 @@ __global__ __launch_bounds__(256) void mutual_finalize_kernel(
             for (int u = 0; u < 8; ++u) x[u] = qa[(size_t)q * 8 + u];
             long long b1 = sfm::DIST_INF, b2 = sfm::DIST_INF;
             int j1 = INT_MAX;
-            for (int j = tid; j < nb; j += 256) {
+            for (int j = tid; j < nb; j += MU_FT) {
                 const long long d = (long long)na_norm[q] + nb_norm[j] - 2LL * mu_dot128(x, dbv + (size_t)j * 8);
                 if (d < b1) { b2 = b1; b1 = d; j1 = j; } else if (d < b2) { b2 = d; }
             }
             rb1[tid] = b1; rb2[tid] = b2; rj1[tid] = j1;
             __syncthreads();
-            for (int st = 128; st > 0; st >>= 1) {
+            for (int st = MU_FT / 2; st > 0; st >>= 1) {
                 if (tid < st) {
                     const long long ob1 = rb1[tid + st], ob2 = rb2[tid + st];
                     const int oj = rj1[tid + st];
@@ -774,7 +787,7 @@ __global__ __launch_bounds__(256) void mutual_finalize_kernel(
             __syncthreads();
         }
         const bool kk = i < na && keepx[tid];
-        base = sfm::compact256(kk, i, jx[tid], dx[tid], base, wsum, om, od);
+        base = sfm::compact_n<MU_FT>(kk, i, jx[tid], dx[tid], base, wsum, om, od);
     }
     if (tid == 0) out_count[p] = base;
 }
@@ -816,7 +829,7 @@ static int mfma_match_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, cons
     int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
     const int n_blk = n_pairs * n_qblk;
     const int grid = 8 * ((n_blk + 7) / 8);  // every XCD gets the same number of block slots
-    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), 0, st, pairs, n_pairs, n_img,
+    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img,
                        pair_order, pair_order + n_pairs);
     SFM_HIP_CHECK(hipGetLastError());
     if (l2) {
@@ -875,7 +888,7 @@ static int mfma_mutual_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* 
     int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
     const int n_blk = n_pairs * n_qblk;
     const int grid = 8 * ((n_blk + 7) / 8);
-    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), 0, st, pairs, n_pairs, n_img,
+    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img,
                        pair_order, pair_order + n_pairs);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_L2, true>), dim3(k_pad / 256, n_img), dim3(256),
@@ -884,7 +897,7 @@ static int mfma_mutual_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* 
     hipLaunchKernelGGL(mfma_mutual_kernel, dim3(grid), dim3(512), 0, st, desc_i8, n_kp, k_max, k_pad,
                        norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk, rowres, colpart);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(mutual_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st,
+    hipLaunchKernelGGL(mutual_finalize_kernel, dim3(n_pairs), dim3(MU_FT), (size_t)k_pad * 8, st,
                        desc_i8, n_kp, k_max, k_pad, norm, pairs, n_qblk, rowres, colpart,
                        prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, out_count,
                        out_match, out_dist);
