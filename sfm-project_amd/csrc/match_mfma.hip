@@ -514,13 +514,15 @@ __device__ __forceinline__ void mu_top2(int& tb, int& ts, int x, int y) {
     tb = top;
 }
 
+// ROWS = false: column side only (the OpenCV cross-check rule needs nothing else).
+template <int D, bool ROWS>
 __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
     const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
     unsigned long long* __restrict__ colpart) {
-    constexpr int D = 128, QT = Geo<D>::QT, QB = Geo<D>::QB, CHUNK = Geo<D>::CHUNK, NK = Geo<D>::NK;
+    constexpr int QT = Geo<D>::QT, QB = Geo<D>::QB, CHUNK = Geo<D>::CHUNK, NK = Geo<D>::NK;
     constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32;
     constexpr int PIECES = CHUNK * D / 1024 / WAVES, RPP = 1024 / D;
     __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
@@ -604,8 +606,10 @@ __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
                     }
 #pragma unroll
                     for (int r = 0; r < 16; r += 2) {
-                        mu_top2(tb[c], ts[c], acc0[r], acc0[r + 1]);
-                        mu_top2(tb[c + 1], ts[c + 1], acc1[r], acc1[r + 1]);
+                        if constexpr (ROWS) {
+                            mu_top2(tb[c], ts[c], acc0[r], acc0[r + 1]);
+                            mu_top2(tb[c + 1], ts[c + 1], acc1[r], acc1[r + 1]);
+                        }
                         // column keys: 256 e + ccol (wraps only for padded-train rows, never merged)
                         const int a0 = (int)(((unsigned)acc0[r] << 8) + (unsigned)ccol[c]);
                         const int a1 = (int)(((unsigned)acc1[r] << 8) + (unsigned)ccol[c + 1]);
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
         if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
         __syncthreads();
     }
-    if (active) {
+    if (ROWS && active) {
 #pragma unroll
         for (int c = 0; c < QT; ++c) {
             const int P1 = __shfl_xor(tb[c], 32), P2 = __shfl_xor(ts[c], 32);
@@ -648,11 +652,12 @@ __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
     for (int j = tid; j < k_pad; j += 512) dst[j] = lds_col[j];
 }
 
-// Exact dot product of two 128-byte i8 rows (v_dot4_i32_i8).
-__device__ __forceinline__ int mu_dot128(const uint4* x, const uint4* y) {
+// Exact dot product of two D-byte i8 rows (v_dot4_i32_i8).
+template <int D>
+__device__ __forceinline__ int mu_dot(const uint4* x, const uint4* y) {
     int s = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < D / 16; ++k) {
         const uint4 u = x[k], v = y[k];
         s = __builtin_amdgcn_sdot4((int)u.x, (int)v.x, s, false);
         s = __builtin_amdgcn_sdot4((int)u.y, (int)v.y, s, false);
@@ -669,6 +674,7 @@ __device__ __forceinline__ int mu_dot128(const uint4* x, const uint4* y) {
 #define MU_FT_THREADS 256
 #endif
 constexpr int MU_FT = MU_FT_THREADS;
+template <int D>
 __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs, int n_qblk,
@@ -691,8 +697,10 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
     const unsigned long long* cp = colpart + (size_t)p * n_qblk * k_pad;
     const int32_t* na_norm = norm + (size_t)a * k_pad;
     const int32_t* nb_norm = norm + (size_t)b * k_pad;
-    const uint4* qa = (const uint4*)(desc + (size_t)a * k_max * 128);
-    const uint4* dbv = (const uint4*)(desc + (size_t)b * k_max * 128);
+    constexpr bool SQ = D == 128;  // L2 reports d^2 (ratio on squares), Hamming d
+    constexpr int RS = D / 16;     // uint4 per feature row
+    const uint4* qa = (const uint4*)(desc + (size_t)a * k_max * D);
+    const uint4* dbv = (const uint4*)(desc + (size_t)b * k_max * D);
     int32_t* om = out_match + (size_t)p * k_max * 2;
     int32_t* od = out_dist + (size_t)p * k_max;
     auto col_winner = [&](int j) {  // train j's nearest query (lowest index), or -1
@@ -724,22 +732,22 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
             const int4 r = rowres[(size_t)p * k_pad + i];
             const long long A = na_norm[i];
             const unsigned long long e = lds_best[i];
-            const long long D = e != ~0ull ? (long long)(e >> 32) : sfm::DIST_INF;
+            const long long Dp = e != ~0ull ? (long long)(e >> 32) : sfm::DIST_INF;  // best proposal
             const long long d1lo = max(A - 2LL * r.x - 1, 0LL);
             const long long d2lo = r.y > MU_E_VALID ? A - 2LL * r.y - 1 : sfm::DIST_INF;
             const long long d2hi = r.y > MU_E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
             // not mutual: no train whose nearest query is i lies within the nearest distance
             // (if i were mutual with its nearest neighbour j1, j1 would propose d1 <= A - 2e1);
             // then the bounds: the ratio test / max_dist cannot pass even at the favourable ends
-            if (D <= A - 2LL * r.x && sfm::ratio_ok(d1lo, d2hi, rnum, rden, true) &&
+            if (Dp <= A - 2LL * r.x && sfm::ratio_ok(d1lo, d2hi, rnum, rden, SQ) &&
                 (max_dist < 0 || d1lo < max_dist)) {
                 if (r.x == r.y) {
                     sl = true;  // nearest neighbour not unique in e: exact row scan
                 } else {        // unique nearest neighbour = the proposing train, d1 = D exactly
-                    d1 = D;
+                    d1 = Dp;
                     jj = (int)(unsigned)e;
-                    if (sfm::ratio_ok(d1, d2lo, rnum, rden, true)) keep = true;
-                    else if (sfm::ratio_ok(d1, d2hi, rnum, rden, true)) sl = true;
+                    if (sfm::ratio_ok(d1, d2lo, rnum, rden, SQ)) keep = true;
+                    else if (sfm::ratio_ok(d1, d2hi, rnum, rden, SQ)) sl = true;
                     keep = keep && (max_dist < 0 || d1 < max_dist);
                 }
             }
@@ -753,13 +761,13 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
         const int ns = nslow;
         for (int s = 0; s < ns; ++s) {  // exact row scan of query i0 + slow[s] (rare)
             const int who = slow[s], q = i0 + who;
-            uint4 x[8];
+            uint4 x[RS];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) x[u] = qa[(size_t)q * 8 + u];
+            for (int u = 0; u < RS; ++u) x[u] = qa[(size_t)q * RS + u];
             long long b1 = sfm::DIST_INF, b2 = sfm::DIST_INF;
             int j1 = INT_MAX;
             for (int j = tid; j < nb; j += MU_FT) {
-                const long long d = (long long)na_norm[q] + nb_norm[j] - 2LL * mu_dot128(x, dbv + (size_t)j * 8);
+                const long long d = (long long)na_norm[q] + nb_norm[j] - 2LL * mu_dot<D>(x, dbv + (size_t)j * RS);
                 if (d < b1) { b2 = b1; b1 = d; j1 = j; } else if (d < b2) { b2 = d; }
             }
             rb1[tid] = b1; rb2[tid] = b2; rj1[tid] = j1;
@@ -778,7 +786,7 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
             if (tid == 0) {
                 const int n1 = rj1[0];
                 bool k = n1 >= 0 && n1 < nb && col_winner(n1) == q;
-                k = k && sfm::ratio_ok(rb1[0], rb2[0], rnum, rden, true);
+                k = k && sfm::ratio_ok(rb1[0], rb2[0], rnum, rden, SQ);
                 k = k && (max_dist < 0 || rb1[0] < max_dist);
                 keepx[who] = k;
                 jx[who] = n1;
@@ -788,6 +796,59 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
         }
         const bool kk = i < na && keepx[tid];
         base = sfm::compact_n<MU_FT>(kk, i, jx[tid], dx[tid], base, wsum, om, od);
+    }
+    if (tid == 0) out_count[p] = base;
+}
+
+
+// Finalize of the column-only kernel, the OpenCV cross-check rule (oracle_match cross_check 2, the
+// reference's BFMatcher(crossCheck=True), code/feature_matching.py:48): every train j proposes
+// (d, j) to its nearest query; each query keeps the smallest proposal (lowest j on ties).
+__global__ __launch_bounds__(256) void opencv_finalize_kernel(
+    const int32_t* __restrict__ n_kp, int k_max, int k_pad, const int32_t* __restrict__ norm,
+    const int32_t* __restrict__ pairs, int n_qblk, const unsigned long long* __restrict__ colpart,
+    long long max_dist, int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
+    int32_t* __restrict__ out_dist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
+    __shared__ int wsum[4];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    if (na <= 0 || nb <= 0) {
+        if (tid == 0) out_count[p] = 0;
+        return;
+    }
+    const unsigned long long* cp = colpart + (size_t)p * n_qblk * k_pad;
+    const int32_t* nb_norm = norm + (size_t)b * k_pad;
+    for (int i = tid; i < na; i += 256) lds_best[i] = ~0ull;
+    __syncthreads();
+    for (int j = tid; j < nb; j += 256) {
+        unsigned long long best = 0;
+        for (int q = 0; q < n_qblk; ++q) best = max(best, cp[(size_t)q * k_pad + j]);
+        if (best == 0) continue;
+        const int nd = (int)((unsigned)(best >> 32) ^ 0x80000000u);  // -d - p_j
+        const int gq = (int)(0xFFFFFFFFu - (unsigned)best);
+        if (gq < 0 || gq >= na) continue;
+        const long long d = -(long long)nd - (nb_norm[j] & 1);
+        atomicMin(&lds_best[gq], ((unsigned long long)d << 32) | (unsigned)j);
+    }
+    __syncthreads();
+    int base = 0;
+    int32_t* om = out_match + (size_t)p * k_max * 2;
+    int32_t* od = out_dist + (size_t)p * k_max;
+    for (int i0 = 0; i0 < na; i0 += 256) {
+        const int i = i0 + tid;
+        bool keep = false;
+        int j = 0, d = 0;
+        if (i < na) {
+            const unsigned long long e = lds_best[i];
+            if (e != ~0ull) {
+                d = (int)(e >> 32);
+                j = (int)(unsigned)e;
+                keep = max_dist < 0 || (long long)d < max_dist;
+            }
+        }
+        base = sfm::compact256(keep, i, j, d, base, wsum, om, od);
     }
     if (tid == 0) out_count[p] = base;
 }
@@ -858,8 +919,9 @@ static int mfma_match_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, cons
     return SFM_OK;
 }
 
-// L2 with the mutual cross check (any ratio): value-only row side + column winners.
-static int mfma_mutual_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp,
+// Mutual (any ratio) or OpenCV cross check, both metrics: value-only row side + column winners
+// (mutual), or the column side alone (OpenCV rule).
+static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const int32_t* n_kp,
                               int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
                               const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
                               int32_t* out_dist) {
@@ -868,7 +930,10 @@ static int mfma_mutual_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* 
         SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_pairs, st));
         return SFM_OK;
     }
-    constexpr int D = 128, QB = Geo<128>::QB;
+    const bool l2 = metric == SFM_METRIC_L2;
+    const bool rows = prm->cross_check == SFM_XC_MUTUAL;
+    const int D = l2 ? 128 : 256;
+    const int QB = l2 ? Geo<128>::QB : Geo<256>::QB;
     const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
     SFM_REQUIRE(k_pad <= KMAX_L2, "sfm_match_batch: MFMA matcher needs k_max <= 4096");
     const int n_qblk = (k_max + QB - 1) / QB;
@@ -888,19 +953,44 @@ static int mfma_mutual_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* 
     int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
     const int n_blk = n_pairs * n_qblk;
     const int grid = 8 * ((n_blk + 7) / 8);
-    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img,
-                       pair_order, pair_order + n_pairs);
+    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
+                       pairs, n_pairs, n_img, pair_order, pair_order + n_pairs);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_L2, true>), dim3(k_pad / 256, n_img), dim3(256),
-                       0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row, (uint4*)desc_i8);
+    if (l2)
+        hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_L2, true>), dim3(k_pad / 256, n_img),
+                           dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row,
+                           (uint4*)desc_i8);
+    else
+        hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_HAMMING, true>), dim3(k_pad / 256, n_img),
+                           dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row,
+                           (uint4*)desc_i8);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(mfma_mutual_kernel, dim3(grid), dim3(512), 0, st, desc_i8, n_kp, k_max, k_pad,
-                       norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk, rowres, colpart);
+#define SFM_MU_SCAN(DD, RR)                                                                       \
+    hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(512), 0, st, desc_i8, n_kp, \
+                       k_max, k_pad, norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk,     \
+                       rowres, colpart)
+    if (l2 && rows) SFM_MU_SCAN(128, true);
+    else if (l2) SFM_MU_SCAN(128, false);
+    else if (rows) SFM_MU_SCAN(256, true);
+    else SFM_MU_SCAN(256, false);
+#undef SFM_MU_SCAN
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(mutual_finalize_kernel, dim3(n_pairs), dim3(MU_FT), (size_t)k_pad * 8, st,
-                       desc_i8, n_kp, k_max, k_pad, norm, pairs, n_qblk, rowres, colpart,
-                       prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, out_count,
-                       out_match, out_dist);
+    if (rows) {
+        if (l2)
+            hipLaunchKernelGGL(mutual_finalize_kernel<128>, dim3(n_pairs), dim3(MU_FT),
+                               (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
+                               n_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
+                               (long long)prm->max_dist, out_count, out_match, out_dist);
+        else
+            hipLaunchKernelGGL(mutual_finalize_kernel<256>, dim3(n_pairs), dim3(MU_FT),
+                               (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
+                               n_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
+                               (long long)prm->max_dist, out_count, out_match, out_dist);
+    } else {
+        hipLaunchKernelGGL(opencv_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st,
+                           n_kp, k_max, k_pad, norm, pairs, n_qblk, colpart,
+                           (long long)prm->max_dist, out_count, out_match, out_dist);
+    }
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
@@ -909,12 +999,11 @@ int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, 
                         int32_t k_max, const int32_t* pairs, int32_t n_pairs,
                         const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
                         int32_t* out_dist) {
-    // Path per rule (cfg3, 1225 pairs x 2048): mutual cross check -> the
-    // value-only-row mutual kernel; ratio test without cross check -> the forward/reverse path
-    // (match_l2fr.hip); everything else (OpenCV rule, no cross check and no ratio) -> the fused
-    // key kernel.  SFM_L2_PATH=mutual|fr|fused overrides where the rule allows it.
+    // Path per rule (cfg3, 1225 pairs x 2048): mutual or OpenCV cross check ->
+    // the value-only-row / column-only kernel; ratio test without cross check -> the forward/
+    // reverse path (match_l2fr.hip); no cross check and no ratio -> the fused key kernel.
+    // SFM_L2_PATH=mutual|fr|fused overrides where the rule allows it.
     const char* pe = getenv("SFM_L2_PATH");
-    const bool xc_mutual = prm->cross_check == SFM_XC_MUTUAL;
     const bool ratio = prm->ratio_den > 0;
     if (pe && strcmp(pe, "fused") == 0)
         return mfma_match_launch(ctx, SFM_METRIC_L2, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
@@ -922,10 +1011,10 @@ int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, 
     if (pe && strcmp(pe, "fr") == 0 && ratio && prm->cross_check != SFM_XC_OPENCV)
         return sfm_match_l2fr_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
                                      out_count, out_match, out_dist);
-    if (xc_mutual)
-        return mfma_mutual_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm, out_count,
-                                  out_match, out_dist);
-    if (ratio && prm->cross_check == SFM_XC_NONE)
+    if (prm->cross_check != SFM_XC_NONE)
+        return mfma_mutual_launch(ctx, SFM_METRIC_L2, desc, n_kp, n_img, k_max, pairs, n_pairs,
+                                  prm, out_count, out_match, out_dist);
+    if (ratio)
         return sfm_match_l2fr_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
                                      out_count, out_match, out_dist);
     return mfma_match_launch(ctx, SFM_METRIC_L2, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
@@ -936,6 +1025,17 @@ int sfm_match_hamming_mfma_launch(sfm_ctx* ctx, const uint8_t* desc, const int32
                                   int32_t n_img, int32_t k_max, const int32_t* pairs,
                                   int32_t n_pairs, const sfm_match_params* prm,
                                   int32_t* out_count, int32_t* out_match, int32_t* out_dist) {
+    // The reference's OpenCV cross-check rule: the column side alone (0.126 vs 0.156 ms at 50 x 500,
+    // 1.30 vs 1.73 ms at 50 x 2048).  Mutual and no cross check: the fused key kernel — with
+    // Hamming distances (0..256) ties in e are the rule, not the exception, and every tie costs the
+    // value-only row side an exact row scan (0.68 vs 0.16 ms).  SFM_HAMMING_PATH=fused|mutual
+    // overrides.
+    const char* pe = getenv("SFM_HAMMING_PATH");
+    const bool col = pe && strcmp(pe, "mutual") == 0 ? prm->cross_check != SFM_XC_NONE
+                                                    : prm->cross_check == SFM_XC_OPENCV;
+    if (col && !(pe && strcmp(pe, "fused") == 0))
+        return mfma_mutual_launch(ctx, SFM_METRIC_HAMMING, desc, n_kp, n_img, k_max, pairs,
+                                  n_pairs, prm, out_count, out_match, out_dist);
     return mfma_match_launch(ctx, SFM_METRIC_HAMMING, desc, n_kp, n_img, k_max, pairs, n_pairs,
                              prm, out_count, out_match, out_dist);
 }

@@ -23,7 +23,7 @@ def main():
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
     for xc, ratio, path in ((1, (4, 5), "mutual"), (1, (4, 5), "fused"), (1, (4, 5), "fr"),
-                            (0, (4, 5), "fr"), (0, (4, 5), "fused"), (2, None, "fused"),
+                            (0, (4, 5), "fr"), (0, (4, 5), "fused"), (2, None, "fused"), (2, None, "colonly"),
                             (1, None, "mutual")):
         os.environ["SFM_L2_PATH"] = path
         out = ctx.match_batch(desc, n_kp, pr, cross_check=xc, ratio=ratio)

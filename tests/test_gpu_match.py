@@ -180,7 +180,7 @@ def test_l2_ratio_path_and_fused_kernel_agree(ctx, K):
     n_kp = s["n_kp"].copy()
     n_kp[2] = K - 101
     pairs = synth.unordered_pairs(4)
-    for xc, ratio in ((1, (4, 5)), (0, (4, 5)), (1, (9, 10)), (1, None)):
+    for xc, ratio in ((1, (4, 5)), (0, (4, 5)), (1, (9, 10)), (1, None), (2, None)):
         outs = []
         for v in (("fr", "fused", "mutual") if ratio else ("mutual", "fused")):
             os.environ["SFM_L2_PATH"] = v
@@ -194,3 +194,21 @@ def test_l2_ratio_path_and_fused_kernel_agree(ctx, K):
             for p in range(len(pairs)):
                 np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
                 np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
+
+
+@pytest.mark.parametrize("xc", [1, 2])
+def test_hamming_column_winner_kernel(ctx, xc):
+    """The column-winner kernel on Hamming (column side only for the OpenCV rule; + value-only
+    rows for mutual, tie-heavy on small integer distances): identical to the oracle."""
+    import os
+    s = synth.make_scene(3, 700, seed=77, orb=True)
+    n_kp = s["n_kp"].copy()
+    n_kp[2] = 433
+    pairs = np.array([[0, 1], [1, 2], [2, 0], [1, 0]], np.int32)
+    os.environ["SFM_HAMMING_PATH"] = "mutual"
+    try:
+        _check_pairs(ctx, s["desc"], n_kp, pairs, metric=1, cross_check=xc, max_dist=26)
+        _check_pairs(ctx, s["desc"], n_kp, pairs, metric=1, cross_check=xc,
+                     ratio=(4, 5) if xc == 1 else None)
+    finally:
+        os.environ.pop("SFM_HAMMING_PATH", None)
