@@ -581,20 +581,30 @@ __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
         if (active) {
             const unsigned char* A = cur;
             const int* Ci = (const int*)(cur + CHUNK * D);
-            for (int tt = 0; tt < nt; ++tt) {
+            // A fragments + accumulator init of tile tt (accumulator register r of this lane is
+            // train row 8*(r/4) + 4*h + r%4)
+            auto load_tile = [&](int tt, v4i (&af)[NK], v16i& init) {
                 const int row = tt * 32 + r32;
                 const int sw = swz<D>(row);
-                v4i af[NK];
 #pragma unroll
                 for (int s = 0; s < NK; ++s)
                     af[s] = *(const v4i*)(A + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
-                v16i init;  // accumulator register r of this lane is train row 8*(r/4) + 4*h + r%4
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
                     init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
                     init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
                 }
+            };
+            v4i af[NK];
+            v16i init;
+#ifdef MU_PF
+            load_tile(0, af, init);
+#endif
+            for (int tt = 0; tt < nt; ++tt) {
+#ifndef MU_PF
+                load_tile(tt, af, init);
+#endif
                 int colacc[16];
 #pragma unroll
                 for (int c = 0; c < QT; c += 2) {
@@ -604,6 +614,10 @@ __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
                         acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
                         acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
                     }
+#ifdef MU_PF
+                    // the next tile's fragments load behind this tile's last epilogue
+                    if (c + 2 == QT && tt + 1 < nt) load_tile(tt + 1, af, init);
+#endif
 #pragma unroll
                     for (int r = 0; r < 16; r += 2) {
                         if constexpr (ROWS) {
