@@ -429,10 +429,18 @@ __global__ __launch_bounds__(256) void ransac_fit_kernel(
         smp[k] = make_float4(pl[idx[k]], pl[kp + idx[k]], pl[2 * kp + idx[k]],
                              pl[3 * kp + idx[k]]);
     float F[9], G[9];
+#ifdef RANSAC_ABL_NOFIT  // ablation: no 8-point fit (timing only; results invalid)
+    const bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) F[k] = smp[k & 7].x * (float)(k + 1) + smp[(k + 3) & 7].w;
+#else
     const bool ok = fit_f8(smp, F);
+#endif
     sampson_prep(F, k1, k2, G);
     int cnt = 0;
+#ifndef RANSAC_ABL_NOPREVIEW  // ablation: no preview (timing only; order degenerates)
     score_matches<false, 8>(S, kp, G, 0, min(PV, M), M, cnt, nullptr);  // 8-match chunks: fewer VGPRs beside the fit
+#endif
     float* gt = hypG + (size_t)p * 9 * n_hyp + h;
 #pragma unroll
     for (int i = 0; i < 9; ++i) gt[(size_t)i * n_hyp] = G[i];

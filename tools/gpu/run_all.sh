@@ -1,4 +1,5 @@
 set -o pipefail
+# GPU-box driver scripts (run through gpurun from the repo root, e.g. gpurun -- bash tools/gpu/run_all.sh TAG).
 TAG=${1:-r1c}
 mkdir -p gpurun_out/prof_$TAG
 export TMPDIR=/tmp
