@@ -515,19 +515,36 @@ __device__ __forceinline__ void mu_top2(int& tb, int& ts, int x, int y) {
 }
 
 // ROWS = false: column side only (the OpenCV cross-check rule needs nothing else).
+// Workgroup shape of the column-winner kernel: MU_WAVES waves x QT query tiles, MU_CHUNK_BYTES of
+// train rows per LDS stage, built for MU_MINW waves per SIMD.  Default 4 waves x 16 KB stages x 2
+// waves/SIMD: interleaved A/B on cfg3 (profiles/r01_k1_shapes.txt), mutual + ratio 1.00 ms against
+// 1.04 (8 waves, 32 KB), 1.05 (8 waves, 16 KB), 1.22 (4 waves, 32 KB) and 1.06 (3 waves/SIMD,
+// spills); the column-only kernel is shape-neutral (0.84 ms).
+#ifndef MU_WAVES
+#define MU_WAVES 4
+#endif
+#ifndef MU_CHUNK_BYTES
+#define MU_CHUNK_BYTES 16384
+#endif
+#ifndef MU_MINW
+#define MU_MINW 2
+#endif
+template <int D> constexpr int mu_qb() { return MU_WAVES * Geo<D>::QT * 32; }
+
 template <int D, bool ROWS>
-__global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
+__global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
     const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
     unsigned long long* __restrict__ colpart) {
-    constexpr int QT = Geo<D>::QT, QB = Geo<D>::QB, CHUNK = Geo<D>::CHUNK, NK = Geo<D>::NK;
-    constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32;
-    constexpr int PIECES = CHUNK * D / 1024 / WAVES, RPP = 1024 / D;
+    constexpr int QT = Geo<D>::QT, QB = mu_qb<D>(), CHUNK = MU_CHUNK_BYTES / D, NK = Geo<D>::NK;
+    constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32, NTHR = 64 * MU_WAVES;
+    constexpr int PIECES = CHUNK * D / 1024 / MU_WAVES, RPP = 1024 / D;
+    static_assert(PIECES >= 1 && CHUNK % 32 == 0 && CHUNK / 4 <= 64, "stage geometry");
     __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
     __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
-    __shared__ unsigned long long lds_col[KMAX_L2];
+    extern __shared__ unsigned long long lds_col[];  // [k_pad], dynamic
 
     const int per_xcd = (int)(gridDim.x >> 3);
     const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
@@ -536,7 +553,7 @@ __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
-    for (int j = tid; j < k_pad; j += 512) lds_col[j] = 0ull;
+    for (int j = tid; j < k_pad; j += NTHR) lds_col[j] = 0ull;
 
     const uint8_t* db = desc + (size_t)b * k_max * D;
     const int32_t* cib = cinit + (size_t)b * k_pad;
@@ -663,7 +680,7 @@ __global__ __launch_bounds__(512, 2) void mfma_mutual_kernel(
         }
     }
     unsigned long long* dst = colpart + ((size_t)p * n_qblk + qb) * k_pad;
-    for (int j = tid; j < k_pad; j += 512) dst[j] = lds_col[j];
+    for (int j = tid; j < k_pad; j += NTHR) dst[j] = lds_col[j];
 }
 
 // Exact dot product of two D-byte i8 rows (v_dot4_i32_i8).
@@ -947,7 +964,7 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     const bool l2 = metric == SFM_METRIC_L2;
     const bool rows = prm->cross_check == SFM_XC_MUTUAL;
     const int D = l2 ? 128 : 256;
-    const int QB = l2 ? Geo<128>::QB : Geo<256>::QB;
+    const int QB = l2 ? mu_qb<128>() : mu_qb<256>();
     const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
     SFM_REQUIRE(k_pad <= KMAX_L2, "sfm_match_batch: MFMA matcher needs k_max <= 4096");
     const int n_qblk = (k_max + QB - 1) / QB;
@@ -980,7 +997,8 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
                            (uint4*)desc_i8);
     SFM_HIP_CHECK(hipGetLastError());
 #define SFM_MU_SCAN(DD, RR)                                                                       \
-    hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(512), 0, st, desc_i8, n_kp, \
+    hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(64 * MU_WAVES),             \
+                       (size_t)k_pad * 8, st, desc_i8, n_kp,                                      \
                        k_max, k_pad, norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk,     \
                        rowres, colpart)
     if (l2 && rows) SFM_MU_SCAN(128, true);

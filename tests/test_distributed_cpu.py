@@ -131,3 +131,13 @@ def test_packed_graph_single_process_roundtrip():
     assert c.tolist() == [0, 2, 0, 1]
     g = match_graph.all_gather_graph(c, pk, [(2, 6)])
     np.testing.assert_array_equal(g.numpy(), rows.numpy())
+
+
+def test_all_gather_packed_graph_gloo_world3(tmp_path):
+    """Three ranks, uneven shards (10 pairs): the exchange still yields the single-process rows."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "graph.npy")
+    mp.spawn(_worker_packed, args=(3, _free_port(), out), nprocs=3, join=True)
+    scene = _scene()
+    full = _rows_for(scene, synth.unordered_pairs(N_IMG), 0)
+    np.testing.assert_array_equal(np.load(out), full)
