@@ -227,16 +227,35 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
         return;
     }
     float sx1 = 0.f, sy1 = 0.f, sx2 = 0.f, sy2 = 0.f;
-    for (int m = l; m < M; m += 64) {
-        const float2 u = *(const float2*)(kps + ((size_t)a * k_max + mt[2 * m]) * 2);
-        const float2 v = *(const float2*)(kps + ((size_t)b * k_max + mt[2 * m + 1]) * 2);
-        sx1 = sx1 + u.x; sy1 = sy1 + u.y; sx2 = sx2 + v.x; sy2 = sy2 + v.y;
-        X1[m] = u.x; Y1[m] = u.y; X2[m] = v.x; Y2[m] = v.y;
+    // four matches per lane in flight (index loads, then the coordinate gathers): one wave per
+    // pair is latency-bound; the sums still accumulate in m order
+    for (int m0 = l; m0 < M; m0 += 256) {
+        int2 id[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int m = m0 + 64 * t;
+            id[t] = m < M ? *(const int2*)(mt + 2 * m) : make_int2(0, 0);
+        }
+        float2 u[4], v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            u[t] = *(const float2*)(kps + ((size_t)a * k_max + id[t].x) * 2);
+            v[t] = *(const float2*)(kps + ((size_t)b * k_max + id[t].y) * 2);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int m = m0 + 64 * t;
+            if (m < M) {
+                sx1 = sx1 + u[t].x; sy1 = sy1 + u[t].y; sx2 = sx2 + v[t].x; sy2 = sy2 + v[t].y;
+                X1[m] = u[t].x; Y1[m] = u[t].y; X2[m] = v[t].x; Y2[m] = v[t].y;
+            }
+        }
     }
     const float fM = (float)M;
     const float mx1 = wave_fixed_sum(sx1) / fM, my1 = wave_fixed_sum(sy1) / fM;
     const float mx2 = wave_fixed_sum(sx2) / fM, my2 = wave_fixed_sum(sy2) / fM;
     float sd1 = 0.f, sd2 = 0.f;
+#pragma unroll 4
     for (int m = l; m < M; m += 64) {
         const float4 w = make_float4(X1[m], Y1[m], X2[m], Y2[m]);
         float dx = w.x - mx1, dy = w.y - my1;
@@ -253,6 +272,7 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
     const float s2 = (mean2 > 0.0f) ? (1.41421356237309515f / mean2) : 1.0f;
     float k1, k2;
     sampson_scales(s1, s2, thr, k1, k2);
+#pragma unroll 4
     for (int m = l; m < M; m += 64) {
         const float x1 = (X1[m] - mx1) * s1, y1 = (Y1[m] - my1) * s1;
         const float x2 = (X2[m] - mx2) * s2, y2 = (Y2[m] - my2) * s2;
@@ -447,17 +467,18 @@ __global__ __launch_bounds__(256) void ransac_fit_kernel(
     prev[(size_t)p * n_hyp + h] = ok ? cnt : -1;
 }
 
-__global__ __launch_bounds__(1024) void ransac_order_kernel(int n_hyp,
-                                                            const int32_t* __restrict__ match_count,
-                                                            const int32_t* __restrict__ prev,
-                                                            uint16_t* __restrict__ order) {
+// 256 threads per pair: every block of a launch is resident at once (the kernel is latency-bound)
+__global__ __launch_bounds__(256) void ransac_order_kernel(int n_hyp,
+                                                           const int32_t* __restrict__ match_count,
+                                                           const int32_t* __restrict__ prev,
+                                                           uint16_t* __restrict__ order) {
     __shared__ int hist[PV + 2];  // bucket = preview count + 1 (degenerate -1 -> 0)
     const int p = blockIdx.x, tid = threadIdx.x;
     if (match_count[p] < 8) return;
     const int32_t* pv = prev + (size_t)p * n_hyp;
     if (tid < PV + 2) hist[tid] = 0;
     __syncthreads();
-    for (int h = tid; h < n_hyp; h += 1024) atomicAdd(&hist[pv[h] + 1], 1);
+    for (int h = tid; h < n_hyp; h += 256) atomicAdd(&hist[pv[h] + 1], 1);
     __syncthreads();
     if (tid == 0) {  // descending exclusive offsets
         int off = 0;
@@ -468,7 +489,7 @@ __global__ __launch_bounds__(1024) void ransac_order_kernel(int n_hyp,
         }
     }
     __syncthreads();
-    for (int h = tid; h < n_hyp; h += 1024)
+    for (int h = tid; h < n_hyp; h += 256)
         order[(size_t)p * n_hyp + atomicAdd(&hist[pv[h] + 1], 1)] = (uint16_t)h;
 }
 
@@ -605,7 +626,7 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
         hipLaunchKernelGGL(ransac_fit_kernel, grid, dim3(256), 0, st, k_max, pairs, match_count,
                            planes, out_norm, prm->seed, prm->thr, H, hypG, prev);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(1024), 0, st, H, match_count,
+        hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                            prev, order);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(ransac_score_kernel<true>, grid, dim3(256), 0, st, k_max, match_count,
