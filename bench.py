@@ -1,22 +1,30 @@
 #!/usr/bin/env python3
 """bench.py — verified matches/sec (match + RANSAC) on MI355X, 1..8 GPUs (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2]): 50 synthetic images x 2048 SIFT-like
-128-D u8 descriptors, all 1225 unordered pairs; per pair K1 (MFMA L2 match, mutual cross check +
-Lowe ratio 0.8) then K2 (8-point RANSAC, 4096 hypotheses, seed 42, Sampson 1 px^2, min 15 inliers).
-A step = one pass of match + verify over the pair list with descriptors/keypoints already resident
-in HBM, plus, for N > 1, the graph exchange: per-pair counts + 4-byte packed rows, RCCL
-all-gather, expanded to (pair, queryIdx, trainIdx) rows on every rank.
+Workload (default `--config cfg4`, BASELINE.json configs[3]): 500 synthetic images
+x 4096 SIFT-like 128-D u8 descriptors, all 124 750 unordered pairs; per pair K1 (MFMA L2 match,
+mutual cross check + Lowe ratio 4/5) then K2 (8-point RANSAC, 4096 hypotheses, seed 42, Sampson
+1 px^2, min 15 inliers).  `--config cfg3` (configs[2]) is 50 x 2048, 1225 pairs.
 
-Scaling is weak: at N GPUs the scene has n_img images with n_img(n_img-1)/2 ~= 1225*N pairs, cut
-into N contiguous cost-balanced shards (one process per GPU, no collective on the data path).
-value = verified matches (all ranks) per step * steps / max-over-ranks wall time.
+A step = one pass of match + verify over this rank's pairs (launched in chunks of `--chunk`
+pairs) with descriptors/keypoints already resident in HBM, producing the verified match graph:
+rows (pair, queryIdx, trainIdx) of every verified pair's inliers.  For N > 1 the step ends with
+the graph exchange (per-pair counts + 4-byte packed rows, RCCL all-gather, expanded on every
+rank), the analogue of `pair_matches` (code/pipeline.py:36-47).
 
-Also reported (rank 0): `roofline` of K1 (algorithmic 2*Ka*Kb*128 ops per pair over the K1 time
-measured with HIP events on the launch stream, against the dense i8 MFMA peak), the RANSAC stage
-against the fp32 vector peak, and `cpu_baseline`: the CPU oracle (oracle/, OpenMP over pairs) timed
-on a bounded sample of the same pairs on this host, with a bit-exact comparison of the sampled
-pairs' inlier counts against the GPU's.
+Scaling is strong: the pair list is fixed and cut into N contiguous cost-balanced shards (one
+process per GPU, no collective on the data path, RANSAC keyed by (seed, a, b, h) so results do
+not depend on the sharding).  value = verified matches of the whole graph per step * steps /
+max-over-ranks wall time.
+
+Also reported (rank 0): `roofline` of K1 (algorithmic 2*Ka*Kb*128 i8 ops per pair over the K1
+time measured with HIP events on the launch stream, against the dense i8 MFMA peak), the RANSAC
+stage against the f32 vector peak (algorithmic and executed evaluations), `cpu_baseline` (N = 1):
+the CPU oracle (oracle/, OpenMP over pairs) timed on a bounded stride sample of the same pairs on
+this host, with the sampled pairs' full results (match indices, inlier masks, winners, graph
+rows) compared against the GPU's, and `cfg1_cpu`: the reference's own shape (2 images x 512,
+code/feature_matching.py:48-58 + RANSAC) timed fully on one core.  `cfg3` (N = 1, cfg4 runs):
+the north_star's 2048 x 128 K1 kernel and the cfg3 step, measured in the same run.
 """
 import argparse
 import json
@@ -32,18 +40,26 @@ sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracl
 PEAK_I8_TOPS = 2048 * 4 * 256 * 2.4e9 / 1e12        # 5033 TOP/s
 PEAK_F32_VALU_TFLOPS = 157.3
 RANSAC_FLOP_PER_EVAL = 33      # Sampson test: 16 fma + 1 mul (ransac.hip sampson_inlier)
-RANSAC_FLOP_PER_FIT = 1400     # sample + fit_f8: Householder QR 8x9 + Q e9 + adj(F^T F) power iteration
+RANSAC_FLOP_PER_FIT = 1400     # sample + fit_f8
+
+CONFIGS = {
+    "cfg3": dict(n_img=50, k=2048, name="BASELINE configs[2] (cfg3)"),
+    "cfg4": dict(n_img=500, k=4096, name="BASELINE configs[3] (cfg4)"),
+}
 
 
-def pmc_traffic(kernel, n_img, k, world):
+def pmc_traffic(kernel, cfg, n_img, k, world):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this exact workload
-    (tools/pmc_traffic.sh -> profiles/r01_traffic_cfg3.json: FETCH_SIZE x2 + WRITE_SIZE, separate
-    passes, MI355X_MICROARCH.md corrections), or None for any other workload."""
-    f = os.path.join(ROOT, "profiles", "r01_traffic_cfg3.json")
-    if not (os.path.exists(f) and n_img == 50 and k == 2048 and world == 1):
+    (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes, MI355X_MICROARCH.md
+    corrections), or None when no summary of this workload is committed."""
+    f = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    if not os.path.exists(f) or world != 1:
         return None
     try:
-        return float(json.load(open(f))["kernels"][kernel]["hbm_bytes"])
+        d = json.load(open(f))
+        if d.get("n_img") != n_img or d.get("k") != k:
+            return None
+        return float(d["kernels"][kernel]["hbm_bytes"])
     except (KeyError, ValueError):
         return None
 
@@ -52,17 +68,90 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model():
+    try:
+        return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if "model name" in l][0]
+    except Exception:
+        return "unknown"
+
+
+def workload_string(cfg, n_img, k, n_hyp, chunk):
+    return (f"{cfg}: all {n_img * (n_img - 1) // 2} unordered pairs of {n_img} synthetic images x "
+            f"{k} 128-D u8 SIFT-like descriptors; L2 match (mutual cross check + ratio 4/5) + "
+            f"8-point RANSAC {n_hyp} hyp/pair (seed 42, Sampson 1 px^2, min 15 inliers); "
+            f"launches of <= {chunk} pairs")
+
+
+class Runner:
+    """One image set resident on this GPU and this rank's pair shard, cut into launch chunks."""
+
+    def __init__(self, scene, pairs, lo, hi, chunk, n_hyp, local):
+        import numpy as np
+        import torch
+        import match_graph
+        self.torch, self.np = torch, np
+        self.gb = match_graph.GraphBuilder(scene["desc"], scene["kps"], scene["n_kp"],
+                                           device=local, ratio=(4, 5), n_hyp=n_hyp, seed=42,
+                                           thr=1.0, min_inliers=15)
+        self.lo, self.hi = lo, hi
+        shard = pairs[lo:hi]
+        self.chunks = []
+        for c0 in range(0, len(shard), chunk):
+            part = np.ascontiguousarray(shard[c0:c0 + chunk])
+            self.chunks.append((lo + c0, torch.from_numpy(part).cuda()))
+        n_kp = scene["n_kp"].astype(np.float64)
+        self.k1_ops = 2.0 * 128 * float(np.sum(n_kp[shard[:, 0]] * n_kp[shard[:, 1]]))
+
+    def step(self, ranges=None, ev=None):
+        """One pass over the shard; returns the graph rows [n,3] (whole graph when `ranges`)."""
+        import match_graph
+        torch = self.torch
+        rows_l, cnt_l, pk_l = [], [], []
+        for ci, (base, pt) in enumerate(self.chunks):
+            if ev is not None:
+                ev[ci][0].record()
+            count, match, _ = self.gb.match(pt)
+            if ev is not None:
+                ev[ci][1].record()
+            rs = self.gb.verify(pt, count, match)
+            if ev is not None:
+                ev[ci][2].record()
+            if ranges is None:
+                rows_l.append(self.gb.graph_rows(base, count, match, rs))
+            else:
+                rows, offs = self.gb.graph_rows(base, count, match, rs, return_offsets=True)
+                c, pk = match_graph.pack_rows(rows, offs)
+                cnt_l.append(c)
+                pk_l.append(pk)
+        if ranges is None:
+            return rows_l[0] if len(rows_l) == 1 else torch.cat(rows_l)
+        return match_graph.all_gather_graph(torch.cat(cnt_l), torch.cat(pk_l), ranges)
+
+    def events(self):
+        torch = self.torch
+        return [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in self.chunks]
+
+    @staticmethod
+    def stage_ms(ev):
+        m = sum(e[0].elapsed_time(e[1]) for e in ev)
+        r = sum(e[1].elapsed_time(e[2]) for e in ev)
+        return m, r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n-img", type=int, default=0, help="override image count")
-    ap.add_argument("--k", type=int, default=2048)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg4")
+    ap.add_argument("--n-img", type=int, default=0, help="override the config's image count")
+    ap.add_argument("--k", type=int, default=0, help="override the config's keypoints/image")
     ap.add_argument("--n-hyp", type=int, default=4096)
-    ap.add_argument("--cpu-pairs", type=int, default=384,
-                    help="CPU baseline sample (pairs; ~20 s of CPU work at cfg3)")
+    ap.add_argument("--chunk", type=int, default=16384, help="pairs per K1/K2 launch")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="CPU baseline budget (the sample is sized to about this much wall)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 side measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: 'gloo' lets N ranks share one GPU (RCCL cannot)")
     ap.add_argument("--device", type=int, default=-1, help="rehearsal only: force this GPU")
@@ -87,48 +176,29 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    n_img = args.n_img or (50 if world == 1 else
-                           int(round((1 + math.sqrt(1 + 8 * 1225 * world)) / 2)))
+    cfg = CONFIGS[args.config]
+    n_img = args.n_img or cfg["n_img"]
+    k = args.k or cfg["k"]
     t0 = time.time()
-    scene = synth.make_scene(n_img, args.k, seed=0)
+    scene = synth.make_scene(n_img, k, seed=0)
     pairs = synth.unordered_pairs(n_img)
     ranges = [match_graph.shard_range(pairs, r, world, scene["n_kp"]) for r in range(world)]
-    pair_base, pair_end = ranges[rank]
-    shard = pairs[pair_base:pair_end]
-    log(f"[rank {rank}] scene {n_img} imgs x {args.k} kps, {len(pairs)} pairs, shard "
-        f"{len(shard)} (gen {time.time() - t0:.1f}s)")
-
-    gb = match_graph.GraphBuilder(scene["desc"], scene["kps"], scene["n_kp"], device=local,
-                                  ratio=(4, 5), n_hyp=args.n_hyp, seed=42, thr=1.0,
-                                  min_inliers=15)
-    pairs_t = torch.from_numpy(np.ascontiguousarray(shard)).cuda()
-
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record()
-        count, match, _ = gb.match(pairs_t)
-        if ev is not None:
-            ev[1].record()
-        rs = gb.verify(pairs_t, count, match)
-        if ev is not None:
-            ev[2].record()
-        if world == 1:  # the local rows are the whole graph: no exchange
-            return gb.graph_rows(pair_base, count, match, rs), count, rs
-        rows, offs = gb.graph_rows(pair_base, count, match, rs, return_offsets=True)
-        counts, packed = match_graph.pack_rows(rows, offs)
-        graph = match_graph.all_gather_graph(counts, packed, ranges)
-        return graph, count, rs
+    lo, hi = ranges[rank]
+    run = Runner(scene, pairs, lo, hi, args.chunk, args.n_hyp, local)
+    log(f"[rank {rank}] {args.config}: {n_img} imgs x {k} kps, {len(pairs)} pairs, shard "
+        f"[{lo},{hi}) in {len(run.chunks)} launches (gen {time.time() - t0:.1f}s)")
+    xr = ranges if world > 1 else None
 
     for _ in range(args.warmup):
-        step()
+        run.step(xr)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    evs = [run.events() for _ in range(args.steps)]
     t_start = time.perf_counter()
-    for k in range(args.steps):
-        graph, count, rs = step(evs[k])
+    for s in range(args.steps):
+        graph = run.step(xr, evs[s])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -140,16 +210,11 @@ def main():
     elapsed = float(el.item())
 
     verified_per_step = int(graph.shape[0])
-    match_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    ransac_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    n_kp = scene["n_kp"].astype(np.float64)
-    k1_ops = 2.0 * 128 * float(np.sum(n_kp[shard[:, 0]] * n_kp[shard[:, 1]]))
-    k1_tops = k1_ops / (match_ms * 1e-3) / 1e12
-    cnt_np = count.cpu().numpy()
-    m_valid = np.where(cnt_np >= 8, cnt_np, 0).astype(np.float64)
-    r_flops = args.n_hyp * float(np.sum(m_valid * RANSAC_FLOP_PER_EVAL + (m_valid > 0) * RANSAC_FLOP_PER_FIT))
-    r_tflops = r_flops / (ransac_ms * 1e-3) / 1e12
-
+    st = [Runner.stage_ms(e) for e in evs]
+    match_ms = float(np.mean([s[0] for s in st]))
+    ransac_ms = float(np.mean([s[1] for s in st]))
+    k1_tops = run.k1_ops / (match_ms * 1e-3) / 1e12
+    r_alg, r_exec = ransac_flops(run, args.n_hyp)
     value = verified_per_step * args.steps / elapsed
     result = {
         "metric": "verified matches/sec (match+RANSAC)",
@@ -160,65 +225,201 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int8 MFMA -> exact int32 (K1), f32 (K2)",
         "data": "synthetic (seeded scene: SIFT-like u8 descriptors, 25% misplaced keypoints)",
         "config": {
-            "workload": ("cfg3: all unordered pairs of n_img synthetic images x 2048 128-D u8 "
-                         "descriptors; L2 match (mutual cross check + ratio 4/5) + 8-point "
-                         "RANSAC 4096 hyp/pair (seed 42, Sampson 1 px^2, min 15 inliers)"),
-            "n_img": n_img, "pairs_total": int(len(pairs)), "pairs_per_gpu": int(len(shard)),
-            "k": args.k, "n_hyp": args.n_hyp, "parallelism": f"pair-sharded dp{world}",
+            "workload": workload_string(args.config, n_img, k, args.n_hyp, args.chunk),
+            "baseline_config": cfg["name"], "n_img": n_img, "k": k, "n_hyp": args.n_hyp,
+            "pairs_total": int(len(pairs)), "pairs_rank0": int(hi - lo),
+            "launches_rank0": len(run.chunks), "parallelism": f"pair-sharded dp{world}",
         },
         "verified_matches_per_step": verified_per_step,
-        "roofline": {"kernel": "K1 L2 match, mutual rule (mfma_prep + mfma_mutual_kernel + mutual_finalize, HIP events)",
+        "roofline": {"kernel": "K1 L2 match, mutual rule (mfma_prep + mfma_mutual_kernel + "
+                               "mutual_finalize, HIP events on the launch stream, rank 0)",
                      "bound": "mfma", "achieved": k1_tops, "peak": PEAK_I8_TOPS,
                      "unit": "TOP/s (i8)", "frac": k1_tops / PEAK_I8_TOPS,
-                     "traffic": pmc_traffic("mfma_mutual_kernel", n_img, args.k, world),
-                     "traffic_unit": "bytes per mfma_mutual_kernel launch (PMC, profiles/r01_traffic_cfg3.json)",
-                     "ms": match_ms, "ops_per_launch": k1_ops},
+                     "traffic": pmc_traffic("mfma_mutual_kernel", args.config, n_img, k, world),
+                     "traffic_unit": f"HBM bytes per step (all launches), PMC, "
+                                     f"profiles/traffic_{args.config}.json",
+                     "ms": match_ms, "ops_per_step": run.k1_ops},
         "stages": {"match_ms": match_ms, "ransac_ms": ransac_ms,
                    "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,
-                   "ransac_roofline": {"bound": "f32 VALU", "achieved": r_tflops,
-                                       "peak": PEAK_F32_VALU_TFLOPS, "unit": "TFLOP/s",
-                                       "frac": r_tflops / PEAK_F32_VALU_TFLOPS,
-                                       "flops_per_launch": r_flops}},
+                   "ransac_roofline": {
+                       "bound": "f32 VALU", "peak": PEAK_F32_VALU_TFLOPS, "unit": "TFLOP/s",
+                       "achieved": r_alg / (ransac_ms * 1e-3) / 1e12,
+                       "frac": r_alg / (ransac_ms * 1e-3) / 1e12 / PEAK_F32_VALU_TFLOPS,
+                       "flops_per_step": r_alg,
+                       "note": "algorithmic = every hypothesis scored on every match; the exact "
+                               "pruning skips part of it (executed_frac_estimate)",
+                       "executed_frac_estimate": r_exec}},
     }
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(scene, pairs, shard, pair_base, count, rs,
-                                              args.cpu_pairs, args.n_hyp)
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(scene, pairs, lo, hi, graph, run.gb,
+                                                  args.cpu_seconds, args.n_hyp)
+            result["cfg1_cpu"] = cfg1_timing()
+        if args.config != "cfg3" and not args.no_cfg3:
+            del run, graph
+            torch.cuda.empty_cache()
+            result["cfg3"] = cfg3_side(args.n_hyp, args.chunk)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(scene, pairs, shard, pair_base, count, rs, n_sample, n_hyp):
+def ransac_flops(run, n_hyp):
+    """Algorithmic K2 flops per step (every hypothesis on every match of pairs with >= 8
+    matches) and the executed fraction estimated from the pruning simulation."""
     import numpy as np
+    cnt = np.concatenate([run.gb._buffers(pt.shape[0])["match"][0].cpu().numpy()
+                          for _, pt in run.chunks[-1:]])
+    # the tentative counts of the last chunk stand for the chunk mix (strong-scaling chunks are
+    # drawn from one scene); scale to the whole shard
+    n_pairs = sum(pt.shape[0] for _, pt in run.chunks)
+    m = np.where(cnt >= 8, cnt, 0).astype(np.float64)
+    per_pair = n_hyp * float(np.mean(m * RANSAC_FLOP_PER_EVAL + (m > 0) * RANSAC_FLOP_PER_FIT))
+    return per_pair * n_pairs, 0.59
+
+
+def cpu_baseline(scene, pairs, lo, hi, graph, gb, seconds, n_hyp):
+    """The oracle timed on a stride sample of this shard, sized to ~`seconds` of wall; the
+    sampled pairs' full results are compared with the GPU's (graph rows of the timed step, and
+    match indices / masks / winners of a separate batch of just the sampled pairs)."""
+    import numpy as np
+    import torch
     import oracle as O
-    threads = min(16, len(os.sched_getaffinity(0)))
+    aff = len(os.sched_getaffinity(0))
+    # the GPU box gives one GPU slot a 16-CPU share of the host (OMP_NUM_THREADS is set to it);
+    # here, without the variable, every CPU in the affinity mask
+    threads = min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff))
     O.set_threads(threads)
-    stride = max(1, len(shard) // max(1, n_sample))
+    shard = pairs[lo:hi]
+    cal = np.ascontiguousarray(shard[:: max(1, len(shard) // threads)][:threads])
+    t0 = time.perf_counter()
+    O.match_verify_batch(scene["desc"], scene["kps"], cal, ratio=(4, 5), H=n_hyp, seed=42,
+                         thr=1.0, min_inl=15)
+    t_cal = time.perf_counter() - t0
+    n_sample = int(max(threads, min(len(shard), seconds / max(t_cal, 1e-3) * len(cal))))
+    stride = max(1, len(shard) // n_sample)
     idx = np.arange(0, len(shard), stride)[:n_sample]
     sample = np.ascontiguousarray(shard[idx])
     t0 = time.perf_counter()
-    tot, nm, ni = O.match_verify_batch(scene["desc"], scene["kps"], sample, ratio=(4, 5), H=n_hyp,
-                                       seed=42, thr=1.0, min_inl=15)
+    tot, nm, ni, full = O.match_verify_batch(scene["desc"], scene["kps"], sample, ratio=(4, 5),
+                                             H=n_hyp, seed=42, thr=1.0, min_inl=15, full=True)
     dt = time.perf_counter() - t0
-    g_cnt = count.cpu().numpy()[idx]
-    g_inl = rs["inl_count"].cpu().numpy()[idx]
-    parity = bool((g_cnt == nm).all() and (np.maximum(g_inl, 0) == ni).all())
-    try:
-        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if "model name" in l][0]
-    except Exception:
-        model = "unknown"
+
+    # GPU: the sampled pairs as one batch (results are batch-composition invariant)
+    pt = torch.from_numpy(sample).cuda()
+    count, match, _, rs = gb.run(pt)
+    g_cnt = count.cpu().numpy()
+    g_match = match.cpu().numpy()
+    g_inl = rs["inl_count"].cpu().numpy()
+    g_bh = rs["best_h"].cpu().numpy()
+    g_mask = rs["mask"].cpu().numpy()
+    ok_cnt = bool((g_cnt == nm).all())
+    ok_idx = ok_mask = True
+    for p in range(len(sample)):
+        m = nm[p]
+        ok_idx &= bool((g_match[p, :m] == full["match"][p, :m]).all())
+        if m >= 8:
+            ok_mask &= bool((g_mask[p, :m] == full["mask"][p, :m]).all()
+                            and g_bh[p] == full["best_h"][p] and g_inl[p] == ni[p])
+    # the timed step's graph rows of the sampled pairs vs the oracle's verified inliers
+    gr = graph.cpu().numpy()
+    gpair = lo + idx
+    sel = np.isin(gr[:, 0], gpair)
+    got = gr[sel]
+    exp = []
+    for p in range(len(sample)):
+        if ni[p] >= 15:
+            mm = full["mask"][p, :nm[p]].astype(bool)
+            q = full["match"][p, :nm[p]][mm]
+            exp.append(np.column_stack([np.full(len(q), gpair[p], np.int32), q]))
+    exp = np.concatenate(exp) if exp else np.zeros((0, 3), np.int32)
+    got = got[np.lexsort((got[:, 1], got[:, 0]))] if len(got) else got
+    ok_rows = bool(got.shape == exp.shape and (got == exp).all())
     return {"value": tot / dt, "unit": "verified matches/s", "cores": threads, "kind": "port",
             "sample": (f"{len(sample)} of {len(shard)} pairs (stride {stride}), full K1+K2 per "
-                       f"pair, OpenMP over pairs, {dt:.1f} s wall on {model}"),
-            "per_pair_ms": dt * 1e3 * threads / len(sample),
-            "inlier_parity_with_gpu": parity}
+                       f"pair, OpenMP over pairs, {dt:.1f} s wall on {model_str(aff)}"),
+            "host_cpus_in_affinity": aff, "cpu_model": cpu_model(),
+            "per_pair_core_ms": dt * 1e3 * threads / len(sample),
+            "parity": {"pairs": int(len(sample)), "match_counts": ok_cnt,
+                       "match_indices": bool(ok_idx),
+                       "inlier_masks_best_h_counts": bool(ok_mask),
+                       "graph_rows_of_timed_step": ok_rows},
+            "inlier_parity_with_gpu": bool(ok_cnt and ok_idx and ok_mask and ok_rows)}
+
+
+def model_str(aff):
+    return f"{cpu_model()} ({aff} CPUs in the affinity mask)"
+
+
+def cfg1_timing():
+    """cfg1 (BASELINE configs[0]): the reference's own shape, one 2-image pair x 512 keypoints,
+    timed fully on ONE core with the oracle: (a) ORB-like 256-bit descriptors, Hamming,
+    OpenCV cross-check rule, `distance < 26` (code/feature_matching.py:48-58) + RANSAC; (b) the
+    north_star's SIFT-like L2 descriptors, mutual + ratio 4/5 + RANSAC.  H = 4096."""
+    import numpy as np
+    import oracle as O
+    import synth
+    O.set_threads(1)
+    out = {"shape": "2 images x 512 keypoints, 1 pair, RANSAC 4096 hyp", "cores": 1,
+           "kind": "port", "cpu_model": cpu_model()}
+    for name, orb, kw in (("orb_hamming_opencv_lt26", True,
+                           dict(metric=1, cross_check=O.XC_OPENCV, max_dist=26)),
+                          ("sift_l2_mutual_ratio", False,
+                           dict(metric=0, cross_check=O.XC_MUTUAL, ratio=(4, 5)))):
+        s = synth.make_scene(2, 512, seed=1, orb=orb)
+        reps, t_m, t_r, n = 0, 0.0, 0.0, 0
+        t_end = time.perf_counter() + 1.5
+        while time.perf_counter() < t_end or reps < 3:
+            t0 = time.perf_counter()
+            q, t, _ = O.match(s["desc"][0], s["desc"][1], **kw)
+            t1 = time.perf_counter()
+            r = O.ransac_f(s["kps"][0][q], s["kps"][1][t], H=4096, seed=42, pa=0, pb=1)
+            t2 = time.perf_counter()
+            t_m += t1 - t0
+            t_r += t2 - t1
+            n = r["count"]
+            reps += 1
+        out[name] = {"match_ms": t_m / reps * 1e3, "ransac_ms": t_r / reps * 1e3,
+                     "pair_ms": (t_m + t_r) / reps * 1e3, "matches": int(len(q)),
+                     "inliers": int(n), "reps": reps}
+    return out
+
+
+def cfg3_side(n_hyp, chunk):
+    """cfg3 (50 x 2048, 1225 pairs) on this GPU: the north_star's 2048 x 128 K1 kernel and the
+    cfg3 step, 10 timed steps after 3 warmups."""
+    import numpy as np
+    import torch
+    import synth
+    scene = synth.make_scene(50, 2048, seed=0)
+    pairs = synth.unordered_pairs(50)
+    run = Runner(scene, pairs, 0, len(pairs), chunk, n_hyp, torch.cuda.current_device())
+    for _ in range(3):
+        run.step()
+    torch.cuda.synchronize()
+    evs = [run.events() for _ in range(10)]
+    t0 = time.perf_counter()
+    for s in range(10):
+        graph = run.step(None, evs[s])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = [Runner.stage_ms(e) for e in evs]
+    m = float(np.mean([s[0] for s in st]))
+    r = float(np.mean([s[1] for s in st]))
+    tops = run.k1_ops / (m * 1e-3) / 1e12
+    return {"workload": workload_string("cfg3", 50, 2048, n_hyp, chunk),
+            "value": graph.shape[0] * 10 / el, "unit": "verified matches/s",
+            "ms_per_step": el / 10 * 1e3, "match_ms": m, "ransac_ms": r,
+            "k1_roofline": {"achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOP/s (i8)",
+                            "frac": tops / PEAK_I8_TOPS,
+                            "traffic": pmc_traffic("mfma_mutual_kernel", "cfg3", 50, 2048, 1)}}
 
 
 if __name__ == "__main__":

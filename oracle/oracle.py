@@ -54,7 +54,7 @@ def _bind(L):
     L.oracle_ransac_f.restype = i32
     L.oracle_ransac_counts.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp]
     L.oracle_match_verify_batch.argtypes = [vp, vp, i32, i32, i32, vp, i32, i32, i32, i64, i32,
-                                            u64, f32, i32, vp, vp]
+                                            u64, f32, i32, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_match_verify_batch.restype = C.c_longlong
     L.oracle_set_threads.argtypes = [i32]
     L.oracle_get_threads.restype = i32
@@ -148,16 +148,31 @@ def ransac_counts(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
 
 
 def match_verify_batch(desc, kps, pairs, ratio=(4, 5), max_dist=-1, H=4096, seed=42, thr=1.0,
-                       min_inl=15):
+                       min_inl=15, full=False):
+    """K1 (mutual + ratio) + K2 per pair, OpenMP over pairs.  Returns (total verified inliers,
+    n_match [P], n_inl [P]); full=True adds a dict with match [P,K,2] (queryIdx, trainIdx),
+    mask [P,K] u8, dist [P,K] i32 (d^2), best_h [P] and F [P,9] f32 (entries past n_match[p]
+    are zero; F and best_h are meaningful for pairs with >= 8 matches)."""
     desc = np.ascontiguousarray(desc, np.uint8)
     kps = np.ascontiguousarray(kps, np.float32)
     pairs = np.ascontiguousarray(pairs, np.int32)
-    P = pairs.shape[0]
+    P, K = pairs.shape[0], desc.shape[1]
     nm = np.zeros(P, np.int32)
     ni = np.zeros(P, np.int32)
+    mt = np.zeros((P, K, 2), np.int32) if full else None
+    mk = np.zeros((P, K), np.uint8) if full else None
+    bh = np.zeros(P, np.int32) if full else None
+    dd = np.zeros((P, K), np.int32) if full else None
+    FF = np.zeros((P, 9), np.float32) if full else None
+    nul = C.c_void_p(None)
     tot = lib().oracle_match_verify_batch(_p(desc), _p(kps), desc.shape[0], desc.shape[1],
                                           desc.shape[2], _p(pairs), P, ratio[0], ratio[1],
-                                          max_dist, H, seed, thr, min_inl, _p(nm), _p(ni))
+                                          max_dist, H, seed, thr, min_inl, _p(nm), _p(ni),
+                                          _p(mt) if full else nul, _p(mk) if full else nul,
+                                          _p(bh) if full else nul, _p(dd) if full else nul,
+                                          _p(FF) if full else nul)
+    if full:
+        return int(tot), nm, ni, dict(match=mt, mask=mk, best_h=bh, dist=dd, F=FF)
     return int(tot), nm, ni
 
 

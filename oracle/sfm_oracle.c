@@ -466,7 +466,14 @@ void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint
 long long oracle_match_verify_batch(const uint8_t* desc, const float* kps, int n_img, int K,
                                     int D, const int32_t* pairs, int P, int ratio_num,
                                     int ratio_den, int64_t max_dist, int H, uint64_t seed,
-                                    float thr, int min_inl, int32_t* n_match, int32_t* n_inl) {
+                                    float thr, int min_inl, int32_t* n_match, int32_t* n_inl,
+                                    int32_t* out_match, uint8_t* out_mask, int32_t* out_best_h,
+                                    int32_t* out_dist, float* out_F) {
+    /* Per pair: K1 (mutual cross check + ratio, code/feature_matching.py:48-58 restated) then K2.
+     * Optional outputs (NULL = not wanted): out_match [P][K][2] (queryIdx, trainIdx) of the
+     * tentative matches, out_mask [P][K] their inlier mask, out_best_h [P] the winning
+     * hypothesis, out_dist [P][K] the matches' d^2, out_F [P][9] the winner's F (normalised
+ * coordinates) -- the full per-pair result bench.py / the tests compare the GPU's against. */
     long long total = 0;
     (void)n_img;
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
@@ -477,7 +484,7 @@ long long oracle_match_verify_batch(const uint8_t* desc, const float* kps, int n
         int64_t* d = (int64_t*)malloc(sizeof(int64_t) * K);
         float* x1 = (float*)malloc(sizeof(float) * 2 * K);
         float* x2 = (float*)malloc(sizeof(float) * 2 * K);
-        uint8_t* mask = (uint8_t*)malloc((size_t)K);
+        uint8_t* mask = (uint8_t*)calloc((size_t)K + 1, 1);
         int M = oracle_match(desc + (size_t)a * K * D, K, desc + (size_t)b * K * D, K, D, 0,
                              SFM_XC_MUTUAL, ratio_num, ratio_den, max_dist, q, t, d);
         for (int m = 0; m < M; ++m) {
@@ -486,13 +493,22 @@ long long oracle_match_verify_batch(const uint8_t* desc, const float* kps, int n
             x2[2 * m] = kps[((size_t)b * K + t[m]) * 2];
             x2[2 * m + 1] = kps[((size_t)b * K + t[m]) * 2 + 1];
         }
-        int32_t bh;
+        int32_t bh = -1;
         float F[9], nrm[6];
         int c = oracle_ransac_f(x1, x2, M, H, seed, (uint32_t)a, (uint32_t)b, thr, &bh, F, nrm,
                                 mask);
         n_match[p] = M;
         n_inl[p] = c < 0 ? 0 : c;
         if (c >= min_inl) total += c;
+        if (out_match) {
+            int32_t* o = out_match + (size_t)p * K * 2;
+            for (int m = 0; m < M; ++m) { o[2 * m] = q[m]; o[2 * m + 1] = t[m]; }
+        }
+        if (out_mask) memcpy(out_mask + (size_t)p * K, mask, (size_t)M);
+        if (out_best_h) out_best_h[p] = bh;
+        if (out_dist)
+            for (int m = 0; m < M; ++m) out_dist[(size_t)p * K + m] = (int32_t)d[m];
+        if (out_F) memcpy(out_F + (size_t)p * 9, F, sizeof(F));
         free(q); free(t); free(d); free(x1); free(x2); free(mask);
     }
     return total;

@@ -53,6 +53,12 @@ int sfm_ctx_create(int32_t device, sfm_ctx** out) {
         sfm::set_error("sfm_ctx_create: hipStreamCreate failed");
         return SFM_ERR_HIP;
     }
+    if (hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        sfm::set_error("sfm_ctx_create: hipEventCreate failed");
+        return SFM_ERR_HIP;
+    }
     c->stream = c->own_stream;
     *out = c;
     return SFM_OK;
@@ -63,6 +69,7 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return SFM_OK;
@@ -70,7 +77,16 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
 
 int sfm_ctx_set_stream(sfm_ctx* ctx, void* hip_stream) {
     SFM_REQUIRE(ctx != nullptr, "sfm_ctx_set_stream: ctx is NULL");
-    ctx->stream = (hipStream_t)hip_stream;  // NULL = the legacy default stream (torch's default)
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the legacy default stream (torch's default)
+    if (s == ctx->stream) return SFM_OK;
+    // Every call on a context shares one device workspace (match partials, RANSAC planes and
+    // G table, BA scratch): work already enqueued on the previous stream must finish with it
+    // before the new stream's kernels reuse it.  One event record + one stream wait, no host
+    // synchronisation.
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    SFM_HIP_CHECK(hipEventRecord(ctx->handoff, ctx->stream));
+    SFM_HIP_CHECK(hipStreamWaitEvent(s, ctx->handoff, 0));
+    ctx->stream = s;
     return SFM_OK;
 }
 

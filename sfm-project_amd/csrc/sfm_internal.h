@@ -10,8 +10,9 @@ struct sfm_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    void* ws = nullptr;          // growable device workspace
+    void* ws = nullptr;          // growable device workspace (shared by every call on ctx)
     size_t ws_bytes = 0;
+    hipEvent_t handoff = nullptr;  // orders the workspace across sfm_ctx_set_stream switches
     int n_cu = 256;
 };
 

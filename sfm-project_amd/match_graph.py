@@ -65,7 +65,12 @@ class GraphBuilder:
         self._bufs = {}
 
     def _buffers(self, P):
-        b = self._bufs.get(P)
+        """Output buffers for a batch of P pairs, reused by every later call with the same P.
+
+        match / verify / run return views of these buffers: a later call with the same P
+        overwrites them (graph_rows copies what it keeps into a fresh tensor).  Up to four batch
+        sizes stay cached, so a chunked pass (equal chunks + one ragged tail) allocates once."""
+        b = self._bufs.pop(P, None)
         if b is None:
             torch, dev, K = self.torch, self.dev, self.k_max
             b = dict(match=(torch.empty(P, dtype=torch.int32, device=dev),
@@ -76,7 +81,9 @@ class GraphBuilder:
                                  mask=torch.empty((P, K), dtype=torch.uint8, device=dev),
                                  F=torch.empty((P, 9), dtype=torch.float32, device=dev),
                                  norm=torch.empty((P, 6), dtype=torch.float32, device=dev)))
-            self._bufs = {P: b}
+            while len(self._bufs) >= 4:
+                self._bufs.pop(next(iter(self._bufs)))
+        self._bufs[P] = b  # most recently used last
         return b
 
     def match(self, pairs_t):
@@ -109,7 +116,7 @@ def all_gather_rows(rows, group=None):
     no all-gatherv)."""
     import torch
     import torch.distributed as dist
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_available() or not dist.is_initialized():
         return rows
     world = dist.get_world_size(group)
     n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
@@ -145,11 +152,12 @@ def all_gather_graph(counts, packed, ranges, group=None):
 
     `ranges` = [(lo, hi)] pair range of every rank (match_graph.shard_range, known to all ranks
     without communication).  Two collectives: the per-pair counts (padded to the longest shard),
-    then the packed rows (padded to the largest row count).  World size 1: local expansion only."""
+    then the packed rows (padded to the largest row count).  No process group: local expansion
+    only (an initialised group of size 1 still runs the collectives)."""
     import torch
     import torch.distributed as dist
     dev = packed.device
-    single = not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1
+    single = not dist.is_available() or not dist.is_initialized()
     if single:
         all_counts, all_rows = [counts], [packed]
     else:

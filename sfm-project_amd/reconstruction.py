@@ -82,7 +82,7 @@ def allreduce_camera_blocks(U, gc, cost, group=None):
     In place; returns (U, gc, cost)."""
     import torch
     import torch.distributed as dist
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_available() or not dist.is_initialized():
         return U, gc, cost
     nu, ng = U.numel(), gc.numel()
     buf = torch.cat([U.reshape(-1), gc.reshape(-1), cost.reshape(-1).to(U.dtype)])
