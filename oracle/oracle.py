@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "lib", "liboracle.so")
+# SFM_ORACLE_LIB: the ASan/UBSan build (oracle/Makefile `sanitize`, tools/oracle_sanitize.sh)
+_LIB_PATH = os.environ.get("SFM_ORACLE_LIB") or os.path.join(_HERE, "lib", "liboracle.so")
 _lib = None
 
 XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2

@@ -515,6 +515,11 @@ long long oracle_match_verify_batch(const uint8_t* desc, const float* kps, int n
 }
 
 /* Thread control for the timed CPU baseline (bench.py reports the count it used). */
+#ifdef _OPENMP
 #include <omp.h>
 void oracle_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
 int oracle_get_threads(void) { return omp_get_max_threads(); }
+#else  /* sanitizer build (oracle/Makefile `sanitize`): serial */
+void oracle_set_threads(int n) { (void)n; }
+int oracle_get_threads(void) { return 1; }
+#endif

@@ -306,6 +306,21 @@ __device__ __forceinline__ int sampson_inlier2(const float G[9], f2 x1, f2 y1, f
     return (e.x > 0.0f ? 1 : 0) + (e.y > 0.0f ? 1 : 0);
 }
 
+// XCD-aware block mapping of the [pair][hypothesis block] grids (fit, score).  Workgroups are
+// dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each XCD with its own 4 MB L2:
+// XCD x gets the contiguous pair range [x*Q, (x+1)*Q) and walks it hypothesis-block-major, so a
+// pair's scoring planes are read through ONE L2 (with grid (P, H/256) and P = 1 mod 8, as at
+// cfg3, every pair's 16 blocks landed on all 8 XCDs) and every pair's first (best-previewed)
+// block still runs before any second block.  Returns false for the padding blocks.
+__device__ __forceinline__ bool xcd_pair_block(int n_pairs, int& p, int& hb) {
+    const int Q = (n_pairs + 7) >> 3;
+    const int x = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
+    hb = j / Q;
+    p = x * Q + (j - hb * Q);
+    return p < n_pairs;
+}
+static inline unsigned xcd_grid(int n_pairs, int n_hb) { return 8u * (unsigned)((n_pairs + 7) >> 3) * (unsigned)n_hb; }
+
 constexpr int CH = 16;         // matches per scalar-load chunk (4 x s_load_dwordx16)
 constexpr int PRUNE_EVERY = 64;
 
@@ -427,10 +442,11 @@ __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[
 }
 
 __global__ __launch_bounds__(256) void ransac_fit_kernel(
-    int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
+    int n_pairs, int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
     const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
     int n_hyp, float* __restrict__ hypG, int32_t* __restrict__ prev) {
-    const int p = blockIdx.x;
+    int p, hb;
+    if (!xcd_pair_block(n_pairs, p, hb)) return;
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int kp = plane_len(k_max);
@@ -440,7 +456,7 @@ __global__ __launch_bounds__(256) void ransac_fit_kernel(
     const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
     float k1, k2;
     sampson_scales(s1, s2, thr, k1, k2);
-    const uint32_t h = blockIdx.y * 256 + threadIdx.x;
+    const uint32_t h = hb * 256 + threadIdx.x;
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
     float4 smp[8];
@@ -495,15 +511,17 @@ __global__ __launch_bounds__(256) void ransac_order_kernel(int n_hyp,
 
 template <bool PRUNE>
 __global__ __launch_bounds__(256) void ransac_score_kernel(
-    int k_max, const int32_t* __restrict__ match_count, const float* __restrict__ planes,
-    int n_hyp, const float* __restrict__ hypG, const int32_t* __restrict__ prev,
-    const uint16_t* __restrict__ order, unsigned long long* __restrict__ best) {
-    const int p = blockIdx.x;
+    int n_pairs, int k_max, const int32_t* __restrict__ match_count,
+    const float* __restrict__ planes, int n_hyp, const float* __restrict__ hypG,
+    const int32_t* __restrict__ prev, const uint16_t* __restrict__ order,
+    unsigned long long* __restrict__ best) {
+    int p, hb;
+    if (!xcd_pair_block(n_pairs, p, hb)) return;
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int kp = plane_len(k_max);
     const cfloat_p S = (cfloat_p)(planes + (size_t)p * 8 * kp + 4 * kp);
-    const uint32_t h = order[(size_t)p * n_hyp + blockIdx.y * 256 + threadIdx.x];
+    const uint32_t h = order[(size_t)p * n_hyp + hb * 256 + threadIdx.x];
     const float* gt = hypG + (size_t)p * 9 * n_hyp + h;
     float G[9];
 #pragma unroll
@@ -623,14 +641,15 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 grid(n_pairs, H / 256);
     if (mode == 0) {
-        hipLaunchKernelGGL(ransac_fit_kernel, grid, dim3(256), 0, st, k_max, pairs, match_count,
-                           planes, out_norm, prm->seed, prm->thr, H, hypG, prev);
+        const dim3 xgrid(xcd_grid(n_pairs, H / 256));
+        hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
+                           match_count, planes, out_norm, prm->seed, prm->thr, H, hypG, prev);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                            prev, order);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(ransac_score_kernel<true>, grid, dim3(256), 0, st, k_max, match_count,
-                           planes, H, hypG, prev, order, best);
+        hipLaunchKernelGGL(ransac_score_kernel<true>, xgrid, dim3(256), 0, st, n_pairs, k_max,
+                           match_count, planes, H, hypG, prev, order, best);
     } else if (mode == 1) {
         hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
                            match_count, planes, out_norm, prm->seed, prm->thr, best);
