@@ -54,6 +54,7 @@ def _bind(L):
     L.oracle_ransac_f.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp, vp, vp, vp]
     L.oracle_ransac_f.restype = i32
     L.oracle_ransac_counts.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp]
+    L.oracle_ransac_masks.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp, vp, vp]
     L.oracle_match_verify_batch.argtypes = [vp, vp, i32, i32, i32, vp, i32, i32, i32, i64, i32,
                                             u64, f32, i32, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_match_verify_batch.restype = C.c_longlong
@@ -146,6 +147,18 @@ def ransac_counts(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
     counts = np.zeros(H, np.int32)
     lib().oracle_ransac_counts(_p(xy1), _p(xy2), xy1.shape[0], H, seed, pa, pb, thr, _p(counts))
     return counts
+
+
+def ransac_masks(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
+    """Per-hypothesis f32-spec decisions: (masks [H,M] u8, idx [H,8] i32, ok [H] bool)."""
+    xy1 = np.ascontiguousarray(xy1, np.float32)
+    xy2 = np.ascontiguousarray(xy2, np.float32)
+    M = xy1.shape[0]
+    masks = np.zeros((H, max(M, 1)), np.uint8)
+    idx = np.zeros((H, 8), np.int32)
+    ok = np.zeros(H, np.int32)
+    lib().oracle_ransac_masks(_p(xy1), _p(xy2), M, H, seed, pa, pb, thr, _p(masks), _p(idx), _p(ok))
+    return masks[:, :M], idx, ok.astype(bool)
 
 
 def match_verify_batch(desc, kps, pairs, ratio=(4, 5), max_dist=-1, H=4096, seed=42, thr=1.0,

@@ -457,6 +457,45 @@ void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint
     free(n1); free(n2); free(X1); free(X2);
 }
 
+/* Per-hypothesis decisions of the f32 spec (tests/perf/ransac_fp64_study.py compares them with an
+ * fp64 evaluation of the same samples): masks [H][M] (1 = inlier; all 0 for a degenerate fit),
+ * idx [H][8] the sample, ok [H] (1 = fit succeeded). */
+void oracle_ransac_masks(const float* xy1, const float* xy2, int M, int H, uint64_t seed,
+                         uint32_t pa, uint32_t pb, float thr, uint8_t* masks, int32_t* idx,
+                         int32_t* ok) {
+    float* n1 = (float*)malloc(sizeof(float) * 2 * M);
+    float* n2 = (float*)malloc(sizeof(float) * 2 * M);
+    float cx1, cy1, s1, cx2, cy2, s2;
+    oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
+    oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
+    float k1, k2;
+    sampson_scales(s1, s2, thr, &k1, &k2);
+    float* X1 = (float*)malloc(sizeof(float) * 2 * M);
+    float* X2 = (float*)malloc(sizeof(float) * 2 * M);
+    sampson_coords(n1, M, k1, X1);
+    sampson_coords(n2, M, k2, X2);
+    for (int h = 0; h < H; ++h) {
+        int32_t* id = idx + (size_t)h * 8;
+        oracle_sample8(seed, pa, pb, (uint32_t)h, M, id);
+        float p1[16], p2[16], F[9];
+        for (int k = 0; k < 8; ++k) {
+            p1[2 * k] = n1[2 * id[k]]; p1[2 * k + 1] = n1[2 * id[k] + 1];
+            p2[2 * k] = n2[2 * id[k]]; p2[2 * k + 1] = n2[2 * id[k] + 1];
+        }
+        uint8_t* mk = masks + (size_t)h * M;
+        ok[h] = oracle_fit_f8(p1, p2, F) == 0;
+        if (ok[h]) {
+            float G[9];
+            sampson_prep(F, k1, k2, G);
+            for (int m = 0; m < M; ++m)
+                mk[m] = (uint8_t)sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m], X2[2 * m + 1]);
+        } else {
+            memset(mk, 0, (size_t)M);
+        }
+    }
+    free(n1); free(n2); free(X1); free(X2);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Batched match + verify over a pair list (the CPU baseline bench.py times; OpenMP over pairs). */
 /* ------------------------------------------------------------------------------------------ */
