@@ -2,15 +2,19 @@
 // DESIGN.md §4.3).  Fills the empty reference module code/3d_reconstruction.py.
 //
 // fp64 throughout.  Deterministic (no float atomics): every accumulation has a fixed order.
-//   ba_obs_kernel          one thread per observation (enough waves to stream HBM): residual,
-//                          J_c (2x8), J_p (2x3) -> res, W = w J_c^T J_p; V_p, g_p by a segmented
-//                          scan of the point terms across the wave (points are point-major
-//                          contiguous), boundary-cut segments to head/tail records.
-//   ba_camera_kernel finish blocks: points spanning waves, empty points, the cost;
-//   ba_final_kernel        camera split sums (only with fewer than 256 cameras).
-//   ba_camera_kernel       block (camera, split): recomputes J_c (cheaper than storing it: HBM is
-//                          the bound) over a contiguous share of the camera's observations
-//                          (cam_ptr/cam_obs CSR), fixed lane-strided order + shuffle tree.
+// Two launches:
+//   ba_jtj_kernel      camera blocks first (block per (camera, split): J_c recomputed from the
+//                      camera's rotation — computed once per block — over a contiguous share of
+//                      the camera's observations (cam_ptr/cam_obs CSR), fixed lane-strided order
+//                      + shuffle tree -> U_c, g_c), then observation blocks (thread per
+//                      observation, enough waves to stream HBM: residual, J_c (2x8), J_p (2x3) ->
+//                      res, W = w J_c^T J_p staged through LDS for coalesced stores; V_p, g_p by a
+//                      segmented scan of the point terms across the wave (points are point-major
+//                      contiguous), boundary-cut segments to head/tail records).  The two halves
+//                      are independent, so the latency-bound camera reduction runs underneath the
+//                      observation stream.
+//   ba_finish_kernel   points spanning waves, empty points, the cost;
+//   ba_final_kernel    camera split sums (only with fewer than 256 cameras).
 // Algorithmic HBM traffic ~300 B/observation; this is an HBM-bound stage.
 #include <algorithm>
 
@@ -26,27 +30,12 @@ struct ObsLin {
     double w, rho;
 };
 
-// Mirrors oracle_ba_obs (oracle/sfm_oracle_ba.c).
-__device__ __forceinline__ void linearize(const double* __restrict__ cam, const double* __restrict__ pp,
-                                          const double X[3], double u, double v, double loss_s,
-                                          bool want_jp, ObsLin& o) {
-    const double r0v = cam[0], r1v = cam[1], r2v = cam[2];
-    const double th2 = r0v * r0v + r1v * r1v + r2v * r2v;
-    double R[9];
-    if (th2 > 1e-20) {
-        const double th = sqrt(th2);
-        double s, c;
-        sincos(th, &s, &c);
-        const double C = 1.0 - c;
-        const double kx = r0v / th, ky = r1v / th, kz = r2v / th;
-        R[0] = c + C * kx * kx;      R[1] = C * kx * ky - s * kz; R[2] = C * kx * kz + s * ky;
-        R[3] = C * ky * kx + s * kz; R[4] = c + C * ky * ky;      R[5] = C * ky * kz - s * kx;
-        R[6] = C * kz * kx - s * ky; R[7] = C * kz * ky + s * kx; R[8] = c + C * kz * kz;
-    } else {
-        R[0] = 1.0;  R[1] = -r2v; R[2] = r1v;
-        R[3] = r2v;  R[4] = 1.0;  R[5] = -r0v;
-        R[6] = -r1v; R[7] = r0v;  R[8] = 1.0;
-    }
+// Mirrors oracle_ba_obs (oracle/sfm_oracle_ba.c).  R = rotmat(cam[0..2]) (camera_model.h; the
+// camera blocks compute it once per camera, the observation blocks once per observation).
+__device__ __forceinline__ void linearize(const double (&R)[9], const double* __restrict__ cam,
+                                          const double* __restrict__ pp, const double X[3],
+                                          double u, double v, double loss_s, bool want_jp,
+                                          ObsLin& o) {
     double Y[3], P[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -94,7 +83,8 @@ __device__ __forceinline__ void linearize(const double* __restrict__ cam, const 
 constexpr int NV = 10;      // per-observation point terms: V upper triangle (6), g_p (3), 0.5 rho
 constexpr int NU = 36 + 8;  // upper triangle of U_c (8x8) + g_c
 constexpr int SPLIT_TARGET = 256;  // camera blocks wanted (splits per camera = this / n_cam); more blocks only
-                                   // add reduction work (measured: 3 splits at 500 cameras 45 us vs 30 us)
+                                   // add reduction work (measured at 500 cameras, merged launch:
+                                   // 2 splits 90 us, 4 splits 113 us vs 1 split 69 us)
 
 __device__ __forceinline__ void write_point(double* __restrict__ V, double* __restrict__ gp, int p,
                                             const double (&a)[NV]) {
@@ -111,17 +101,26 @@ __device__ __forceinline__ void write_point(double* __restrict__ V, double* __re
 // Points whose observations lie inside one wave are written here; the segments cut by a wave
 // boundary go to head/tail records that the finish blocks combine.  The cost (sum of rho/2)
 // is reduced per wave.  All orders are fixed: deterministic.
-__global__ __launch_bounds__(256) void ba_obs_kernel(
-    int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
+// W (192 B per observation) leaves through LDS: each lane writes its 24 doubles to a padded
+// per-wave image (row stride 25 doubles: conflict-free ds_write_b64), then the wave stores its
+// 12 KB block with 16-B lane-contiguous stores (1 KB per instruction) instead of 12 stores of
+// 16-B pieces at a 192-B lane stride.
+constexpr int WROW = 25;  // doubles per staged W row (24 + 1 pad)
+constexpr int OBS_LDS = 64 * WROW;  // doubles per wave
+
+__device__ __forceinline__ void obs_block(
+    int ob, int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
     const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
     const int32_t* __restrict__ pt_idx, const int32_t* __restrict__ pt_ptr,
     const double* __restrict__ uv, double loss_s, double* __restrict__ W,
     double* __restrict__ res, double* __restrict__ V, double* __restrict__ gp,
-    double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_wave) {
-    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_wave,
+    double* __restrict__ lds) {
+    const int o = ob * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const int wv = o >> 6;  // global wave index (blocks are whole waves)
     const bool valid = o < n_obs;
+    double* wimg = lds + (threadIdx.x >> 6) * OBS_LDS;
     int p = -1;
     double t[NV];
 #pragma unroll
@@ -131,15 +130,17 @@ __global__ __launch_bounds__(256) void ba_obs_kernel(
         p = pt_idx[o];
         const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
         const double2 z = *(const double2*)(uv + 2 * (size_t)o);
+        const double* cam = cams + 8 * (size_t)c;
+        double R[9];
+        rotmat(cam[0], cam[1], cam[2], R);
         ObsLin L;
-        linearize(cams + 8 * (size_t)c, pp + 2 * (size_t)c, X, z.x, z.y, loss_s, true, L);
+        linearize(R, cam, pp + 2 * (size_t)c, X, z.x, z.y, loss_s, true, L);
         *(double2*)(res + 2 * (size_t)o) = make_double2(L.r[0], L.r[1]);
-        double2* Wo = (double2*)(W + 24 * (size_t)o);
+        double* wr = wimg + lane * WROW;
 #pragma unroll
-        for (int q = 0; q < 12; ++q) {
-            const int i0 = (2 * q) / 3, j0 = (2 * q) % 3, i1 = (2 * q + 1) / 3, j1 = (2 * q + 1) % 3;
-            Wo[q] = make_double2(L.w * (L.Jc[i0] * L.Jp[j0] + L.Jc[8 + i0] * L.Jp[3 + j0]),
-                                 L.w * (L.Jc[i1] * L.Jp[j1] + L.Jc[8 + i1] * L.Jp[3 + j1]));
+        for (int q = 0; q < 24; ++q) {
+            const int i = q / 3, j = q % 3;
+            wr[q] = L.w * (L.Jc[i] * L.Jp[j] + L.Jc[8 + i] * L.Jp[3 + j]);
         }
         int k = 0;
 #pragma unroll
@@ -149,6 +150,19 @@ __global__ __launch_bounds__(256) void ba_obs_kernel(
 #pragma unroll
         for (int i = 0; i < 3; ++i) t[6 + i] = L.w * (L.Jp[i] * L.r[0] + L.Jp[3 + i] * L.r[1]);
         t[9] = 0.5 * L.rho;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {   // the wave's W block: 64 rows x 24 doubles, contiguous in W from observation wv*64
+        const int nrow = min(64, n_obs - (wv << 6));
+        double2* Wo = (double2*)(W + 24 * ((size_t)wv << 6));
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const int e = q * 64 + lane;          // double pair e of the block
+            const int row = e / 12, col = 2 * (e - 12 * row);
+            if (row < nrow) Wo[e] = make_double2(wimg[row * WROW + col], wimg[row * WROW + col + 1]);
+        }
     }
     // cost: plain fixed-order wave sum, one entry per wave
     double cw = t[9];
@@ -185,42 +199,30 @@ __global__ __launch_bounds__(256) void ba_obs_kernel(
     }
 }
 
-// Block (camera c, split s): fixed-order partial U_c / g_c over its share of the camera's
-// observations (J_c recomputed: cheaper than storing it, HBM is the bound).
-__device__ void finish_block(int fb, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
-                             const double* __restrict__ seg, const int32_t* __restrict__ seg_pt,
-                             double* __restrict__ V, double* __restrict__ gp,
-                             const double* __restrict__ cost_wave, double* __restrict__ cost);
-
-// Blocks [0, n_cam * splits): (camera c, split s) fixed-order U_c / g_c over a contiguous share of
-// the camera's observations — written directly when splits == 1, else as partials for
-// ba_final_kernel.  Blocks past that: finish_block (points spanning waves, empty points, cost),
-// which only needs the observation kernel's output.
-__global__ __launch_bounds__(256) void ba_camera_kernel(
-    const double* __restrict__ cams, const double* __restrict__ pp, const double* __restrict__ pts,
-    const int32_t* __restrict__ pt_idx, const double* __restrict__ uv,
-    const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ cam_obs, double loss_s,
-    int n_cam, int splits, double* __restrict__ part, double* __restrict__ U,
-    double* __restrict__ gc, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
-    const double* __restrict__ seg, const int32_t* __restrict__ seg_pt, double* __restrict__ V,
-    double* __restrict__ gp, const double* __restrict__ cost_wave, double* __restrict__ cost) {
-    __shared__ double red[4][NU];
-    const int b = blockIdx.x, tid = threadIdx.x;
-    if (b >= n_cam * splits) {
-        finish_block(b - n_cam * splits, n_wave, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_wave,
-                     cost);
-        return;
-    }
+// Block (camera c, split s): fixed-order partial U_c / g_c over a contiguous share of the
+// camera's observations (J_c recomputed from the camera's rotation, computed once per block:
+// cheaper than storing J_c, HBM is the bound) — written directly when splits == 1, else as
+// partials for ba_final_kernel.
+__device__ __forceinline__ void camera_block(
+    int b, const double* __restrict__ cams, const double* __restrict__ pp,
+    const double* __restrict__ pts, const int32_t* __restrict__ pt_idx,
+    const double* __restrict__ uv, const int32_t* __restrict__ cam_ptr,
+    const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
+    double* __restrict__ U, double* __restrict__ gc, double* __restrict__ lds) {
+    double (*red)[NU] = (double (*)[NU])lds;  // [4][NU]
+    const int tid = threadIdx.x;
     const int c = b / splits, s = b - c * splits;
     double acc[NU];
 #pragma unroll
     for (int i = 0; i < NU; ++i) acc[i] = 0.0;
     const double* cam = cams + 8 * (size_t)c;
+    double R[9];
+    rotmat(cam[0], cam[1], cam[2], R);
     const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
     const int len = (c1 - c0 + splits - 1) / splits;
     const int e0 = c0 + s * len, e1 = min(c1, e0 + len);
     // four observations per step: the dependent gathers (cam_obs -> pt_idx -> point, uv) of all
-    // four are issued before any is used (memory-level parallelism; the kernel is latency-bound)
+    // four are issued before any is used (memory-level parallelism; the blocks are latency-bound)
     for (int e = e0 + tid; e < e1; e += 4 * 256) {
         int o[4], pi[4];
         double X[4][3], u[4], v[4];
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(256) void ba_camera_kernel(
         for (int q = 0; q < 4; ++q) {
             if (o[q] < 0) break;
             ObsLin L;
-            linearize(cam, pp + 2 * (size_t)c, X[q], u[q], v[q], loss_s, false, L);
+            linearize(R, cam, pp + 2 * (size_t)c, X[q], u[q], v[q], loss_s, false, L);
             int t = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -280,6 +282,41 @@ __global__ __launch_bounds__(256) void ba_camera_kernel(
     }
 }
 
+// One launch for both independent halves of the linearisation: blocks [0, n_camb) are the
+// latency-bound camera blocks (dispatched first), the rest the HBM-streaming observation blocks,
+// so the camera reduction runs underneath the observation stream instead of after it.  The
+// finish blocks (which read the observation blocks' segment records) are a second launch.
+__global__ __launch_bounds__(256) void ba_jtj_kernel(
+    int n_camb, int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
+    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
+    const int32_t* __restrict__ pt_idx, const int32_t* __restrict__ pt_ptr,
+    const double* __restrict__ uv, const int32_t* __restrict__ cam_ptr,
+    const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
+    double* __restrict__ U, double* __restrict__ gc, double* __restrict__ W,
+    double* __restrict__ res, double* __restrict__ V, double* __restrict__ gp,
+    double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_wave) {
+    __shared__ double lds[4 * OBS_LDS];
+    const int b = blockIdx.x;
+    if (b < n_camb)
+        camera_block(b, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U, gc,
+                     lds);
+    else
+        obs_block(b - n_camb, n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res,
+                  V, gp, seg, seg_pt, cost_wave, lds);
+}
+
+__device__ void finish_block(int fb, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
+                             const double* __restrict__ seg, const int32_t* __restrict__ seg_pt,
+                             double* __restrict__ V, double* __restrict__ gp,
+                             const double* __restrict__ cost_wave, double* __restrict__ cost);
+
+__global__ __launch_bounds__(256) void ba_finish_kernel(
+    int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
+    const int32_t* __restrict__ seg_pt, double* __restrict__ V, double* __restrict__ gp,
+    const double* __restrict__ cost_wave, double* __restrict__ cost) {
+    finish_block(blockIdx.x, n_wave, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_wave, cost);
+}
+
 // Finish work (256-thread block fb): points spanning waves (the point whose tail record wave g
 // wrote owns tail + the head records of the following waves up to its last observation, fixed
 // order), zero V_p / g_p for points without observations, and (block 0) the cost as a
@@ -292,7 +329,8 @@ __device__ void finish_block(int fb, int n_wave, int n_pt, const int32_t* __rest
     const int g = fb * 256 + tid;
     if (fb == 0) {
         __shared__ double red[4];
-        double s = 0.0;
+        double s = 0.0;  // fixed order (w = tid, tid + 256, ...); unrolled so the loads overlap
+#pragma unroll 8
         for (int w = tid; w < n_wave; w += 256) s += cost_wave[w];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) s += __shfl_down(s, off, 64);
@@ -499,19 +537,17 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     int32_t* seg_pt = (int32_t*)(ws + sb);
     double* cost_wave = (double*)(ws + sb + ib);
     double* part = (double*)(ws + sb + ib + cb);
-    // observation kernel (HBM streaming) -> camera reduction (gathers now L2-warm) plus, in the
-    // same launch, the finish blocks (points spanning waves, empty points, cost)
-    if (n_obs > 0) {
-        hipLaunchKernelGGL(ba_obs_kernel, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs,
-                           cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res, V, gp, seg,
-                           seg_pt, cost_wave);
-        SFM_HIP_CHECK(hipGetLastError());
-    }
+    // camera blocks + observation blocks in one launch, then the finish blocks
+    const int n_camb = n_cam * splits;
+    const int n_obsb = (n_obs + 255) / 256;
+    hipLaunchKernelGGL(ba_jtj_kernel, dim3(n_camb + n_obsb), dim3(256), 0, st, n_camb, n_obs,
+                       cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, cam_ptr, cam_obs, loss_s,
+                       splits, part, U, gc, W, res, V, gp, seg, seg_pt, cost_wave);
+    SFM_HIP_CHECK(hipGetLastError());
     const int nw = n_obs > 0 ? n_wave : 0;
     const int n_fin = std::max(std::max((nw + 255) / 256, (n_pt + 255) / 256), 1);
-    hipLaunchKernelGGL(ba_camera_kernel, dim3(n_cam * splits + n_fin), dim3(256), 0, st, cams, pp,
-                       pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, n_cam, splits, part, U, gc, nw,
-                       n_pt, pt_ptr, seg, seg_pt, V, gp, cost_wave, cost);
+    hipLaunchKernelGGL(ba_finish_kernel, dim3(n_fin), dim3(256), 0, st, nw, n_pt, pt_ptr, seg,
+                       seg_pt, V, gp, cost_wave, cost);
     SFM_HIP_CHECK(hipGetLastError());
     if (splits > 1) {
         hipLaunchKernelGGL(ba_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, st,
