@@ -75,6 +75,9 @@ int32_t sfm_version(void);
  *   out_count [n_pairs] i32           matches per pair
  *   out_match [n_pairs][k_max][2] i32 (queryIdx, trainIdx), ascending queryIdx
  *   out_dist  [n_pairs][k_max] i32    d^2 (L2) or Hamming distance
+ * Limits: k_max <= 8192.  L2 above 4096 needs a cross-check rule (SFM_XC_MUTUAL / SFM_XC_OPENCV:
+ * the column-winner kernel); the ratio-only and no-rule L2 paths stop at 4096.  Hamming above
+ * 4096 runs the VALU popcount kernel.
  */
 int sfm_match_batch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
                     int32_t k_max, int32_t dim, const int32_t* pairs, int32_t n_pairs,
@@ -151,7 +154,11 @@ typedef struct sfm_ba_solve_params {
     double lambda;    /* Marquardt damping λ (>= 0) */
     double tol;       /* relative CG residual |r|/|b| */
     int32_t max_iter; /* CG iteration cap */
-    int32_t _pad;
+    int32_t poll;     /* convergence poll: every `poll` CG iterations (0 = every 8) the host reads
+                         the device's convergence flag (one 4-byte copy + stream sync) and stops
+                         enqueueing once it is set; < 0 = never (fully asynchronous: all max_iter
+                         iterations are enqueued, the converged ones exit at once).  Results are
+                         identical either way. */
 } sfm_ba_solve_params;
 
 int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
@@ -159,6 +166,13 @@ int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
                  const int32_t* cam_ptr, const int32_t* cam_obs, const double* U, const double* V,
                  const double* W, const double* gc, const double* gp,
                  const sfm_ba_solve_params* prm, double* dc, double* dp, double* info);
+/* Fixed parameters (the gauge: the reference camera's pose and one translation coordinate of a
+ * second camera; known intrinsics f, k1): in place on sfm_ba_jtj's U [n_cam][8][8], W [n_obs][8][3]
+ * and g_c [n_cam][8], the rows/columns of the parameters marked in fixed [n_cam][8] (u8, 1 =
+ * fixed) become the identity's, their g_c entries and W rows 0 — sfm_ba_solve then returns
+ * δ = 0 for them exactly.  Call after sfm_ba_jtj (and after any camera-block all-reduce). */
+int sfm_ba_fix_params(sfm_ctx* ctx, int32_t n_cam, int32_t n_obs, const int32_t* cam_idx,
+                      const uint8_t* fixed, double* U, double* W, double* gc);
 int sfm_ba_cost(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* pp, int32_t n_pt,
                 const double* pts, int32_t n_obs, const int32_t* cam_idx, const int32_t* pt_idx,
                 const double* uv, double loss_s, double* cost);

@@ -182,7 +182,8 @@ def update(cams, pts, dc, dp):
     """cams ⊕ dc (left rotation increment, additive t, f, k1), pts + dp."""
     out = np.array(cams, np.float64, copy=True)
     for c in range(len(out)):
-        out[c, :3] = _angle_axis(_rotmat(dc[c, :3]) @ _rotmat(out[c, :3]))
+        if np.any(dc[c, :3] != 0.0):  # δr = 0 exactly (a held rotation) keeps r bit for bit
+            out[c, :3] = _angle_axis(_rotmat(dc[c, :3]) @ _rotmat(out[c, :3]))
         out[c, 3:] += dc[c, 3:]
     return out, np.asarray(pts, np.float64) + dp
 
@@ -191,14 +192,33 @@ def cost(cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0):
     return O.ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s)["cost"]
 
 
+def fix_params(lin, cam_idx, fixed):
+    """Fixed parameters (sfm_ba_fix_params, csrc/ba_solve.hip): rows/columns of U for the
+    parameters marked in fixed [n_cam, 8] become the identity's, their g_c entries and W rows 0,
+    so the damped Schur solve returns delta = 0 for them.  In place; returns lin."""
+    if fixed is None:
+        return lin
+    fixed = np.asarray(fixed, bool)
+    U, W, gc = lin["U"], lin["W"], lin["gc"]
+    for c, i in zip(*np.nonzero(fixed)):
+        U[c, i, :] = 0.0
+        U[c, :, i] = 0.0
+        U[c, i, i] = 1.0
+        gc[c, i] = 0.0
+    rows = fixed[np.asarray(cam_idx)]             # [n_obs, 8]
+    W[rows] = 0.0
+    return lin
+
+
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0, max_iter=50, lam0=1e-4,
-                  ftol=1e-12, max_cg=200, cg_tol=1e-10):
-    """LM loop of the spec; returns (cams, pts, history [(cost, lam, accepted, cg_iters)])."""
+                  ftol=1e-12, max_cg=200, cg_tol=1e-10, fixed=None):
+    """LM loop of the spec; returns (cams, pts, history [(cost, lam, accepted, cg_iters)]).
+    fixed: optional [n_cam, 8] bool mask of parameters held at their values (fix_params)."""
     cams = np.array(cams, np.float64, copy=True)
     pts = np.array(pts, np.float64, copy=True)
     lam, nu = lam0, 2.0
     hist = []
-    lin = O.ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s)
+    lin = fix_params(O.ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s), cam_idx, fixed)
     for _ in range(max_iter):
         dc, dp, it, _ = schur_pcg(lin["U"], lin["V"], lin["W"], lin["gc"], lin["gp"], cam_idx,
                                   pt_idx, lam, max_cg, cg_tol)
@@ -216,7 +236,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0, max_iter=50, l
             hist.append((new, lam, True, it))
             if old - new <= ftol * old:
                 break
-            lin = O.ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s)
+            lin = fix_params(O.ba_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s), cam_idx, fixed)
         else:
             lam *= nu
             nu *= 2.0

@@ -442,7 +442,7 @@ __global__ __launch_bounds__(1024) void ba_cost_final(int n_blk, const double* _
 }
 
 // cams ⊕ dc: R <- exp([δr]x) R (the left increment the Jacobians are taken in), t, f, k1
-// additive; points additive.  Thread per camera / point.  Mirrors oracle/ba_lm.py update().
+// additive; points additive; δr = 0 exactly keeps r.  Thread per camera / point.  Mirrors oracle/ba_lm.py update().
 __global__ __launch_bounds__(256) void ba_update_kernel(int n_cam, const double* __restrict__ cams,
                                                         const double* __restrict__ dc, int n_pt,
                                                         const double* __restrict__ pts,
@@ -485,7 +485,10 @@ __global__ __launch_bounds__(256) void ba_update_kernel(int n_cam, const double*
             o0 = th * a0 / n; o1 = th * a1 / n; o2 = th * a2 / n;
         }
         double* out = cams_out + 8 * (size_t)i;
-        out[0] = o0; out[1] = o1; out[2] = o2;
+        // δr = 0 exactly (a held rotation): exp(0) = I, keep r bit for bit instead of the
+        // rounding of the log map of R(r)
+        const bool keep = d[0] == 0.0 && d[1] == 0.0 && d[2] == 0.0;
+        out[0] = keep ? c[0] : o0; out[1] = keep ? c[1] : o1; out[2] = keep ? c[2] : o2;
 #pragma unroll
         for (int k = 3; k < 8; ++k) out[k] = c[k] + d[k];
     }

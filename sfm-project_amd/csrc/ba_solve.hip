@@ -729,7 +729,18 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, rrc, state);
     SFM_HIP_CHECK(hipGetLastError());
     const int vblk = (8 * n_cam + 255) / 256;
+    const int poll = prm->poll == 0 ? 8 : prm->poll;
+    if (poll > 0 && !ctx->pinned)
+        SFM_HIP_CHECK(hipHostMalloc((void**)&ctx->pinned, 64, hipHostMallocDefault));
     for (int k = 0; k < prm->max_iter; ++k) {
+        // state->done is set by bas_pcg_point of the first iteration after convergence: once it
+        // reads 1, every later iteration would exit at once, so stop enqueueing them
+        if (poll > 0 && k > 0 && k % poll == 0) {
+            SFM_HIP_CHECK(hipMemcpyAsync(ctx->pinned, &state->done, sizeof(int32_t),
+                                         hipMemcpyDeviceToHost, st));
+            SFM_HIP_CHECK(hipStreamSynchronize(st));
+            if (ctx->pinned[0] != 0) break;
+        }
         hipLaunchKernelGGL(bas_pcg_point, dim3(gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
                            pt_ptr, cam_idx, Wp, Vinv, z, pv, rzc, rrc, tol, state, t);
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
@@ -744,5 +755,57 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, gblk, U, gc, dc, mpart, rrc,
                        state, bad, info);
     SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
+// ---- fixed parameters (gauge / known intrinsics) ------------------------------------------------
+//
+// Holds the parameters marked in `fixed` [n_cam][8] at their values for the solve: their rows and
+// columns of U become those of the identity, their g_c entries and their rows of every W_o are
+// zeroed.  The Schur system then decouples them with right-hand side 0, so δ = 0 for them exactly
+// and the LM model terms (gᵀδ, δᵀJᵀJδ) do not see them.  Mirrors oracle/ba_lm.py fix_params().
+namespace {
+__global__ __launch_bounds__(256) void bas_fix_cam(int n_cam, const uint8_t* __restrict__ fixed,
+                                                   double* __restrict__ U,
+                                                   double* __restrict__ gc) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (camera, i, j)
+    if (g >= n_cam * 64) return;
+    const int c = g >> 6, i = (g >> 3) & 7, j = g & 7;
+    const bool fi = fixed[8 * (size_t)c + i] != 0, fj = fixed[8 * (size_t)c + j] != 0;
+    if (fi || fj) U[g] = (i == j) ? 1.0 : 0.0;
+    if (j == 0 && fi) gc[8 * (size_t)c + i] = 0.0;
+}
+
+__global__ __launch_bounds__(256) void bas_fix_obs(int n_obs, const int32_t* __restrict__ cam_idx,
+                                                   const uint8_t* __restrict__ fixed,
+                                                   double* __restrict__ W) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (observation, row i of W_o)
+    if (g >= n_obs * 8) return;
+    const int o = g >> 3, i = g & 7;
+    if (fixed[8 * (size_t)cam_idx[o] + i]) {
+        double* w = W + 24 * (size_t)o + 3 * i;
+        w[0] = 0.0; w[1] = 0.0; w[2] = 0.0;
+    }
+}
+}  // namespace
+
+extern "C" int sfm_ba_fix_params(sfm_ctx* ctx, int32_t n_cam, int32_t n_obs,
+                                 const int32_t* cam_idx, const uint8_t* fixed, double* U,
+                                 double* W, double* gc) {
+    SFM_REQUIRE(ctx != nullptr, "sfm_ba_fix_params: ctx is NULL");
+    SFM_REQUIRE(n_cam >= 0 && n_obs >= 0, "sfm_ba_fix_params: negative size");
+    if (n_cam == 0) return SFM_OK;
+    SFM_REQUIRE(fixed && U && gc && (n_obs == 0 || (cam_idx && W)),
+                "sfm_ba_fix_params: NULL array");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    hipLaunchKernelGGL(bas_fix_cam, dim3((64 * n_cam + 255) / 256), dim3(256), 0, st, n_cam,
+                       fixed, U, gc);
+    SFM_HIP_CHECK(hipGetLastError());
+    if (n_obs > 0) {
+        hipLaunchKernelGGL(bas_fix_obs, dim3((8 * n_obs + 255) / 256), dim3(256), 0, st, n_obs,
+                           cam_idx, fixed, W);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
     return SFM_OK;
 }

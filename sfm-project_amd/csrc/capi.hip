@@ -70,6 +70,7 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return SFM_OK;
@@ -115,7 +116,11 @@ int sfm_match_batch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int3
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     if (prm->metric == SFM_METRIC_L2) {
         SFM_REQUIRE(dim == 128, "sfm_match_batch: L2 metric needs dim == 128");
-        SFM_REQUIRE(k_max <= 4096, "sfm_match_batch: L2 k_max > 4096 not supported");
+        // cross-check rules: the column-winner kernel, k_max <= 8192 (COLMAP-style 8192 SIFT);
+        // ratio-only and no-rule paths: the fused key / forward-reverse kernels, k_max <= 4096
+        SFM_REQUIRE(k_max <= 8192, "sfm_match_batch: L2 k_max > 8192 not supported");
+        SFM_REQUIRE(k_max <= 4096 || prm->cross_check != SFM_XC_NONE,
+                    "sfm_match_batch: L2 k_max > 4096 needs a cross-check rule");
         return sfm_match_l2_launch(ctx, desc, n_kp, n_img, k_max, pairs, n_pairs, prm, out_count,
                                    out_match, out_dist);
     }

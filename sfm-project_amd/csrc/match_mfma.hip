@@ -52,7 +52,9 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int WAVES = 8;              // waves per workgroup
 constexpr int STAGE_BYTES = 32768;    // train bytes per LDS stage (CHUNK = STAGE_BYTES / D rows)
 constexpr int KALIGN = 256;           // tables are padded to a multiple of 256 (row-key index field)
-constexpr int KMAX_L2 = 4096;         // largest k_max handled by this kernel (LDS column state)
+constexpr int KMAX_L2 = 4096;         // largest k_max of the fused key kernel (static LDS column state)
+constexpr int KMAX_MU = 8192;         // largest k_max of the column-winner kernel (dynamic LDS:
+                                      // k_pad u64 = 64 KB at 8192, beside the 33 KB of stages)
 
 // Feature geometry per metric: D i8 features per row; QT query tiles (32 each) per wave.
 //   L2:      D = 128 (x ^ 0x80 = x - 128),              QT = 4 -> 1024 queries per workgroup
@@ -966,7 +968,28 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     const int D = l2 ? 128 : 256;
     const int QB = l2 ? mu_qb<128>() : mu_qb<256>();
     const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
-    SFM_REQUIRE(k_pad <= KMAX_L2, "sfm_match_batch: MFMA matcher needs k_max <= 4096");
+    SFM_REQUIRE(k_pad <= KMAX_MU, "sfm_match_batch: cross-check matcher needs k_max <= 8192");
+    if (k_pad * 8 > 65536 - 1024) {  // the column state past 64 KB of dynamic LDS (k_max > 8064)
+        static bool raised = false;  // once per process: the attribute is a property of the kernel
+        if (!raised) {
+            const int want = KMAX_MU * 8;
+            SFM_HIP_CHECK(hipFuncSetAttribute((const void*)mfma_mutual_kernel<128, true>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, want));
+            SFM_HIP_CHECK(hipFuncSetAttribute((const void*)mfma_mutual_kernel<128, false>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, want));
+            SFM_HIP_CHECK(hipFuncSetAttribute((const void*)mfma_mutual_kernel<256, true>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, want));
+            SFM_HIP_CHECK(hipFuncSetAttribute((const void*)mfma_mutual_kernel<256, false>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, want));
+            SFM_HIP_CHECK(hipFuncSetAttribute((const void*)mutual_finalize_kernel<128>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, want));
+            SFM_HIP_CHECK(hipFuncSetAttribute((const void*)mutual_finalize_kernel<256>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, want));
+            SFM_HIP_CHECK(hipFuncSetAttribute((const void*)opencv_finalize_kernel,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, want));
+            raised = true;
+        }
+    }
     const int n_qblk = (k_max + QB - 1) / QB;
     const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
     const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);

@@ -13,6 +13,7 @@ struct sfm_ctx {
     void* ws = nullptr;          // growable device workspace (shared by every call on ctx)
     size_t ws_bytes = 0;
     hipEvent_t handoff = nullptr;  // orders the workspace across sfm_ctx_set_stream switches
+    int32_t* pinned = nullptr;     // small pinned host buffer (device -> host flag reads)
     int n_cu = 256;
 };
 

@@ -66,6 +66,7 @@ class Reconstruction:
         self.points = None
         self.has_point = None
         self.history = []
+        self.gauge = None          # (reference camera, scale camera) of the initial pair
 
 
 def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
@@ -126,6 +127,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             rec.points[common[ok]] = pts[ok]
             rec.has_point[common[ok]] = True
             rec.registered[[a, b]] = True
+            rec.gauge = (a, b)
             say(f"initial pair ({a}, {b}): {len(r)} verified matches, {int(ok.sum())} points")
             break
     if not rec.registered.any():
@@ -191,14 +193,18 @@ def _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev):
 
 def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device):
     """Global LM over the registered cameras and the triangulated points (GPU), then drop points
-    whose mean reprojection error stays above max_err."""
+    whose mean reprojection error stays above max_err.  Gauge: the initial pair's first camera
+    keeps its pose and the second one translation coordinate (the scale); the intrinsics are
+    known, so f and k1 are held too (reconstruction.gauge_mask)."""
     use = rec.registered[timg] & rec.has_point[obs_track]
+    ref, second = rec.gauge
+    fixed = reconstruction.gauge_mask(rec.cams, ref=ref, second=second, fix_intrinsics=True)
     tr = obs_track[use]
     pts_ids, pt_idx = np.unique(tr, return_inverse=True)
     cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
                                                    timg[use], pt_idx.astype(np.int32),
                                                    obs_xy[use], loss_s=loss_s, max_iter=ba_iter,
-                                                   device=device)
+                                                   device=device, fixed=fixed)
     reg = rec.registered
     rec.cams[reg] = cams[reg]
     rec.points[pts_ids] = pts

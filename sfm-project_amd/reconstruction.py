@@ -145,9 +145,9 @@ class BAProblem:
         return self.ctx.ba_jtj(cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv,
                                self.pt_ptr, self.cam_ptr, self.cam_obs, loss_s=loss_s)
 
-    def solve(self, lin, lam, max_iter=100, tol=1e-10):
+    def solve(self, lin, lam, max_iter=100, tol=1e-10, poll=0):
         return self.ctx.ba_solve(lin, self.cam_idx, self.pt_idx, self.pt_ptr, self.cam_ptr,
-                                 self.cam_obs, lam, max_iter=max_iter, tol=tol)
+                                 self.cam_obs, lam, max_iter=max_iter, tol=tol, poll=poll)
 
     def cost(self, cams, pts, loss_s=0.0):
         return self.ctx.ba_cost(cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv, loss_s)
@@ -156,9 +156,52 @@ class BAProblem:
         return self.ctx.ba_update(cams, dc, pts, dp)
 
 
+def gauge_mask(cams, ref: int = 0, second=None, fix_intrinsics: bool = False,
+               registered=None):
+    """[n_cam, 8] bool mask of the parameters to hold in bundle adjustment.
+
+    The reprojection error is invariant under a similarity of the whole scene (7 DoF: rotation,
+    translation, scale), so without a gauge the reduced camera system is singular and only the LM
+    damping keeps it solvable.  This fixes the reference camera's pose (angle-axis + t: 6) and
+    the scale: the coordinate k of the second camera's translation relative to the reference
+    centre, t2 - R2 R_ref^T t_ref (in camera 2's frame: what a scaling about the reference centre
+    multiplies), with the largest magnitude — held by fixing t2[k].  fix_intrinsics additionally
+    holds f and k1 of every camera (calibrated cameras).  `second`: the second camera (default:
+    the registered camera farthest from the reference); `registered`: optional bool mask of
+    the cameras that take part."""
+    cams = np.asarray(cams, np.float64)
+    n = len(cams)
+    fixed = np.zeros((n, 8), bool)
+    if fix_intrinsics:
+        fixed[:, 6:8] = True
+    if n == 0:
+        return fixed
+    reg = np.ones(n, bool) if registered is None else np.asarray(registered, bool)
+    fixed[ref, :6] = True
+    R = lambda c: _rotmat_np(cams[c, :3])
+    C = lambda c: -R(c).T @ cams[c, 3:6]
+    if second is None:
+        cand = [c for c in np.nonzero(reg)[0] if c != ref]
+        if not cand:
+            return fixed
+        second = max(cand, key=lambda c: np.linalg.norm(C(c) - C(ref)))
+    rel = cams[second, 3:6] - R(second) @ R(ref).T @ cams[ref, 3:6]
+    fixed[second, 3 + int(np.argmax(np.abs(rel)))] = True
+    return fixed
+
+
+def _rotmat_np(r):
+    th = np.linalg.norm(r)
+    if th < 1e-12:
+        return np.eye(3)
+    k = r / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
                   lam0: float = 1e-4, ftol: float = 1e-12, max_cg: int = 200,
-                  cg_tol: float = 1e-10, device: int = 0):
+                  cg_tol: float = 1e-10, device: int = 0, fixed=None):
     """Levenberg-Marquardt on paper eq. (1): every step on the GPU
     (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
     accept / reject it.
@@ -167,16 +210,28 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     the cost decreases, then λ *= max(1/3, 1 - (2ρ-1)³); otherwise λ *= ν, ν *= 2.  Stops after
     `max_iter` steps, when an accepted step lowers the cost by <= ftol·cost, or when λ > 1e16.
 
+    fixed: optional [n_cam, 8] bool mask of parameters held at their values (gauge_mask;
+    sfm_ba_fix_params after every linearisation).
+
     Returns (cams [n_cam,8], pts [n_pt,3], history [(cost, λ, accepted, cg_iterations)])."""
     import torch
     n_cam, n_pt = len(cams), len(pts)
     prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(prob.dev)
     cams_d, pts_d = T(cams), T(pts)
+    fixed_d = None
+    if fixed is not None and np.any(fixed):
+        fixed_d = torch.from_numpy(np.ascontiguousarray(fixed, np.uint8).reshape(n_cam, 8)).to(prob.dev)
+
+    def linearize(c, p):
+        lin = prob.linearize(c, p, loss_s)
+        if fixed_d is not None:
+            prob.ctx.ba_fix_params(lin, prob.cam_idx, fixed_d)
+        return lin
     lam, nu = lam0, 2.0
     hist = []
     old = float(prob.cost(cams_d, pts_d, loss_s).item())
-    lin = prob.linearize(cams_d, pts_d, loss_s)
+    lin = linearize(cams_d, pts_d)
     for _ in range(max_iter):
         dc, dp, info = prob.solve(lin, lam, max_cg, cg_tol)
         c2, p2 = prob.update(cams_d, dc, pts_d, dp)
@@ -194,7 +249,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             old = new
             if done:
                 break
-            lin = prob.linearize(cams_d, pts_d, loss_s)
+            lin = linearize(cams_d, pts_d)
         else:
             lam *= nu
             nu *= 2.0

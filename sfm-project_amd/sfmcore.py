@@ -23,7 +23,8 @@ XC_NONE, XC_MUTUAL, XC_OPENCV = 0, 1, 2
 EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_sync",
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
-            "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch"]
+            "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
+            "sfm_ba_fix_params"]
 
 
 class SfmCoreError(RuntimeError):
@@ -37,7 +38,7 @@ class MatchParams(C.Structure):
 
 class BaSolveParams(C.Structure):
     _fields_ = [("lam", C.c_double), ("tol", C.c_double), ("max_iter", C.c_int32),
-                ("_pad", C.c_int32)]
+                ("poll", C.c_int32)]
 
 
 class RegisterParams(C.Structure):
@@ -87,6 +88,7 @@ def load_library(path: str = LIB_PATH):
                                    C.POINTER(BaSolveParams), vp, vp, vp]
         L.sfm_ba_cost.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp]
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
+        L.sfm_ba_fix_params.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp]
         L.sfm_register_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(RegisterParams),
                                          vp, vp, vp, vp]
         L.sfm_triangulate.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]
@@ -289,9 +291,10 @@ class Context:
         return pts, stats
 
     def ba_solve(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, max_iter=100,
-                 tol=1e-10, out=None):
+                 tol=1e-10, out=None, poll=0):
         """Damped Schur-complement PCG step from the ba_jtj blocks `lin`; returns
-        (dc [n_cam,8], dp [n_pt,3], info [5] f64 device tensor)."""
+        (dc [n_cam,8], dp [n_pt,3], info [5] f64 device tensor).  poll: convergence poll period
+        in CG iterations (0 = 8; < 0 = none, fully asynchronous), see include/sfmcore.h."""
         torch = self.torch
         U = lin["U"]
         dev = U.device
@@ -302,7 +305,7 @@ class Context:
                    torch.empty((npt, 3), dtype=f64, device=dev),
                    torch.empty(5, dtype=f64, device=dev))
         dc, dp, info = out
-        prm = BaSolveParams(float(lam), float(tol), int(max_iter), 0)
+        prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll))
         self._bind_stream()
         _check(self.lib.sfm_ba_solve(self.handle, nc, npt, no, _ptr(cam_idx), _ptr(pt_idx),
                                      _ptr(pt_ptr), _ptr(cam_ptr), _ptr(cam_obs), _ptr(U),
@@ -310,6 +313,16 @@ class Context:
                                      _ptr(lin["gp"]), C.byref(prm), _ptr(dc), _ptr(dp),
                                      _ptr(info)))
         return dc, dp, info
+
+    def ba_fix_params(self, lin, cam_idx, fixed):
+        """In place on ba_jtj's blocks `lin` (U, W, gc): hold the parameters marked in fixed
+        [n_cam,8] u8 device tensor (see include/sfmcore.h sfm_ba_fix_params).  Returns lin."""
+        U = lin["U"]
+        nc, no = U.shape[0], cam_idx.shape[0]
+        self._bind_stream()
+        _check(self.lib.sfm_ba_fix_params(self.handle, nc, no, _ptr(cam_idx), _ptr(fixed),
+                                          _ptr(U), _ptr(lin["W"]), _ptr(lin["gc"])))
+        return lin
 
     def ba_cost(self, cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0, out=None):
         torch = self.torch

@@ -57,6 +57,16 @@ def main():
         c2, p2 = P.update(cams, dc, pts, dp)
         P.cost(c2, p2)
     t_step = timed(lm_step, 5)
+
+    def lm_step_default(poll):  # what bundle_adjust runs: max_cg = 200, cg_tol = 1e-10
+        ln = P.linearize(cams, pts)
+        dc, dp, _ = P.solve(ln, lam, max_iter=200, tol=1e-10, poll=poll)
+        c2, p2 = P.update(cams, dc, pts, dp)
+        P.cost(c2, p2)
+    t_def = timed(lambda: lm_step_default(0), 5)
+    t_def_async = timed(lambda: lm_step_default(-1), 5)
+    _, _, info = P.solve(lin, lam, max_iter=200, tol=1e-10)
+    it10 = int(info[0].item())
     t_jtj = timed(lambda: P.linearize(cams, pts), 10)
     out = {
         "stage": "K4 BA step (Schur-complement PCG)", "n_cam": n_cam, "n_pt": n_pt, "n_obs": n_obs,
@@ -65,6 +75,8 @@ def main():
                      "achieved_GBs": bytes_it / (per_it * 1e-3) / 1e9, "peak_GBs": PEAK_HBM / 1e9,
                      "frac": bytes_it / (per_it * 1e-3) / PEAK_HBM},
         "cg_iters_to_1e-6": it6, "lm_step_ms": t_step, "jtj_ms": t_jtj,
+        "default_lm_step": {"max_cg": 200, "cg_tol": 1e-10, "cg_iters": it10,
+                            "ms_poll_every_8": t_def, "ms_no_poll_all_launches": t_def_async},
     }
     print(json.dumps(out))
 

@@ -103,3 +103,34 @@ def test_lm_matches_scipy_least_squares():
     err_ref, cost_ref = _scipy_solution(prob)
     assert np.abs(err - err_ref).max() < 1e-4            # px, the north_star BA tolerance
     assert abs(o["cost"] - cost_ref) <= 1e-9 * cost_ref
+
+
+def test_fixed_params_give_zero_step():
+    """fix_params (the spec of sfm_ba_fix_params): the damped Schur solve returns exactly 0 for
+    every held parameter, and the free parameters still solve the reduced system."""
+    prob = synth.make_ba_problem(7, 150, obs_per_pt=4, seed=8, perturb=2e-3)
+    rng = np.random.default_rng(1)
+    fixed = rng.random((7, 8)) < 0.3
+    fixed[:, 6:] = True
+    lin = L.fix_params(_lin(prob), prob["cam_idx"], fixed)
+    dc, dp, it, _ = L.schur_pcg(lin["U"], lin["V"], lin["W"], lin["gc"], lin["gp"],
+                                prob["cam_idx"], prob["pt_idx"], 1e-3, 500, 1e-12)
+    assert (dc[fixed] == 0.0).all() and np.abs(dc[~fixed]).max() > 0
+    dcd, dpd = L.solve_dense(lin["U"], lin["V"], lin["W"], lin["gc"], lin["gp"],
+                             prob["cam_idx"], prob["pt_idx"], 1e-3)
+    np.testing.assert_allclose(dc, dcd, rtol=0, atol=1e-8 * np.abs(dcd).max())
+
+
+def test_gauge_fixed_lm_reaches_the_same_optimum():
+    """The 7-DoF similarity gauge (reference pose + one translation coordinate of a second
+    camera, reconstruction.gauge_mask) removes the null space without changing the optimum: the
+    converged cost equals the gauge-free one, and the held parameters do not move."""
+    import reconstruction as R
+    prob = synth.make_ba_problem(8, 200, obs_per_pt=4, seed=9, perturb=3e-3)
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    fixed = R.gauge_mask(prob["cams"], ref=0)
+    assert fixed.sum() == 7 and fixed[0, :6].all()
+    cg, pg, hg = L.bundle_adjust(*args, max_iter=100, fixed=fixed)
+    cf, pf, hf = L.bundle_adjust(*args, max_iter=100)
+    assert abs(hg[-1][0] - hf[-1][0]) <= 1e-7 * hf[-1][0]
+    np.testing.assert_array_equal(cg[fixed], prob["cams"][fixed])

@@ -227,3 +227,37 @@ def test_rccl_world1_graph_allgather_and_camera_allreduce():
         assert torch.equal(U, U0) and torch.equal(gc, gc0) and float(cost) == 3.5
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k,xc,ratio", [(8192, O.XC_MUTUAL, (4, 5)), (6000, O.XC_OPENCV, None),
+                                        (5000, O.XC_MUTUAL, None)])
+def test_l2_above_4096_cross_check_then_ransac(ctx, k, xc, ratio):
+    """L2 k_max above 4096 (COLMAP-style 8192 SIFT): the column-winner kernel with its column
+    state past 64 KB of LDS, ragged sizes, then RANSAC on the matches; vs the oracle."""
+    import torch
+    s = synth.make_scene(3, k, seed=23)
+    n_kp = np.array([k, k - 371, k - 13], np.int32)
+    pairs = np.array([[0, 1], [2, 0], [1, 2]], np.int32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    cnt, mt, dist = ctx.match_batch(T(s["desc"]), T(n_kp), T(pairs), cross_check=xc, ratio=ratio)
+    rs = ctx.ransac_batch(T(s["kps"]), T(pairs), cnt, mt, n_hyp=1024, seed=42, thr=1.0)
+    torch.cuda.synchronize()
+    cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+    for p, (a, b) in enumerate(pairs):
+        q, t, d = O.match(s["desc"][a][:n_kp[a]], s["desc"][b][:n_kp[b]], 0, xc, ratio)
+        assert cnt[p] == len(q) > 1000
+        np.testing.assert_array_equal(mt[p, :cnt[p], 0], q)
+        np.testing.assert_array_equal(mt[p, :cnt[p], 1], t)
+        np.testing.assert_array_equal(dist[p, :cnt[p]], d)
+        r = O.ransac_f(s["kps"][a][q], s["kps"][b][t], H=1024, seed=42, pa=int(a), pb=int(b))
+        assert int(rs["inl_count"][p]) == r["count"] and int(rs["best_h"][p]) == r["best_h"]
+        np.testing.assert_array_equal(rs["mask"][p, :cnt[p]].cpu().numpy(), r["mask"])
+
+
+def test_l2_above_4096_without_cross_check_refused(ctx):
+    import torch
+    d = torch.zeros((2, 5000, 128), dtype=torch.uint8, device="cuda")
+    n = torch.full((2,), 5000, dtype=torch.int32, device="cuda")
+    pr = torch.tensor([[0, 1]], dtype=torch.int32, device="cuda")
+    with pytest.raises(sfmcore.SfmCoreError, match="cross-check"):
+        ctx.match_batch(d, n, pr, cross_check=sfmcore.XC_NONE, ratio=(4, 5))
