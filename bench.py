@@ -49,9 +49,10 @@ CONFIGS = {
 
 
 def pmc_traffic(kernel, cfg, n_img, k, world):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this exact workload
-    (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes, MI355X_MICROARCH.md
-    corrections), or None when no summary of this workload is committed."""
+    """HBM bytes per step (all launches of the step, like `achieved`) of `kernel` from the
+    committed PMC summary of this exact workload (tools/pmc_traffic.sh: FETCH_SIZE x2 +
+    WRITE_SIZE, separate passes, MI355X_MICROARCH.md corrections), or None when no summary of
+    this workload is committed."""
     f = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
     if not os.path.exists(f) or world != 1:
         return None
@@ -59,7 +60,7 @@ def pmc_traffic(kernel, cfg, n_img, k, world):
         d = json.load(open(f))
         if d.get("n_img") != n_img or d.get("k") != k:
             return None
-        return float(d["kernels"][kernel]["hbm_bytes"])
+        return float(d["kernels"][kernel]["hbm_bytes_per_step"])
     except (KeyError, ValueError):
         return None
 
