@@ -532,6 +532,10 @@ __device__ __forceinline__ void mu_top2(int& tb, int& ts, int x, int y) {
 #define MU_MINW 2
 #endif
 template <int D> constexpr int mu_qb() { return MU_WAVES * Geo<D>::QT * 32; }
+#ifdef MU_CLOCK
+constexpr int MU_CLOCK_SLOTS = 1 << 16;
+__device__ unsigned long long g_mu_clock[4 * MU_CLOCK_SLOTS];
+#endif
 
 template <int D, bool ROWS>
 __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
@@ -663,6 +667,9 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
             }
         }
     };
+#ifdef MU_CLOCK  // diagnostic build only: in-kernel clock (MI355X_MICROARCH.md "DVFS give-back" 6)
+    const unsigned long long t0c = __builtin_amdgcn_s_memtime(), t0r = __builtin_amdgcn_s_memrealtime();
+#endif
     if (n_chunk > 0) stage(0, lds0);
     __syncthreads();
     for (int ch = 0; ch < n_chunk; ch += 2) {
@@ -671,6 +678,15 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
         if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
         __syncthreads();
     }
+#ifdef MU_CLOCK
+    {   // stamps to a buffer of their own, read only by sfm_debug_clock_stamps (never an output)
+        const unsigned long long t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0 && blockIdx.x < MU_CLOCK_SLOTS) {
+            unsigned long long* d = g_mu_clock + 4 * (size_t)blockIdx.x;
+            d[0] = t0c; d[1] = t0r; d[2] = t1c; d[3] = t1r;
+        }
+    }
+#endif
     if (ROWS && active) {
 #pragma unroll
         for (int c = 0; c < QT; ++c) {
@@ -1094,3 +1110,14 @@ int sfm_match_hamming_mfma_launch(sfm_ctx* ctx, const uint8_t* desc, const int32
     return mfma_match_launch(ctx, SFM_METRIC_HAMMING, desc, n_kp, n_img, k_max, pairs, n_pairs,
                              prm, out_count, out_match, out_dist);
 }
+
+#ifdef MU_CLOCK
+// Diagnostic build only (tools/build_variant.sh clock -DMU_CLOCK): the per-block (memtime start,
+// realtime start, memtime end, realtime end) stamps of the last mfma_mutual_kernel launch.
+extern "C" int sfm_debug_clock_stamps(unsigned long long* host, int32_t n_blocks) {
+    const size_t n = 4 * (size_t)std::min(n_blocks, MU_CLOCK_SLOTS);
+    SFM_HIP_CHECK(hipDeviceSynchronize());
+    SFM_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mu_clock), n * sizeof(unsigned long long)));
+    return SFM_OK;
+}
+#endif

@@ -1,0 +1,67 @@
+"""In-kernel clock of the K1 mutual kernel (MI355X_MICROARCH.md "DVFS give-back" item 6): with the
+diagnostic library (tools/build_variant.sh clock -DMU_CLOCK; SFMCORE_LIB=.../libsfmcore_clock.so)
+every block stamps s_memtime / s_memrealtime around its train loop.  After >= 2 s of back-to-back
+launches on the cfg3 workload (K=, N_IMG= override), the stamps of the last launch give the clock
+(delta memtime / delta realtime x 100 MHz, median over blocks) and the shader cycles per 32-train
+tile per wave.  Usage: SFMCORE_LIB=... python tests/perf/k1_clock.py"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd")]
+
+import numpy as np
+import torch
+
+import sfmcore
+import synth
+
+
+def main():
+    n_img = int(os.environ.get("N_IMG", "50"))
+    K = int(os.environ.get("K", "2048"))
+    s = synth.make_scene(n_img, K, seed=0)
+    pairs = synth.unordered_pairs(n_img)
+    ctx = sfmcore.context(0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
+    out = ctx.match_batch(desc, n_kp, pr, ratio=(4, 5))
+    torch.cuda.synchronize()
+    t0, n = time.time(), 0
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    while time.time() - t0 < 2.5:
+        ev[0].record()
+        for _ in range(20):
+            out = ctx.match_batch(desc, n_kp, pr, ratio=(4, 5), out=out)
+        ev[1].record()
+        torch.cuda.synchronize()
+        n += 20
+    ms = ev[0].elapsed_time(ev[1]) / 20
+    qb = 512                                      # MU_WAVES (4) x QT (4) x 32 queries per block
+    n_blk = len(pairs) * ((K + qb - 1) // qb)
+    grid = 8 * ((n_blk + 7) // 8)
+    buf = np.zeros(4 * grid, np.uint64)
+    L = sfmcore.load_library()
+    L.sfm_debug_clock_stamps.argtypes = [C.c_void_p, C.c_int32]
+    assert L.sfm_debug_clock_stamps(buf.ctypes.data_as(C.c_void_p), grid) == 0
+    st = buf.reshape(-1, 4).astype(np.float64)
+    st = st[st[:, 2] > st[:, 0]]
+    cyc = st[:, 2] - st[:, 0]
+    wall = (st[:, 3] - st[:, 1]) / 100e6
+    clk = cyc / wall
+    tiles = K // 32                               # per wave: every train tile of the pair
+    res = {"workload": f"{len(pairs)} pairs x {K}", "launches": n, "launch_ms": ms,
+           "blocks": int(len(st)), "clock_GHz_median": float(np.median(clk) / 1e9),
+           "clock_GHz_p10_p90": [float(np.percentile(clk, 10) / 1e9),
+                                 float(np.percentile(clk, 90) / 1e9)],
+           "block_cycles_median": float(np.median(cyc)),
+           "cycles_per_tile_wave_median": float(np.median(cyc) / tiles),
+           "block_us_median": float(np.median(wall) * 1e6)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -22,9 +22,12 @@ def main():
     ctx = sfmcore.context(0)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
-    for xc, ratio, path in ((1, (4, 5), "mutual"), (1, (4, 5), "fused"), (1, (4, 5), "fr"),
-                            (0, (4, 5), "fr"), (0, (4, 5), "fused"), (2, None, "fused"), (2, None, "colonly"),
-                            (1, None, "mutual")):
+    cases = ((1, (4, 5), "mutual"), (1, (4, 5), "fused"), (1, (4, 5), "fr"),
+             (0, (4, 5), "fr"), (0, (4, 5), "fused"), (2, None, "fused"), (2, None, "colonly"),
+             (1, None, "mutual"))
+    if os.environ.get("K1_ONLY_BENCH_RULE"):  # the bench's rule only (mutual + ratio 4/5)
+        cases = cases[:1]
+    for xc, ratio, path in cases:
         os.environ["SFM_L2_PATH"] = path
         out = ctx.match_batch(desc, n_kp, pr, cross_check=xc, ratio=ratio)
         torch.cuda.synchronize()
