@@ -226,6 +226,30 @@ int sfm_register_batch(sfm_ctx* ctx, int32_t n_img, const int32_t* corr_ptr, con
                        const sfm_register_params* prm, double* out_cams, int32_t* out_count,
                        int32_t* out_key, uint8_t* out_mask);
 
+/* ---- ORB feature extraction -------------------------------------------------------------------
+ * replaces cv2.ORB_create() + orb.detectAndCompute(gray, None) of
+ * code/feature_matching.py:42-45 (OpenCV defaults: 500 features, scale 1.2, 8 levels, edge 31,
+ * patch 31, FAST 20, Harris score), batched over images of one size.  The spec is the build's
+ * integer-exact restatement of the published algorithm (oracle/sfm_oracle_orb.c header; parity
+ * against OpenCV itself unpinned: no cv2 here).
+ *   images    [n_img][H][W] u8 (device)
+ *   out_kp    [n_img][n_features][6] f32: x, y (level-0 pixels), size, angle (deg), Harris
+ *             response, octave — level order, best Harris first within a level
+ *   out_desc  [n_img][n_features][32] u8 (256-bit rBRIEF, OpenCV bit order)
+ *   out_count [n_img] i32 keypoints found (<= n_features)
+ */
+typedef struct sfm_orb_params {
+    int32_t n_features;      /* 500 */
+    int32_t n_levels;        /* 8 (<= 16) */
+    double scale_factor;     /* 1.2 */
+    int32_t fast_threshold;  /* 20 */
+    int32_t _pad;
+} sfm_orb_params;
+
+int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img, int32_t H, int32_t W,
+                  const sfm_orb_params* prm, float* out_kp, uint8_t* out_desc,
+                  int32_t* out_count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,19 @@ def _bind(L):
     L.oracle_reg_p3p.restype = i32
     L.oracle_reg_ransac.argtypes = [i32, vp, vp, vp, u32, i32, u64, f64, vp, vp, vp, vp]
     L.oracle_reg_ransac.restype = i32
+    L.oracle_orb_levels.argtypes = [i32, i32, i32, f64, i32, vp, vp, vp, vp]
+    L.oracle_orb_pattern.argtypes = [vp]
+    L.oracle_orb_resize.argtypes = [vp, i32, i32, i32, i32, vp]
+    L.oracle_orb_blur.argtypes = [vp, i32, i32, vp]
+    L.oracle_orb_fast_score.argtypes = [vp, i32, i32, i32]
+    L.oracle_orb_fast_score.restype = i32
+    L.oracle_orb_harris.argtypes = [vp, i32, i32, i32]
+    L.oracle_orb_harris.restype = i64
+    L.oracle_orb_moments.argtypes = [vp, i32, i32, i32, vp, vp]
+    L.oracle_orb_round_div.argtypes = [i64, i64]
+    L.oracle_orb_round_div.restype = i64
+    L.oracle_orb.argtypes = [vp, i32, i32, i32, i32, f64, i32, vp, vp, vp]
+    L.oracle_orb.restype = i32
 
 
 def match(A, B, metric=0, cross_check=XC_MUTUAL, ratio=None, max_dist=-1):
@@ -247,3 +260,65 @@ def reg_ransac(xy, X, intr, img=0, n_hyp=1024, seed=42, thr=4.0):
     cnt = lib().oracle_reg_ransac(n, _p(xy), _p(X), _p(intr), img, n_hyp, seed, thr, _p(key),
                                   _p(R), _p(t), _p(mask))
     return dict(count=int(cnt), key=int(key[0]), R=R.reshape(3, 3), t=t, mask=mask[:n])
+
+
+# ---- ORB extraction spec (oracle/sfm_oracle_orb.c) ----------------------------------------------
+
+def orb(img, nfeat=500, nlevels=8, scale=1.2, fast_thr=20):
+    """Returns (kp [n,6] f32 (x, y, size, angle, response, octave), desc [n,32] u8,
+    level counts [nlevels])."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    kp = np.zeros((max(nfeat, 1), 6), np.float32)
+    desc = np.zeros((max(nfeat, 1), 32), np.uint8)
+    lc = np.zeros(nlevels, np.int32)
+    n = lib().oracle_orb(_p(img), H, W, nfeat, nlevels, scale, fast_thr, _p(kp), _p(desc), _p(lc))
+    return kp[:n], desc[:n], lc
+
+
+def orb_levels(W, H, nlevels=8, scale=1.2, nfeat=500):
+    Wl = np.zeros(nlevels, np.int32); Hl = np.zeros(nlevels, np.int32)
+    sc = np.zeros(nlevels); nl = np.zeros(nlevels, np.int32)
+    lib().oracle_orb_levels(W, H, nlevels, scale, nfeat, _p(Wl), _p(Hl), _p(sc), _p(nl))
+    return Wl, Hl, sc, nl
+
+
+def orb_pattern():
+    pat = np.zeros((256, 4), np.int32)
+    lib().oracle_orb_pattern(_p(pat))
+    return pat
+
+
+def orb_resize(img, Hl, Wl):
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros((Hl, Wl), np.uint8)
+    lib().oracle_orb_resize(_p(img), img.shape[0], img.shape[1], Hl, Wl, _p(out))
+    return out
+
+
+def orb_blur(L):
+    L = np.ascontiguousarray(L, np.uint8)
+    out = np.zeros_like(L)
+    lib().oracle_orb_blur(_p(L), L.shape[0], L.shape[1], _p(out))
+    return out
+
+
+def orb_fast_score(L, x, y):
+    L = np.ascontiguousarray(L, np.uint8)
+    return int(lib().oracle_orb_fast_score(_p(L), L.shape[1], x, y))
+
+
+def orb_harris(L, x, y):
+    L = np.ascontiguousarray(L, np.uint8)
+    return int(lib().oracle_orb_harris(_p(L), L.shape[1], x, y))
+
+
+def orb_moments(L, x, y):
+    L = np.ascontiguousarray(L, np.uint8)
+    a, b = C.c_int64(), C.c_int64()
+    lib().oracle_orb_moments(_p(L), L.shape[1], x, y, C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def orb_round_div(n, R2):
+    return int(lib().oracle_orb_round_div(int(n), int(R2)))

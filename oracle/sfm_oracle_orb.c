@@ -1,0 +1,323 @@
+/*
+ * CPU restatement of the build's ORB extraction spec (TEST INFRASTRUCTURE ONLY: the checker of
+ * sfm-project_amd/csrc/orb.hip; imported by tests/ through oracle.py, never by the product).
+ *
+ * Reference: code/feature_matching.py:42-45 (cv2.ORB_create() + detectAndCompute, OpenCV
+ * defaults nfeatures 500, scaleFactor 1.2, nlevels 8, edgeThreshold 31, patchSize 31, FAST
+ * threshold 20, HARRIS_SCORE, WTA_K 2).  OpenCV is absent here, so this is the
+ * published ORB algorithm (Rublee et al. 2011; OpenCV's documented pipeline) written as an
+ * integer-exact spec — PARITY UNPINNED against OpenCV itself.  Deviations that are deliberate
+ * (DESIGN.md §4.10): the BRIEF test pattern is generated from a seeded RNG (BRIEF's G II
+ * sampling) instead of OpenCV's learned bit_pattern_31_ table; pyramid, blur and Harris are
+ * defined in fixed-point / integer arithmetic; ties are broken in raster order.
+ *
+ * Per image (u8 [H][W]):
+ *   levels      l = 0..L-1, sc_l = 1.2^l (repeated multiplication), W_l = lround(W / sc_l);
+ *               level l >= 1 is a bilinear resample of level 0 with 11-bit weights
+ *               (OpenCV INTER_LINEAR's convention sx = (dx + 0.5) W / W_l - 0.5, edge replicate);
+ *   budget      n_l = lround(nfeat (1 - 1/s) / (1 - (1/s)^L) (1/s)^l), the last level the rest;
+ *   FAST-9      on [31, W_l - 31) x [31, H_l - 31): score = max over the 16 arcs of 9 contiguous
+ *               circle pixels of max(min(I_k - p), min(p - I_k)); corner iff score > threshold;
+ *   NMS         score strictly greater than all 8 neighbours; candidates in raster order, at
+ *               most 32768 per level;
+ *   selection   the 2 n_l best by FAST score (ties: raster order), then the n_l best by the
+ *               Harris response R = 25 (a b - c^2) - (a + b)^2 (= 25 (det - 0.04 tr^2)) of the
+ *               3x3-Sobel structure tensor summed over a 7x7 window (ties: raster order);
+ *   orientation intensity centroid over the disk u^2 + v^2 <= 15^2 of the level image;
+ *   descriptor  256 tests on a 7x7 Gaussian (sigma 2, weights 18 34 49 54 49 34 18 / 256)
+ *               blur of the level, each point rotated by (m10, m01) / |m| and rounded EXACTLY
+ *               (k = floor(n / r + 1/2) by integer comparisons, r = |m|), bit = I(p1) < I(p2).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORB_EDGE 31
+#define ORB_MAXC 32768
+#define ORB_RADIUS 15
+
+static const int FAST_DX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+static const int FAST_DY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+static const int BLUR_W[7] = {18, 34, 49, 54, 49, 34, 18};
+
+/* ---- host-side tables (mirrored by the C-ABI's host code, capi side of csrc/orb.hip) ------- */
+
+void oracle_orb_levels(int W, int H, int nlevels, double scale, int nfeat, int32_t* Wl,
+                       int32_t* Hl, double* scl, int32_t* nl) {
+    double sc = 1.0;
+    for (int l = 0; l < nlevels; ++l) {
+        scl[l] = sc;
+        Wl[l] = (int32_t)lround((double)W / sc);
+        Hl[l] = (int32_t)lround((double)H / sc);
+        sc *= scale;
+    }
+    const double factor = 1.0 / scale;
+    double fp = 1.0;
+    for (int l = 0; l < nlevels; ++l) fp *= factor;
+    double nd = (double)nfeat * (1.0 - factor) / (1.0 - fp);
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; ++l) {
+        nl[l] = (int32_t)lround(nd);
+        sum += nl[l];
+        nd *= factor;
+    }
+    nl[nlevels - 1] = nfeat - sum > 0 ? nfeat - sum : 0;
+}
+
+static uint64_t sm_next(uint64_t* s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static int pattern_coord(uint64_t* s) {
+    double g = 0.0;
+    for (int i = 0; i < 12; ++i) g += (double)(sm_next(s) >> 11) * (1.0 / 9007199254740992.0);
+    g -= 6.0;
+    long v = lround(6.2 * g);
+    return (int)(v < -13 ? -13 : (v > 13 ? 13 : v));
+}
+
+/* 256 tests (x1, y1, x2, y2), BRIEF G II: i.i.d. ~N(0, (31/5)^2) clipped to [-13, 13]. */
+void oracle_orb_pattern(int32_t* pat) {
+    uint64_t s = 0x5EED0B5EULL;
+    for (int t = 0; t < 256; ++t) {
+        int x1 = pattern_coord(&s), y1 = pattern_coord(&s), x2, y2;
+        do {
+            x2 = pattern_coord(&s);
+            y2 = pattern_coord(&s);
+        } while (x2 == x1 && y2 == y1);
+        pat[4 * t] = x1; pat[4 * t + 1] = y1; pat[4 * t + 2] = x2; pat[4 * t + 3] = y2;
+    }
+}
+
+/* resample map of one axis: n_out entries (i0, i1, w) */
+void oracle_orb_axis_map(int n_in, int n_out, int32_t* map) {
+    const double r = (double)n_in / (double)n_out;
+    for (int d = 0; d < n_out; ++d) {
+        const double sx = ((double)d + 0.5) * r - 0.5;
+        int x0 = (int)floor(sx);
+        int w = (int)lround((sx - (double)x0) * 2048.0);
+        if (x0 < 0) { x0 = 0; w = 0; }
+        int x1 = x0 + 1;
+        if (x0 >= n_in - 1) { x0 = n_in - 1; x1 = n_in - 1; w = 0; }
+        map[3 * d] = x0; map[3 * d + 1] = x1; map[3 * d + 2] = w;
+    }
+}
+
+/* ---- per-level image operations ------------------------------------------------------------ */
+
+void oracle_orb_resize(const uint8_t* img, int H, int W, int Hl, int Wl, uint8_t* out) {
+    int32_t* mx = (int32_t*)malloc(sizeof(int32_t) * 3 * Wl);
+    int32_t* my = (int32_t*)malloc(sizeof(int32_t) * 3 * Hl);
+    oracle_orb_axis_map(W, Wl, mx);
+    oracle_orb_axis_map(H, Hl, my);
+    for (int y = 0; y < Hl; ++y) {
+        const uint8_t* r0 = img + (size_t)my[3 * y] * W;
+        const uint8_t* r1 = img + (size_t)my[3 * y + 1] * W;
+        const int wy = my[3 * y + 2];
+        for (int x = 0; x < Wl; ++x) {
+            const int x0 = mx[3 * x], x1 = mx[3 * x + 1], wx = mx[3 * x + 2];
+            const int t0 = r0[x0] * (2048 - wx) + r0[x1] * wx;
+            const int t1 = r1[x0] * (2048 - wx) + r1[x1] * wx;
+            out[(size_t)y * Wl + x] = (uint8_t)((t0 * (2048 - wy) + t1 * wy + (1 << 21)) >> 22);
+        }
+    }
+    free(mx);
+    free(my);
+}
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+void oracle_orb_blur(const uint8_t* L, int H, int W, uint8_t* out) {
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            int acc = 0;
+            for (int j = -3; j <= 3; ++j) {
+                const uint8_t* row = L + (size_t)clampi(y + j, 0, H - 1) * W;
+                int h = 0;
+                for (int i = -3; i <= 3; ++i) h += BLUR_W[i + 3] * row[clampi(x + i, 0, W - 1)];
+                acc += BLUR_W[j + 3] * h;
+            }
+            out[(size_t)y * W + x] = (uint8_t)((acc + 32768) >> 16);
+        }
+}
+
+int oracle_orb_fast_score(const uint8_t* L, int W, int x, int y) {
+    const int p = L[(size_t)y * W + x];
+    int d[16];
+    for (int k = 0; k < 16; ++k) d[k] = (int)L[(size_t)(y + FAST_DY[k]) * W + x + FAST_DX[k]] - p;
+    int best = 0;
+    for (int s = 0; s < 16; ++s) {
+        int b = 255, k = 255;
+        for (int i = 0; i < 9; ++i) {
+            const int v = d[(s + i) & 15];
+            if (v < b) b = v;
+            if (-v < k) k = -v;
+        }
+        const int m = b > k ? b : k;
+        if (m > best) best = m;
+    }
+    return best;
+}
+
+int64_t oracle_orb_harris(const uint8_t* L, int W, int x, int y) {
+    int64_t a = 0, b = 0, c = 0;
+    for (int v = -3; v <= 3; ++v)
+        for (int u = -3; u <= 3; ++u) {
+            const uint8_t* m = L + (size_t)(y + v) * W + (x + u);
+            const int ix = (m[-W + 1] + 2 * m[1] + m[W + 1]) - (m[-W - 1] + 2 * m[-1] + m[W - 1]);
+            const int iy = (m[W - 1] + 2 * m[W] + m[W + 1]) - (m[-W - 1] + 2 * m[-W] + m[-W + 1]);
+            a += (int64_t)ix * ix;
+            b += (int64_t)iy * iy;
+            c += (int64_t)ix * iy;
+        }
+    return 25 * (a * b - c * c) - (a + b) * (a + b);
+}
+
+void oracle_orb_moments(const uint8_t* L, int W, int x, int y, int64_t* m10, int64_t* m01) {
+    int64_t s10 = 0, s01 = 0;
+    for (int v = -ORB_RADIUS; v <= ORB_RADIUS; ++v)
+        for (int u = -ORB_RADIUS; u <= ORB_RADIUS; ++u) {
+            if (u * u + v * v > ORB_RADIUS * ORB_RADIUS) continue;
+            const int I = L[(size_t)(y + v) * W + x + u];
+            s10 += (int64_t)u * I;
+            s01 += (int64_t)v * I;
+        }
+    *m10 = s10;
+    *m01 = s01;
+}
+
+/* B r <= A with r = sqrt(R2), exactly */
+static int le_r(int64_t B, int64_t A, int64_t R2) {
+    if (B <= 0 && A >= 0) return 1;
+    if (B > 0 && A < 0) return 0;
+    if (B >= 0) return B * B * R2 <= A * A;
+    return B * B * R2 >= A * A;
+}
+
+/* floor(n / sqrt(R2) + 1/2), exactly (R2 > 0) */
+int64_t oracle_orb_round_div(int64_t n, int64_t R2) {
+    int64_t k = (int64_t)floor((double)n / sqrt((double)R2) + 0.5);
+    while (!le_r(2 * k - 1, 2 * n, R2)) --k;
+    while (le_r(2 * k + 1, 2 * n, R2)) ++k;
+    return k;
+}
+
+void oracle_orb_describe(const uint8_t* B, int W, int x, int y, int64_t m10, int64_t m01,
+                         const int32_t* pat, uint8_t* desc) {
+    const int64_t R2 = m10 * m10 + m01 * m01;
+    memset(desc, 0, 32);
+    for (int t = 0; t < 256; ++t) {
+        int q[4];
+        for (int e = 0; e < 2; ++e) {
+            const int64_t px = pat[4 * t + 2 * e], py = pat[4 * t + 2 * e + 1];
+            if (R2 == 0) {
+                q[2 * e] = (int)px;
+                q[2 * e + 1] = (int)py;
+            } else {
+                q[2 * e] = (int)oracle_orb_round_div(px * m10 - py * m01, R2);
+                q[2 * e + 1] = (int)oracle_orb_round_div(px * m01 + py * m10, R2);
+            }
+        }
+        const int i1 = B[(size_t)(y + q[1]) * W + x + q[0]];
+        const int i2 = B[(size_t)(y + q[3]) * W + x + q[2]];
+        if (i1 < i2) desc[t >> 3] |= (uint8_t)(1u << (t & 7));
+    }
+}
+
+/* ---- the whole extraction ------------------------------------------------------------------ */
+
+typedef struct { int x, y, s; int64_t r; int idx; } orb_cand;
+
+static int cmp_harris(const void* a, const void* b) {
+    const orb_cand* p = (const orb_cand*)a;
+    const orb_cand* q = (const orb_cand*)b;
+    if (p->r != q->r) return p->r > q->r ? -1 : 1;
+    return p->idx - q->idx;
+}
+
+/* kp [nfeat][6] (x, y, size, angle deg, response, octave) f32, desc [nfeat][32]; returns the
+ * number of keypoints; lvl_count [nlevels] per level. */
+int oracle_orb(const uint8_t* img, int H, int W, int nfeat, int nlevels, double scale,
+               int fast_thr, float* kp, uint8_t* desc, int32_t* lvl_count) {
+    int32_t Wl[32], Hl[32], nl[32];
+    double scl[32];
+    int32_t pat[1024];
+    if (nlevels > 32) return -1;
+    oracle_orb_levels(W, H, nlevels, scale, nfeat, Wl, Hl, scl, nl);
+    oracle_orb_pattern(pat);
+    int out = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        lvl_count[l] = 0;
+        const int w = Wl[l], h = Hl[l];
+        if (w <= 2 * ORB_EDGE || h <= 2 * ORB_EDGE || nl[l] <= 0) continue;
+        uint8_t* L = (uint8_t*)malloc((size_t)w * h);
+        uint8_t* Bl = (uint8_t*)malloc((size_t)w * h);
+        uint8_t* S = (uint8_t*)calloc((size_t)w * h, 1);
+        if (l == 0) memcpy(L, img, (size_t)w * h);
+        else oracle_orb_resize(img, H, W, h, w, L);
+        oracle_orb_blur(L, h, w, Bl);
+        for (int y = ORB_EDGE; y < h - ORB_EDGE; ++y)
+            for (int x = ORB_EDGE; x < w - ORB_EDGE; ++x) {
+                const int s = oracle_orb_fast_score(L, w, x, y);
+                S[(size_t)y * w + x] = (uint8_t)(s > fast_thr ? s : 0);
+            }
+        orb_cand* c = (orb_cand*)malloc(sizeof(orb_cand) * ORB_MAXC);
+        int nc = 0;
+        for (int y = ORB_EDGE; y < h - ORB_EDGE && nc < ORB_MAXC; ++y)
+            for (int x = ORB_EDGE; x < w - ORB_EDGE && nc < ORB_MAXC; ++x) {
+                const int s = S[(size_t)y * w + x];
+                if (!s) continue;
+                int keep = 1;
+                for (int dy = -1; dy <= 1 && keep; ++dy)
+                    for (int dx = -1; dx <= 1; ++dx)
+                        if ((dx || dy) && S[(size_t)(y + dy) * w + x + dx] >= s) { keep = 0; break; }
+                if (keep) { c[nc].x = x; c[nc].y = y; c[nc].s = s; c[nc].idx = nc; ++nc; }
+            }
+        /* the 2 n_l best FAST scores, ties in raster order */
+        const int a = 2 * nl[l];
+        int hist[256] = {0};
+        for (int i = 0; i < nc; ++i) hist[c[i].s]++;
+        int T = 0, above = 0;
+        if (nc > a) {
+            for (T = 255; T > 0; --T) {
+                if (above + hist[T] >= a) break;
+                above += hist[T];
+            }
+        }
+        int n1 = 0, ties = 0;
+        for (int i = 0; i < nc; ++i) {
+            int take = nc <= a || c[i].s > T;
+            if (!take && c[i].s == T && ties < a - above) { take = 1; ++ties; }
+            if (take) {
+                c[n1] = c[i];
+                c[n1].idx = n1;
+                ++n1;
+            }
+        }
+        for (int i = 0; i < n1; ++i) c[i].r = oracle_orb_harris(L, w, c[i].x, c[i].y);
+        qsort(c, n1, sizeof(orb_cand), cmp_harris);
+        const int n2 = n1 < nl[l] ? n1 : nl[l];
+        for (int i = 0; i < n2; ++i) {
+            int64_t m10, m01;
+            oracle_orb_moments(L, w, c[i].x, c[i].y, &m10, &m01);
+            double ang = atan2((double)m01, (double)m10) * (180.0 / 3.14159265358979323846);
+            if (ang < 0.0) ang += 360.0;
+            float* k = kp + 6 * (size_t)out;
+            k[0] = (float)((double)c[i].x * scl[l]);
+            k[1] = (float)((double)c[i].y * scl[l]);
+            k[2] = (float)(31.0 * scl[l]);
+            k[3] = (float)ang;
+            k[4] = (float)((double)c[i].r / 25.0);
+            k[5] = (float)l;
+            oracle_orb_describe(Bl, w, c[i].x, c[i].y, m10, m01, pat, desc + 32 * (size_t)out);
+            ++out;
+        }
+        lvl_count[l] = n2;
+        free(c); free(S); free(Bl); free(L);
+    }
+    return out;
+}

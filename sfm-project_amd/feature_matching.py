@@ -2,12 +2,14 @@
 
 `pipeline.py` star-imports this module (code/pipeline.py:2) and uses `os`, `np`, `cv2`
 (code/pipeline.py:14,15,19) and `extract_and_match` (code/pipeline.py:41).  The module keeps those
-names and signatures; the matching arithmetic — cv2.BFMatcher(NORM_HAMMING, crossCheck=True).match
-at code/feature_matching.py:48-50 — runs in libsfmcore's HIP kernels instead of OpenCV.
-
-Feature EXTRACTION (ORB, code/feature_matching.py:42-45) is out of the hot-path scope and still
-needs OpenCV; this container has no cv2, so `extract_and_match` raises ImportError there while the
-descriptor-level entry `match_descriptors` works on any uint8 descriptor arrays.
+names and signatures; the arithmetic runs in libsfmcore's HIP kernels instead of OpenCV:
+  * ORB extraction — cv2.ORB_create() + detectAndCompute at code/feature_matching.py:42-45 —
+    is `sfm_orb_batch` (csrc/orb.hip; the build's integer-exact ORB spec, oracle/sfm_oracle_orb.c;
+    parity against OpenCV itself unpinned), batched over images and done ONCE per image by
+    `extract_all` / `pipeline_pair_matches` instead of 2 x N(N-1) times;
+  * matching — cv2.BFMatcher(NORM_HAMMING, crossCheck=True).match at :48-50 — is
+    `sfm_match_batch`.
+Only image I/O and drawing (`read_img`, `extract_and_match_draw`) still need cv2.
 """
 from __future__ import annotations
 
@@ -49,8 +51,8 @@ class DMatch:
 
 def _require_cv2(what: str):
     if cv2 is None:
-        raise ImportError(f"{what} needs OpenCV (cv2), which is not installed; use "
-                          "match_descriptors() on precomputed descriptors")
+        raise ImportError(f"{what} needs OpenCV (cv2) for image I/O / drawing, which is not "
+                          "installed; extraction and matching run without it")
 
 
 def read_img(path):
@@ -170,17 +172,67 @@ def match_all_pairs(descriptors, norm: str = "hamming", cross_check=True,
     return out
 
 
-def extract_all(images, nfeatures: int = 500):
-    """ORB once per image (code/feature_matching.py:42-45 extracts 2 x N(N-1) times): returns
-    (keypoints, descriptors) lists.  Needs cv2."""
-    _require_cv2("extract_all")
-    orb = cv2.ORB_create(nfeatures)
-    kps, des = [], []
-    for img in images:
-        k, d = orb.detectAndCompute(img, None)
-        kps.append(k)
-        des.append(d)
-    return kps, des
+class KeyPoint:
+    """cv2.KeyPoint-compatible record (pt, size, angle, response, octave, class_id)."""
+
+    __slots__ = ("pt", "size", "angle", "response", "octave", "class_id")
+
+    def __init__(self, x, y, size, angle=-1.0, response=0.0, octave=0, class_id=-1):
+        self.pt = (float(x), float(y))
+        self.size = float(size)
+        self.angle = float(angle)
+        self.response = float(response)
+        self.octave = int(octave)
+        self.class_id = int(class_id)
+
+    def __repr__(self):
+        return (f"<KeyPoint pt=({self.pt[0]:g}, {self.pt[1]:g}) size={self.size:g} "
+                f"angle={self.angle:.2f} octave={self.octave}>")
+
+
+ORB_DEFAULTS = dict(n_features=500, n_levels=8, scale_factor=1.2, fast_threshold=20)
+
+
+def _orb_gpu(images, device=0, **kw):
+    """GPU ORB over a list of grayscale u8 images; images of one size share one launch.
+    Returns per image (kp [n,6] f32, desc [n,32] u8) numpy arrays."""
+    import torch
+    prm = dict(ORB_DEFAULTS, **kw)
+    ctx = sfmcore.context(device)
+    dev = torch.device("cuda", device)
+    out = [None] * len(images)
+    groups = {}
+    for i, im in enumerate(images):
+        groups.setdefault(np.asarray(im).shape, []).append(i)
+    for shape, idx in groups.items():
+        if len(shape) != 2:
+            raise ValueError(f"ORB needs 2-D grayscale images, got shape {shape}")
+        batch = torch.from_numpy(np.ascontiguousarray(
+            np.stack([np.asarray(images[i], np.uint8) for i in idx]))).to(dev)
+        kp, desc, cnt = ctx.orb_batch(batch, **prm)
+        kp, desc, cnt = kp.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+        for j, i in enumerate(idx):
+            out[i] = (kp[j, :cnt[j]], desc[j, :cnt[j]])
+    return out
+
+
+def _keypoints(kp):
+    return [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp]
+
+
+def detect_and_compute(gray, nfeatures: int = 500, device: int = 0):
+    """orb.detectAndCompute(gray, None) (code/feature_matching.py:44) on the GPU: returns
+    ([KeyPoint], descriptors u8 [n,32] or None when nothing is found, as OpenCV)."""
+    kp, desc = _orb_gpu([gray], device, n_features=nfeatures)[0]
+    return _keypoints(kp), (desc if len(desc) else None)
+
+
+def extract_all(images, nfeatures: int = 500, device: int = 0):
+    """ORB once per image, batched on the GPU (the reference extracts 2 x N(N-1) times,
+    code/pipeline.py:38-41 -> code/feature_matching.py:42-45): returns (keypoints, descriptors)
+    lists."""
+    res = _orb_gpu(list(images), device, n_features=nfeatures)
+    return ([_keypoints(k) for k, _ in res], [d if len(d) else None for _, d in res])
 
 
 def pipeline_pair_matches(images):
@@ -201,24 +253,23 @@ def _max_dist(metric, max_distance):
 
 def extract_and_match(gray1, gray2):
     """code/feature_matching.py:41-60: ORB on both images, BF Hamming + crossCheck, sorted,
-    prefix with distance < 26.  Matching runs on the GPU; extraction needs cv2."""
-    _require_cv2("extract_and_match")
-    orb = cv2.ORB_create()
-    kp1, des1 = orb.detectAndCompute(gray1, None)
-    kp2, des2 = orb.detectAndCompute(gray2, None)
+    prefix with distance < 26 — extraction and matching on the GPU."""
+    (_, des1), (_, des2) = _orb_gpu([gray1, gray2])
     return match_descriptors(des1, des2, "hamming", True, REFERENCE_MAX_HAMMING)
 
 
 def extract_and_match_draw(gray1, gray2):
-    """code/feature_matching.py:15-37: as extract_and_match, then draws the matches."""
+    """code/feature_matching.py:15-37: as extract_and_match, then draws the matches (the drawing
+    needs cv2 and matplotlib)."""
     _require_cv2("extract_and_match_draw")
     import matplotlib.pyplot as plt
-    orb = cv2.ORB_create()
-    kp1, des1 = orb.detectAndCompute(gray1, None)
-    kp2, des2 = orb.detectAndCompute(gray2, None)
+    kp1, des1 = detect_and_compute(gray1)
+    kp2, des2 = detect_and_compute(gray2)
     cropped = match_descriptors(des1, des2, "hamming", True, REFERENCE_MAX_HAMMING)
+    ck1 = [cv2.KeyPoint(k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave) for k in kp1]
+    ck2 = [cv2.KeyPoint(k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave) for k in kp2]
     cvm = [cv2.DMatch(m.queryIdx, m.trainIdx, m.imgIdx, m.distance) for m in cropped]
-    img = cv2.drawMatches(gray1, kp1, gray2, kp2, cvm, None,
+    img = cv2.drawMatches(gray1, ck1, gray2, ck2, cvm, None,
                           flags=cv2.DrawMatchesFlags_NOT_DRAW_SINGLE_POINTS)
     plt.imshow(img), plt.show()
     return cropped

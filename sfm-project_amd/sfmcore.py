@@ -24,7 +24,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
-            "sfm_ba_fix_params"]
+            "sfm_ba_fix_params", "sfm_orb_batch"]
 
 
 class SfmCoreError(RuntimeError):
@@ -44,6 +44,11 @@ class BaSolveParams(C.Structure):
 class RegisterParams(C.Structure):
     _fields_ = [("n_hyp", C.c_int32), ("refine", C.c_int32), ("thr", C.c_double),
                 ("seed", C.c_uint64)]
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("n_features", C.c_int32), ("n_levels", C.c_int32), ("scale_factor", C.c_double),
+                ("fast_threshold", C.c_int32), ("_pad", C.c_int32)]
 
 
 class RansacParams(C.Structure):
@@ -89,6 +94,7 @@ def load_library(path: str = LIB_PATH):
         L.sfm_ba_cost.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp]
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
         L.sfm_ba_fix_params.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp]
+        L.sfm_orb_batch.argtypes = [vp, vp, i32, i32, i32, C.POINTER(OrbParams), vp, vp, vp]
         L.sfm_register_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(RegisterParams),
                                          vp, vp, vp, vp]
         L.sfm_triangulate.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp, vp]
@@ -167,6 +173,26 @@ class Context:
         _check(self.lib.sfm_match_batch(self.handle, _ptr(desc), _ptr(n_kp), n_img, k_max, dim,
                                         _ptr(pairs), P, C.byref(prm), _ptr(out[0]), _ptr(out[1]),
                                         _ptr(out[2])))
+        return out
+
+    # ---- feature extraction ----------------------------------------------------------------
+    def orb_batch(self, images, n_features=500, n_levels=8, scale_factor=1.2, fast_threshold=20,
+                  out=None):
+        """images [n_img,H,W] u8 device tensor.  Returns (kp [n_img,n_features,6] f32,
+        desc [n_img,n_features,32] u8, count [n_img] i32) device tensors (see sfmcore.h)."""
+        torch = self.torch
+        if images.dtype != torch.uint8 or not images.is_cuda or not images.is_contiguous():
+            raise SfmCoreError("orb_batch: expected a contiguous u8 device tensor [n_img,H,W]")
+        n_img, H, W = images.shape
+        dev = images.device
+        if out is None:
+            out = (torch.empty((n_img, n_features, 6), dtype=torch.float32, device=dev),
+                   torch.empty((n_img, n_features, 32), dtype=torch.uint8, device=dev),
+                   torch.empty(n_img, dtype=torch.int32, device=dev))
+        prm = OrbParams(int(n_features), int(n_levels), float(scale_factor), int(fast_threshold), 0)
+        self._bind_stream()
+        _check(self.lib.sfm_orb_batch(self.handle, _ptr(images), n_img, H, W, C.byref(prm),
+                                      _ptr(out[0]), _ptr(out[1]), _ptr(out[2])))
         return out
 
     # ---- geometric verification ------------------------------------------------------------

@@ -173,3 +173,35 @@ def make_ba_problem(n_cam: int, n_pt: int, obs_per_pt: int = 5, seed: int = 0,
     cams[:, :6] += rng.normal(0.0, perturb, size=(n_cam, 6))
     pts = pts_true + rng.normal(0.0, 10 * perturb, size=pts_true.shape)
     return dict(cams=cams, pp=pp, pts=pts, cam_idx=cam_idx, pt_idx=pt_idx, uv=uv)
+
+
+def make_image(H: int, W: int, seed: int = 0, n_shapes: int = 120) -> np.ndarray:
+    """Grayscale u8 test image with corners for the ORB extractor: a smooth gradient background
+    and `n_shapes` filled rectangles, triangles and discs of random intensity, lightly blurred,
+    plus pixel noise.  Seeded (PCG64), so every machine draws the same image."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    img = 60.0 + 40.0 * (xx / max(W, 1)) + 30.0 * (yy / max(H, 1))
+    for _ in range(n_shapes):
+        kind = rng.integers(0, 3)
+        cx, cy = rng.uniform(0, W), rng.uniform(0, H)
+        r = rng.uniform(0.02, 0.08) * min(H, W) + 3
+        val = rng.uniform(0, 255)
+        if kind == 0:
+            a = rng.uniform(0, np.pi)
+            u = (xx - cx) * np.cos(a) + (yy - cy) * np.sin(a)
+            v = -(xx - cx) * np.sin(a) + (yy - cy) * np.cos(a)
+            m = (np.abs(u) < r) & (np.abs(v) < 0.6 * r)
+        elif kind == 1:
+            m = (xx - cx) ** 2 + (yy - cy) ** 2 < r * r
+        else:
+            p = rng.uniform(-r, r, size=(3, 2)) + [cx, cy]
+            d = lambda i, j: ((p[j, 0] - p[i, 0]) * (yy - p[i, 1]) - (p[j, 1] - p[i, 1]) * (xx - p[i, 0]))
+            s1, s2, s3 = d(0, 1), d(1, 2), d(2, 0)
+            m = ((s1 >= 0) & (s2 >= 0) & (s3 >= 0)) | ((s1 <= 0) & (s2 <= 0) & (s3 <= 0))
+        img[m] = val
+    k = np.array([1.0, 4.0, 6.0, 4.0, 1.0]) / 16.0
+    img = np.apply_along_axis(lambda r: np.convolve(r, k, mode="same"), 1, img)
+    img = np.apply_along_axis(lambda c: np.convolve(c, k, mode="same"), 0, img)
+    img += rng.normal(0.0, 2.0, size=img.shape)
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8))

@@ -29,11 +29,17 @@ def test_3d_reconstruction_module_loads_under_reference_name():
     assert hasattr(m, "build_jtj") and hasattr(m, "reprojection_errors")
 
 
-def test_extract_and_match_without_cv2_raises_clearly():
-    if fm.cv2 is not None:
-        pytest.skip("cv2 present")
-    with pytest.raises(ImportError, match="OpenCV"):
+def test_extract_and_match_needs_the_gpu_not_cv2():
+    """Extraction and matching run on the GPU (no cv2 needed); without a device the product
+    path fails loudly — there is no CPU fallback.  Image I/O and drawing still need cv2."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by tests/test_gpu_orb.py")
+    with pytest.raises(sfmcore.SfmCoreError, match="no CPU fallback"):
         fm.extract_and_match(np.zeros((8, 8), np.uint8), np.zeros((8, 8), np.uint8))
+    if fm.cv2 is None:
+        with pytest.raises(ImportError, match="OpenCV"):
+            fm.read_img("x.png")
 
 
 def test_dmatch_record():
@@ -126,9 +132,12 @@ def test_graph_npz_roundtrip(tmp_path):
     assert [(a, b) for a, b, _ in g["pair_matches"]] == [tuple(pairs[0]), tuple(pairs[4])]
 
 
-def test_pair_record_and_pipeline_entry_need_cv2():
+def test_pair_record_and_pipeline_entry_need_the_gpu():
+    import torch
     p = fm.Pair(1, 2, [fm.DMatch(0, 1, 0, 3.0)])
     assert (p.img_inx_1, p.img_inx_2, len(p.matches)) == (1, 2, 1)
-    if fm.cv2 is None:
-        with pytest.raises(ImportError):
+    k = fm.KeyPoint(3.0, 4.0, 31.0, 90.0, 1.5, 2)
+    assert k.pt == (3.0, 4.0) and k.octave == 2 and k.class_id == -1
+    if not torch.cuda.is_available():
+        with pytest.raises(sfmcore.SfmCoreError):
             fm.pipeline_pair_matches([np.zeros((8, 8), np.uint8)] * 2)
