@@ -676,8 +676,9 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     SFM_REQUIRE(n_cam > 0 && n_pt >= 0 && n_obs >= 0, "sfm_ba_solve: bad size");
     SFM_REQUIRE(prm->max_iter >= 0 && prm->lambda >= 0.0 && prm->tol >= 0.0,
                 "sfm_ba_solve: max_iter, lambda and tol must be >= 0");
-    SFM_REQUIRE(cam_idx && pt_idx && pt_ptr && cam_ptr && cam_obs && U && V && W && gc && gp && dc &&
-                    dp && info,
+    // per-observation arrays may be NULL without observations, per-point ones without points
+    SFM_REQUIRE(cam_ptr && U && gc && dc && info && (n_obs == 0 || (cam_idx && pt_idx && cam_obs && W)) &&
+                    (n_pt == 0 || (pt_ptr && V && gp && dp)),
                 "sfm_ba_solve: NULL array");
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;

@@ -197,6 +197,8 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
     keeps its pose and the second one translation coordinate (the scale); the intrinsics are
     known, so f and k1 are held too (reconstruction.gauge_mask)."""
     use = rec.registered[timg] & rec.has_point[obs_track]
+    if not use.any():
+        return
     ref, second = rec.gauge
     fixed = reconstruction.gauge_mask(rec.cams, ref=ref, second=second, fix_intrinsics=True)
     tr = obs_track[use]

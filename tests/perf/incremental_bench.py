@@ -25,7 +25,8 @@ def main():
     n_img, n_kp = (a + [50, 2048][len(a):])[:2]
     scene = synth.make_scene(n_img, n_kp, seed=21, k1_range=0.02)
     intr = np.c_[scene["cams"][:, 6:8], scene["pp"]]
-    incremental.reconstruct(scene["desc"][:4], scene["kps"][:4], scene["n_kp"][:4], intr[:4])
+    w = np.linspace(0, n_img - 1, 4).astype(int)          # warm-up on 4 well-separated views
+    incremental.reconstruct(scene["desc"][w], scene["kps"][w], scene["n_kp"][w], intr[w])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rec = incremental.reconstruct(scene["desc"], scene["kps"], scene["n_kp"], intr,

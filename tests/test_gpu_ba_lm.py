@@ -166,3 +166,24 @@ def test_bundle_adjust_gauge_and_known_intrinsics():
     assert hist[-1][0] < 0.1 * L.cost(*args)
     fcams, _, _ = R.bundle_adjust(*args, max_iter=60)
     assert np.abs(fcams[:, 6] - prob["cams"][:, 6]).max() > 1e-6   # the free gauge lets f move
+
+
+def test_solve_without_observations():
+    """An empty problem (no points, no observations; e.g. the incremental driver before any
+    point survives): the solve runs on U / g_c alone, δc = -(U + λ diag U)⁻¹ g_c."""
+    import torch
+    import sfmcore
+    ctx = sfmcore.context(0)
+    f64, i32 = torch.float64, torch.int32
+    U = torch.eye(8, dtype=f64, device="cuda").repeat(2, 1, 1) * 2.0
+    lin = dict(U=U, V=torch.empty((0, 3, 3), dtype=f64, device="cuda"),
+               W=torch.empty((0, 8, 3), dtype=f64, device="cuda"),
+               gc=torch.ones((2, 8), dtype=f64, device="cuda"),
+               gp=torch.empty((0, 3), dtype=f64, device="cuda"))
+    e = torch.empty(0, dtype=i32, device="cuda")
+    cam_ptr = torch.zeros(3, dtype=i32, device="cuda")
+    pt_ptr = torch.zeros(1, dtype=i32, device="cuda")
+    dc, dp, info = ctx.ba_solve(lin, e, e, pt_ptr, cam_ptr, e, 0.5, max_iter=20, tol=1e-12)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(dc.cpu().numpy(), -1.0 / 3.0, rtol=1e-12)
+    assert dp.numel() == 0
