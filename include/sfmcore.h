@@ -101,6 +101,16 @@ int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_
                        int32_t* out_inl_count, int32_t* out_best_h, uint8_t* out_mask,
                        float* out_F, float* out_norm);
 
+/* Diagnostic companion of sfm_ransac_f_batch: the inlier count of EVERY hypothesis (no pruning),
+ * out_counts [n_pairs][n_hyp] i32 (-1: degenerate sample or fewer than 8 matches), computed by the
+ * score kernel of sfm_ransac_f_batch with pruning off; out_norm as above.  The exhaustive parity
+ * tests compare it with the oracle's per-hypothesis counts.
+ */
+int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
+                      const int32_t* pairs, int32_t n_pairs, const int32_t* match_count,
+                      const int32_t* matches, const sfm_ransac_params* prm, int32_t* out_counts,
+                      float* out_norm);
+
 /* ---- verified match graph -------------------------------------------------------------------
  * Replaces the pair_matches list of code/pipeline.py:42-47 (Pair(img_inx_1, img_inx_2, matches)
  * for every non-empty pair) for a batch: rows (pair_base + pair, queryIdx, trainIdx) of the RANSAC

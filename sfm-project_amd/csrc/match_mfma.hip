@@ -534,7 +534,8 @@ __device__ __forceinline__ void mu_top2(int& tb, int& ts, int x, int y) {
 template <int D> constexpr int mu_qb() { return MU_WAVES * Geo<D>::QT * 32; }
 #ifdef MU_CLOCK
 constexpr int MU_CLOCK_SLOTS = 1 << 16;
-__device__ unsigned long long g_mu_clock[4 * MU_CLOCK_SLOTS];
+constexpr int MU_CLOCK_W = 8;  // per block: loop memtime/realtime start+end, entry/exit realtime, HW_ID, XCC_ID
+__device__ unsigned long long g_mu_clock[MU_CLOCK_W * MU_CLOCK_SLOTS];
 #endif
 
 template <int D, bool ROWS>
@@ -552,6 +553,9 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
     extern __shared__ unsigned long long lds_col[];  // [k_pad], dynamic
 
+#ifdef MU_CLOCK
+    const unsigned long long tin = __builtin_amdgcn_s_memrealtime();
+#endif
     const int per_xcd = (int)(gridDim.x >> 3);
     const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
     if (sblk >= n_blk) return;  // block-uniform, before any barrier
@@ -682,8 +686,10 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     {   // stamps to a buffer of their own, read only by sfm_debug_clock_stamps (never an output)
         const unsigned long long t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
         if (tid == 0 && blockIdx.x < MU_CLOCK_SLOTS) {
-            unsigned long long* d = g_mu_clock + 4 * (size_t)blockIdx.x;
-            d[0] = t0c; d[1] = t0r; d[2] = t1c; d[3] = t1r;
+            unsigned long long* d = g_mu_clock + MU_CLOCK_W * (size_t)blockIdx.x;
+            d[0] = t0c; d[1] = t0r; d[2] = t1c; d[3] = t1r; d[4] = tin;
+            d[6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+            d[7] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
         }
     }
 #endif
@@ -699,6 +705,11 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     }
     unsigned long long* dst = colpart + ((size_t)p * n_qblk + qb) * k_pad;
     for (int j = tid; j < k_pad; j += NTHR) dst[j] = lds_col[j];
+#ifdef MU_CLOCK
+    __syncthreads();
+    if (tid == 0 && blockIdx.x < MU_CLOCK_SLOTS)
+        g_mu_clock[MU_CLOCK_W * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // Exact dot product of two D-byte i8 rows (v_dot4_i32_i8).
@@ -1115,7 +1126,7 @@ int sfm_match_hamming_mfma_launch(sfm_ctx* ctx, const uint8_t* desc, const int32
 // Diagnostic build only (tools/build_variant.sh clock -DMU_CLOCK): the per-block (memtime start,
 // realtime start, memtime end, realtime end) stamps of the last mfma_mutual_kernel launch.
 extern "C" int sfm_debug_clock_stamps(unsigned long long* host, int32_t n_blocks) {
-    const size_t n = 4 * (size_t)std::min(n_blocks, MU_CLOCK_SLOTS);
+    const size_t n = MU_CLOCK_W * (size_t)std::min(n_blocks, MU_CLOCK_SLOTS);
     SFM_HIP_CHECK(hipDeviceSynchronize());
     SFM_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mu_clock), n * sizeof(unsigned long long)));
     return SFM_OK;

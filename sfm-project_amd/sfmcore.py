@@ -24,7 +24,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
-            "sfm_ba_fix_params", "sfm_orb_batch"]
+            "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts"]
 
 
 class SfmCoreError(RuntimeError):
@@ -87,6 +87,8 @@ def load_library(path: str = LIB_PATH):
                                       vp, vp, vp]
         L.sfm_ransac_f_batch.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
                                          C.POINTER(RansacParams), vp, vp, vp, vp, vp]
+        L.sfm_ransac_counts.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
+                                        C.POINTER(RansacParams), vp, vp]
         L.sfm_ba_jtj.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp,
                                  vp, vp, vp, vp, vp, vp]
         L.sfm_ba_solve.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -220,6 +222,25 @@ class Context:
                                            _ptr(out["inl_count"]), _ptr(out["best_h"]),
                                            _ptr(out["mask"]), _ptr(out["F"]), _ptr(out["norm"])))
         return out
+
+    def ransac_counts(self, kps, pairs, count, match, n_hyp=4096, seed=42, thr=1.0):
+        """Diagnostic: the inlier count of every hypothesis ([P, n_hyp] i32 device tensor, -1 for
+        degenerate samples / pairs with < 8 matches) and norm [P,6], by the same score path as
+        ransac_batch (sfm_ransac_counts)."""
+        torch = self.torch
+        n_img, k_max, _ = kps.shape
+        P = pairs.shape[0]
+        dev = kps.device
+        if kps.dtype != torch.float32 or not kps.is_contiguous():
+            raise SfmCoreError("ransac_counts: kps must be contiguous float32")
+        counts = torch.empty((P, n_hyp), dtype=torch.int32, device=dev)
+        norm = torch.empty((P, 6), dtype=torch.float32, device=dev)
+        prm = RansacParams(int(n_hyp), 0, float(thr), 0, int(seed))
+        self._bind_stream()
+        _check(self.lib.sfm_ransac_counts(self.handle, _ptr(kps), n_img, k_max, _ptr(pairs), P,
+                                          _ptr(count), _ptr(match), C.byref(prm), _ptr(counts),
+                                          _ptr(norm)))
+        return counts, norm
 
     # ---- verified match graph --------------------------------------------------------------
     def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15,

@@ -43,12 +43,14 @@ def main():
     qb = 512                                      # MU_WAVES (4) x QT (4) x 32 queries per block
     n_blk = len(pairs) * ((K + qb - 1) // qb)
     grid = 8 * ((n_blk + 7) // 8)
-    buf = np.zeros(4 * grid, np.uint64)
+    W = 8
+    buf = np.zeros(W * grid, np.uint64)
     L = sfmcore.load_library()
     L.sfm_debug_clock_stamps.argtypes = [C.c_void_p, C.c_int32]
     assert L.sfm_debug_clock_stamps(buf.ctypes.data_as(C.c_void_p), grid) == 0
-    st = buf.reshape(-1, 4).astype(np.float64)
-    st = st[st[:, 2] > st[:, 0]]
+    raw = buf.reshape(-1, W)
+    raw = raw[raw[:, 2] > raw[:, 0]]
+    st = raw[:, :4].astype(np.float64)
     cyc = st[:, 2] - st[:, 0]
     wall = (st[:, 3] - st[:, 1]) / 100e6
     clk = cyc / wall
@@ -60,6 +62,36 @@ def main():
            "block_cycles_median": float(np.median(cyc)),
            "cycles_per_tile_wave_median": float(np.median(cyc) / tiles),
            "block_us_median": float(np.median(wall) * 1e6)}
+    # whole-block lifetime (entry -> after the colpart store) and the per-CU timeline
+    t_in, t_out = raw[:, 4].astype(np.int64), raw[:, 5].astype(np.int64)
+    l0, l1 = raw[:, 1].astype(np.int64), raw[:, 3].astype(np.int64)
+    cu = ((raw[:, 7].astype(np.int64) & 15) << 8) | ((raw[:, 6].astype(np.int64) >> 8) & 255)
+    life = (t_out - t_in) / 100.0  # us
+    res["block_life_us_median"] = float(np.median(life))
+    res["prologue_us_median"] = float(np.median((l0 - t_in) / 100.0))
+    res["epilogue_us_median"] = float(np.median((t_out - l1) / 100.0))
+    span = (t_out.max() - t_in.min()) / 100.0
+    res["launch_span_us"] = float(span)
+    ucu = np.unique(cu)
+    res["cus_seen"] = int(len(ucu))
+    occ, idle_gap = [], []
+    for c in ucu:
+        m = cu == c
+        occ.append(life[m].sum() / span)
+        a, b = np.sort(t_in[m]), np.sort(t_out[m])
+        # slots: a block starts when another leaves; gaps = entry - the latest exit before it
+        ex = np.sort(t_out[m])
+        for t in a[2:]:
+            k = np.searchsorted(ex, t) - 1
+            if k >= 0:
+                idle_gap.append((t - ex[k]) / 100.0)
+    res["blocks_per_cu_mean"] = float(len(raw) / len(ucu))
+    res["cu_block_occupancy_mean"] = float(np.mean(occ))  # sum of block lifetimes / span (2 = full)
+    res["refill_gap_us_median"] = float(np.median(idle_gap)) if idle_gap else None
+    first = np.sort(t_in)[:512]
+    last = np.sort(t_out)[-512:]
+    res["first_512_entries_spread_us"] = float((first.max() - first.min()) / 100.0)
+    res["last_512_exits_spread_us"] = float((last.max() - last.min()) / 100.0)
     print(json.dumps(res))
 
 

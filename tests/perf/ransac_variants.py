@@ -1,4 +1,5 @@
-"""Times the K2 RANSAC schedules (SFM_RANSAC_MODE 0 ordered, 1 single-pass pruned, 2 unpruned) on
+"""Times the K2 RANSAC schedules (SFM_RANSAC_MODE 0 ordered, 1 single-pass pruned, 2 unpruned,
+3 ordered on the certified f16-MFMA filter; MODES=0,3 selects) on
 the cfg3 workload and checks each against the CPU oracle on a sample of pairs.
 Usage: python tests/perf/ransac_variants.py"""
 import os
@@ -33,7 +34,7 @@ def main():
         M = cnt_np[p]
         ref[p] = O.ransac_f(s["kps"][a][mt_np[p, :M, 0]], s["kps"][b][mt_np[p, :M, 1]], H=4096,
                             seed=42, pa=int(a), pb=int(b))
-    for v in (0, 1, 2):
+    for v in [int(x) for x in os.environ.get("MODES", "0,1,2").split(",")]:
         os.environ["SFM_RANSAC_MODE"] = str(v)
         for _ in range(2):
             out = ctx.ransac_batch(kps, pr, cnt, mt, n_hyp=4096)
