@@ -208,26 +208,10 @@ __device__ __forceinline__ float wave_fixed_sum(float partial) {
 // plane stride per pair: 8 planes of k_pl floats (k_pl multiple of 16: 64-B aligned planes)
 __host__ __device__ __forceinline__ int plane_len(int k_max) { return (k_max + 15) & ~15; }
 
-// ---- operands of the MFMA Sampson filter (DESIGN.md §4.2 "certified MFMA scoring") ------------
-// Every value v enters v_mfma_f32_32x32x16_f16 as an f16 pair v = vh + vl (+ at most 2^-22|v|, or
-// 2^-25 absolute where vl is subnormal; gfx950 keeps f16 subnormals, tools/probe_mfma_f16.hip).
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef float f16v __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ void split16(float v, _Float16& h, _Float16& l) {
-    h = (_Float16)v;
-    l = (_Float16)(v - (float)h);  // v - h is exact in f32
-}
-__device__ __forceinline__ uint4 h8_bits(h8 v) { return __builtin_bit_cast(uint4, v); }
-// Per-pair scale record (mscale[p][MS_W]): [0] 2^-alpha, [1] 2^alpha, [2..5] max |x1'|,|y1'|,|x2'|,
-// |y2'|, [6..14] max |u'_k|, [15] 1 if the pair cannot use the filter (non-finite coordinates).
-constexpr int MS_W = 16;
-constexpr int MREC_CH = 6;  // 16-B operand chunks per match (see ransac_prep_kernel)
-
 __global__ __launch_bounds__(64) void ransac_prep_kernel(
     const float* __restrict__ kps, int k_max, const int32_t* __restrict__ pairs,
     const int32_t* __restrict__ match_count, const int32_t* __restrict__ matches, float thr,
-    float* __restrict__ planes, float* __restrict__ out_norm, int n_pairs, uint4* __restrict__ mrec,
-    float* __restrict__ mscale) {
+    float* __restrict__ planes, float* __restrict__ out_norm) {
     const int p = blockIdx.x, l = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int M = match_count[p];
@@ -288,73 +272,19 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
     const float s2 = (mean2 > 0.0f) ? (1.41421356237309515f / mean2) : 1.0f;
     float k1, k2;
     sampson_scales(s1, s2, thr, k1, k2);
-    float xm = 0.0f;
 #pragma unroll 4
     for (int m = l; m < M; m += 64) {
         const float x1 = (X1[m] - mx1) * s1, y1 = (Y1[m] - my1) * s1;
         const float x2 = (X2[m] - mx2) * s2, y2 = (Y2[m] - my2) * s2;
         X1[m] = x1; Y1[m] = y1; X2[m] = x2; Y2[m] = y2;
-        const float X1s = x1 * k1, Y1s = y1 * k1, X2s = x2 * k2, Y2s = y2 * k2;
-        S[m] = X1s;
-        S[kp + m] = Y1s;
-        S[2 * kp + m] = X2s;
-        S[3 * kp + m] = Y2s;
-        xm = fmaxf(xm, fmaxf(fmaxf(fabsf(X1s), fabsf(Y1s)), fmaxf(fabsf(X2s), fabsf(Y2s))));
+        S[m] = x1 * k1;
+        S[kp + m] = y1 * k1;
+        S[2 * kp + m] = x2 * k2;
+        S[3 * kp + m] = y2 * k2;
     }
     if (l == 0) {
         float* o = out_norm + p * 6;
         o[0] = mx1; o[1] = my1; o[2] = s1; o[3] = mx2; o[4] = my2; o[5] = s2;
-    }
-    if (!mrec) return;
-    // MFMA operand records.  alpha: the scaled coordinates x' = X 2^-alpha stay below 2^6 and the
-    // products u' below 2^12 (f16 range with headroom); scaling by powers of two is exact.
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) xm = fmaxf(xm, __shfl_xor(xm, off, 64));
-    const bool finite = isfinite(xm);
-    int e = 0;
-    if (finite && xm > 0.0f) frexpf(xm, &e);
-    const float sc = ldexpf(1.0f, 6 - e), isc = ldexpf(1.0f, e - 6);
-    float am[13];
-#pragma unroll
-    for (int k = 0; k < 13; ++k) am[k] = 0.0f;
-    const size_t cs = (size_t)n_pairs * kp;  // chunk stride
-    uint4* R = mrec + (size_t)p * kp;
-    for (int m = l; m < M; m += 64) {
-        const float x1 = S[m] * sc, y1 = S[kp + m] * sc, x2 = S[2 * kp + m] * sc,
-                    y2 = S[3 * kp + m] * sc;
-        // u'_k = x2'_i x1'_j (x'_2 = 1), k = 3i + j: the monomials of r = X2^T G X1
-        const float u[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.0f};
-        am[0] = fmaxf(am[0], fabsf(x1)); am[1] = fmaxf(am[1], fabsf(y1));
-        am[2] = fmaxf(am[2], fabsf(x2)); am[3] = fmaxf(am[3], fabsf(y2));
-        _Float16 uh[9], ul[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            am[4 + k] = fmaxf(am[4 + k], fabsf(u[k]));
-            split16(u[k], uh[k], ul[k]);
-        }
-        _Float16 x1h, x1l, y1h, y1l, x2h, x2l, y2h, y2l;
-        split16(x1, x1h, x1l); split16(y1, y1h, y1l);
-        split16(x2, x2h, x2l); split16(y2, y2h, y2l);
-        const _Float16 z = (_Float16)0.0f;
-        // chunk 0/1: lanes 0-31 of the a-forms (x1') and b-forms (x2'): all four hi/lo products
-        R[m] = h8_bits(h8{x1h, x1l, x1h, x1l, y1h, y1l, y1h, y1l});
-        R[cs + m] = h8_bits(h8{x2h, x2l, x2h, x2l, y2h, y2l, y2h, y2l});
-        // chunks 2-5: the r-form, k = 0..4 and 5..8, three products per term [uh, ul, uh]
-        R[2 * cs + m] = h8_bits(h8{uh[0], ul[0], uh[0], uh[1], ul[1], uh[1], uh[2], ul[2]});
-        R[3 * cs + m] = h8_bits(h8{uh[2], uh[3], ul[3], uh[3], uh[4], ul[4], uh[4], z});
-        R[4 * cs + m] = h8_bits(h8{uh[5], ul[5], uh[5], uh[6], ul[6], uh[6], uh[7], ul[7]});
-        R[5 * cs + m] = h8_bits(h8{uh[7], uh[8], ul[8], uh[8], z, z, z, z});
-    }
-#pragma unroll
-    for (int k = 0; k < 13; ++k)
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) am[k] = fmaxf(am[k], __shfl_xor(am[k], off, 64));
-    if (l == 0) {
-        float* o = mscale + (size_t)p * MS_W;
-        o[0] = sc; o[1] = isc;
-#pragma unroll
-        for (int k = 0; k < 13; ++k) o[2 + k] = am[k];
-        o[15] = (finite && isfinite(am[4]) && am[4] < 16384.0f) ? 0.0f : 1.0f;
     }
 }
 
@@ -614,229 +544,6 @@ __global__ __launch_bounds__(256) void ransac_score_kernel(
     if ((threadIdx.x & 63) == 0) atomicMax(&best[p], key);
 }
 
-// ---- certified MFMA scoring (the default score kernel) -------------------------
-//
-// Same contract as ransac_score_kernel: every count is the f32 spec's (sampson_inlier) exactly.
-// Per 32 matches x 32 hypotheses the five forms of the Sampson test, a0 = (G X1)_0, a1, b0 = (G^T X2)_0,
-// b1 and r = X2^T G X1, are v_mfma_f32_32x32x16_f16 products of f16 hi/lo splits of the spec's own
-// f32 operands (a/b forms: four hi/lo products per term, r: nine monomials u'_k = x2'_i x1'_j with
-// three products each, two MFMAs), so the VALU keeps only den = a0^2+a1^2+b0^2+b1^2, P = den - r^2
-// (5 ops) and the decision.  With S the sum of |terms| of a form (bounded per hypothesis from the
-// pair's operand maxima), each form is within Delta = 2^-17 S (+ a subnormal term) of the exact
-// value (split 3*2^-22 S, MFMA accumulation <= 64 * 2^-24 S against 5.2 measured, the spec's own
-// f32 evaluation 2^-21 S).  With delta = 2^-14, |P - e_spec| <= delta_t (den + r^2) + kappa,
-// delta_t = 2.2 delta + 2^-19, kappa = 2.2 (4 Da^2 + Dr^2)(1/delta + 1) (AM-GM on the cross terms);
-// hence sign(P) = sign(e_spec) unless |P| <= 3 delta_t den + 2 kappa (the r^2 > 2 den case is
-// covered by the 2 kappa term since then |P| >= r^2/2).  Such an evaluation is "flagged" and the
-// lane recounts its 16 rows of that tile with the exact f32 spec (sampson_inlier on the planes).
-// All scalings (X 2^-alpha, homogeneous factors, the per-hypothesis power-of-two lambda) are exact
-// and the sign of den - r^2 is invariant under them.
-//
-// Layout: A = matches (lane l: row l%32), B = hypotheses (column l%32), 2 hypothesis tiles (64
-// hypotheses, the same ranks as ransac_score_kernel) per wave; accumulator register r of lane l is
-// match row 8(r/4) + 4(l/32) + r%4.  Pruning per hypothesis tile with the same exact rule.
-constexpr float MF_DELTA = 6.103515625e-05f;  // 2^-14
-__device__ __forceinline__ h8 h8_of(uint4 v) { return __builtin_bit_cast(h8, v); }
-
-struct MfHyp {
-    h8 a0, a1, b0, b1, r1, r2;  // B operands of this lane's half
-    float mu, kap;              // flag iff |P| <= mu*den + kap
-};
-
-__device__ __forceinline__ void mf_hyp_setup(const float G[9], const float* __restrict__ ms, int h,
-                                             float margin_scale, MfHyp& o) {
-    const float sc = ms[0], isc = ms[1];
-    // g''_k = G_k 2^{-alpha n_k} (n_k = homogeneous indices of k = 3i+j), r-form g''_k 2^alpha
-    const int nk[9] = {0, 0, 1, 0, 0, 1, 1, 1, 2};
-    float ga[9], gb[9];
-    float mx = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        ga[k] = nk[k] == 0 ? G[k] : (nk[k] == 1 ? G[k] * sc : (G[k] * sc) * sc);
-        gb[k] = ga[k] * isc;
-        mx = fmaxf(mx, fmaxf(fabsf(ga[k]), fabsf(gb[k])));
-    }
-    const bool bad = !(mx > 0.0f && isfinite(mx)) || ms[15] != 0.0f;
-    int e = 0;
-    if (!bad) frexpf(mx, &e);
-    const float lam = ldexpf(1.0f, 14 - e);  // max |B| in [2^13, 2^14)
-    _Float16 ah[9], al[9], bh[9], bl[9];
-    float sga = 0.0f, sgb = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        ga[k] = bad ? 0.0f : ga[k] * lam;
-        gb[k] = bad ? 0.0f : gb[k] * lam;
-        split16(ga[k], ah[k], al[k]);
-        split16(gb[k], bh[k], bl[k]);
-        sga += fabsf(ga[k]);
-        sgb += fabsf(gb[k]);
-    }
-    const _Float16 z = (_Float16)0.0f;
-    auto form = [&](int k0, int k1, int k2) {  // [g0h g0h g0l g0l g1h g1h g1l g1l | g2h g2l 0 ...]
-        return h == 0 ? h8{ah[k0], ah[k0], al[k0], al[k0], ah[k1], ah[k1], al[k1], al[k1]}
-                      : h8{ah[k2], al[k2], z, z, z, z, z, z};
-    };
-    o.a0 = form(0, 1, 2);
-    o.a1 = form(3, 4, 5);
-    o.b0 = form(0, 3, 6);
-    o.b1 = form(1, 4, 7);
-    o.r1 = h == 0 ? h8{bh[0], bh[0], bl[0], bh[1], bh[1], bl[1], bh[2], bh[2]}
-                  : h8{bl[2], bh[3], bh[3], bl[3], bh[4], bh[4], bl[4], z};
-    o.r2 = h == 0 ? h8{bh[5], bh[5], bl[5], bh[6], bh[6], bl[6], bh[7], bh[7]}
-                  : h8{bl[7], bh[8], bh[8], bl[8], z, z, z, z};
-    // error scale of each form: S = sum |B_k| max|A_k| over the pair's matches
-    const float* am = ms + 2;
-    const float sa0 = fabsf(ga[0]) * am[0] + fabsf(ga[1]) * am[1] + fabsf(ga[2]);
-    const float sa1 = fabsf(ga[3]) * am[0] + fabsf(ga[4]) * am[1] + fabsf(ga[5]);
-    const float sb0 = fabsf(ga[0]) * am[2] + fabsf(ga[3]) * am[3] + fabsf(ga[6]);
-    const float sb1 = fabsf(ga[1]) * am[2] + fabsf(ga[4]) * am[3] + fabsf(ga[7]);
-    float sr = 0.0f, sau = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        sr += fabsf(gb[k]) * am[4 + k];
-        sau += am[4 + k];
-    }
-    const float sa = fmaxf(fmaxf(sa0, sa1), fmaxf(sb0, sb1));
-    const float c17 = 7.62939453125e-06f, c22 = 2.384185791015625e-07f;  // 2^-17, 2^-22
-    const float da = c17 * sa + c22 * (sga + am[0] + am[1] + am[2] + am[3] + 1.0f);
-    const float dr = c17 * sr + c22 * (sgb + sau);
-    const float kappa = 2.2f * (4.0f * da * da + dr * dr) * (1.0f / MF_DELTA + 1.0f);
-    const float dt = 2.2f * MF_DELTA + 1.9073486328125e-06f;  // + 2^-19
-    o.mu = 3.0f * dt * margin_scale;
-    o.kap = bad ? INFINITY : 2.0f * kappa * margin_scale;
-}
-
-// exact f32 spec recount of this lane's 16 rows of the tile at m0 (the flagged fix-up)
-__device__ __forceinline__ int mf_exact_rows(const float* __restrict__ gt, int n_hyp, const float* __restrict__ S,
-                                             int kp, int m0, int h, int M) {
-    float G[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) G[i] = gt[(size_t)i * n_hyp];
-    int c = 0;
-#pragma unroll 1
-    for (int r = 0; r < 16; ++r) {
-        const int m = m0 + 8 * (r >> 2) + 4 * h + (r & 3);
-        if (m < M) c += sampson_inlier(G, S[m], S[kp + m], S[2 * kp + m], S[3 * kp + m]);
-    }
-    return c;
-}
-
-// COUNTS: no pruning, every hypothesis's count to out_counts[p][h] (sfm_ransac_counts)
-template <bool COUNTS>
-__global__ __launch_bounds__(256, 2) void ransac_score_mfma_kernel(
-    int n_pairs, int k_max, const int32_t* __restrict__ match_count, const float* __restrict__ planes,
-    int n_hyp, const float* __restrict__ hypG, const int32_t* __restrict__ prev,
-    const uint16_t* __restrict__ order, const uint4* __restrict__ mrec, const float* __restrict__ mscale,
-    float margin_scale, unsigned long long* __restrict__ best, int32_t* __restrict__ out_counts) {
-    int p, hb;
-    if (!xcd_pair_block(n_pairs, p, hb)) return;
-    const int M = match_count[p];
-    if (M < 8) return;  // block-uniform
-    const int kp = plane_len(k_max);
-    const float* S = planes + (size_t)p * 8 * kp + 4 * kp;
-    const float* ms = mscale + (size_t)p * MS_W;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-    uint32_t hid[2];
-    int pc[2], cnt[2];
-    MfHyp hy[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        hid[t] = order[(size_t)p * n_hyp + hb * 256 + wave * 64 + t * 32 + c32];
-        const float* gt = hypG + (size_t)p * 9 * n_hyp + hid[t];
-        float G[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) G[i] = gt[(size_t)i * n_hyp];
-        pc[t] = prev[(size_t)p * n_hyp + hid[t]];
-        cnt[t] = h == 0 ? max(pc[t], 0) : 0;  // the two halves' counts are summed
-        mf_hyp_setup(G, ms, h, margin_scale, hy[t]);
-    }
-    bool alive[2] = {true, true};
-    const size_t cs = (size_t)n_pairs * kp;
-    const uint4* R = mrec + (size_t)p * kp;
-    const h8 one1 = h8{(_Float16)1.0f, (_Float16)1.0f, (_Float16)0.0f, (_Float16)0.0f,
-                       (_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f};
-    const f16v zero = {};
-    unsigned long long bk = 0;
-#pragma unroll 1
-    for (int m0 = PV; m0 < M; m0 += 32) {
-        const int i = min(m0 + c32, M - 1);
-        const h8 ax1 = h == 0 ? h8_of(R[i]) : one1;
-        const h8 ax2 = h == 0 ? h8_of(R[cs + i]) : one1;
-        const h8 au1 = h8_of(R[(2 + h) * cs + i]);
-        const h8 au2 = h8_of(R[(4 + h) * cs + i]);
-        const bool full = m0 + 32 <= M;
-        if (!COUNTS && ((m0 - PV) & 63) == 0)  // bound for the check at the end of these 64 matches
-            bk = __hip_atomic_load(best + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            if (!alive[t]) continue;
-            const f16v A0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax1, hy[t].a0, zero, 0, 0, 0);
-            const f16v A1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax1, hy[t].a1, zero, 0, 0, 0);
-            const f16v B0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax2, hy[t].b0, zero, 0, 0, 0);
-            const f16v B1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax2, hy[t].b1, zero, 0, 0, 0);
-            f16v Rr = __builtin_amdgcn_mfma_f32_32x32x16_f16(au1, hy[t].r1, zero, 0, 0, 0);
-            Rr = __builtin_amdgcn_mfma_f32_32x32x16_f16(au2, hy[t].r2, Rr, 0, 0, 0);
-            const int c0 = cnt[t];
-            int ct = 0;
-            bool flag = false;
-            if (full) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float den = fmaf(A0[r], A0[r], fmaf(A1[r], A1[r], fmaf(B0[r], B0[r], B1[r] * B1[r])));
-                    const float P = fmaf(-Rr[r], Rr[r], den);
-                    ct += P > 0.0f ? 1 : 0;
-                    flag = flag || !(fabsf(P) > fmaf(hy[t].mu, den, hy[t].kap));
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const bool v = m0 + 8 * (r >> 2) + 4 * h + (r & 3) < M;
-                    const float den = fmaf(A0[r], A0[r], fmaf(A1[r], A1[r], fmaf(B0[r], B0[r], B1[r] * B1[r])));
-                    const float P = fmaf(-Rr[r], Rr[r], den);
-                    ct += (v && P > 0.0f) ? 1 : 0;
-                    flag = flag || (v && !(fabsf(P) > fmaf(hy[t].mu, den, hy[t].kap)));
-                }
-            }
-            cnt[t] = c0 + ct;
-            if (__ballot(flag) != 0ull) {  // rare: exact recount of the flagged lanes' rows
-                if (flag)
-                    cnt[t] = c0 + mf_exact_rows(hypG + (size_t)p * 9 * n_hyp + hid[t], n_hyp, S, kp,
-                                                m0, h, M);
-            }
-        }
-        if (!COUNTS && ((m0 + 32 - PV) & 63) == 0 && m0 + 32 < M) {
-            const int bound = (int)(bk >> 32) - 1;
-            const int rem = M - m0 - 32;
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                if (!alive[t]) continue;
-                const int tot = cnt[t] + __shfl_xor(cnt[t], 32, 64);
-                if (__all(tot + rem < bound)) alive[t] = false;
-            }
-            if (!alive[0] && !alive[1]) return;  // wave-uniform
-        }
-    }
-    unsigned long long key = 0;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        int tot = cnt[t] + __shfl_xor(cnt[t], 32, 64);
-        if (pc[t] < 0) tot = -1;
-        if (COUNTS) {
-            if (h == 0) out_counts[(size_t)p * n_hyp + hid[t]] = tot;
-        } else if (alive[t]) {
-            const unsigned long long k = ((unsigned long long)(unsigned)(tot + 1) << 32) | (0xFFFFFFFFu - hid[t]);
-            key = k > key ? k : key;
-        }
-    }
-    if (COUNTS) return;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const unsigned long long o = __shfl_xor(key, off, 64);
-        key = o > key ? o : key;
-    }
-    if (lane == 0 && key != 0ull) atomicMax(&best[p], key);
-}
-
 __global__ __launch_bounds__(256) void ransac_final_kernel(
     int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
     const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
@@ -892,19 +599,11 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
 // SFM_RANSAC_MODE (same results in every mode; for measuring the schedules):
 //   0 ordered (fit + preview, per-pair ordering, ordered pruned scoring) — default
 //   1 single pass with pruning, 2 single pass without pruning (lane per hypothesis)
-//   3 ordered, scored by the certified f16-MFMA filter (ransac_score_mfma_kernel): exact, but
-//     slower than mode 0, kept for measurement
-// SFM_RANSAC_MFMA_MARGIN (float >= 1, default 1): widens the certified margin (tests: forces the
-// exact fix-up path).
+// (A certified f16-MFMA scorer, exact but 4.5x slower, was mode 3 at commit 8912e00)
 static int ransac_mode() {
     const char* e = getenv("SFM_RANSAC_MODE");
     const int v = e ? atoi(e) : 0;
-    return (v < 0 || v > 3) ? 0 : v;
-}
-static float mfma_margin() {
-    const char* e = getenv("SFM_RANSAC_MFMA_MARGIN");
-    const float v = e ? (float)atof(e) : 1.0f;
-    return v >= 1.0f ? v : 1.0f;
+    return (v < 0 || v > 2) ? 0 : v;
 }
 
 namespace {
@@ -914,27 +613,21 @@ struct RansacWs {
     float* hypG;
     int32_t* prev;
     uint16_t* order;
-    uint4* mrec;
-    float* mscale;
 };
-// Workspace of one batch.  ordered: hypothesis table, previews, order; mfma: operand records.
-int ransac_ws(sfm_ctx* ctx, int n_pairs, int kp, int H, bool ordered, bool mfma, RansacWs& w) {
+// Workspace of one batch.  ordered: hypothesis table, previews, order.
+int ransac_ws(sfm_ctx* ctx, int n_pairs, int kp, int H, bool ordered, RansacWs& w) {
     const size_t plb = sfm::align_up((size_t)n_pairs * 8 * kp * sizeof(float), 256);
     const size_t bb = sfm::align_up((size_t)n_pairs * sizeof(unsigned long long), 256);
     const size_t gb = ordered ? sfm::align_up((size_t)n_pairs * 9 * H * sizeof(float), 256) : 0;
     const size_t vb = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(int32_t), 256) : 0;
     const size_t ob = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(uint16_t), 256) : 0;
-    const size_t rb = mfma ? sfm::align_up((size_t)MREC_CH * n_pairs * kp * sizeof(uint4), 256) : 0;
-    const size_t sb = mfma ? sfm::align_up((size_t)n_pairs * MS_W * sizeof(float), 256) : 0;
-    char* ws = (char*)sfm::workspace(ctx, plb + bb + gb + vb + ob + rb + sb + 1024);
+    char* ws = (char*)sfm::workspace(ctx, plb + bb + gb + vb + ob + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     w.planes = (float*)ws;
     w.best = (unsigned long long*)(ws + plb);
     w.hypG = (float*)(ws + plb + bb);
     w.prev = (int32_t*)(ws + plb + bb + gb);
     w.order = (uint16_t*)(ws + plb + bb + gb + vb);
-    w.mrec = mfma ? (uint4*)(ws + plb + bb + gb + vb + ob) : nullptr;
-    w.mscale = mfma ? (float*)(ws + plb + bb + gb + vb + ob + rb) : nullptr;
     return SFM_OK;
 }
 }  // namespace
@@ -964,15 +657,14 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
     const int kp = plane_len(std::max(k_max, 1));
     const int H = prm->n_hyp;
     const int mode = ransac_mode();
-    const bool ordered = mode == 0 || mode == 3, mfma = mode == 3;
+    const bool ordered = mode == 0;
     SFM_REQUIRE(!ordered || H <= 65536, "sfm_ransac_f_batch: n_hyp > 65536");
     RansacWs w;
-    const int rc = ransac_ws(ctx, n_pairs, kp, H, ordered, mfma, w);
+    const int rc = ransac_ws(ctx, n_pairs, kp, H, ordered, w);
     if (rc != SFM_OK) return rc;
     SFM_HIP_CHECK(hipMemsetAsync(w.best, 0, (size_t)n_pairs * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(ransac_prep_kernel, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
-                       match_count, matches, prm->thr, w.planes, out_norm, n_pairs, w.mrec,
-                       w.mscale);
+                       match_count, matches, prm->thr, w.planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 grid(n_pairs, H / 256);
     if (ordered) {
@@ -983,13 +675,8 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
         hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                            w.prev, w.order);
         SFM_HIP_CHECK(hipGetLastError());
-        if (mfma)
-            hipLaunchKernelGGL(ransac_score_mfma_kernel<false>, xgrid, dim3(256), 0, st, n_pairs,
-                               k_max, match_count, w.planes, H, w.hypG, w.prev, w.order, w.mrec,
-                               w.mscale, mfma_margin(), w.best, (int32_t*)nullptr);
-        else
-            hipLaunchKernelGGL(ransac_score_kernel<true>, xgrid, dim3(256), 0, st, n_pairs, k_max,
-                               match_count, w.planes, H, w.hypG, w.prev, w.order, w.best);
+        hipLaunchKernelGGL(ransac_score_kernel<true>, xgrid, dim3(256), 0, st, n_pairs, k_max,
+                           match_count, w.planes, H, w.hypG, w.prev, w.order, w.best);
     } else if (mode == 1) {
         hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
                            match_count, w.planes, out_norm, prm->seed, prm->thr, w.best);
@@ -1016,15 +703,13 @@ extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, 
     hipStream_t st = ctx->stream;
     const int kp = plane_len(std::max(k_max, 1));
     const int H = prm->n_hyp;
-    const bool mfma = ransac_mode() == 3;
     RansacWs w;
-    const int rc = ransac_ws(ctx, n_pairs, kp, H, true, mfma, w);
+    const int rc = ransac_ws(ctx, n_pairs, kp, H, true, w);
     if (rc != SFM_OK) return rc;
     // pairs with fewer than 8 matches: every count -1
     SFM_HIP_CHECK(hipMemsetAsync(out_counts, 0xFF, (size_t)n_pairs * H * sizeof(int32_t), st));
     hipLaunchKernelGGL(ransac_prep_kernel, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
-                       match_count, matches, prm->thr, w.planes, out_norm, n_pairs, w.mrec,
-                       w.mscale);
+                       match_count, matches, prm->thr, w.planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 xgrid(xcd_grid(n_pairs, H / 256));
     hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
@@ -1033,14 +718,8 @@ extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, 
     hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                        w.prev, w.order);
     SFM_HIP_CHECK(hipGetLastError());
-    if (mfma)
-        hipLaunchKernelGGL(ransac_score_mfma_kernel<true>, xgrid, dim3(256), 0, st, n_pairs, k_max,
-                           match_count, w.planes, H, w.hypG, w.prev, w.order, w.mrec, w.mscale,
-                           mfma_margin(), w.best, out_counts);
-    else
-        hipLaunchKernelGGL((ransac_score_kernel<false, true>), xgrid, dim3(256), 0, st, n_pairs,
-                           k_max, match_count, w.planes, H, w.hypG, w.prev, w.order, w.best,
-                           out_counts);
+    hipLaunchKernelGGL((ransac_score_kernel<false, true>), xgrid, dim3(256), 0, st, n_pairs, k_max,
+                       match_count, w.planes, H, w.hypG, w.prev, w.order, w.best, out_counts);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }

@@ -1,5 +1,5 @@
-"""Times the K2 RANSAC schedules (SFM_RANSAC_MODE 0 ordered, 1 single-pass pruned, 2 unpruned,
-3 ordered on the certified f16-MFMA filter; MODES=0,3 selects) on
+"""Times the K2 RANSAC schedules (SFM_RANSAC_MODE 0 ordered, 1 single-pass pruned, 2 unpruned;
+MODES=0,1 selects) on
 the cfg3 workload and checks each against the CPU oracle on a sample of pairs.
 Usage: python tests/perf/ransac_variants.py"""
 import os

@@ -124,16 +124,15 @@ def test_ransac_preview_boundaries(ctx, M):
 
 
 def test_ransac_schedules_agree(ctx):
-    """The K2 schedules (ordered on the certified MFMA filter, single-pass pruned, unpruned, ordered
-    on the VALU scorer; SFM_RANSAC_MODE) differ only in which work is skipped and how decisions
-    are certified: every output must be identical."""
+    """The three K2 schedules (ordered, single-pass pruned, unpruned; SFM_RANSAC_MODE) differ only
+    in which work is skipped: every output must be identical."""
     import os
     s = synth.make_scene(8, 1024, seed=12)
     pairs = synth.unordered_pairs(8)
     outs = []
     old = os.environ.get("SFM_RANSAC_MODE")
     try:
-        for mode in ("0", "1", "2", "3"):
+        for mode in ("0", "1", "2"):
             os.environ["SFM_RANSAC_MODE"] = mode
             outs.append(_run(ctx, s, pairs, H=1024))
     finally:
@@ -149,37 +148,18 @@ def test_ransac_schedules_agree(ctx):
             np.testing.assert_array_equal(o["mask"][p, :cnt[p]], outs[0][2]["mask"][p, :cnt[p]])
 
 
-def _env(name, value):
-    import os
-    old = os.environ.get(name)
-    if value is None:
-        os.environ.pop(name, None)
-    else:
-        os.environ[name] = value
-    return old
-
-
-@pytest.mark.parametrize("thr,mode,margin", [(1.0, None, None), (4.0, None, None),
-                                             (0.25, None, None), (1.0, "3", None),
-                                             (4.0, "3", None), (1.0, "3", "1e6")])
-def test_ransac_counts_every_hypothesis(ctx, thr, mode, margin):
+@pytest.mark.parametrize("thr", [1.0, 4.0, 0.25])
+def test_ransac_counts_every_hypothesis(ctx, thr):
     """EVERY hypothesis gets the f32 spec's count (sfm_ransac_counts: the score kernel without
-    pruning), not only the winner — on the default VALU scorer and on the certified f16-MFMA
-    filter (SFM_RANSAC_MODE=3); margin=1e6 widens its certified band so that most decisions take
-    the exact fix-up path (SFM_RANSAC_MFMA_MARGIN)."""
+    pruning), not only the winner."""
     import torch
     s = synth.make_scene(6, 1024, seed=77)
     pairs = synth.unordered_pairs(6)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     pr = T(pairs)
     cnt, mt, _ = ctx.match_batch(T(s["desc"]), T(s["n_kp"]), pr, ratio=(4, 5))
-    old = _env("SFM_RANSAC_MFMA_MARGIN", margin), _env("SFM_RANSAC_MODE", mode)
-    try:
-        counts, norm = ctx.ransac_counts(T(s["kps"]), pr, cnt, mt, n_hyp=512, thr=thr)
-        torch.cuda.synchronize()
-    finally:
-        _env("SFM_RANSAC_MFMA_MARGIN", old[0])
-        _env("SFM_RANSAC_MODE", old[1])
+    counts, norm = ctx.ransac_counts(T(s["kps"]), pr, cnt, mt, n_hyp=512, thr=thr)
+    torch.cuda.synchronize()
     counts, cnt, mt = counts.cpu().numpy(), cnt.cpu().numpy(), mt.cpu().numpy()
     for p, (a, b) in enumerate(pairs):
         M = cnt[p]
@@ -188,11 +168,9 @@ def test_ransac_counts_every_hypothesis(ctx, thr, mode, margin):
         np.testing.assert_array_equal(counts[p], ref, err_msg=f"pair {p} (M={M})")
 
 
-@pytest.mark.parametrize("mode", [None, "3"])
-def test_ransac_counts_k4096_and_tails(ctx, mode):
-    """cfg4-sized pairs (K = 4096, ~1000+ tentative matches) and match counts around the preview,
-    the 16-match VALU chunks and the 32-row MFMA tiles: every hypothesis count equals the
-    oracle's."""
+def test_ransac_counts_k4096_and_tails(ctx):
+    """cfg4-sized pairs (K = 4096, ~1000+ tentative matches) and match counts around the 64-match
+    preview and the 16-match scoring chunks: every hypothesis count equals the oracle's."""
     import torch
     s = synth.make_scene(3, 4096, seed=5)
     pairs = synth.unordered_pairs(3)
@@ -200,18 +178,14 @@ def test_ransac_counts_k4096_and_tails(ctx, mode):
     pr = T(pairs)
     cnt, mt, _ = ctx.match_batch(T(s["desc"]), T(s["n_kp"]), pr, ratio=(4, 5))
     cnt_h, mt_h = cnt.cpu().numpy(), mt.cpu().numpy()
-    # truncated copies of pair 0 around the preview (64), the VALU chunks (16) and MFMA tiles (32)
+    # truncated copies of pair 0 around the preview (64) and the scoring chunks (16)
     Ms = [9, 64, 65, 79, 80, 95, 96, 97, 129, 161, 200]
     P = len(pairs) + len(Ms)
     pairs2 = np.concatenate([pairs, np.repeat(pairs[:1], len(Ms), 0)]).astype(np.int32)
     cnt2 = np.concatenate([cnt_h, np.minimum(Ms, cnt_h[0])]).astype(np.int32)
     mt2 = np.concatenate([mt_h, np.repeat(mt_h[:1], len(Ms), 0)])
-    old = _env("SFM_RANSAC_MODE", mode)
-    try:
-        counts, _ = ctx.ransac_counts(T(s["kps"]), T(pairs2), T(cnt2), T(mt2), n_hyp=256)
-        counts = counts.cpu().numpy()
-    finally:
-        _env("SFM_RANSAC_MODE", old)
+    counts, _ = ctx.ransac_counts(T(s["kps"]), T(pairs2), T(cnt2), T(mt2), n_hyp=256)
+    counts = counts.cpu().numpy()
     for p in range(P):
         a, b = pairs2[p]
         M = cnt2[p]
