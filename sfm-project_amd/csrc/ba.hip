@@ -2,17 +2,17 @@
 // DESIGN.md §4.3).  Fills the empty reference module code/3d_reconstruction.py.
 //
 // fp64 throughout.  Deterministic (no float atomics): every accumulation has a fixed order.
-// Two launches:
-//   ba_jtj_kernel      camera blocks first (block per (camera, split): J_c recomputed from the
-//                      camera's rotation — computed once per block — over a contiguous share of
-//                      the camera's observations (cam_ptr/cam_obs CSR), fixed lane-strided order
-//                      + shuffle tree -> U_c, g_c), then observation blocks (thread per
-//                      observation, enough waves to stream HBM: residual, J_c (2x8), J_p (2x3) ->
-//                      res, W = w J_c^T J_p staged through LDS for coalesced stores; V_p, g_p by a
-//                      segmented scan of the point terms across the wave (points are point-major
-//                      contiguous), boundary-cut segments to head/tail records).  The two halves
-//                      are independent, so the latency-bound camera reduction runs underneath the
-//                      observation stream.
+// Kernels:
+//   ba_jtj_kernel      camera waves first (wave per (camera, split), four per block: J_c
+//                      recomputed from the camera's rotation — computed once per wave — over a
+//                      contiguous share of the camera's observations (cam_ptr/cam_obs CSR), fixed
+//                      lane-strided order + shuffle tree -> U_c, g_c), then observation blocks
+//                      (thread per observation, enough waves to stream HBM: residual, J_c (2x8),
+//                      J_p (2x3) -> res, W = w J_c^T J_p staged through LDS for coalesced stores;
+//                      V_p, g_p by a segmented scan of the point terms across the wave (points are
+//                      point-major contiguous), boundary-cut segments to head/tail records.  The
+//                      two halves are independent, so the latency-bound camera reduction runs
+//                      underneath the observation stream.
 //   ba_finish_kernel   points spanning waves, empty points, the cost;
 //   ba_final_kernel    camera split sums (only with fewer than 256 cameras).
 // Algorithmic HBM traffic ~300 B/observation; this is an HBM-bound stage.
@@ -82,8 +82,11 @@ __device__ __forceinline__ void linearize(const double (&R)[9], const double* __
 
 constexpr int NV = 10;      // per-observation point terms: V upper triangle (6), g_p (3), 0.5 rho
 constexpr int NU = 36 + 8;  // upper triangle of U_c (8x8) + g_c
-constexpr int SPLIT_TARGET = 256;  // camera blocks wanted (splits per camera = this / n_cam); more blocks only
-                                   // add reduction work (measured at 500 cameras, merged launch:
+#ifndef CAM_MLP
+#define CAM_MLP 4  // observations whose gathers a camera-wave lane keeps in flight
+#endif
+constexpr int SPLIT_TARGET = 256;  // camera waves wanted (splits per camera = this / n_cam); more only
+                                   // add reduction work (block-per-camera version at 500 cameras:
                                    // 2 splits 90 us, 4 splits 113 us vs 1 split 69 us)
 
 __device__ __forceinline__ void write_point(double* __restrict__ V, double* __restrict__ gp, int p,
@@ -101,11 +104,13 @@ __device__ __forceinline__ void write_point(double* __restrict__ V, double* __re
 // Points whose observations lie inside one wave are written here; the segments cut by a wave
 // boundary go to head/tail records that the finish blocks combine.  The cost (sum of rho/2)
 // is reduced per wave.  All orders are fixed: deterministic.
-// W (192 B per observation) leaves through LDS: each lane writes its 24 doubles to a padded
-// per-wave image (row stride 25 doubles: conflict-free ds_write_b64), then the wave stores its
-// 12 KB block with 16-B lane-contiguous stores (1 KB per instruction) instead of 12 stores of
-// 16-B pieces at a 192-B lane stride.
-constexpr int WROW = 25;  // doubles per staged W row (24 + 1 pad)
+// W (192 B per observation) leaves through LDS in two halves of 12 doubles: each lane writes its
+// half row to a padded per-wave image (row stride 13 doubles: conflict-free ds_write_b64), then
+// the wave stores the half rows with 16-B lane-contiguous stores (96-B runs) instead of 12 stores
+// of 16-B pieces at a 192-B lane stride.  Half images keep the block at 26 KB of LDS (six blocks
+// per CU at the kernel's 78 VGPRs).
+constexpr int WHALF = 12;           // doubles per staged half row
+constexpr int WROW = WHALF + 1;     // + 1 pad
 constexpr int OBS_LDS = 64 * WROW;  // doubles per wave
 
 __device__ __forceinline__ void obs_block(
@@ -114,8 +119,9 @@ __device__ __forceinline__ void obs_block(
     const int32_t* __restrict__ pt_idx, const int32_t* __restrict__ pt_ptr,
     const double* __restrict__ uv, double loss_s, double* __restrict__ W,
     double* __restrict__ res, double* __restrict__ V, double* __restrict__ gp,
-    double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_wave,
+    double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_blk,
     double* __restrict__ lds) {
+    __shared__ double cred[4];
     const int o = ob * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const int wv = o >> 6;  // global wave index (blocks are whole waves)
@@ -125,6 +131,7 @@ __device__ __forceinline__ void obs_block(
     double t[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) t[k] = 0.0;
+    ObsLin Lw;
     if (valid) {
         const int c = cam_idx[o];
         p = pt_idx[o];
@@ -136,12 +143,7 @@ __device__ __forceinline__ void obs_block(
         ObsLin L;
         linearize(R, cam, pp + 2 * (size_t)c, X, z.x, z.y, loss_s, true, L);
         *(double2*)(res + 2 * (size_t)o) = make_double2(L.r[0], L.r[1]);
-        double* wr = wimg + lane * WROW;
-#pragma unroll
-        for (int q = 0; q < 24; ++q) {
-            const int i = q / 3, j = q % 3;
-            wr[q] = L.w * (L.Jc[i] * L.Jp[j] + L.Jc[8 + i] * L.Jp[3 + j]);
-        }
+        Lw = L;
         int k = 0;
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -151,24 +153,42 @@ __device__ __forceinline__ void obs_block(
         for (int i = 0; i < 3; ++i) t[6 + i] = L.w * (L.Jp[i] * L.r[0] + L.Jp[3 + i] * L.r[1]);
         t[9] = 0.5 * L.rho;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     {   // the wave's W block: 64 rows x 24 doubles, contiguous in W from observation wv*64
         const int nrow = min(64, n_obs - (wv << 6));
         double2* Wo = (double2*)(W + 24 * ((size_t)wv << 6));
+        double* wr = wimg + lane * WROW;
 #pragma unroll
-        for (int q = 0; q < 12; ++q) {
-            const int e = q * 64 + lane;          // double pair e of the block
-            const int row = e / 12, col = 2 * (e - 12 * row);
-            if (row < nrow) Wo[e] = make_double2(wimg[row * WROW + col], wimg[row * WROW + col + 1]);
+        for (int hf = 0; hf < 2; ++hf) {
+            if (valid) {
+#pragma unroll
+                for (int k = 0; k < WHALF; ++k) {
+                    const int q = WHALF * hf + k, i = q / 3, j = q % 3;
+                    wr[k] = Lw.w * (Lw.Jc[i] * Lw.Jp[j] + Lw.Jc[8 + i] * Lw.Jp[3 + j]);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const int e = q * 64 + lane;  // double pair e of the half block
+                const int row = e / 6, col = 2 * (e - 6 * row);
+                if (row < nrow)
+                    Wo[12 * row + 6 * hf + col / 2] =
+                        make_double2(wimg[row * WROW + col], wimg[row * WROW + col + 1]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
-    // cost: plain fixed-order wave sum, one entry per wave
+    // cost: fixed-order wave sums, then the block's four in order: one entry per block
     double cw = t[9];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) cw += __shfl_down(cw, off, 64);
-    if (lane == 0) cost_wave[wv] = cw;
+    if (lane == 0) cred[threadIdx.x >> 6] = cw;
+    __syncthreads();
+    if (threadIdx.x == 0) cost_blk[ob] = ((cred[0] + cred[1]) + cred[2]) + cred[3];
     // segmented inclusive scan over runs of equal point id (contiguous by construction)
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -199,39 +219,49 @@ __device__ __forceinline__ void obs_block(
     }
 }
 
-// Block (camera c, split s): fixed-order partial U_c / g_c over a contiguous share of the
-// camera's observations (J_c recomputed from the camera's rotation, computed once per block:
-// cheaper than storing J_c, HBM is the bound) — written directly when splits == 1, else as
-// partials for ba_final_kernel.
-__device__ __forceinline__ void camera_block(
-    int b, const double* __restrict__ cams, const double* __restrict__ pp,
+// Wave (camera c, split s): fixed-order partial U_c / g_c over a contiguous share of the camera's
+// observations (J_c recomputed from the camera's rotation, computed once per wave: cheaper than
+// storing J_c, HBM is the bound), lane-strided order + shuffle tree — written directly when
+// splits == 1, else as partials for ba_final_kernel.  One camera per WAVE (four per block): the
+// camera work holds a quarter of the block slots it held as block-per-camera, so the observation
+// blocks of the same launch stream underneath it from the start.
+__device__ __forceinline__ void camera_wave(
+    int cw, const double* __restrict__ cams, const double* __restrict__ pp,
     const double* __restrict__ pts, const int32_t* __restrict__ pt_idx,
     const double* __restrict__ uv, const int32_t* __restrict__ cam_ptr,
     const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
-    double* __restrict__ U, double* __restrict__ gc, double* __restrict__ lds) {
-    double (*red)[NU] = (double (*)[NU])lds;  // [4][NU]
-    const int tid = threadIdx.x;
-    const int c = b / splits, s = b - c * splits;
+    double* __restrict__ U, double* __restrict__ gc) {
+    const int lane = threadIdx.x & 63;
+    const int c = cw / splits, s = cw - c * splits;
     double acc[NU];
 #pragma unroll
     for (int i = 0; i < NU; ++i) acc[i] = 0.0;
     const double* cam = cams + 8 * (size_t)c;
     double R[9];
+#ifdef BA_ABL_NOROT  // ablation (timing only)
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+#else
     rotmat(cam[0], cam[1], cam[2], R);
+#endif
     const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
     const int len = (c1 - c0 + splits - 1) / splits;
     const int e0 = c0 + s * len, e1 = min(c1, e0 + len);
-    // four observations per step: the dependent gathers (cam_obs -> pt_idx -> point, uv) of all
-    // four are issued before any is used (memory-level parallelism; the blocks are latency-bound)
-    for (int e = e0 + tid; e < e1; e += 4 * 256) {
-        int o[4], pi[4];
-        double X[4][3], u[4], v[4];
+    // CAM_MLP observations per step: the dependent gathers (cam_obs -> pt_idx -> point, uv) of
+    // all of them are issued before any is used (memory-level parallelism; latency-bound waves)
+    for (int e = e0 + lane; e < e1; e += CAM_MLP * 64) {
+        int o[CAM_MLP], pi[CAM_MLP];
+        double X[CAM_MLP][3], u[CAM_MLP], v[CAM_MLP];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = (e + q * 256 < e1) ? cam_obs[e + q * 256] : -1;
+        for (int q = 0; q < CAM_MLP; ++q) o[q] = (e + q * 64 < e1) ? cam_obs[e + q * 64] : -1;
+#ifdef BA_ABL_NOGATHER  // ablation (timing only): observation data from the camera-major position
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pi[q] = o[q] >= 0 ? pt_idx[o[q]] : 0;
+        for (int q = 0; q < CAM_MLP; ++q) { pi[q] = (e + q * 64) % 100000; o[q] = o[q] >= 0 ? e + q * 64 : -1; }
+#else
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < CAM_MLP; ++q) pi[q] = o[q] >= 0 ? pt_idx[o[q]] : 0;
+#endif
+#pragma unroll
+        for (int q = 0; q < CAM_MLP; ++q) {
             const int oo = o[q] >= 0 ? o[q] : 0;
             X[q][0] = pts[3 * (size_t)pi[q]];
             X[q][1] = pts[3 * (size_t)pi[q] + 1];
@@ -240,7 +270,7 @@ __device__ __forceinline__ void camera_block(
             v[q] = uv[2 * (size_t)oo + 1];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < CAM_MLP; ++q) {
             if (o[q] < 0) break;
             ObsLin L;
             linearize(R, cam, pp + 2 * (size_t)c, X[q], u[q], v[q], loss_s, false, L);
@@ -254,6 +284,7 @@ __device__ __forceinline__ void camera_block(
             for (int i = 0; i < 8; ++i) acc[36 + i] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
         }
     }
+#ifndef BA_ABL_NORED  // ablation (timing only): no cross-lane reduction
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
         double v = acc[i];
@@ -261,77 +292,86 @@ __device__ __forceinline__ void camera_block(
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
         acc[i] = v;
     }
-    if ((tid & 63) == 0) {
+#endif
+    if (lane != 0) return;
+    if (splits > 1) {
+        double* o = part + ((size_t)c * splits + s) * NU;
 #pragma unroll
-        for (int i = 0; i < NU; ++i) red[tid >> 6][i] = acc[i];
+        for (int i = 0; i < NU; ++i) o[i] = acc[i];
+        return;
     }
-    __syncthreads();
-    if (tid < NU) {
-        const double v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-        if (splits > 1) {
-            part[((size_t)c * splits + s) * NU + tid] = v;
-        } else if (tid >= 36) {
-            gc[8 * (size_t)c + tid - 36] = v;
-        } else {
-            int i = 0, t = tid;
-            while (t >= 8 - i) { t -= 8 - i; ++i; }
-            const int j = i + t;
-            U[64 * (size_t)c + 8 * i + j] = v;
-            U[64 * (size_t)c + 8 * j + i] = v;
+    double* Uc = U + 64 * (size_t)c;
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = i; j < 8; ++j) {
+            Uc[8 * i + j] = acc[t];
+            Uc[8 * j + i] = acc[t];
+            ++t;
         }
-    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gc[8 * (size_t)c + i] = acc[36 + i];
 }
 
 // One launch for both independent halves of the linearisation: blocks [0, n_camb) are the
-// latency-bound camera blocks (dispatched first), the rest the HBM-streaming observation blocks,
-// so the camera reduction runs underneath the observation stream instead of after it.  The
-// finish blocks (which read the observation blocks' segment records) are a second launch.
+// latency-bound camera waves (four cameras per block, dispatched first), the rest the
+// HBM-streaming observation blocks, so the camera reduction runs underneath the observation
+// stream instead of after it.  The finish blocks (which read the observation blocks' segment
+// records) are a second launch.  (Measured alternative: the camera kernel on a forked
+// high-priority stream — the cross-queue join left ~18 us idle per call)
 __global__ __launch_bounds__(256) void ba_jtj_kernel(
-    int n_camb, int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
-    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
-    const int32_t* __restrict__ pt_idx, const int32_t* __restrict__ pt_ptr,
-    const double* __restrict__ uv, const int32_t* __restrict__ cam_ptr,
-    const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
-    double* __restrict__ U, double* __restrict__ gc, double* __restrict__ W,
-    double* __restrict__ res, double* __restrict__ V, double* __restrict__ gp,
-    double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_wave) {
+    int n_camb, int n_camw, int n_obs, const double* __restrict__ cams,
+    const double* __restrict__ pp, const double* __restrict__ pts,
+    const int32_t* __restrict__ cam_idx, const int32_t* __restrict__ pt_idx,
+    const int32_t* __restrict__ pt_ptr, const double* __restrict__ uv,
+    const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ cam_obs, double loss_s,
+    int splits, double* __restrict__ part, double* __restrict__ U, double* __restrict__ gc,
+    double* __restrict__ W, double* __restrict__ res, double* __restrict__ V,
+    double* __restrict__ gp, double* __restrict__ seg, int32_t* __restrict__ seg_pt,
+    double* __restrict__ cost_blk) {
     __shared__ double lds[4 * OBS_LDS];
     const int b = blockIdx.x;
-    if (b < n_camb)
-        camera_block(b, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U, gc,
-                     lds);
-    else
+    if (b < n_camb) {
+        const int cw = b * 4 + (threadIdx.x >> 6);
+        if (cw < n_camw)
+            camera_wave(cw, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U,
+                        gc);
+    } else {
         obs_block(b - n_camb, n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res,
-                  V, gp, seg, seg_pt, cost_wave, lds);
+                  V, gp, seg, seg_pt, cost_blk, lds);
+    }
 }
 
-__device__ void finish_block(int fb, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
-                             const double* __restrict__ seg, const int32_t* __restrict__ seg_pt,
-                             double* __restrict__ V, double* __restrict__ gp,
-                             const double* __restrict__ cost_wave, double* __restrict__ cost);
+__device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
+                             const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
+                             const int32_t* __restrict__ seg_pt, double* __restrict__ V,
+                             double* __restrict__ gp, const double* __restrict__ cost_blk,
+                             double* __restrict__ cost);
 
 __global__ __launch_bounds__(256) void ba_finish_kernel(
-    int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
-    const int32_t* __restrict__ seg_pt, double* __restrict__ V, double* __restrict__ gp,
-    const double* __restrict__ cost_wave, double* __restrict__ cost) {
-    finish_block(blockIdx.x, n_wave, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_wave, cost);
+    int n_wave, int n_blk, int n_pt, const int32_t* __restrict__ pt_ptr,
+    const double* __restrict__ seg, const int32_t* __restrict__ seg_pt, double* __restrict__ V,
+    double* __restrict__ gp, const double* __restrict__ cost_blk, double* __restrict__ cost) {
+    finish_block(blockIdx.x, n_wave, n_blk, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost);
 }
 
 // Finish work (256-thread block fb): points spanning waves (the point whose tail record wave g
 // wrote owns tail + the head records of the following waves up to its last observation, fixed
 // order), zero V_p / g_p for points without observations, and (block 0) the cost as a
-// fixed-order sum of the per-wave shares.
-__device__ void finish_block(int fb, int n_wave, int n_pt, const int32_t* __restrict__ pt_ptr,
-                             const double* __restrict__ seg, const int32_t* __restrict__ seg_pt,
-                             double* __restrict__ V, double* __restrict__ gp,
-                             const double* __restrict__ cost_wave, double* __restrict__ cost) {
+// fixed-order sum of the per-block shares.
+__device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
+                             const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
+                             const int32_t* __restrict__ seg_pt, double* __restrict__ V,
+                             double* __restrict__ gp, const double* __restrict__ cost_blk,
+                             double* __restrict__ cost) {
     const int tid = threadIdx.x;
     const int g = fb * 256 + tid;
     if (fb == 0) {
         __shared__ double red[4];
         double s = 0.0;  // fixed order (w = tid, tid + 256, ...); unrolled so the loads overlap
 #pragma unroll 8
-        for (int w = tid; w < n_wave; w += 256) s += cost_wave[w];
+        for (int w = tid; w < n_blk; w += 256) s += cost_blk[w];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) s += __shfl_down(s, off, 64);
         if ((tid & 63) == 0) red[tid >> 6] = s;
@@ -526,31 +566,37 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     SFM_REQUIRE(cams && pp && pts && cam_idx && pt_idx && uv && pt_ptr && cam_ptr && cam_obs && U &&
                     V && W && gc && gp && res,
                 "sfm_ba_jtj: NULL array");
-    // workspace: segment records (2 per wave) | their point ids | cost per wave | camera partials
+    // workspace: segment records (2 per wave) | their point ids | cost per block | camera partials
     const int n_wave = (n_obs + 63) / 64;
-    // few cameras: split each camera's observations so the grid still fills the chip
+    const int n_obsb = (n_obs + 255) / 256;
+    // few cameras: split each camera's observations so the camera waves still fill the chip
     const int splits = std::max(1, std::min(16, (SPLIT_TARGET + n_cam - 1) / n_cam));
     const size_t sb = sfm::align_up(sizeof(double) * NV * 2 * (size_t)std::max(n_wave, 1), 256);
     const size_t ib = sfm::align_up(sizeof(int32_t) * 2 * (size_t)std::max(n_wave, 1), 256);
-    const size_t cb = sfm::align_up(sizeof(double) * (size_t)std::max(n_wave, 1), 256);
+    const size_t cb = sfm::align_up(sizeof(double) * (size_t)std::max(n_obsb, 1), 256);
     const size_t pb = sizeof(double) * NU * (size_t)n_cam * splits;
     char* ws = (char*)sfm::workspace(ctx, sb + ib + cb + pb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     double* seg = (double*)ws;
     int32_t* seg_pt = (int32_t*)(ws + sb);
-    double* cost_wave = (double*)(ws + sb + ib);
+    double* cost_blk = (double*)(ws + sb + ib);
     double* part = (double*)(ws + sb + ib + cb);
-    // camera blocks + observation blocks in one launch, then the finish blocks
-    const int n_camb = n_cam * splits;
-    const int n_obsb = (n_obs + 255) / 256;
-    hipLaunchKernelGGL(ba_jtj_kernel, dim3(n_camb + n_obsb), dim3(256), 0, st, n_camb, n_obs,
-                       cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, cam_ptr, cam_obs, loss_s,
-                       splits, part, U, gc, W, res, V, gp, seg, seg_pt, cost_wave);
+    // camera waves (four per block) + observation blocks in one launch, then the finish blocks
+    const int n_camw = n_cam * splits;
+    const int n_camb = (n_camw + 3) / 4;
+#ifdef BA_ABL_CAMONLY  // ablation (timing only): camera waves alone
+    const int n_ob_launch = 0;
+#else
+    const int n_ob_launch = n_obsb;
+#endif
+    hipLaunchKernelGGL(ba_jtj_kernel, dim3(n_camb + n_ob_launch), dim3(256), 0, st, n_camb, n_camw,
+                       n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, cam_ptr, cam_obs, loss_s,
+                       splits, part, U, gc, W, res, V, gp, seg, seg_pt, cost_blk);
     SFM_HIP_CHECK(hipGetLastError());
     const int nw = n_obs > 0 ? n_wave : 0;
     const int n_fin = std::max(std::max((nw + 255) / 256, (n_pt + 255) / 256), 1);
-    hipLaunchKernelGGL(ba_finish_kernel, dim3(n_fin), dim3(256), 0, st, nw, n_pt, pt_ptr, seg,
-                       seg_pt, V, gp, cost_wave, cost);
+    hipLaunchKernelGGL(ba_finish_kernel, dim3(n_fin), dim3(256), 0, st, nw, n_obs > 0 ? n_obsb : 0,
+                       n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost);
     SFM_HIP_CHECK(hipGetLastError());
     if (splits > 1) {
         hipLaunchKernelGGL(ba_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, st,
