@@ -10,12 +10,13 @@
 // Parity against OpenCV itself is unpinned (no cv2 here); against the oracle it is bit-exact.
 //
 // Kernels (grid y = image):
-//   orb_pyr_kernel     thread per pyramid pixel: level 0 copied, level l >= 1 resampled
-//   orb_blur_kernel    thread per pixel: 7x7 separable Gaussian, fixed point
-//   orb_fast_kernel    thread per pixel: FAST-9 score inside the 31-pixel border (0 elsewhere)
-//   orb_nms_kernel     thread per pixel: strict 3x3 maximum flag
-//   orb_rows_kernel    wave per level row: survivors per row (ballot), and with the row offsets
-//                      from orb_scan_kernel the raster-order candidate list (x, y, score packed)
+//   orb_tile_kernel    block per 64 x 32 level tile: pyramid pixels (level 0 copied, level l >= 1
+//                      resampled) with a halo in LDS, 7x7 separable Gaussian (fixed point),
+//                      FAST-9 score inside the 31-pixel border, strict 3x3 maximum -> pyramid,
+//                      blur and the kept scores
+//                      and the survivor count of every 64-pixel row segment
+//   orb_scan_kernel    block per (image, level): row positions in raster order
+//   orb_cand_kernel    wave per level row: the raster-order candidate list (x, y, score packed)
 //   orb_select_kernel  block per (image, level): FAST-score top 2 n_l by histogram threshold,
 //                      Harris, LDS bitonic sort, orientation and descriptors of the n_l best
 //   orb_pack_kernel    block per image: levels' slots -> one dense list per image
@@ -38,184 +39,304 @@ struct OrbLevels {
     int32_t nlev;
     int32_t W[MAXLEV], H[MAXLEV], n[MAXLEV], slot[MAXLEV];  // slot: first output slot of level
     int64_t off[MAXLEV + 1];         // pixel offset of each level in an image's pyramid
-    int64_t rowoff[MAXLEV + 1];      // row offset of each level (row-count arrays)
     int32_t mapx[MAXLEV], mapy[MAXLEV];  // offsets (entries of 3 ints) into the axis-map table
+    int32_t ntx[MAXLEV];              // TW x TH tiles per level row
+    int32_t pitch[MAXLEV];            // bytes per level row in pyr / blur / nms (multiple of 64)
+    int32_t tileoff[MAXLEV + 1];      // first tile of each level (orb_tile_kernel grid x)
+    int64_t segoff[MAXLEV + 1];       // first 64-pixel row segment (row-major: y * ntx + tile x)
+    int64_t rowoff[MAXLEV + 1];       // first row of each level (row position arrays)
     double sc[MAXLEV];
 };
 
 __constant__ int c_fast_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_fast_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-__constant__ int c_blur_w[7] = {18, 34, 49, 54, 49, 34, 18};
 
-__device__ __forceinline__ int find_level(const OrbLevels& L, int64_t i) {
+// ---- fused front end: pyramid, blur, FAST, NMS per 64 x 32 tile ------------------------------
+//
+// Block per (level tile, image).  The tile's pyramid pixels with a 4-pixel halo are computed once
+// into LDS (level 0 copied, level l >= 1 resampled from the image through the axis maps; halo
+// coordinates clamped to the level, which is exactly the blur's border rule) and written out for
+// the select kernel; the 7x7 blur runs as a horizontal pass into LDS and a vertical pass
+// (the same integer sum as the 2-D formula); FAST scores of the tile plus a 1-pixel ring go to
+// LDS, and the strict 3x3 maximum writes nms = score where kept, else 0 (one byte array instead
+// of score + flag: a kept score is >= 1).  Every value is an integer function of the same inputs
+// as oracle/sfm_oracle_orb.c: bit-exact by construction.
+constexpr int TW = 64, TH = 32;         // tile (output pixels)
+constexpr int PW = TW + 8, PH = TH + 8;  // pyramid tile + 4-pixel halo (FAST 3 + NMS 1)
+
+// FAST-9 scores of two pixels at once (packed i16 lanes: v_pk_min_i16 / v_pk_max_i16) from the 16
+// circle differences: best over the 16 arcs of 9 of max(min d, min -d), with the arc minima by
+// min of three 3-runs — exactly the spec's arc loop (integer min/max, |d| <= 255).
+typedef short s2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s2 smin(s2 a, s2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ s2 fast_score2(const s2 (&d)[16]) {
+    s2 nd[16], mn3[16], nm3[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) nd[i] = -d[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        mn3[i] = smin(smin(d[i], d[(i + 1) & 15]), d[(i + 2) & 15]);
+        nm3[i] = smin(smin(nd[i], nd[(i + 1) & 15]), nd[(i + 2) & 15]);
+    }
+    s2 best = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const s2 b9 = smin(smin(mn3[i], mn3[(i + 3) & 15]), mn3[(i + 6) & 15]);
+        const s2 k9 = smin(smin(nm3[i], nm3[(i + 3) & 15]), nm3[(i + 6) & 15]);
+        best = smax(best, smax(b9, k9));
+    }
+    return best;
+}
+
+__global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict__ imgs, int H,
+                                                       int W, OrbLevels L,
+                                                       const int32_t* __restrict__ maps, int thr,
+                                                       uint8_t* __restrict__ pyr,
+                                                       uint8_t* __restrict__ blur,
+                                                       uint8_t* __restrict__ nms,
+                                                       int32_t* __restrict__ segcnt) {
+    __shared__ __attribute__((aligned(16))) uint8_t P[PH][PW];
+    __shared__ int Hb[TH + 6][TW];
+    __shared__ uint8_t S[TH + 2][TW + 2];
+    __shared__ int MX[PW][3], MY[PH][3];
+    __shared__ __attribute__((aligned(4))) uint8_t Ob[TH][TW], On[TH][TW];  // blur / nms out
+    const int tid = threadIdx.x;
+    const int t = blockIdx.x;
     int l = 0;
-    while (l + 1 < L.nlev && i >= L.off[l + 1]) ++l;
-    return l;
-}
-
-__global__ __launch_bounds__(256) void orb_pyr_kernel(const uint8_t* __restrict__ imgs, int H,
-                                                      int W, OrbLevels L,
-                                                      const int32_t* __restrict__ maps,
-                                                      uint8_t* __restrict__ pyr) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    while (l + 1 < L.nlev && t >= L.tileoff[l + 1]) ++l;
+    const int tl = t - L.tileoff[l];
+    const int w = L.W[l], h = L.H[l], pw = L.pitch[l];
+    const int ty0 = tl / L.ntx[l], tx0 = tl - ty0 * L.ntx[l];
+    const int y0 = ty0 * TH, x0 = tx0 * TW;
     const int64_t tot = L.off[L.nlev];
-    if (i >= tot) return;
+    const size_t ib = (size_t)blockIdx.y * tot + L.off[l];
     const uint8_t* img = imgs + (size_t)blockIdx.y * H * W;
-    uint8_t* out = pyr + (size_t)blockIdx.y * tot;
-    const int l = find_level(L, i);
-    const int64_t p = i - L.off[l];
-    const int w = L.W[l];
-    const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
-    if (l == 0) {
-        out[i] = img[(size_t)y * W + x];
-        return;
-    }
-    const int32_t* mx = maps + 3 * (L.mapx[l] + x);
-    const int32_t* my = maps + 3 * (L.mapy[l] + y);
-    const uint8_t* r0 = img + (size_t)my[0] * W;
-    const uint8_t* r1 = img + (size_t)my[1] * W;
-    const int wx = mx[2], wy = my[2];
-    const int t0 = r0[mx[0]] * (2048 - wx) + r0[mx[1]] * wx;
-    const int t1 = r1[mx[0]] * (2048 - wx) + r1[mx[1]] * wx;
-    out[i] = (uint8_t)((t0 * (2048 - wy) + t1 * wy + (1 << 21)) >> 22);
-}
-
-__global__ __launch_bounds__(256) void orb_blur_kernel(const uint8_t* __restrict__ pyr, OrbLevels L,
-                                                       uint8_t* __restrict__ blur) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t tot = L.off[L.nlev];
-    if (i >= tot) return;
-    const int l = find_level(L, i);
-    const int64_t p = i - L.off[l];
-    const int w = L.W[l], h = L.H[l];
-    const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
-    const uint8_t* lv = pyr + (size_t)blockIdx.y * tot + L.off[l];
-    int acc = 0;
-#pragma unroll
-    for (int j = -3; j <= 3; ++j) {
-        const uint8_t* row = lv + (size_t)min(max(y + j, 0), h - 1) * w;
-        int s = 0;
-#pragma unroll
-        for (int q = -3; q <= 3; ++q) s += c_blur_w[q + 3] * row[min(max(x + q, 0), w - 1)];
-        acc += c_blur_w[j + 3] * s;
-    }
-    blur[(size_t)blockIdx.y * tot + i] = (uint8_t)((acc + 32768) >> 16);
-}
-
-__global__ __launch_bounds__(256) void orb_fast_kernel(const uint8_t* __restrict__ pyr, OrbLevels L,
-                                                       int thr, uint8_t* __restrict__ score) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t tot = L.off[L.nlev];
-    if (i >= tot) return;
-    const int l = find_level(L, i);
-    const int64_t p = i - L.off[l];
-    const int w = L.W[l], h = L.H[l];
-    const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
-    int s = 0;
-    if (x >= EDGE && x < w - EDGE && y >= EDGE && y < h - EDGE) {
-        const uint8_t* lv = pyr + (size_t)blockIdx.y * tot + L.off[l];
-        const int c = lv[(size_t)y * w + x];
-        int d[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = (int)lv[(size_t)(y + c_fast_dy[k]) * w + x + c_fast_dx[k]] - c;
-        int best = 0;
-#pragma unroll
-        for (int st = 0; st < 16; ++st) {
-            int b = 255, k = 255;
-#pragma unroll
-            for (int q = 0; q < 9; ++q) {
-                const int v = d[(st + q) & 15];
-                b = min(b, v);
-                k = min(k, -v);
+    // 1. pyramid tile with halo (clamped coordinates)
+    if (l > 0) {
+        for (int k = tid; k < PW + PH; k += 256) {
+            if (k < PW) {
+                const int cx = min(max(x0 - 4 + k, 0), w - 1);
+                const int32_t* m = maps + 3 * (L.mapx[l] + cx);
+                MX[k][0] = m[0]; MX[k][1] = m[1]; MX[k][2] = m[2];
+            } else {
+                const int r = k - PW, cy = min(max(y0 - 4 + r, 0), h - 1);
+                const int32_t* m = maps + 3 * (L.mapy[l] + cy);
+                MY[r][0] = m[0]; MY[r][1] = m[1]; MY[r][2] = m[2];
             }
-            best = max(best, max(b, k));
         }
-        s = best > thr ? best : 0;
+        __syncthreads();
     }
-    score[(size_t)blockIdx.y * tot + i] = (uint8_t)s;
+    {   // every load of the thread issued before any is used (the fill is latency-bound)
+        constexpr int PN = (PH * PW + 255) / 256;
+        int v[PN];
+#pragma unroll
+        for (int q = 0; q < PN; ++q) {
+            const int k = tid + q * 256;
+            v[q] = 0;
+            if (k < PH * PW) {
+                const int r = k / PW, c = k - r * PW;
+                if (l == 0) {
+                    const int cy = min(max(y0 - 4 + r, 0), h - 1), cx = min(max(x0 - 4 + c, 0), w - 1);
+                    v[q] = img[(size_t)cy * W + cx];
+                } else {
+                    const uint8_t* r0 = img + (size_t)MY[r][0] * W;
+                    const uint8_t* r1 = img + (size_t)MY[r][1] * W;
+                    const int wx = MX[c][2], wy = MY[r][2];
+                    const int t0 = r0[MX[c][0]] * (2048 - wx) + r0[MX[c][1]] * wx;
+                    const int t1 = r1[MX[c][0]] * (2048 - wx) + r1[MX[c][1]] * wx;
+                    v[q] = (t0 * (2048 - wy) + t1 * wy + (1 << 21)) >> 22;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PN; ++q) {
+            const int k = tid + q * 256;
+            if (k < PH * PW) P[k / PW][k - (k / PW) * PW] = (uint8_t)v[q];
+        }
+    }
+    __syncthreads();
+    // 2. pyramid out; horizontal blur of rows y0-3 .. y0+TH+2.  Every phase below issues the LDS
+    //    reads of a batch of pixels before any arithmetic (compile-time trip counts, no data-
+    //    dependent branches): the phases are LDS-latency chains otherwise.
+    // (rows are pitch-padded to 64 B: a tile row is one aligned 64-B run; dword stores, columns
+    //  past the level width land in the padding)
+#pragma unroll
+    for (int q = 0; q < TH * TW / 1024; ++q) {
+        const int k = tid + q * 256, r = k >> 4, c4 = (k & 15) * 4;
+        if (y0 + r < h)
+            *(uint32_t*)(pyr + ib + (size_t)(y0 + r) * pw + x0 + c4) = *(const uint32_t*)&P[r + 4][c4 + 4];
+    }
+    {
+        constexpr int HN = ((TH + 6) * TW + 255) / 256;  // 10 (the last partly)
+#pragma unroll
+        for (int q0 = 0; q0 < HN; q0 += 5) {
+            int v[5][7];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const int k = min(tid + (q0 + q) * 256, (TH + 6) * TW - 1);
+                const int r = k / TW, c = k - r * TW;
+#pragma unroll
+                for (int j = 0; j < 7; ++j) v[q][j] = P[r + 1][c + 1 + j];  // pixel (y0-3+r, x0+c-3+j)
+            }
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const int k = tid + (q0 + q) * 256;
+                if (q0 + q < HN && k < (TH + 6) * TW)
+                    Hb[k / TW][k % TW] = 18 * v[q][0] + 34 * v[q][1] + 49 * v[q][2] + 54 * v[q][3] +
+                                         49 * v[q][4] + 34 * v[q][5] + 18 * v[q][6];
+            }
+        }
+    }
+    // 3. FAST scores of the tile + 1-pixel ring (0 outside the EDGE border), two pixels per batch
+    //    (packed in the i16 halves of one register)
+    {
+        constexpr int FN = ((TH + 2) * (TW + 2) + 255) / 256;  // 9
+#pragma unroll
+        for (int q0 = 0; q0 < FN; q0 += 2) {
+            s2 d[16];
+            int cv[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int k = min(tid + (q0 + q) * 256, (TH + 2) * (TW + 2) - 1);
+                const int r = k / (TW + 2), c = k - r * (TW + 2);
+                const int py = r + 3, px = c + 3;  // P coordinates of the pixel
+                cv[q] = P[py][px];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) d[e][q] = (short)P[py + c_fast_dy[e]][px + c_fast_dx[e]];
+            }
+#pragma unroll
+            for (int e = 0; e < 16; ++e) d[e] = d[e] - s2{(short)cv[0], (short)cv[1]};
+            const s2 best = fast_score2(d);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int k = tid + (q0 + q) * 256;
+                if (q0 + q >= FN || k >= (TH + 2) * (TW + 2)) continue;
+                const int r = k / (TW + 2), c = k - r * (TW + 2);
+                const int gy = y0 - 1 + r, gx = x0 - 1 + c;
+                const bool inside = gx >= EDGE && gx < w - EDGE && gy >= EDGE && gy < h - EDGE;
+                const int b = best[q];
+                S[r][c] = (uint8_t)(inside && b > thr ? b : 0);
+            }
+        }
+    }
+    __syncthreads();
+    // 4. vertical blur and the strict 3x3 maximum of the tile; wave = one 64-pixel row segment
+    //    per step (lane = column): its survivors are counted for the candidate scatter
+    const int lane = tid & 63;
+#pragma unroll
+    for (int q0 = 0; q0 < TH / 4; q0 += 4) {
+        int hv[4][7], sv[4][9];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = (tid >> 6) + 4 * (q0 + q), c = lane;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) hv[q][j] = Hb[r + j][c];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) sv[q][j] = S[r + j / 3][c + j % 3];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = (tid >> 6) + 4 * (q0 + q), c = lane;
+            const bool in = y0 + r < h && x0 + c < w;
+            bool keep = false;
+            if (in) {
+                const int acc = 18 * hv[q][0] + 34 * hv[q][1] + 49 * hv[q][2] + 54 * hv[q][3] +
+                                49 * hv[q][4] + 34 * hv[q][5] + 18 * hv[q][6];
+                Ob[r][c] = (uint8_t)((acc + 32768) >> 16);
+                const int s0 = sv[q][4];
+                keep = s0 != 0;  // nonzero only inside the EDGE border
+#pragma unroll
+                for (int j = 0; j < 9; ++j)
+                    if (j != 4 && sv[q][j] >= s0) keep = false;
+            }
+            On[r][c] = keep ? (uint8_t)sv[q][4] : (uint8_t)0;
+            const unsigned long long m = __ballot(keep);
+            if (lane == 0 && y0 + r < h)
+                segcnt[(size_t)blockIdx.y * L.segoff[L.nlev] + L.segoff[l] +
+                       (int64_t)(y0 + r) * L.ntx[l] + tx0] = __popcll(m);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < TH * TW / 1024; ++q) {
+        const int k = tid + q * 256, r = k >> 4, c4 = (k & 15) * 4;
+        if (y0 + r < h) {
+            const size_t o = ib + (size_t)(y0 + r) * pw + x0 + c4;
+            *(uint32_t*)(blur + o) = *(const uint32_t*)&Ob[r][c4];
+            *(uint32_t*)(nms + o) = *(const uint32_t*)&On[r][c4];
+        }
+    }
 }
 
-__global__ __launch_bounds__(256) void orb_nms_kernel(const uint8_t* __restrict__ score, OrbLevels L,
-                                                      uint8_t* __restrict__ flag) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t tot = L.off[L.nlev];
-    if (i >= tot) return;
-    const int l = find_level(L, i);
-    const int64_t p = i - L.off[l];
-    const int w = L.W[l], h = L.H[l];
-    const int y = (int)(p / w), x = (int)(p - (int64_t)y * w);
-    const uint8_t* sc = score + (size_t)blockIdx.y * tot + L.off[l];
-    int keep = 0;
-    const int s = sc[(size_t)y * w + x];
-    if (s && x >= EDGE && x < w - EDGE && y >= EDGE && y < h - EDGE) {
-        keep = 1;
-#pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-            for (int dx = -1; dx <= 1; ++dx)
-                if ((dx || dy) && sc[(size_t)(y + dy) * w + x + dx] >= s) keep = 0;
-    }
-    flag[(size_t)blockIdx.y * tot + i] = (uint8_t)keep;
-}
-
-// Wave per level row (grid x = global row / 4, 4 waves per block).  pass 0: survivors per row;
-// pass 1: write them, packed (y << 20 | x << 8 | score), at the row's offset (raster order).
-__global__ __launch_bounds__(256) void orb_rows_kernel(int pass, const uint8_t* __restrict__ flag,
-                                                       const uint8_t* __restrict__ score,
-                                                       OrbLevels L, int32_t* __restrict__ rowcnt,
+// Wave per level row (4 per block): the row's survivors, packed (y << 20 | x << 8 | score), at
+// the row's raster-order position (orb_scan_kernel) + the exclusive sum of its segment counts
+// (the tile kernel's, one lane per segment); the segments' bytes are loaded eight at a time.
+__global__ __launch_bounds__(256) void orb_cand_kernel(const uint8_t* __restrict__ nms,
+                                                       OrbLevels L, const int32_t* __restrict__ segcnt,
                                                        const int32_t* __restrict__ rowpos,
                                                        int32_t* __restrict__ cand) {
     const int lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t nrows = L.rowoff[L.nlev];
-    if (r >= nrows) return;  // wave-uniform
+    const int64_t rg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (rg >= L.rowoff[L.nlev]) return;  // wave-uniform
     int l = 0;
-    while (l + 1 < L.nlev && r >= L.rowoff[l + 1]) ++l;
-    const int y = (int)(r - L.rowoff[l]);
-    const int w = L.W[l], h = L.H[l];
+    while (l + 1 < L.nlev && rg >= L.rowoff[l + 1]) ++l;
+    const int y = (int)(rg - L.rowoff[l]);
+    const int w = L.W[l], h = L.H[l], ntx = L.ntx[l];
+    if (y < EDGE || y >= h - EDGE) return;  // no survivors
     const size_t img = blockIdx.y;
-    const int64_t tot = L.off[L.nlev];
-    const size_t gr = img * (size_t)nrows + r;
-    if (y < EDGE || y >= h - EDGE) {
-        if (pass == 0 && lane == 0) rowcnt[gr] = 0;
-        return;
+    const int64_t nseg = L.segoff[L.nlev];
+    const int sc = lane < ntx ? segcnt[img * nseg + L.segoff[l] + (int64_t)y * ntx + lane] : 0;
+    int incl = sc;  // inclusive scan over the row's segments
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
     }
-    const uint8_t* fl = flag + img * tot + L.off[l] + (size_t)y * w;
-    const uint8_t* sc = score + img * tot + L.off[l] + (size_t)y * w;
-    int n = 0;
-    int pos = pass ? rowpos[gr] : 0;
+    const int base = rowpos[img * L.rowoff[L.nlev] + rg];
+    const uint8_t* row = nms + img * L.off[L.nlev] + L.off[l] + (size_t)y * L.pitch[l];
     int32_t* out = cand + (img * L.nlev + l) * (size_t)MAXC;
-    for (int x0 = EDGE; x0 < w - EDGE; x0 += 64) {
-        const int x = x0 + lane;
-        const bool f = x < w - EDGE && fl[x];
-        const unsigned long long m = __ballot(f);
-        if (pass && f) {
-            const int k = pos + n + __popcll(m & ((1ull << lane) - 1ull));
-            if (k < MAXC) out[k] = (int32_t)(((unsigned)y << 20) | ((unsigned)x << 8) | sc[x]);
+    for (int t0 = 0; t0 < ntx; t0 += 8) {
+        int v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int x = (t0 + j) * TW + lane;
+            v[j] = (t0 + j < ntx && x < w) ? row[x] : 0;
         }
-        n += __popcll(m);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const unsigned long long m = __ballot(v[j] != 0);
+            if (m == 0ull) continue;  // wave-uniform
+            const int sb = __shfl(incl - sc, t0 + j, 64);  // exclusive base of segment t0 + j
+            if (v[j] != 0) {
+                const int k = base + sb + __popcll(m & ((1ull << lane) - 1ull));
+                const int x = (t0 + j) * TW + lane;
+                if (k < MAXC) out[k] = (int32_t)(((unsigned)y << 20) | ((unsigned)x << 8) | (unsigned)v[j]);
+            }
+        }
     }
-    if (pass == 0 && lane == 0) rowcnt[gr] = n;
 }
 
-// Block per (image, level): exclusive scan of the level's row counts (fixed order) -> row
-// positions and the level's candidate count (capped at MAXC).
-__global__ __launch_bounds__(256) void orb_scan_kernel(OrbLevels L, const int32_t* __restrict__ rowcnt,
+// Block per (image, level): row totals (sum of the row's segment counts), exclusive scan over the
+// rows (fixed order) -> row positions, and the level's candidate count (capped at MAXC).
+__global__ __launch_bounds__(256) void orb_scan_kernel(OrbLevels L, const int32_t* __restrict__ segcnt,
                                                        int32_t* __restrict__ rowpos,
                                                        int32_t* __restrict__ ncand) {
     __shared__ int carry;
     __shared__ int wsum[4];
     const int l = blockIdx.x, tid = threadIdx.x;
     const size_t img = blockIdx.y;
-    const int64_t nrows = L.rowoff[L.nlev];
-    const int32_t* rc = rowcnt + img * nrows + L.rowoff[l];
-    int32_t* rp = rowpos + img * nrows + L.rowoff[l];
-    const int h = L.H[l];
+    const int64_t nseg = L.segoff[L.nlev];
+    const int ntx = L.ntx[l], h = L.H[l];
+    const int32_t* sg = segcnt + img * nseg + L.segoff[l];
+    int32_t* rp = rowpos + img * L.rowoff[L.nlev] + L.rowoff[l];
     if (tid == 0) carry = 0;
     __syncthreads();
     for (int y0 = 0; y0 < h; y0 += 256) {
         const int y = y0 + tid;
-        const int v = y < h ? rc[y] : 0;
+        int v = 0;
+        if (y >= EDGE && y < h - EDGE)
+            for (int t = 0; t < ntx; ++t) v += sg[(int64_t)y * ntx + t];
         int incl = v;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -265,7 +386,7 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
     const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const size_t img = blockIdx.y;
     const int nl = L.n[l];
-    const int w = L.W[l];
+    const int pw = L.pitch[l];
     if (tid == 0) lvl_count[img * L.nlev + l] = 0;
     if (nl <= 0) return;
     const int nc = ncand[img * L.nlev + l];
@@ -334,9 +455,9 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
             long long A = 0, B = 0, C = 0;
             for (int v = -3; v <= 3; ++v)
                 for (int u = -3; u <= 3; ++u) {
-                    const uint8_t* m = lv + (size_t)(y + v) * w + (x + u);
-                    const int ix = (m[-w + 1] + 2 * m[1] + m[w + 1]) - (m[-w - 1] + 2 * m[-1] + m[w - 1]);
-                    const int iy = (m[w - 1] + 2 * m[w] + m[w + 1]) - (m[-w - 1] + 2 * m[-w] + m[-w + 1]);
+                    const uint8_t* m = lv + (size_t)(y + v) * pw + (x + u);
+                    const int ix = (m[-pw + 1] + 2 * m[1] + m[pw + 1]) - (m[-pw - 1] + 2 * m[-1] + m[pw - 1]);
+                    const int iy = (m[pw - 1] + 2 * m[pw] + m[pw + 1]) - (m[-pw - 1] + 2 * m[-pw] + m[-pw + 1]);
                     A += (long long)ix * ix;
                     B += (long long)iy * iy;
                     C += (long long)ix * iy;
@@ -372,7 +493,7 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
         const int y = (int)(c >> 20), x = (int)((c >> 8) & 4095u);
         long long m10 = 0, m01 = 0;
         for (int v = -RADIUS; v <= RADIUS; ++v) {
-            const uint8_t* row = lv + (size_t)(y + v) * w + x;
+            const uint8_t* row = lv + (size_t)(y + v) * pw + x;
             for (int u = -RADIUS; u <= RADIUS; ++u) {
                 if (u * u + v * v > RADIUS * RADIUS) continue;
                 const int I = row[u];
@@ -405,8 +526,8 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
                     q[2 * e + 1] = round_div(px * m01 + py * m10, R2);
                 }
             }
-            const int i1 = bl[(size_t)(y + q[1]) * w + x + q[0]];
-            const int i2 = bl[(size_t)(y + q[3]) * w + x + q[2]];
+            const int i1 = bl[(size_t)(y + q[1]) * pw + x + q[0]];
+            const int i2 = bl[(size_t)(y + q[3]) * pw + x + q[2]];
             if (i1 < i2) words[t >> 5] |= 1u << (t & 31);
         }
         uint4* d = (uint4*)(slot_desc + 32 * o);
@@ -528,7 +649,6 @@ extern "C" int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img,
     L.n[nlev - 1] = std::max(nfeat - sum, 0);
     int slot = 0, nmap = 0;
     L.off[0] = 0;
-    L.rowoff[0] = 0;
     for (int l = 0; l < nlev; ++l) {
         SFM_REQUIRE(L.W[l] >= 1 && L.H[l] >= 1, "sfm_orb_batch: too many levels for the image size");
         // levels with no room inside the border or no budget detect nothing
@@ -536,39 +656,52 @@ extern "C" int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img,
         SFM_REQUIRE(2 * L.n[l] <= SEL_MAX, "sfm_orb_batch: n_features too large (per-level 2 n_l <= 1024)");
         L.slot[l] = slot;
         slot += L.n[l];
-        L.off[l + 1] = L.off[l] + (int64_t)L.W[l] * L.H[l];
-        L.rowoff[l + 1] = L.rowoff[l] + L.H[l];
+        L.pitch[l] = (L.W[l] + 63) & ~63;
+        L.off[l + 1] = L.off[l] + (int64_t)L.pitch[l] * L.H[l];
         L.mapx[l] = nmap;
         nmap += L.W[l];
         L.mapy[l] = nmap;
         nmap += L.H[l];
     }
+    int ntile = 0;
+    int64_t nseg = 0, nrow = 0;
+    for (int l = 0; l < nlev; ++l) {
+        L.tileoff[l] = ntile;
+        L.segoff[l] = nseg;
+        L.rowoff[l] = nrow;
+        nrow += L.H[l];
+        L.ntx[l] = (L.W[l] + TW - 1) / TW;
+        ntile += L.ntx[l] * ((L.H[l] + TH - 1) / TH);
+        nseg += (int64_t)L.ntx[l] * L.H[l];
+    }
+    L.tileoff[nlev] = ntile;
+    L.segoff[nlev] = nseg;
+    L.rowoff[nlev] = nrow;
     std::vector<int32_t> host(3 * (size_t)nmap + 1024);
     for (int l = 1; l < nlev; ++l) {
         axis_map(W, L.W[l], host.data() + 3 * (size_t)L.mapx[l]);
         axis_map(H, L.H[l], host.data() + 3 * (size_t)L.mapy[l]);
     }
     make_pattern(host.data() + 3 * (size_t)nmap);
-    // workspace: tables | pyramid | blur | score | flags | row counts, positions | candidates |
+    // workspace: tables | pyramid | blur | nms scores | segment counts | row positions | candidates |
     // candidate counts | level counts | slots (kp, desc)
-    const size_t tot = (size_t)L.off[nlev], nrows = (size_t)L.rowoff[nlev];
+    const size_t tot = (size_t)L.off[nlev];
     const size_t b_tab = sfm::align_up(sizeof(int32_t) * host.size(), 256);
     const size_t b_img = sfm::align_up(tot * n_img, 256);
-    const size_t b_rows = sfm::align_up(sizeof(int32_t) * nrows * n_img, 256);
+    const size_t b_rows = sfm::align_up(sizeof(int32_t) * (size_t)nseg * n_img, 256);  // >= rows
     const size_t b_cand = sizeof(int32_t) * (size_t)MAXC * nlev * n_img;
     const size_t b_cnt = sfm::align_up(sizeof(int32_t) * (size_t)nlev * n_img, 256);
     const size_t b_skp = sfm::align_up(sizeof(float) * 6 * (size_t)nfeat * n_img, 256);
     const size_t b_sd = sfm::align_up((size_t)32 * nfeat * n_img, 256);
-    char* ws = (char*)sfm::workspace(ctx, b_tab + 4 * b_img + 2 * b_rows + b_cand + 2 * b_cnt +
+    char* ws = (char*)sfm::workspace(ctx, b_tab + 3 * b_img + 2 * b_rows + b_cand + 2 * b_cnt +
                                               b_skp + b_sd);
     if (!ws) return SFM_ERR_NOMEM;
     int32_t* tab = (int32_t*)ws;
     uint8_t* pyr = (uint8_t*)(ws + b_tab);
     uint8_t* blur = pyr + b_img;
-    uint8_t* score = blur + b_img;
-    uint8_t* flag = score + b_img;
-    int32_t* rowcnt = (int32_t*)(flag + b_img);
-    int32_t* rowpos = (int32_t*)((char*)rowcnt + b_rows);
+    uint8_t* nms = blur + b_img;
+    int32_t* segcnt = (int32_t*)(nms + b_img);
+    int32_t* rowpos = (int32_t*)((char*)segcnt + b_rows);
     int32_t* cand = (int32_t*)((char*)rowpos + b_rows);
     int32_t* ncand = (int32_t*)((char*)cand + b_cand);
     int32_t* lvl = (int32_t*)((char*)ncand + b_cnt);
@@ -578,24 +711,14 @@ extern "C" int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img,
                                  hipMemcpyHostToDevice, st));
     const int32_t* maps = tab;
     const int32_t* pattern = tab + 3 * (size_t)nmap;
-    const dim3 gpix((unsigned)((tot + 255) / 256), (unsigned)n_img);
-    hipLaunchKernelGGL(orb_pyr_kernel, gpix, dim3(256), 0, st, images, H, W, L, maps, pyr);
+    hipLaunchKernelGGL(orb_tile_kernel, dim3((unsigned)ntile, (unsigned)n_img), dim3(256), 0, st,
+                       images, H, W, L, maps, prm->fast_threshold, pyr, blur, nms, segcnt);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(orb_blur_kernel, gpix, dim3(256), 0, st, pyr, L, blur);
-    SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(orb_fast_kernel, gpix, dim3(256), 0, st, pyr, L, prm->fast_threshold, score);
-    SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(orb_nms_kernel, gpix, dim3(256), 0, st, score, L, flag);
-    SFM_HIP_CHECK(hipGetLastError());
-    const dim3 grow((unsigned)((nrows + 3) / 4), (unsigned)n_img);
-    hipLaunchKernelGGL(orb_rows_kernel, grow, dim3(256), 0, st, 0, flag, score, L, rowcnt,
-                       rowpos, cand);
-    SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(orb_scan_kernel, dim3(nlev, n_img), dim3(256), 0, st, L, rowcnt, rowpos,
+    hipLaunchKernelGGL(orb_scan_kernel, dim3(nlev, n_img), dim3(256), 0, st, L, segcnt, rowpos,
                        ncand);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(orb_rows_kernel, grow, dim3(256), 0, st, 1, flag, score, L, rowcnt,
-                       rowpos, cand);
+    hipLaunchKernelGGL(orb_cand_kernel, dim3((unsigned)((nrow + 3) / 4), (unsigned)n_img), dim3(256),
+                       0, st, nms, L, segcnt, rowpos, cand);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(orb_select_kernel, dim3(nlev, n_img), dim3(256), 0, st, pyr, blur, L,
                        cand, ncand, pattern, nfeat, skp, sdesc, lvl);
