@@ -101,6 +101,8 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
     __shared__ uint8_t S[TH + 2][TW + 2];
     __shared__ int MX[PW][3], MY[PH][3];
     __shared__ __attribute__((aligned(4))) uint8_t Ob[TH][TW], On[TH][TW];  // blur / nms out
+    __shared__ uint16_t flist[(TH + 2) * (TW + 2)];                          // FAST candidates
+    __shared__ int fcount;
     const int tid = threadIdx.x;
     const int t = blockIdx.x;
     int l = 0;
@@ -188,35 +190,54 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
             }
         }
     }
-    // 3. FAST scores of the tile + 1-pixel ring (0 outside the EDGE border), two pixels per batch
-    //    (packed in the i16 halves of one register)
+    // 3. FAST scores of the tile + 1-pixel ring (0 outside the EDGE border).  Compass points 0, 4,
+    //    8, 12: every 9-arc holds two of them, so a pixel with fewer than two brighter (or darker)
+    //    than thr has best <= thr, score 0 exactly.  Passing pixels (a few % on textured images,
+    //    but in most waves) are appended to an LDS list and scored densely, two per lane in the
+    //    i16 halves of a register.
     {
-        constexpr int FN = ((TH + 2) * (TW + 2) + 255) / 256;  // 9
+        constexpr int FT = (TH + 2) * (TW + 2), FN = (FT + 255) / 256;  // 9
+        if (tid == 0) fcount = 0;
+        __syncthreads();
 #pragma unroll
-        for (int q0 = 0; q0 < FN; q0 += 2) {
+        for (int q = 0; q < FN; ++q) {
+            const int k = tid + q * 256;
+            if (k >= FT) continue;
+            const int r = k / (TW + 2), c = k - r * (TW + 2);
+            const int gy = y0 - 1 + r, gx = x0 - 1 + c;
+            const int py = r + 3, px = c + 3;  // P coordinates of the pixel
+            const int cv = P[py][px];
+            const int c0 = (int)P[py + 3][px] - cv, c4 = (int)P[py][px + 3] - cv;
+            const int c8 = (int)P[py - 3][px] - cv, c12 = (int)P[py][px - 3] - cv;
+            const int nb = (c0 > thr) + (c4 > thr) + (c8 > thr) + (c12 > thr);
+            const int nd = (c0 < -thr) + (c4 < -thr) + (c8 < -thr) + (c12 < -thr);
+            const bool inside = gx >= EDGE && gx < w - EDGE && gy >= EDGE && gy < h - EDGE;
+            S[r][c] = 0;
+            if (inside && (nb >= 2 || nd >= 2)) flist[atomicAdd(&fcount, 1)] = (uint16_t)k;
+        }
+        __syncthreads();
+        const int nf = fcount;
+        for (int i0 = 2 * tid; i0 < nf; i0 += 512) {
             s2 d[16];
-            int cv[2];
+            int kk[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const int k = min(tid + (q0 + q) * 256, (TH + 2) * (TW + 2) - 1);
+                const int k = flist[min(i0 + q, nf - 1)];
+                kk[q] = k;
                 const int r = k / (TW + 2), c = k - r * (TW + 2);
-                const int py = r + 3, px = c + 3;  // P coordinates of the pixel
-                cv[q] = P[py][px];
+                const int py = r + 3, px = c + 3;
+                const int cv = P[py][px];
 #pragma unroll
-                for (int e = 0; e < 16; ++e) d[e][q] = (short)P[py + c_fast_dy[e]][px + c_fast_dx[e]];
+                for (int e = 0; e < 16; ++e)
+                    d[e][q] = (short)((int)P[py + c_fast_dy[e]][px + c_fast_dx[e]] - cv);
             }
-#pragma unroll
-            for (int e = 0; e < 16; ++e) d[e] = d[e] - s2{(short)cv[0], (short)cv[1]};
             const s2 best = fast_score2(d);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const int k = tid + (q0 + q) * 256;
-                if (q0 + q >= FN || k >= (TH + 2) * (TW + 2)) continue;
-                const int r = k / (TW + 2), c = k - r * (TW + 2);
-                const int gy = y0 - 1 + r, gx = x0 - 1 + c;
-                const bool inside = gx >= EDGE && gx < w - EDGE && gy >= EDGE && gy < h - EDGE;
+                if (i0 + q >= nf) continue;
+                const int k = kk[q], r = k / (TW + 2), c = k - r * (TW + 2);
                 const int b = best[q];
-                S[r][c] = (uint8_t)(inside && b > thr ? b : 0);
+                S[r][c] = (uint8_t)(b > thr ? b : 0);
             }
         }
     }
@@ -444,28 +465,36 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
         __syncthreads();
     }
     const int n1 = min(s_sel, SEL_MAX);
-    // ---- Harris response of the selected candidates ----
+    // ---- Harris response of the selected candidates: wave per candidate, lane per window pixel
+    //      (the integer sums are order-free) ----
     int np2 = 1;
     while (np2 < n1) np2 <<= 1;
-    for (int k = tid; k < np2; k += 256) {
-        long long R = LLONG_MIN;
-        if (k < n1) {
-            const unsigned c = sel_c[k];
-            const int y = (int)(c >> 20), x = (int)((c >> 8) & 4095u);
-            long long A = 0, B = 0, C = 0;
-            for (int v = -3; v <= 3; ++v)
-                for (int u = -3; u <= 3; ++u) {
-                    const uint8_t* m = lv + (size_t)(y + v) * pw + (x + u);
-                    const int ix = (m[-pw + 1] + 2 * m[1] + m[pw + 1]) - (m[-pw - 1] + 2 * m[-1] + m[pw - 1]);
-                    const int iy = (m[pw - 1] + 2 * m[pw] + m[pw + 1]) - (m[-pw - 1] + 2 * m[-pw] + m[-pw + 1]);
-                    A += (long long)ix * ix;
-                    B += (long long)iy * iy;
-                    C += (long long)ix * iy;
-                }
-            R = 25 * (A * B - C * C) - (A + B) * (A + B);
-        }
-        sel_r[k] = R;
+    for (int k = n1 + tid; k < np2; k += 256) {
+        sel_r[k] = LLONG_MIN;
         sel_i[k] = k;
+    }
+    for (int k = wv; k < n1; k += 4) {
+        const unsigned c = sel_c[k];
+        const int y = (int)(c >> 20), x = (int)((c >> 8) & 4095u);
+        int A = 0, B = 0, C = 0;  // |ix|, |iy| <= 1020: 49 squares < 2^31
+        if (lane < 49) {
+            const int v = lane / 7 - 3, u = lane % 7 - 3;
+            const uint8_t* m = lv + (size_t)(y + v) * pw + (x + u);
+            const int ix = (m[-pw + 1] + 2 * m[1] + m[pw + 1]) - (m[-pw - 1] + 2 * m[-1] + m[pw - 1]);
+            const int iy = (m[pw - 1] + 2 * m[pw] + m[pw + 1]) - (m[-pw - 1] + 2 * m[-pw] + m[-pw + 1]);
+            A = ix * ix; B = iy * iy; C = ix * iy;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            A += __shfl_xor(A, off, 64);
+            B += __shfl_xor(B, off, 64);
+            C += __shfl_xor(C, off, 64);
+        }
+        if (lane == 0) {
+            const long long a = A, b = B, cc = C;
+            sel_r[k] = 25 * (a * b - cc * cc) - (a + b) * (a + b);
+            sel_i[k] = k;
+        }
     }
     __syncthreads();
     // ---- bitonic sort: R descending, raster index ascending ----
@@ -487,33 +516,42 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
             __syncthreads();
         }
     const int n2 = min(n1, nl);
-    // ---- orientation and descriptor of the n_l best ----
-    for (int k = tid; k < n2; k += 256) {
+    // ---- orientation and descriptor of the n_l best: wave per keypoint (lanes over the disk,
+    //      then over the 256 tests: four ballots give the eight descriptor words) ----
+    for (int k = wv; k < n2; k += 4) {
         const unsigned c = sel_c[sel_i[k]];
         const int y = (int)(c >> 20), x = (int)((c >> 8) & 4095u);
-        long long m10 = 0, m01 = 0;
-        for (int v = -RADIUS; v <= RADIUS; ++v) {
-            const uint8_t* row = lv + (size_t)(y + v) * pw + x;
-            for (int u = -RADIUS; u <= RADIUS; ++u) {
-                if (u * u + v * v > RADIUS * RADIUS) continue;
-                const int I = row[u];
-                m10 += (long long)u * I;
-                m01 += (long long)v * I;
-            }
+        int a10 = 0, a01 = 0;  // |sum| <= 709 * 15 * 255 < 2^31
+        for (int e = lane; e < (2 * RADIUS + 1) * (2 * RADIUS + 1); e += 64) {
+            const int v = e / (2 * RADIUS + 1) - RADIUS, u = e % (2 * RADIUS + 1) - RADIUS;
+            if (u * u + v * v > RADIUS * RADIUS) continue;
+            const int I = lv[(size_t)(y + v) * pw + x + u];
+            a10 += u * I;
+            a01 += v * I;
         }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            a10 += __shfl_xor(a10, off, 64);
+            a01 += __shfl_xor(a01, off, 64);
+        }
+        const long long m10 = a10, m01 = a01;
         const long long R2 = m10 * m10 + m01 * m01;
-        double ang = atan2((double)m01, (double)m10) * (180.0 / 3.14159265358979323846);
-        if (ang < 0.0) ang += 360.0;
         const size_t o = img * (size_t)nfeat + L.slot[l] + k;
-        float* kp = slot_kp + 6 * o;
-        kp[0] = (float)((double)x * L.sc[l]);
-        kp[1] = (float)((double)y * L.sc[l]);
-        kp[2] = (float)(31.0 * L.sc[l]);
-        kp[3] = (float)ang;
-        kp[4] = (float)((double)sel_r[k] / 25.0);
-        kp[5] = (float)l;
-        unsigned words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int t = 0; t < 256; ++t) {
+        if (lane == 0) {
+            double ang = atan2((double)m01, (double)m10) * (180.0 / 3.14159265358979323846);
+            if (ang < 0.0) ang += 360.0;
+            float* kp = slot_kp + 6 * o;
+            kp[0] = (float)((double)x * L.sc[l]);
+            kp[1] = (float)((double)y * L.sc[l]);
+            kp[2] = (float)(31.0 * L.sc[l]);
+            kp[3] = (float)ang;
+            kp[4] = (float)((double)sel_r[k] / 25.0);
+            kp[5] = (float)l;
+        }
+        unsigned words[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = 64 * j + lane;
             int q[4];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
@@ -528,11 +566,15 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
             }
             const int i1 = bl[(size_t)(y + q[1]) * pw + x + q[0]];
             const int i2 = bl[(size_t)(y + q[3]) * pw + x + q[2]];
-            if (i1 < i2) words[t >> 5] |= 1u << (t & 31);
+            const unsigned long long bits = __ballot(i1 < i2);
+            words[2 * j] = (unsigned)bits;
+            words[2 * j + 1] = (unsigned)(bits >> 32);
         }
-        uint4* d = (uint4*)(slot_desc + 32 * o);
-        d[0] = make_uint4(words[0], words[1], words[2], words[3]);
-        d[1] = make_uint4(words[4], words[5], words[6], words[7]);
+        if (lane == 0) {
+            uint4* d = (uint4*)(slot_desc + 32 * o);
+            d[0] = make_uint4(words[0], words[1], words[2], words[3]);
+            d[1] = make_uint4(words[4], words[5], words[6], words[7]);
+        }
     }
     if (tid == 0) lvl_count[img * L.nlev + l] = n2;
 }
