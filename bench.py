@@ -256,6 +256,16 @@ def main():
                                "pruning skips part of it (executed_frac_estimate)",
                        "executed_frac_estimate": r_exec}},
     }
+    # step-level fraction = sum of the stages' roofline times / measured step time
+    # (K1 at the dense-i8 peak; K2 at the f32 VALU peak on the executed share of the work)
+    t_k1 = run.k1_ops / (PEAK_I8_TOPS * 1e12)
+    t_k2 = r_alg * r_exec / (PEAK_F32_VALU_TFLOPS * 1e12)
+    step_s = elapsed / args.steps
+    result["step_roofline"] = {
+        "frac": (t_k1 + t_k2) / step_s, "k1_ideal_ms": t_k1 * 1e3, "k2_ideal_ms": t_k2 * 1e3,
+        "step_ms": step_s * 1e3,
+        "note": "sum of stage roofline times / measured step; K2 ideal on the executed "
+                "(pruned) share of the algorithmic flops"}
 
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
