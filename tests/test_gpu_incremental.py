@@ -51,3 +51,26 @@ def test_incremental_reconstruction_matches_truth():
     s, Rm, t = _umeyama(c_est, c_true)
     aligned = (s * (Rm @ c_est.T)).T + t
     assert np.abs(aligned - c_true).max() < 0.02 * 8.0   # 2 % of the ring radius
+
+
+def test_incremental_reconstruction_cfg5_scale():
+    """BASELINE cfg5 scale on one GPU: 500 images x 4096 keypoints, all 124 750 pairs matched and
+    verified, tracks, registration, triangulation and LM bundle adjustment (DESIGN 4.9;
+    profiles/r02/incremental_500x4096.json)."""
+    n_img = 500
+    scene = synth.make_scene(n_img, 4096, seed=21, k1_range=0.02)
+    intr = np.c_[scene["cams"][:, 6:8], scene["pp"]]
+    rec = incremental.reconstruct(scene["desc"], scene["kps"], scene["n_kp"], intr)
+    assert rec.registered.all()
+    tptr, timg, tkp = rec.tracks
+    obs_track = np.repeat(np.arange(len(tptr) - 1), np.diff(tptr))
+    use = rec.has_point[obs_track]
+    assert use.sum() > 10000
+    pts_ids, pt_idx = np.unique(obs_track[use], return_inverse=True)
+    err = R.reprojection_errors(rec.cams, scene["pp"], rec.points[pts_ids], timg[use],
+                                pt_idx.astype(np.int32), scene["kps"][timg[use], tkp[use]])
+    assert np.median(err) < 0.8                       # px; keypoint noise sigma 0.5 px
+    c_est, c_true = _centres(rec.cams), _centres(scene["cams"])
+    s, Rm, t = _umeyama(c_est, c_true)
+    aligned = (s * (Rm @ c_est.T)).T + t
+    assert np.abs(aligned - c_true).max() < 0.005 * 8.0   # 0.5 % of the ring radius
