@@ -38,6 +38,9 @@ sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracl
 
 # MI355X dense peaks (MI355X_MICROARCH.md): i8 MFMA 2x bf16 = 2048 op/clk/SIMD * 1024 SIMD * 2.4 GHz
 PEAK_I8_TOPS = 2048 * 4 * 256 * 2.4e9 / 1e12        # 5033 TOP/s
+# practical dense-i8 ceiling of this chip: MFMA-only loop, random register operands, every CU busy
+# (the clock drops to 1.71-1.74 GHz: 3460-3480 TOP/s = 69 % of nominal; tools/mfma_peak.hip)
+PRACTICAL_I8_TOPS = 3470.0
 PEAK_F32_VALU_TFLOPS = 157.3
 RANSAC_FLOP_PER_EVAL = 33      # Sampson test: 16 fma + 1 mul (ransac.hip sampson_inlier)
 RANSAC_FLOP_PER_FIT = 1400     # sample + fit_f8
@@ -244,7 +247,11 @@ def main():
                      "traffic": pmc_traffic("mfma_mutual_kernel", args.config, n_img, k, world),
                      "traffic_unit": f"HBM bytes per step (all launches), PMC, "
                                      f"profiles/traffic_{args.config}.json",
-                     "ms": match_ms, "ops_per_step": run.k1_ops},
+                     "ms": match_ms, "ops_per_step": run.k1_ops,
+                     "practical_peak": PRACTICAL_I8_TOPS,
+                     "frac_of_practical": k1_tops / PRACTICAL_I8_TOPS,
+                     "practical_peak_note": "i8 MFMA-only loop on random operands holds 1.71 GHz "
+                                            "(profiles/r02/mfma_peak_i8.json, tools/mfma_peak.hip)"},
         "stages": {"match_ms": match_ms, "ransac_ms": ransac_ms,
                    "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,
                    "ransac_roofline": {
@@ -429,6 +436,7 @@ def cfg3_side(n_hyp, chunk):
             "value": graph.shape[0] * 10 / el, "unit": "verified matches/s",
             "ms_per_step": el / 10 * 1e3, "match_ms": m, "ransac_ms": r,
             "k1_roofline": {"achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOP/s (i8)",
+                            "frac_of_practical": tops / PRACTICAL_I8_TOPS,
                             "frac": tops / PEAK_I8_TOPS,
                             "traffic": pmc_traffic("mfma_mutual_kernel", "cfg3", 50, 2048, 1)}}
 
