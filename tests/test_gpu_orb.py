@@ -48,6 +48,16 @@ def test_orb_full_hd_and_parameters(ctx):
     assert _check(img[0], kp[0], desc[0], cnt[0], **kw) > 900
 
 
+@pytest.mark.parametrize("hw", [(257, 331), (719, 1283)])
+def test_orb_odd_sizes(ctx, hw):
+    """Widths and heights that are no multiple of the 64 x 32 tiles or the 64-B level pitch, two
+    images per batch."""
+    imgs = np.stack([synth.make_image(*hw, seed=s) for s in (21, 22)])
+    kp, desc, cnt = _gpu_orb(ctx, imgs)
+    for i in range(len(imgs)):
+        assert _check(imgs[i], kp[i], desc[i], cnt[i]) > 0
+
+
 @pytest.mark.parametrize("hw", [(100, 80), (61, 70), (40, 40)])
 def test_orb_small_images(ctx, hw):
     """Levels without room inside the 31-pixel border detect nothing (fewer keypoints or 0)."""

@@ -1,4 +1,5 @@
-// Practical ceiling of v_mfma_i32_32x32x32_i8 on this MI355X: every CU busy
+// Practical ceilings on this MI355X: v_mfma_i32_32x32x32_i8 (K1) and packed f32
+// FMA on the VALU (v_pk_fma_f32, K2 §4.2).  MFMA: every CU busy
 // with MFMA-only waves (operands in registers, no memory in the loop), on random and on zero
 // operands, 1 and 2 waves per SIMD.  Reports TOP/s against the nominal 5033 TOP/s dense-i8 peak
 // and the in-kernel clock (s_memtime / s_memrealtime, MI355X_MICROARCH.md "DVFS give-back" 6).
@@ -37,6 +38,35 @@ __global__ __launch_bounds__(256) void mfma_loop(const int* __restrict__ src, in
     int r = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) r += acc0[k] ^ acc1[k] ^ acc2[k] ^ acc3[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+    if (threadIdx.x == 0) {
+        unsigned long long* d = stamps + 4 * blockIdx.x;
+        d[0] = t0c; d[1] = t0r; d[2] = t1c; d[3] = t1r;
+    }
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+// 8 independent v_pk_fma_f32 chains per lane (x = x * m + c keeps the values bounded)
+__global__ __launch_bounds__(256) void pkfma_loop(const float* __restrict__ src, int iters,
+                                                  float* __restrict__ out,
+                                                  unsigned long long* __restrict__ stamps) {
+    const int lane = threadIdx.x & 63;
+    f2v x[8], m, c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = f2v{src[(lane * 8 + k) & 4095], src[(lane * 8 + k + 7) & 4095]};
+    m = f2v{0.999f, 0.998f};
+    c = f2v{src[lane & 4095] * 1e-3f, src[(lane + 1) & 4095] * 1e-3f};
+    const unsigned long long t0c = __builtin_amdgcn_s_memtime(), t0r = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = __builtin_elementwise_fma(x[k], m, c);
+    }
+    const unsigned long long t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
+    float r = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r += x[k].x + x[k].y;
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
     if (threadIdx.x == 0) {
         unsigned long long* d = stamps + 4 * blockIdx.x;
@@ -96,6 +126,43 @@ int main(int argc, char** argv) {
                    first ? "" : ", ", data ? "zero" : "random", wps, ms, tops, tops / 5033.1648,
                    clk / 1e9, tops / (2048.0 * 4 * dev_cu * clk / 1e12));
             first = false;
+        }
+    }
+    {   // packed f32 FMA on the VALU, random operands, 2 and 8 waves per SIMD
+        std::vector<float> hf(4096);
+        srand(9);
+        for (auto& v : hf) v = (float)rand() / RAND_MAX;
+        float* fsrc;
+        (void)hipMalloc(&fsrc, hf.size() * 4);
+        (void)hipMemcpy(fsrc, hf.data(), hf.size() * 4, hipMemcpyHostToDevice);
+        const int fit = iters * 2;
+        for (int wps : {2, 8}) {
+            const int blocks = dev_cu * wps;
+            for (int rep = 0; rep < 3; ++rep)
+                hipLaunchKernelGGL(pkfma_loop, dim3(blocks), dim3(256), 0, 0, fsrc, fit, (float*)out, st);
+            (void)hipDeviceSynchronize();
+            float ms_sum = 0;
+            int n = 0;
+            (void)hipEventRecord(e0, 0);
+            do {
+                hipLaunchKernelGGL(pkfma_loop, dim3(blocks), dim3(256), 0, 0, fsrc, fit, (float*)out, st);
+                ++n;
+                (void)hipEventRecord(e1, 0);
+                (void)hipEventSynchronize(e1);
+                (void)hipEventElapsedTime(&ms_sum, e0, e1);
+            } while (ms_sum < 2500.0);
+            const double ms = ms_sum / n;
+            std::vector<unsigned long long> s(4 * blocks);
+            (void)hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost);
+            double clk = 0;
+            for (int b = 0; b < blocks; ++b)
+                clk += (double)(s[4 * b + 2] - s[4 * b]) / ((double)(s[4 * b + 3] - s[4 * b + 1]) / 100e6);
+            clk /= blocks;
+            const double flops = 4.0 * 16 * 8 * (double)fit * 256 * blocks;  // 2 fma x 2 flop per pk
+            const double tf = flops / (ms * 1e-3) / 1e12;
+            printf(", {\"op\": \"v_pk_fma_f32\", \"waves_per_simd\": %d, \"launch_ms\": %.4f, "
+                   "\"TFLOPS\": %.1f, \"frac_of_157.3\": %.4f, \"clock_GHz\": %.3f}",
+                   wps, ms, tf, tf / 157.3, clk / 1e9);
         }
     }
     printf("]\n");
