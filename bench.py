@@ -38,9 +38,11 @@ sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd"), os.path.join(ROOT, "oracl
 
 # MI355X dense peaks (MI355X_MICROARCH.md): i8 MFMA 2x bf16 = 2048 op/clk/SIMD * 1024 SIMD * 2.4 GHz
 PEAK_I8_TOPS = 2048 * 4 * 256 * 2.4e9 / 1e12        # 5033 TOP/s
-# practical dense-i8 ceiling of this chip: MFMA-only loop, random register operands, every CU busy
-# (the clock drops to 1.71-1.74 GHz: 3460-3480 TOP/s = 69 % of nominal; tools/mfma_peak.hip)
-PRACTICAL_I8_TOPS = 3470.0
+# practical ceilings of this chip (tools/mfma_peak.hip, profiles/r02/mfma_peak_i8.json): i8
+# MFMA-only loop on random register operands, every CU busy — the clock drops to 1.71-1.78 GHz,
+# 3460-3514 TOP/s = 69-70 % of nominal; v_pk_fma_f32 loop 141 TFLOP/s = 90 % of 157.3
+PRACTICAL_I8_TOPS = 3490.0
+PRACTICAL_F32_VALU_TFLOPS = 141.0
 PEAK_F32_VALU_TFLOPS = 157.3
 RANSAC_FLOP_PER_EVAL = 33      # Sampson test: 16 fma + 1 mul (ransac.hip sampson_inlier)
 RANSAC_FLOP_PER_FIT = 1400     # sample + fit_f8
@@ -250,7 +252,7 @@ def main():
                      "ms": match_ms, "ops_per_step": run.k1_ops,
                      "practical_peak": PRACTICAL_I8_TOPS,
                      "frac_of_practical": k1_tops / PRACTICAL_I8_TOPS,
-                     "practical_peak_note": "i8 MFMA-only loop on random operands holds 1.71 GHz "
+                     "practical_peak_note": "i8 MFMA-only loop on random operands holds ~1.75 GHz "
                                             "(profiles/r02/mfma_peak_i8.json, tools/mfma_peak.hip)"},
         "stages": {"match_ms": match_ms, "ransac_ms": ransac_ms,
                    "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,
@@ -261,7 +263,10 @@ def main():
                        "flops_per_step": r_alg,
                        "note": "algorithmic = every hypothesis scored on every match; the exact "
                                "pruning skips part of it (executed_frac_estimate)",
-                       "executed_frac_estimate": r_exec}},
+                       "executed_frac_estimate": r_exec,
+                       "practical_peak": PRACTICAL_F32_VALU_TFLOPS,
+                       "executed_frac_of_practical":
+                           r_alg * r_exec / (ransac_ms * 1e-3) / 1e12 / PRACTICAL_F32_VALU_TFLOPS}},
     }
     # step-level fraction = sum of the stages' roofline times / measured step time
     # (K1 at the dense-i8 peak; K2 at the f32 VALU peak on the executed share of the work)
