@@ -258,18 +258,81 @@ def extract_and_match(gray1, gray2):
     return match_descriptors(des1, des2, "hamming", True, REFERENCE_MAX_HAMMING)
 
 
+_RING3 = None
+
+
+def _ring3():
+    """Offsets of a radius-3 circle outline (midpoint rule), as cv2.circle draws it."""
+    global _RING3
+    if _RING3 is None:
+        pts = set()
+        x, y, d = 0, 3, 1 - 3
+        while x <= y:
+            for sx, sy in ((x, y), (y, x)):
+                for a, b in ((sx, sy), (-sx, sy), (sx, -sy), (-sx, -sy)):
+                    pts.add((a, b))
+            if d < 0:
+                d += 2 * x + 3
+            else:
+                d += 2 * (x - y) + 5
+                y -= 1
+            x += 1
+        _RING3 = np.array(sorted(pts), np.int64)
+    return _RING3
+
+
+def draw_matches(gray1, kp1, gray2, kp2, matches, seed: int = 0):
+    """numpy restatement of cv2.drawMatches(..., flags=NOT_DRAW_SINGLE_POINTS) for the debug path
+    of code/feature_matching.py:34-35: the two images side by side (RGB), each match a random
+    colour, a radius-3 circle at both keypoints and a 1-pixel line between them.  Returns
+    uint8 [max(h1, h2), w1 + w2, 3]."""
+    g1, g2 = np.asarray(gray1, np.uint8), np.asarray(gray2, np.uint8)
+    h1, w1 = g1.shape[:2]
+    h2, w2 = g2.shape[:2]
+    out = np.zeros((max(h1, h2), w1 + w2, 3), np.uint8)
+    out[:h1, :w1] = g1[..., None] if g1.ndim == 2 else g1
+    out[:h2, w1:] = g2[..., None] if g2.ndim == 2 else g2
+    H, W = out.shape[:2]
+    rng = np.random.default_rng(seed)
+    ring = _ring3()
+
+    def put(xs, ys, col):
+        ok = (xs >= 0) & (xs < W) & (ys >= 0) & (ys < H)
+        out[ys[ok], xs[ok]] = col
+
+    for m in matches:
+        col = rng.integers(0, 256, 3, dtype=np.uint8)
+        x1, y1 = (int(round(v)) for v in kp1[m.queryIdx].pt)
+        x2, y2 = (int(round(v)) for v in kp2[m.trainIdx].pt)
+        x2 += w1
+        n = max(abs(x2 - x1), abs(y2 - y1)) + 1
+        t = np.linspace(0.0, 1.0, n)
+        put(np.rint(x1 + (x2 - x1) * t).astype(np.int64), np.rint(y1 + (y2 - y1) * t).astype(np.int64),
+            col)
+        for cx, cy in ((x1, y1), (x2, y2)):
+            put(cx + ring[:, 0], cy + ring[:, 1], col)
+    return out
+
+
 def extract_and_match_draw(gray1, gray2):
-    """code/feature_matching.py:15-37: as extract_and_match, then draws the matches (the drawing
-    needs cv2 and matplotlib)."""
-    _require_cv2("extract_and_match_draw")
-    import matplotlib.pyplot as plt
+    """code/feature_matching.py:15-37: as extract_and_match, then draws the matches
+    (cv2.drawMatches when cv2 is present, else the numpy draw_matches) and shows them with
+    matplotlib (a no-op on a headless backend).  Returns the cropped matches."""
     kp1, des1 = detect_and_compute(gray1)
     kp2, des2 = detect_and_compute(gray2)
     cropped = match_descriptors(des1, des2, "hamming", True, REFERENCE_MAX_HAMMING)
-    ck1 = [cv2.KeyPoint(k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave) for k in kp1]
-    ck2 = [cv2.KeyPoint(k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave) for k in kp2]
-    cvm = [cv2.DMatch(m.queryIdx, m.trainIdx, m.imgIdx, m.distance) for m in cropped]
-    img = cv2.drawMatches(gray1, ck1, gray2, ck2, cvm, None,
-                          flags=cv2.DrawMatchesFlags_NOT_DRAW_SINGLE_POINTS)
-    plt.imshow(img), plt.show()
+    if cv2 is not None:
+        ck1 = [cv2.KeyPoint(k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave) for k in kp1]
+        ck2 = [cv2.KeyPoint(k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave) for k in kp2]
+        cvm = [cv2.DMatch(m.queryIdx, m.trainIdx, m.imgIdx, m.distance) for m in cropped]
+        img = cv2.drawMatches(gray1, ck1, gray2, ck2, cvm, None,
+                              flags=cv2.DrawMatchesFlags_NOT_DRAW_SINGLE_POINTS)
+    else:
+        img = draw_matches(gray1, kp1, gray2, kp2, cropped)
+    try:
+        import matplotlib.pyplot as plt
+    except ImportError:  # drawing is a debug aid only
+        plt = None
+    if plt is not None:
+        plt.imshow(img), plt.show()
     return cropped

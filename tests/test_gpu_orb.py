@@ -107,3 +107,18 @@ def test_extract_and_match_on_gpu_without_cv2():
     ok = sum(abs(kp1[m.queryIdx].pt[0] - 17 - kp2[m.trainIdx].pt[0]) < 1.5
              and abs(kp1[m.queryIdx].pt[1] - kp2[m.trainIdx].pt[1]) < 1.5 for m in ms)
     assert ok > 0.85 * len(ms)   # the rest: repeated texture and the replicated right margin
+
+
+def test_extract_and_match_draw_without_cv2(monkeypatch):
+    """The reference's debug entry (code/feature_matching.py:15-37) on the GPU with the numpy
+    drawMatches: the same matches as extract_and_match, and the drawing shown (headless)."""
+    import feature_matching as fm
+    shown = []
+    import matplotlib.pyplot as plt
+    monkeypatch.setattr(plt, "show", lambda *a, **k: shown.append(True))
+    img = synth.make_image(480, 640, seed=5)
+    sh = np.zeros_like(img)
+    sh[:, :-17] = img[:, 17:]
+    ms = fm.extract_and_match_draw(img, sh)
+    assert ms == fm.extract_and_match(img, sh) and len(ms) > 100
+    assert shown

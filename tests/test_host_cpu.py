@@ -141,3 +141,22 @@ def test_pair_record_and_pipeline_entry_need_the_gpu():
     if not torch.cuda.is_available():
         with pytest.raises(sfmcore.SfmCoreError):
             fm.pipeline_pair_matches([np.zeros((8, 8), np.uint8)] * 2)
+
+
+def test_draw_matches_numpy():
+    """numpy drawMatches (the cv2-free debug path): canvas layout, circles and line pixels in the
+    match colour, single points not drawn."""
+    import numpy as np
+    import feature_matching as fm
+    g1 = np.full((40, 50), 10, np.uint8)
+    g2 = np.full((60, 30), 200, np.uint8)
+    kp1 = [fm.KeyPoint(10, 20, 31), fm.KeyPoint(40, 5, 31)]
+    kp2 = [fm.KeyPoint(5, 50, 31), fm.KeyPoint(20, 10, 31)]
+    img = fm.draw_matches(g1, kp1, g2, kp2, [fm.DMatch(0, 1, 0, 3.0)])
+    assert img.shape == (60, 80, 3) and img.dtype == np.uint8
+    assert (img[50:, :50] == 0).all()                     # below image 1: empty
+    col = img[20, 13]                                     # ring point (r = 3) right of kp1[0]
+    assert not (col == 10).all()
+    assert (img[10, 50 + 23] == col).all()                # ring of kp2[1] (shifted by w1 = 50)
+    assert (img[15, 41] == col).all()                     # on the line (10,20) -> (70,10)
+    assert (img[5, 43] == 10).all() and (img[50, 58] == 200).all()  # unmatched points not drawn
