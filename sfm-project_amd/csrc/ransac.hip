@@ -312,11 +312,15 @@ __device__ __forceinline__ int sampson_inlier2(const float G[9], f2 x1, f2 y1, f
 // pair's scoring planes are read through ONE L2 (with grid (P, H/256) and P = 1 mod 8, as at
 // cfg3, every pair's 16 blocks landed on all 8 XCDs) and every pair's first (best-previewed)
 // block still runs before any second block.  Returns false for the padding blocks.
-__device__ __forceinline__ bool xcd_pair_block(int n_pairs, int& p, int& hb) {
+__device__ __forceinline__ bool xcd_pair_block(int n_pairs, int n_hb, int gp, int& p, int& hb) {
     const int Q = (n_pairs + 7) >> 3;
     const int x = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
-    hb = j / Q;
-    p = x * Q + (j - hb * Q);
+    // the XCD's pairs in groups of gp, hb-major inside a group: the best-previewed block of a pair
+    // still runs first, and the group's match planes stay in the XCD's L2 while its blocks run
+    const int g = j / (gp * n_hb), r = j - g * gp * n_hb;
+    const int gsz = min(gp, Q - g * gp);
+    hb = r / gsz;
+    p = x * Q + g * gp + (r - hb * gsz);
     return p < n_pairs;
 }
 static inline unsigned xcd_grid(int n_pairs, int n_hb) { return 8u * (unsigned)((n_pairs + 7) >> 3) * (unsigned)n_hb; }
@@ -400,13 +404,14 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
 // Exact pruning only removes a wave once every lane is provably beaten, so it pays most when the
 // strong hypotheses are scored first and the weak ones end up together in the same waves.
 //   ransac_fit_kernel    lane per hypothesis: sample + fit, Sampson count over the first PV matches
-//                        (the "preview", same op sequence), G to a [pair][9][H] table.
+//                        (the "preview", same op sequence), G + preview to a [pair][H] record table.
 //   ransac_order_kernel  block per pair: counting sort of the hypotheses by preview count,
 //                        descending (order within a bucket is irrelevant: the winner key carries h).
 //   ransac_score_kernel  rank r of pair p scores hypothesis order[p][r] from match PV on, starting
 //                        from its preview count, with the same exact pruning; grid x = pair so the
 //                        best-previewed block of every pair runs first and publishes a strong bound.
 constexpr int PV = 64;  // preview matches (multiple of CH)
+constexpr int HREC = 12;  // hypothesis record: G[9], preview count (int bits), 2 pad floats
 
 // counts inliers of G over matches [m, mend) into cnt; with PRUNE checks the published bound every
 // PRUNE_EVERY matches and returns false (wave-uniform) when no lane can still win.
@@ -444,9 +449,9 @@ __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[
 __global__ __launch_bounds__(256) void ransac_fit_kernel(
     int n_pairs, int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
     const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
-    int n_hyp, float* __restrict__ hypG, int32_t* __restrict__ prev) {
+    int n_hyp, int gp, float* __restrict__ hypG, int32_t* __restrict__ prev) {
     int p, hb;
-    if (!xcd_pair_block(n_pairs, p, hb)) return;
+    if (!xcd_pair_block(n_pairs, n_hyp >> 8, gp, p, hb)) return;
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int kp = plane_len(k_max);
@@ -477,10 +482,12 @@ __global__ __launch_bounds__(256) void ransac_fit_kernel(
 #ifndef RANSAC_ABL_NOPREVIEW  // ablation: no preview (timing only; order degenerates)
     score_matches<false, 8>(S, kp, G, 0, min(PV, M), M, cnt, nullptr);  // 8-match chunks: fewer VGPRs beside the fit
 #endif
-    float* gt = hypG + (size_t)p * 9 * n_hyp + h;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) gt[(size_t)i * n_hyp] = G[i];
-    prev[(size_t)p * n_hyp + h] = ok ? cnt : -1;
+    const int pc = ok ? cnt : -1;
+    float4* rec = (float4*)(hypG + ((size_t)p * n_hyp + h) * HREC);
+    rec[0] = make_float4(G[0], G[1], G[2], G[3]);
+    rec[1] = make_float4(G[4], G[5], G[6], G[7]);
+    rec[2] = make_float4(G[8], __int_as_float(pc), 0.0f, 0.0f);
+    prev[(size_t)p * n_hyp + h] = pc;  // also dense, for the order kernel's coalesced read
 }
 
 // 256 threads per pair: every block of a launch is resident at once (the kernel is latency-bound)
@@ -513,21 +520,21 @@ __global__ __launch_bounds__(256) void ransac_order_kernel(int n_hyp,
 template <bool PRUNE, bool COUNTS = false>
 __global__ __launch_bounds__(256) void ransac_score_kernel(
     int n_pairs, int k_max, const int32_t* __restrict__ match_count,
-    const float* __restrict__ planes, int n_hyp, const float* __restrict__ hypG,
-    const int32_t* __restrict__ prev, const uint16_t* __restrict__ order,
-    unsigned long long* __restrict__ best, int32_t* __restrict__ out_counts = nullptr) {
+    const float* __restrict__ planes, int n_hyp, int gp, const float* __restrict__ hypG,
+    const uint16_t* __restrict__ order, unsigned long long* __restrict__ best, int32_t* __restrict__ out_counts = nullptr) {
     int p, hb;
-    if (!xcd_pair_block(n_pairs, p, hb)) return;
+    if (!xcd_pair_block(n_pairs, n_hyp >> 8, gp, p, hb)) return;
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int kp = plane_len(k_max);
     const cfloat_p S = (cfloat_p)(planes + (size_t)p * 8 * kp + 4 * kp);
     const uint32_t h = order[(size_t)p * n_hyp + hb * 256 + threadIdx.x];
-    const float* gt = hypG + (size_t)p * 9 * n_hyp + h;
-    float G[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) G[i] = gt[(size_t)i * n_hyp];
-    const int pc = prev[(size_t)p * n_hyp + h];
+    // h is a permutation of the pair's hypotheses: one 48-byte record per hypothesis keeps the
+    // lane's fetch to 1-2 cache lines (a [9][H] table scattered it over 9; PMC)
+    const float4* rec = (const float4*)(hypG + ((size_t)p * n_hyp + h) * HREC);
+    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+    const float G[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+    const int pc = __float_as_int(r2.y);
     int cnt = max(pc, 0);
     if (M > PV && !score_matches<PRUNE>(S, kp, G, PV, M, M, cnt, best + p)) return;
     if (pc < 0) cnt = -1;
@@ -606,6 +613,17 @@ static int ransac_mode() {
     return (v < 0 || v > 2) ? 0 : v;
 }
 
+// Pairs per XCD group of the ordered schedule (xcd_pair_block).  Measured (profiles/r02/
+// ransac_group_ab.txt): groups of 64 -3.9 % K2 at cfg4 (244 pairs per XCD per launch; the group's
+// planes stay in L2), +1-2 % at cfg3 (154 per XCD; bounds publish later) -> 64 above 192 pairs
+// per XCD, one group below.  SFM_RANSAC_GROUP overrides (A/B only).
+static int ransac_group(int n_pairs) {
+    const int q = std::max((n_pairs + 7) >> 3, 1);
+    const char* e = getenv("SFM_RANSAC_GROUP");
+    const int v = e ? atoi(e) : (q > 192 ? 64 : q);
+    return (v <= 0 || v > q) ? q : v;
+}
+
 namespace {
 struct RansacWs {
     float* planes;
@@ -618,7 +636,7 @@ struct RansacWs {
 int ransac_ws(sfm_ctx* ctx, int n_pairs, int kp, int H, bool ordered, RansacWs& w) {
     const size_t plb = sfm::align_up((size_t)n_pairs * 8 * kp * sizeof(float), 256);
     const size_t bb = sfm::align_up((size_t)n_pairs * sizeof(unsigned long long), 256);
-    const size_t gb = ordered ? sfm::align_up((size_t)n_pairs * 9 * H * sizeof(float), 256) : 0;
+    const size_t gb = ordered ? sfm::align_up((size_t)n_pairs * HREC * H * sizeof(float), 256) : 0;
     const size_t vb = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(int32_t), 256) : 0;
     const size_t ob = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(uint16_t), 256) : 0;
     char* ws = (char*)sfm::workspace(ctx, plb + bb + gb + vb + ob + 1024);
@@ -669,14 +687,15 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
     const dim3 grid(n_pairs, H / 256);
     if (ordered) {
         const dim3 xgrid(xcd_grid(n_pairs, H / 256));
+        const int gp = ransac_group(n_pairs);
         hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
-                           match_count, w.planes, out_norm, prm->seed, prm->thr, H, w.hypG, w.prev);
+                           match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG, w.prev);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                            w.prev, w.order);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(ransac_score_kernel<true>, xgrid, dim3(256), 0, st, n_pairs, k_max,
-                           match_count, w.planes, H, w.hypG, w.prev, w.order, w.best);
+                           match_count, w.planes, H, gp, w.hypG, w.order, w.best);
     } else if (mode == 1) {
         hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
                            match_count, w.planes, out_norm, prm->seed, prm->thr, w.best);
@@ -712,14 +731,15 @@ extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, 
                        match_count, matches, prm->thr, w.planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 xgrid(xcd_grid(n_pairs, H / 256));
+    const int gp = ransac_group(n_pairs);
     hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
-                       match_count, w.planes, out_norm, prm->seed, prm->thr, H, w.hypG, w.prev);
+                       match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG, w.prev);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                        w.prev, w.order);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL((ransac_score_kernel<false, true>), xgrid, dim3(256), 0, st, n_pairs, k_max,
-                       match_count, w.planes, H, w.hypG, w.prev, w.order, w.best, out_counts);
+                       match_count, w.planes, H, gp, w.hypG, w.order, w.best, out_counts);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
