@@ -262,7 +262,8 @@ def main():
                        "frac": r_alg / (ransac_ms * 1e-3) / 1e12 / PEAK_F32_VALU_TFLOPS,
                        "flops_per_step": r_alg,
                        "note": "algorithmic = every hypothesis scored on every match; the exact "
-                               "pruning skips part of it (executed_frac_estimate)",
+                               "pruning skips part of it (executed_frac_estimate: PMC-measured "
+                               "on a cfg4 pair sample, profiles/r02/pmc_ransac_exec_cfg4.txt)",
                        "executed_frac_estimate": r_exec,
                        "practical_peak": PRACTICAL_F32_VALU_TFLOPS,
                        "executed_frac_of_practical":
@@ -296,7 +297,10 @@ def main():
 
 def ransac_flops(run, n_hyp):
     """Algorithmic K2 flops per step (every hypothesis on every match of pairs with >= 8
-    matches) and the executed fraction estimated from the pruning simulation."""
+    matches) and the executed fraction of the scoring: 0.586 measured on a 2048-pair stride sample
+    of the cfg4 scene (SQ_INSTS_VALU of the pruned vs the unpruned score kernel,
+    tools/pmc_ransac_exec.sh, profiles/r02/pmc_ransac_exec_cfg4.txt); 0.59 in the cfg3 pruning
+    simulation."""
     import numpy as np
     cnt = np.concatenate([run.gb._buffers(pt.shape[0])["match"][0].cpu().numpy()
                           for _, pt in run.chunks[-1:]])
@@ -305,7 +309,7 @@ def ransac_flops(run, n_hyp):
     n_pairs = sum(pt.shape[0] for _, pt in run.chunks)
     m = np.where(cnt >= 8, cnt, 0).astype(np.float64)
     per_pair = n_hyp * float(np.mean(m * RANSAC_FLOP_PER_EVAL + (m > 0) * RANSAC_FLOP_PER_FIT))
-    return per_pair * n_pairs, 0.59
+    return per_pair * n_pairs, 0.586
 
 
 def cpu_baseline(scene, pairs, lo, hi, graph, gb, seconds, n_hyp):
