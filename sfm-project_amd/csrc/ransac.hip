@@ -410,7 +410,10 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
 //   ransac_score_kernel  rank r of pair p scores hypothesis order[p][r] from match PV on, starting
 //                        from its preview count, with the same exact pruning; grid x = pair so the
 //                        best-previewed block of every pair runs first and publishes a strong bound.
-constexpr int PV = 64;  // preview matches (multiple of CH)
+#ifndef RANSAC_PV
+#define RANSAC_PV 64
+#endif
+constexpr int PV = RANSAC_PV;  // preview matches (multiple of CH and of 8)
 constexpr int HREC = 12;  // hypothesis record: G[9], preview count (int bits), 2 pad floats
 
 // counts inliers of G over matches [m, mend) into cnt; with PRUNE checks the published bound every
