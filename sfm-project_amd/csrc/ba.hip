@@ -83,9 +83,13 @@ __device__ __forceinline__ void linearize(const double (&R)[9], const double* __
 constexpr int NV = 10;      // per-observation point terms: V upper triangle (6), g_p (3), 0.5 rho
 constexpr int NU = 36 + 8;  // upper triangle of U_c (8x8) + g_c
 #ifndef CAM_MLP
-#define CAM_MLP 4  // observations whose gathers a camera-wave lane keeps in flight
+#define CAM_MLP 2  // observations whose gathers a camera-wave lane keeps in flight (2: 196 VGPRs,
+                   // 60.3 us vs 61-62 with 4 at 220 VGPRs, profiles/r02/k3_ba_ab.txt)
 #endif
-constexpr int SPLIT_TARGET = 256;  // camera waves wanted (splits per camera = this / n_cam); more only
+#ifndef BA_SPLIT_TARGET
+#define BA_SPLIT_TARGET 256
+#endif
+constexpr int SPLIT_TARGET = BA_SPLIT_TARGET;  // camera waves wanted (splits per camera = this / n_cam); more only
                                    // add reduction work (block-per-camera version at 500 cameras:
                                    // 2 splits 90 us, 4 splits 113 us vs 1 split 69 us)
 

@@ -148,6 +148,36 @@ def test_ransac_schedules_agree(ctx):
             np.testing.assert_array_equal(o["mask"][p, :cnt[p]], outs[0][2]["mask"][p, :cnt[p]])
 
 
+def test_ransac_pair_groups_agree(ctx):
+    """The ordered schedule's pair groups per XCD (ransac.hip xcd_pair_block / ransac_group;
+    SFM_RANSAC_GROUP) only change the block order: 465 pairs (59 per XCD, the last XCD short) with
+    groups of 1, 5, 7 and 64 (one group) give identical outputs, and a sample matches the oracle."""
+    import os
+    s = synth.make_scene(31, 512, seed=21)
+    pairs = synth.unordered_pairs(31)
+    outs = []
+    old = os.environ.get("SFM_RANSAC_GROUP")
+    try:
+        for g in ("64", "1", "5", "7"):
+            os.environ["SFM_RANSAC_GROUP"] = g
+            outs.append(_run(ctx, s, pairs, H=512))
+    finally:
+        if old is None:
+            os.environ.pop("SFM_RANSAC_GROUP", None)
+        else:
+            os.environ["SFM_RANSAC_GROUP"] = old
+    cnt, mt, ref = outs[0]
+    for _, _, o in outs[1:]:
+        for k in ("inl_count", "best_h", "F"):
+            np.testing.assert_array_equal(o[k], ref[k])
+        for p in range(len(pairs)):
+            np.testing.assert_array_equal(o["mask"][p, :cnt[p]], ref["mask"][p, :cnt[p]])
+    for p in range(0, len(pairs), 37):
+        a, b = pairs[p]
+        r = _oracle(s, a, b, mt[p, :cnt[p], 0], mt[p, :cnt[p], 1], 512, 42, 1.0)
+        assert ref["inl_count"][p] == r["count"] and ref["best_h"][p] == r["best_h"]
+
+
 @pytest.mark.parametrize("thr", [1.0, 4.0, 0.25])
 def test_ransac_counts_every_hypothesis(ctx, thr):
     """EVERY hypothesis gets the f32 spec's count (sfm_ransac_counts: the score kernel without
