@@ -114,6 +114,11 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
     const int64_t tot = L.off[L.nlev];
     const size_t ib = (size_t)blockIdx.y * tot + L.off[l];
     const uint8_t* img = imgs + (size_t)blockIdx.y * H * W;
+    // the tile's uniform bases: per-lane offsets below are 32-bit
+    const size_t tb = ib + (size_t)y0 * pw + x0;
+    uint8_t* tpyr = pyr + tb;
+    int32_t* tseg = segcnt + (size_t)blockIdx.y * L.segoff[L.nlev] + L.segoff[l] +
+                    (int64_t)y0 * L.ntx[l] + tx0;
     // 1. pyramid tile with halo (clamped coordinates)
     if (l > 0) {
         for (int k = tid; k < PW + PH; k += 256) {
@@ -121,40 +126,54 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
                 const int cx = min(max(x0 - 4 + k, 0), w - 1);
                 const int32_t* m = maps + 3 * (L.mapx[l] + cx);
                 MX[k][0] = m[0]; MX[k][1] = m[1]; MX[k][2] = m[2];
-            } else {
+            } else {  // source rows as byte offsets (< 4095 * 4095 < 2^24)
                 const int r = k - PW, cy = min(max(y0 - 4 + r, 0), h - 1);
                 const int32_t* m = maps + 3 * (L.mapy[l] + cy);
-                MY[r][0] = m[0]; MY[r][1] = m[1]; MY[r][2] = m[2];
+                MY[r][0] = (int)__umul24((unsigned)m[0], (unsigned)W);
+                MY[r][1] = (int)__umul24((unsigned)m[1], (unsigned)W);
+                MY[r][2] = m[2];
             }
         }
         __syncthreads();
     }
     {   // every load of the thread issued before any is used (the fill is latency-bound)
         constexpr int PN = (PH * PW + 255) / 256;
-        int v[PN];
+        int v[PN], rr[PN], cc[PN];
+        // (row, column) of k = tid + 256 q stepped without divisions: 256 = 3 PW + 40
+        rr[0] = tid / PW;
+        cc[0] = tid - rr[0] * PW;
+#pragma unroll
+        for (int q = 1; q < PN; ++q) {
+            const int c = cc[q - 1] + (256 - (256 / PW) * PW);
+            const bool wrap = c >= PW;
+            cc[q] = wrap ? c - PW : c;
+            rr[q] = rr[q - 1] + 256 / PW + (wrap ? 1 : 0);
+        }
 #pragma unroll
         for (int q = 0; q < PN; ++q) {
             const int k = tid + q * 256;
             v[q] = 0;
             if (k < PH * PW) {
-                const int r = k / PW, c = k - r * PW;
+                const int r = rr[q], c = cc[q];
+                // 32-bit offsets off the image's uniform base (SGPR-base loads, no 64-bit
+                // address math per pixel); 24-bit products (every operand < 2^24: exact)
                 if (l == 0) {
                     const int cy = min(max(y0 - 4 + r, 0), h - 1), cx = min(max(x0 - 4 + c, 0), w - 1);
-                    v[q] = img[(size_t)cy * W + cx];
+                    v[q] = img[__umul24((unsigned)cy, (unsigned)W) + (unsigned)cx];
                 } else {
-                    const uint8_t* r0 = img + (size_t)MY[r][0] * W;
-                    const uint8_t* r1 = img + (size_t)MY[r][1] * W;
-                    const int wx = MX[c][2], wy = MY[r][2];
-                    const int t0 = r0[MX[c][0]] * (2048 - wx) + r0[MX[c][1]] * wx;
-                    const int t1 = r1[MX[c][0]] * (2048 - wx) + r1[MX[c][1]] * wx;
-                    v[q] = (t0 * (2048 - wy) + t1 * wy + (1 << 21)) >> 22;
+                    const unsigned o0 = (unsigned)MY[r][0], o1 = (unsigned)MY[r][1];
+                    const unsigned c0 = (unsigned)MX[c][0], c1 = (unsigned)MX[c][1];
+                    const unsigned wx = (unsigned)MX[c][2], wy = (unsigned)MY[r][2];
+                    const unsigned t0 = __umul24(img[o0 + c0], 2048u - wx) + __umul24(img[o0 + c1], wx);
+                    const unsigned t1 = __umul24(img[o1 + c0], 2048u - wx) + __umul24(img[o1 + c1], wx);
+                    v[q] = (int)((__umul24(t0, 2048u - wy) + __umul24(t1, wy) + (1u << 21)) >> 22);
                 }
             }
         }
 #pragma unroll
         for (int q = 0; q < PN; ++q) {
             const int k = tid + q * 256;
-            if (k < PH * PW) P[k / PW][k - (k / PW) * PW] = (uint8_t)v[q];
+            if (k < PH * PW) P[rr[q]][cc[q]] = (uint8_t)v[q];
         }
     }
     __syncthreads();
@@ -167,7 +186,8 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
     for (int q = 0; q < TH * TW / 1024; ++q) {
         const int k = tid + q * 256, r = k >> 4, c4 = (k & 15) * 4;
         if (y0 + r < h)
-            *(uint32_t*)(pyr + ib + (size_t)(y0 + r) * pw + x0 + c4) = *(const uint32_t*)&P[r + 4][c4 + 4];
+            *(uint32_t*)(tpyr + __umul24((unsigned)r, (unsigned)pw) + (unsigned)c4) =
+                *(const uint32_t*)&P[r + 4][c4 + 4];
     }
     {
         constexpr int HN = ((TH + 6) * TW + 255) / 256;  // 10 (the last partly)
@@ -199,11 +219,18 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
         constexpr int FT = (TH + 2) * (TW + 2), FN = (FT + 255) / 256;  // 9
         if (tid == 0) fcount = 0;
         __syncthreads();
+        int fr = tid / (TW + 2), fc = tid - fr * (TW + 2);  // stepped as in the fill
 #pragma unroll
         for (int q = 0; q < FN; ++q) {
             const int k = tid + q * 256;
+            if (q > 0) {
+                fc += 256 - (256 / (TW + 2)) * (TW + 2);
+                const bool wrap = fc >= TW + 2;
+                fc = wrap ? fc - (TW + 2) : fc;
+                fr += 256 / (TW + 2) + (wrap ? 1 : 0);
+            }
             if (k >= FT) continue;
-            const int r = k / (TW + 2), c = k - r * (TW + 2);
+            const int r = fr, c = fc;
             const int gy = y0 - 1 + r, gx = x0 - 1 + c;
             const int py = r + 3, px = c + 3;  // P coordinates of the pixel
             const int cv = P[py][px];
@@ -262,9 +289,13 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
             const bool in = y0 + r < h && x0 + c < w;
             bool keep = false;
             if (in) {
-                const int acc = 18 * hv[q][0] + 34 * hv[q][1] + 49 * hv[q][2] + 54 * hv[q][3] +
-                                49 * hv[q][4] + 34 * hv[q][5] + 18 * hv[q][6];
-                Ob[r][c] = (uint8_t)((acc + 32768) >> 16);
+                // hv <= 255 * 256: 24-bit products, the sum < 2^24 (exact)
+                const unsigned acc =
+                    __umul24((unsigned)hv[q][0], 18u) + __umul24((unsigned)hv[q][1], 34u) +
+                    __umul24((unsigned)hv[q][2], 49u) + __umul24((unsigned)hv[q][3], 54u) +
+                    __umul24((unsigned)hv[q][4], 49u) + __umul24((unsigned)hv[q][5], 34u) +
+                    __umul24((unsigned)hv[q][6], 18u);
+                Ob[r][c] = (uint8_t)((acc + 32768u) >> 16);
                 const int s0 = sv[q][4];
                 keep = s0 != 0;  // nonzero only inside the EDGE border
 #pragma unroll
@@ -274,8 +305,7 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
             On[r][c] = keep ? (uint8_t)sv[q][4] : (uint8_t)0;
             const unsigned long long m = __ballot(keep);
             if (lane == 0 && y0 + r < h)
-                segcnt[(size_t)blockIdx.y * L.segoff[L.nlev] + L.segoff[l] +
-                       (int64_t)(y0 + r) * L.ntx[l] + tx0] = __popcll(m);
+                tseg[__umul24((unsigned)r, (unsigned)L.ntx[l])] = __popcll(m);
         }
     }
     __syncthreads();
@@ -283,9 +313,9 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
     for (int q = 0; q < TH * TW / 1024; ++q) {
         const int k = tid + q * 256, r = k >> 4, c4 = (k & 15) * 4;
         if (y0 + r < h) {
-            const size_t o = ib + (size_t)(y0 + r) * pw + x0 + c4;
-            *(uint32_t*)(blur + o) = *(const uint32_t*)&Ob[r][c4];
-            *(uint32_t*)(nms + o) = *(const uint32_t*)&On[r][c4];
+            const unsigned o = __umul24((unsigned)r, (unsigned)pw) + (unsigned)c4;
+            *(uint32_t*)(blur + tb + o) = *(const uint32_t*)&Ob[r][c4];
+            *(uint32_t*)(nms + tb + o) = *(const uint32_t*)&On[r][c4];
         }
     }
 }
