@@ -69,10 +69,47 @@ class Reconstruction:
         self.gauge = None          # (reference camera, scale camera) of the initial pair
 
 
+def _match_graph(gb, pairs, pairs_t, n_kp, group):
+    """Verified graph rows [n,3] (global pair, queryIdx, trainIdx) and every pair's inlier count.
+    Under an initialised torch.distributed group (one process per GPU) each rank matches and
+    verifies its contiguous shard_range of the pairs and the packed graph is all-gathered (the
+    bench's exchange); the rows come back in pair order, so the result is the
+    single-process one, bit for bit."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if world == 1:
+        count, match, _, rs = gb.run(pairs_t)
+        return gb.graph_rows(0, count, match, rs), rs["inl_count"].cpu().numpy()
+    rank = dist.get_rank(group)
+    ranges = [match_graph.shard_range(pairs, r, world, n_kp) for r in range(world)]
+    lo, hi = ranges[rank]
+    dev = pairs_t.device
+    if hi > lo:
+        count, match, _, rs = gb.run(pairs_t[lo:hi].contiguous())
+        rows, offs = gb.graph_rows(lo, count, match, rs, return_offsets=True)
+        cnt, packed = match_graph.pack_rows(rows, offs)
+        inl_loc = rs["inl_count"]
+    else:  # more ranks than pairs
+        cnt = torch.zeros(0, dtype=torch.int32, device=dev)
+        packed = torch.zeros(0, dtype=torch.int32, device=dev)
+        inl_loc = torch.zeros(0, dtype=torch.int32, device=dev)
+    graph = match_graph.all_gather_graph(cnt, packed, ranges, group)
+    maxp = max(max(h - l for l, h in ranges), 1)
+    ipad = torch.full((maxp,), -1, dtype=torch.int32, device=dev)
+    ipad[:hi - lo] = inl_loc
+    iall = match_graph._gather(ipad, world, group)
+    inl = torch.cat([iall[r, :h - l] for r, (l, h) in enumerate(ranges)])
+    return graph, inl.cpu().numpy()
+
+
 def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
-                ba_iter=20, loss_s=2.0, device=0, log=None):
+                ba_iter=20, loss_s=2.0, device=0, log=None, group=None):
     """desc [n_img,K,D] u8, kps [n_img,K,2] pixels, n_kp [n_img], intr [n_img,4] = (f, k1, cx, cy).
-    Returns a Reconstruction (cams [n_img,8], registered mask, points per track, track arrays)."""
+    Returns a Reconstruction (cams [n_img,8], registered mask, points per track, track arrays).
+    With torch.distributed initialised (one process per GPU, `group` or the default group) the
+    all-pairs matching + verification is sharded across the ranks and the graph all-gathered; the
+    later stages are deterministic, so every rank returns the single-process reconstruction."""
     import torch
     dev = torch.device("cuda", device)
     ctx = sfmcore.context(device)
@@ -82,9 +119,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     pairs = np.array([(a, b) for a in range(n_img) for b in range(a + 1, n_img)], np.int32)
     gb = match_graph.GraphBuilder(desc, kps, n_kp, device=device)
     pairs_t = torch.from_numpy(pairs).to(dev)
-    count, match, _, rs = gb.run(pairs_t)
-    rows = gb.graph_rows(0, count, match, rs)
-    inl = rs["inl_count"].cpu().numpy()
+    rows, inl = _match_graph(gb, pairs, pairs_t, n_kp, group)
     ptr_t, timg_t, tkp_t = match_graph.build_tracks(rows, pairs_t, n_kp, min_track, device)
     tptr, timg, tkp = (t.cpu().numpy() for t in (ptr_t, timg_t, tkp_t))
     n_tr = len(tptr) - 1
