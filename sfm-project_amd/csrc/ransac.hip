@@ -34,12 +34,20 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        // one 32x32->64 product per multiplier (v_mad_u64_u32) instead of mul_hi + mul_lo
+        const uint64_t m0 = (uint64_t)0xD2511F53u * c0, m1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(m0 >> 32), lo0 = (uint32_t)m0;
+        const uint32_t hi1 = (uint32_t)(m1 >> 32), lo1 = (uint32_t)m1;
         const uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
         c0 = n0; c1 = n1; c2 = n2; c3 = n3;
     }
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// pl[i] through a 32-bit byte offset (the plane block of a pair is < 4 GB): the load takes the
+// pair's uniform base in SGPRs and no per-lane 64-bit address arithmetic
+__device__ __forceinline__ float ldf(const float* __restrict__ pl, int i) {
+    return *(const float*)((const char*)pl + ((uint32_t)i << 2));
 }
 
 __device__ __forceinline__ void sample8(uint64_t seed, uint32_t pa, uint32_t pb, uint32_t h, int M,
@@ -354,8 +362,8 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
     float4 smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        smp[k] = make_float4(pl[idx[k]], pl[kp + idx[k]], pl[2 * kp + idx[k]],
-                             pl[3 * kp + idx[k]]);
+        smp[k] = make_float4(ldf(pl, idx[k]), ldf(pl, kp + idx[k]), ldf(pl, 2 * kp + idx[k]),
+                             ldf(pl, 3 * kp + idx[k]));
     float F[9], G[9];
     const bool ok = fit_f8(smp, F);
     sampson_prep(F, k1, k2, G);
@@ -470,8 +478,8 @@ __global__ __launch_bounds__(256) void ransac_fit_kernel(
     float4 smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        smp[k] = make_float4(pl[idx[k]], pl[kp + idx[k]], pl[2 * kp + idx[k]],
-                             pl[3 * kp + idx[k]]);
+        smp[k] = make_float4(ldf(pl, idx[k]), ldf(pl, kp + idx[k]), ldf(pl, 2 * kp + idx[k]),
+                             ldf(pl, 3 * kp + idx[k]));
     float F[9], G[9];
 #ifdef RANSAC_ABL_NOFIT  // ablation: no 8-point fit (timing only; results invalid)
     const bool ok = true;
@@ -582,8 +590,8 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
     float4 smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        smp[k] = make_float4(pl[idx[k]], pl[kp + idx[k]], pl[2 * kp + idx[k]],
-                             pl[3 * kp + idx[k]]);
+        smp[k] = make_float4(ldf(pl, idx[k]), ldf(pl, kp + idx[k]), ldf(pl, 2 * kp + idx[k]),
+                             ldf(pl, 3 * kp + idx[k]));
     float F[9], G[9];
     const bool ok = fit_f8(smp, F);
     sampson_prep(F, k1, k2, G);
