@@ -1,7 +1,11 @@
 // 8-point fundamental-matrix RANSAC (K2).
 //
 // Fills the empty reference module code/geometric_verification.py (placeholder at
-// code/pipeline.py:60).  Three kernels per batch of pairs:
+// code/pipeline.py:60).  Default schedule (SFM_RANSAC_MODE 0, "ordered"; described above
+// ransac_fit_kernel): ransac_prep -> ransac_fit (sample, fit, 64-match preview, one 48-byte record
+// per hypothesis) -> ransac_order (per-pair sort by preview) -> ransac_score (pruned scoring in
+// preview order; an XCD's pairs in groups, hb-major inside a group, xcd_pair_block) ->
+// ransac_final.  The single-pass schedules (modes 1, 2) use three kernels per batch of pairs:
 //   ransac_prep   one wave per pair: gathers the tentative-match pixel coordinates, Hartley-
 //                 normalises each side with a fixed-order wave reduction and writes 8 planes per
 //                 pair: the normalised x1|y1|x2|y2 (fits) and the Sampson-scaled X1|Y1|X2|Y2
