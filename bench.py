@@ -153,7 +153,10 @@ def main():
     ap.add_argument("--n-img", type=int, default=0, help="override the config's image count")
     ap.add_argument("--k", type=int, default=0, help="override the config's keypoints/image")
     ap.add_argument("--n-hyp", type=int, default=4096)
-    ap.add_argument("--chunk", type=int, default=16384, help="pairs per K1/K2 launch")
+    ap.add_argument("--chunk", type=int, default=131072,
+                    help="pairs per K1/K2 launch (default: a cfg4 shard in one launch, ~90 GB of "
+                         "buffers at N = 1; same graph checksum as 16384-pair chunks, 1.7-2.2 %% "
+                         "faster, profiles/r02/bench_chunk_ab.txt)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU baseline budget (the sample is sized to about this much wall)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -216,6 +219,7 @@ def main():
     elapsed = float(el.item())
 
     verified_per_step = int(graph.shape[0])
+    checksum = graph_checksum(torch, graph)  # after the timed region
     st = [Runner.stage_ms(e) for e in evs]
     match_ms = float(np.mean([s[0] for s in st]))
     ransac_ms = float(np.mean([s[1] for s in st]))
@@ -242,6 +246,7 @@ def main():
             "launches_rank0": len(run.chunks), "parallelism": f"pair-sharded dp{world}",
         },
         "verified_matches_per_step": verified_per_step,
+        "graph_checksum": checksum,
         "roofline": {"kernel": "K1 L2 match, mutual rule (mfma_prep + mfma_mutual_kernel + "
                                "mutual_finalize, HIP events on the launch stream, rank 0)",
                      "bound": "mfma", "achieved": k1_tops, "peak": PEAK_I8_TOPS,
@@ -293,6 +298,19 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def graph_checksum(torch, graph):
+    """Order-sensitive checksum of the verified graph rows [n,3] (pair, queryIdx, trainIdx):
+    sum over rows of ((pair * 1000003 + q * 1009 + t) mod P) * (row + 1) mod P, P = 2^31 - 1, in
+    int64 on the device.  Equal checksums across launch chunkings / rank counts = the same graph."""
+    if graph.shape[0] == 0:
+        return 0
+    P = 2147483647
+    g = graph.long()
+    v = (g[:, 0] * 1000003 + g[:, 1] * 1009 + g[:, 2]) % P
+    w = torch.arange(1, g.shape[0] + 1, device=g.device, dtype=torch.int64) % P
+    return int(((v * w) % P).sum().item() % P)
 
 
 def ransac_flops(run, n_hyp):

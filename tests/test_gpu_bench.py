@@ -42,3 +42,4 @@ def test_bench_json_contract():
     assert 0.0 < r["frac"] < 1.0
     # the cfg3 verified graph is fixed by the oracle-checked kernels (tests/test_gpu_fullsize.py)
     assert d["verified_matches_per_step"] == 554010
+    assert isinstance(d["graph_checksum"], int) and 0 <= d["graph_checksum"] < 2147483647
