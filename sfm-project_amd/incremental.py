@@ -61,6 +61,7 @@ def relative_pose(x1, x2):
 
 class Reconstruction:
     def __init__(self, n_img):
+        self.timings = {}          # wall seconds per stage (each stage ends in a device sync)
         self.cams = np.zeros((n_img, 8))
         self.registered = np.zeros(n_img, bool)
         self.points = None
@@ -110,16 +111,27 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     With torch.distributed initialised (one process per GPU, `group` or the default group) the
     all-pairs matching + verification is sharded across the ranks and the graph all-gathered; the
     later stages are deterministic, so every rank returns the single-process reconstruction."""
+    import time
     import torch
     dev = torch.device("cuda", device)
     ctx = sfmcore.context(device)
     say = log or (lambda *a: None)
+    tim = {}
+
+    def lap(key, t0):
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        tim[key] = tim.get(key, 0.0) + (t1 - t0)
+        return t1
+
+    tk = time.perf_counter()
     n_img = len(desc)
     intr = np.asarray(intr, np.float64)
     pairs = np.array([(a, b) for a in range(n_img) for b in range(a + 1, n_img)], np.int32)
     gb = match_graph.GraphBuilder(desc, kps, n_kp, device=device)
     pairs_t = torch.from_numpy(pairs).to(dev)
     rows, inl = _match_graph(gb, pairs, pairs_t, n_kp, group)
+    tk = lap("match_verify", tk)
     ptr_t, timg_t, tkp_t = match_graph.build_tracks(rows, pairs_t, n_kp, min_track, device)
     tptr, timg, tkp = (t.cpu().numpy() for t in (ptr_t, timg_t, tkp_t))
     n_tr = len(tptr) - 1
@@ -129,6 +141,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     say(f"graph: {len(rows)} verified matches, {n_tr} tracks")
 
     rec = Reconstruction(n_img)
+    rec.timings = tim
+    tk = lap("tracks", tk)
     rec.points = np.zeros((n_tr, 3))
     rec.has_point = np.zeros(n_tr, bool)
     rec.tracks = (tptr, timg, tkp)
@@ -136,11 +150,15 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
 
     # ---- initial pair: most verified inliers; relative pose from that pair's RANSAC-verified
     # matches (tracks may still carry a wrong observation), then its tracks are triangulated
-    rows_np = rows.cpu().numpy()
+    # rows are pair-major in pair order: a pair's rows are one slice (no host copy of the graph)
+    pair_col = rows[:, 0].contiguous()
     order = np.argsort(-inl, kind="stable")
     for p in order[:10]:
         a, b = (int(v) for v in pairs[p])
-        r = rows_np[rows_np[:, 0] == p]
+        pv = torch.tensor([int(p)], dtype=pair_col.dtype, device=dev)
+        lo = int(torch.searchsorted(pair_col, pv).item())
+        hi = int(torch.searchsorted(pair_col, pv, right=True).item())
+        r = rows[lo:hi].cpu().numpy()
         if len(r) < 50:
             continue
         xa = _undistort(kps_np[a, r[:, 1]], intr[a])
@@ -167,24 +185,33 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             break
     if not rec.registered.any():
         raise RuntimeError("reconstruct: no initial pair with enough well-conditioned matches")
+    tk = lap("initial_pair", tk)
     _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device)
+    tk = lap("bundle_adjust", tk)
+    tim["rounds"] = 0
 
     # ---- register, triangulate, adjust until no image can be added
     while not rec.registered.all():
-        cand = [i for i in range(n_img) if not rec.registered[i]]
-        corr = [(i, np.nonzero((timg == i) & rec.has_point[obs_track])[0]) for i in cand]
-        corr = [(i, o) for i, o in corr if len(o) >= 30]
-        if not corr:
+        # 2-D/3-D correspondences of every unregistered image with >= 30 of them, grouped by
+        # image (ascending) and ascending observation index within an image: one pass
+        obs_sel = np.nonzero(rec.has_point[obs_track] & ~rec.registered[timg])[0]
+        by_img = np.argsort(timg[obs_sel], kind="stable")
+        obs_sel = obs_sel[by_img]
+        img_u, img_n = np.unique(timg[obs_sel], return_counts=True)
+        keep = img_n >= 30
+        if not keep.any():
             break
-        ids = np.array([i for i, _ in corr], np.int32)
-        cptr = np.r_[0, np.cumsum([len(o) for _, o in corr])].astype(np.int32)
-        sel = np.concatenate([o for _, o in corr])
+        ids = img_u[keep].astype(np.int32)
+        cptr = np.r_[0, np.cumsum(img_n[keep])].astype(np.int32)
+        sel = obs_sel[np.repeat(keep, img_n)]
         T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
         cams_r, cnt, _, _ = ctx.register_batch(T(cptr, np.int32), T(obs_xy[sel], np.float64),
                                                T(rec.points[obs_track[sel]], np.float64),
                                                T(intr[ids], np.float64), T(ids, np.int32),
                                                n_hyp=n_hyp, thr=reg_thr)
         cams_r, cnt = cams_r.cpu().numpy(), cnt.cpu().numpy()
+        tk = lap("register", tk)
+        tim["rounds"] += 1
         added = 0
         for j, i in enumerate(ids):
             if cnt[j] >= 30:
@@ -195,18 +222,27 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         if not added:
             break
         _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev)
+        tk = lap("triangulate", tk)
         _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device)
+        tk = lap("bundle_adjust", tk)
     return rec
 
 
 def _triangulate(ctx, cams, intr, imgs, tracks, tptr, timg, obs_xy, dev):
     """Triangulate `tracks` from their observations in the images `imgs` (GPU kernel)."""
     import torch
-    imgs = np.asarray(imgs)
-    obs = [np.arange(tptr[t], tptr[t + 1]) for t in tracks]
-    obs = [o[np.isin(timg[o], imgs)] for o in obs]
-    ptr = np.r_[0, np.cumsum([len(o) for o in obs])].astype(np.int32)
-    o = np.concatenate(obs) if obs else np.zeros(0, np.int64)
+    tracks = np.asarray(tracks, np.int64)
+    in_img = np.zeros(len(cams), bool)
+    in_img[np.asarray(imgs, np.int64)] = True
+    # every observation of the tracks (track order, ascending within a track), kept if its image
+    # is in `imgs`: vectorised CSR gather
+    lens = (tptr[tracks + 1] - tptr[tracks]).astype(np.int64)
+    start = np.r_[0, np.cumsum(lens)[:-1]]
+    o = np.arange(int(lens.sum()), dtype=np.int64) + np.repeat(tptr[tracks] - start, lens)
+    keep = in_img[timg[o]]
+    o = o[keep]
+    per = np.bincount(np.repeat(np.arange(len(tracks)), lens)[keep], minlength=len(tracks))
+    ptr = np.r_[0, np.cumsum(per)].astype(np.int32)
     T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
     pts, st = ctx.triangulate(T(cams, np.float64), T(intr[:, 2:4], np.float64), T(ptr, np.int32),
                               T(timg[o], np.int32), T(obs_xy[o], np.float64))

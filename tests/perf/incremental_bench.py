@@ -48,7 +48,8 @@ def main():
         "points": int(rec.has_point.sum()), "observations": int(use.sum()),
         "median_reproj_px": float(np.median(err)), "mean_reproj_px": float(err.mean()),
         "max_centre_err_rel_radius": float(np.abs(al - _centres(scene["cams"][reg])).max() / 8.0),
-        "ba_history": rec.history}))
+        "ba_history": rec.history,
+        "stage_s": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in rec.timings.items()}}))
 
 
 if __name__ == "__main__":
