@@ -43,3 +43,28 @@ def test_bench_json_contract():
     # the cfg3 verified graph is fixed by the oracle-checked kernels (tests/test_gpu_fullsize.py)
     assert d["verified_matches_per_step"] == 554010
     assert isinstance(d["graph_checksum"], int) and 0 <= d["graph_checksum"] < 2147483647
+
+
+def test_bench_two_ranks_same_graph():
+    """bench.py's N > 1 path (shard_range, per-rank K1 + K2, packed graph all-gather) as a 2-rank
+    torch.distributed.run job (gloo, both ranks on GPU 0: RCCL cannot share a device) on cfg3:
+    the gathered graph equals the single-process one (graph_checksum, verified count)."""
+    import socket
+    def run(extra, nproc):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        pre = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+                str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port)]
+               if nproc > 1 else [sys.executable])
+        cmd = pre + [os.path.join(ROOT, "bench.py"), "--config", "cfg3", "--steps", "1",
+                     "--warmup", "1", "--no-cpu-baseline"] + extra
+        out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, OMP_NUM_THREADS="4"))
+        assert out.returncode == 0, out.stderr[-3000:]
+        return json.loads([l for l in out.stdout.splitlines() if l.strip()][-1])
+    one = run([], 1)
+    two = run(["--gpus", "2", "--dist-backend", "gloo", "--device", "0"], 2)
+    assert two["n_gpus"] == 2 and two["config"]["pairs_total"] == 1225
+    assert two["verified_matches_per_step"] == one["verified_matches_per_step"] == 554010
+    assert two["graph_checksum"] == one["graph_checksum"]
