@@ -176,6 +176,24 @@ int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
                  const int32_t* cam_ptr, const int32_t* cam_obs, const double* U, const double* V,
                  const double* W, const double* gc, const double* gp,
                  const sfm_ba_solve_params* prm, double* dc, double* dp, double* info);
+/* Multi-GPU form of sfm_ba_solve (observations sharded by point, one process per
+ * GPU).  V, W, gp, dp, pt_ptr and the observation arrays are this rank's point shard (point and
+ * observation indices local to it); U and gc are the GLOBAL camera blocks (sfm_ba_jtj on the
+ * shard, then an all-reduce of U/gc, then sfm_ba_fix_params).  Every camera-space sum over
+ * observations is written to the caller's device buffer comm (>= 44 * n_cam doubles) and
+ * `allreduce(user, comm, n)` must sum comm[0, n) over all ranks in place, ordered on the
+ * context's stream (e.g. an RCCL all-reduce enqueued on it), and return 0: once per solve with
+ * n = 44 n_cam, once per CG iteration with n = 8 n_cam, once with n = 2.  All camera-space
+ * state is then replicated, so every rank takes the same CG decisions and returns the same
+ * dc and info; dp is the shard's.  Same result as sfm_ba_solve on the whole problem up to the
+ * summation order (fp64).  No counterpart in the reference (its BA module is empty). */
+typedef int (*sfm_allreduce_fn)(void* user, double* buf, int64_t n);
+int sfm_ba_solve_sharded(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+                         const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
+                         const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
+                         const double* V, const double* W, const double* gc, const double* gp,
+                         const sfm_ba_solve_params* prm, sfm_allreduce_fn allreduce, void* user,
+                         double* comm, double* dc, double* dp, double* info);
 /* Fixed parameters (the gauge: the reference camera's pose and one translation coordinate of a
  * second camera; known intrinsics f, k1): in place on sfm_ba_jtj's U [n_cam][8][8], W [n_obs][8][3]
  * and g_c [n_cam][8], the rows/columns of the parameters marked in fixed [n_cam][8] (u8, 1 =

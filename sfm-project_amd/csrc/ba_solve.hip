@@ -162,17 +162,24 @@ __device__ bool inv8_spd(const double (&S)[64], double (&M)[64]) {
 // Block per camera: S_cc = U_d - Σ_o W_o V_d⁻¹ W_oᵀ (upper triangle, 36 sums) and
 // b_c = -g_c + Σ_o W_o v_g (8 sums) over the camera's observations (cam_obs order, lane-strided,
 // fixed tree); then the preconditioner block M_c = S_cc⁻¹ and the CG start.
+// Sharded solve (points split over ranks): phase 1 writes the 44 local sums to comm[44c..] and
+// stops; after the all-reduce of comm, phase 2 takes the sums from comm (phase 0: unsharded).
 __global__ __launch_bounds__(CT) void bas_camera_setup(
     int n_cam, int n_obs, const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ ptc,
     const double* __restrict__ U, const double* __restrict__ Wc, const double* __restrict__ Vinv,
     const double* __restrict__ vg, const double* __restrict__ gc, double lam,
     double* __restrict__ Ud, double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ pv,
-    double* __restrict__ rz_c, double* __restrict__ bb_c, int32_t* __restrict__ bad) {
+    double* __restrict__ rz_c, double* __restrict__ bb_c, int32_t* __restrict__ bad, int phase,
+    double* __restrict__ comm) {
     constexpr int N = 44;
     __shared__ double red[4][N];
     __shared__ double tot[N];
     const int c = blockIdx.x, tid = threadIdx.x;
+    if (phase == 2) {
+        if (tid < N) tot[tid] = comm[N * (size_t)c + tid];
+        __syncthreads();
+    } else {
     double acc[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) acc[i] = 0.0;
@@ -200,7 +207,12 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[36 + i] += w[3 * i] * g[0] + w[3 * i + 1] * g[1] + w[3 * i + 2] * g[2];
     }
+    if (phase == 1) {
+        block_sum<N>(acc, red, comm + N * (size_t)c);
+        return;
+    }
     block_sum<N>(acc, red, tot);
+    }
     if (tid == 0) {
         const double* Uc = U + 64 * (size_t)c;
         double S[64], M[64], ud[64];
@@ -416,11 +428,14 @@ __global__ __launch_bounds__(256) void bas_pcg_point(
 constexpr int CC = SFM_BA_CC;  // threads per camera block in the CG camera pass
 
 // Block per camera: p_k stored; q_c = U_d p_c - Σ_o W_o t_p; p_c·q_c.
+// Sharded solve: phase 1 writes the local Σ_o W_o t_p to comm[8c..] and stops; after the
+// all-reduce of comm, phase 2 finishes the camera from it (phase 0: unsharded).
 __global__ __launch_bounds__(CC) void bas_pcg_camera(
     int k, int n_cam, int n_obs, const int32_t* __restrict__ cam_ptr,
     const int32_t* __restrict__ ptc, const double* __restrict__ Wc, const double* __restrict__ t,
     const double* __restrict__ Ud, const double* __restrict__ z, double* __restrict__ pv,
-    const PcgState* __restrict__ st, double* __restrict__ q, double* __restrict__ pq) {
+    const PcgState* __restrict__ st, double* __restrict__ q, double* __restrict__ pq, int phase,
+    double* __restrict__ comm) {
     __shared__ double red[CC / 64][8];
     __shared__ double pc_s[8];
     if (st->done) return;
@@ -430,7 +445,8 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.0;
     const size_t n = (size_t)n_obs;
-    for (int e = cam_ptr[c] + tid; e < cam_ptr[c + 1]; e += CC) {
+    const int e_end = phase == 2 ? 0 : cam_ptr[c + 1];
+    for (int e = (phase == 2 ? 0 : cam_ptr[c]) + tid; e < e_end; e += CC) {
         const double* Wo = Wc + e;
         const double* tp = t + 3 * (size_t)ptc[e];
         const double t0 = tp[0], t1 = tp[1], t2 = tp[2];
@@ -459,6 +475,11 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
         double wt = 0.0;
 #pragma unroll
         for (int w = 0; w < CC / 64; ++w) wt += red[w][tid];
+        if (phase == 1) {
+            comm[8 * (size_t)c + tid] = wt;
+            return;
+        }
+        if (phase == 2) wt = comm[8 * (size_t)c + tid];
         const double* u = Ud + 64 * (size_t)c + 8 * tid;
         double sU = 0.0;
 #pragma unroll
@@ -625,6 +646,18 @@ __global__ __launch_bounds__(256) void bas_backsub(int n_pt, int n_obs,
     }
 }
 
+// Sharded solve, one block: this rank's point-block partials of bas_backsub summed into
+// comm[0..2) (fixed order), the operand of the all-reduce that precedes bas_model.
+__global__ __launch_bounds__(1024) void bas_mpart_total(int n_pblk, const double* __restrict__ mpart,
+                                                        double* __restrict__ comm) {
+    __shared__ double red[16];
+    double a = 0.0, b = 0.0;
+    for (int k = threadIdx.x; k < n_pblk; k += 1024) { a += mpart[2 * (size_t)k]; b += mpart[2 * (size_t)k + 1]; }
+    const double sa = block_sum1024(a, red);
+    const double sb = block_sum1024(b, red);
+    if (threadIdx.x == 0) { comm[0] = sa; comm[1] = sb; }
+}
+
 // One block: camera terms (g_c·δc, δcᵀ U δc) + the point-block partials -> info.
 //   info = {iterations, |r|/|b|, gᵀδ, δᵀ JᵀJ δ, preconditioner fallback (0/1)}
 __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const double* __restrict__ U,
@@ -666,12 +699,29 @@ __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const d
 
 }  // namespace
 
-extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
-                            const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
-                            const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
-                            const double* V, const double* W, const double* gc, const double* gp,
-                            const sfm_ba_solve_params* prm, double* dc, double* dp,
-                            double* info) {
+// The solve; `allreduce` == nullptr: unsharded.  Otherwise the points (V, gp, dp, pt_ptr and the
+// observations) are this rank's shard, the camera blocks (U, gc) are the all-reduced global ones,
+// and every camera-space partial that sums over observations goes through comm + allreduce:
+// the 44 setup sums per camera once, Σ_o W_o t_p (8 per camera) per CG iteration, and the 2
+// point-side LM model terms.  Everything downstream of an all-reduce is computed from replicated
+// values, so every rank takes the same CG decisions (the convergence poll included) and calls
+// `allreduce` the same number of times.
+static int ba_solve_impl(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+                         const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
+                         const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
+                         const double* V, const double* W, const double* gc, const double* gp,
+                         const sfm_ba_solve_params* prm, sfm_allreduce_fn allreduce, void* user,
+                         double* comm, double* dc, double* dp, double* info) {
+    const bool sharded = allreduce != nullptr;
+    SFM_REQUIRE(!sharded || comm != nullptr, "sfm_ba_solve_sharded: comm is NULL");
+#define SFM_ALLREDUCE(n)                                                                       \
+    do {                                                                                       \
+        SFM_HIP_CHECK(hipGetLastError());                                                      \
+        if (allreduce(user, comm, (int64_t)(n)) != 0) {                                        \
+            sfm::set_error("sfm_ba_solve_sharded: the all-reduce callback failed");            \
+            return SFM_ERR_INVALID;                                                            \
+        }                                                                                      \
+    } while (0)
     SFM_REQUIRE(ctx != nullptr && prm != nullptr, "sfm_ba_solve: ctx/prm is NULL");
     SFM_REQUIRE(n_cam > 0 && n_pt >= 0 && n_obs >= 0, "sfm_ba_solve: bad size");
     SFM_REQUIRE(prm->max_iter >= 0 && prm->lambda >= 0.0 && prm->tol >= 0.0,
@@ -724,8 +774,15 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
                            pt_idx, W, Wp, Wc, ptc);
         SFM_HIP_CHECK(hipGetLastError());
     }
+    if (sharded) {
+        hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
+                           ptc, U, Wc, Vinv, vg, gc, lam, Ud, Mc, dc, r, z, pv, rzc, rrc, bad, 1,
+                           comm);
+        SFM_ALLREDUCE(44 * (size_t)n_cam);
+    }
     hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr, ptc,
-                       U, Wc, Vinv, vg, gc, lam, Ud, Mc, dc, r, z, pv, rzc, rrc, bad);
+                       U, Wc, Vinv, vg, gc, lam, Ud, Mc, dc, r, z, pv, rzc, rrc, bad,
+                       sharded ? 2 : 0, comm);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, rrc, state);
     SFM_HIP_CHECK(hipGetLastError());
@@ -744,8 +801,13 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
         }
         hipLaunchKernelGGL(bas_pcg_point, dim3(gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
                            pt_ptr, cam_idx, Wp, Vinv, z, pv, rzc, rrc, tol, state, t);
+        if (sharded) {
+            hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs,
+                               cam_ptr, ptc, Wc, t, Ud, z, pv, state, q, pq, 1, comm);
+            SFM_ALLREDUCE(8 * (size_t)n_cam);
+        }
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
-                           ptc, Wc, t, Ud, z, pv, state, q, pq);
+                           ptc, Wc, t, Ud, z, pv, state, q, pq, sharded ? 2 : 0, comm);
         hipLaunchKernelGGL(bas_pcg_vec, dim3(vblk), dim3(256), 0, st, k, n_cam, Mc, dc, r, z, pv, q,
                            pq, rzc, rrc, state);
     }
@@ -753,10 +815,38 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     hipLaunchKernelGGL(bas_backsub, dim3(gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr, cam_idx, Wp, V,
                        Vinv, vg, gp, dc, dp, mpart);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, gblk, U, gc, dc, mpart, rrc,
-                       state, bad, info);
+    if (sharded) {
+        hipLaunchKernelGGL(bas_mpart_total, dim3(1), dim3(1024), 0, st, gblk, mpart, comm);
+        SFM_ALLREDUCE(2);
+    }
+    hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, sharded ? 1 : gblk, U, gc, dc,
+                       sharded ? comm : mpart, rrc, state, bad, info);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
+#undef SFM_ALLREDUCE
+}
+
+extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+                            const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
+                            const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
+                            const double* V, const double* W, const double* gc, const double* gp,
+                            const sfm_ba_solve_params* prm, double* dc, double* dp,
+                            double* info) {
+    return ba_solve_impl(ctx, n_cam, n_pt, n_obs, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
+                         W, gc, gp, prm, nullptr, nullptr, nullptr, dc, dp, info);
+}
+
+extern "C" int sfm_ba_solve_sharded(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+                                    const int32_t* cam_idx, const int32_t* pt_idx,
+                                    const int32_t* pt_ptr, const int32_t* cam_ptr,
+                                    const int32_t* cam_obs, const double* U, const double* V,
+                                    const double* W, const double* gc, const double* gp,
+                                    const sfm_ba_solve_params* prm, sfm_allreduce_fn allreduce,
+                                    void* user, double* comm, double* dc, double* dp,
+                                    double* info) {
+    SFM_REQUIRE(allreduce != nullptr, "sfm_ba_solve_sharded: allreduce callback is NULL");
+    return ba_solve_impl(ctx, n_cam, n_pt, n_obs, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
+                         W, gc, gp, prm, allreduce, user, comm, dc, dp, info);
 }
 
 // ---- fixed parameters (gauge / known intrinsics) ------------------------------------------------

@@ -105,12 +105,15 @@ def _match_graph(gb, pairs, pairs_t, n_kp, group):
 
 
 def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
-                ba_iter=20, loss_s=2.0, device=0, log=None, group=None):
+                ba_iter=20, loss_s=2.0, device=0, log=None, group=None, shard_ba=False):
     """desc [n_img,K,D] u8, kps [n_img,K,2] pixels, n_kp [n_img], intr [n_img,4] = (f, k1, cx, cy).
     Returns a Reconstruction (cams [n_img,8], registered mask, points per track, track arrays).
     With torch.distributed initialised (one process per GPU, `group` or the default group) the
     all-pairs matching + verification is sharded across the ranks and the graph all-gathered; the
-    later stages are deterministic, so every rank returns the single-process reconstruction."""
+    later stages are deterministic, so every rank returns the single-process reconstruction.
+    shard_ba additionally shards every bundle adjustment by point (reconstruction.bundle_adjust
+    shard=True: camera-block and per-CG-iteration all-reduces); the ranks then still agree with
+    each other exactly, and with the single-process run up to the fp64 summation order."""
     import time
     import torch
     dev = torch.device("cuda", device)
@@ -186,7 +189,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     if not rec.registered.any():
         raise RuntimeError("reconstruct: no initial pair with enough well-conditioned matches")
     tk = lap("initial_pair", tk)
-    _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device)
+    _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
+            shard_ba, group)
     tk = lap("bundle_adjust", tk)
     tim["rounds"] = 0
 
@@ -223,7 +227,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             break
         _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev)
         tk = lap("triangulate", tk)
-        _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device)
+        _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
+                shard_ba, group)
         tk = lap("bundle_adjust", tk)
     return rec
 
@@ -262,7 +267,8 @@ def _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev):
     rec.has_point[todo[ok]] = True
 
 
-def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device):
+def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
+            shard_ba=False, group=None):
     """Global LM over the registered cameras and the triangulated points (GPU), then drop points
     whose mean reprojection error stays above max_err.  Gauge: the initial pair's first camera
     keeps its pose and the second one translation coordinate (the scale); the intrinsics are
@@ -277,7 +283,8 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
     cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
                                                    timg[use], pt_idx.astype(np.int32),
                                                    obs_xy[use], loss_s=loss_s, max_iter=ba_iter,
-                                                   device=device, fixed=fixed)
+                                                   device=device, fixed=fixed, shard=shard_ba,
+                                                   group=group)
     reg = rec.registered
     rec.cams[reg] = cams[reg]
     rec.points[pts_ids] = pts

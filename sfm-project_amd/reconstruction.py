@@ -199,9 +199,25 @@ def _rotmat_np(r):
     return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
 
 
+def make_allreduce(group=None):
+    """In-place fp64 sum over the ranks of `group`: RCCL (`nccl`) on the current stream for device
+    tensors; gloo through a host copy (the CPU tests and the same-GPU rehearsals)."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        def allreduce(t):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    else:
+        def allreduce(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            t.copy_(h)
+    return allreduce
+
+
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
                   lam0: float = 1e-4, ftol: float = 1e-12, max_cg: int = 200,
-                  cg_tol: float = 1e-10, device: int = 0, fixed=None):
+                  cg_tol: float = 1e-10, device: int = 0, fixed=None, shard: bool = False,
+                  group=None):
     """Levenberg-Marquardt on paper eq. (1): every step on the GPU
     (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
     accept / reject it.
@@ -213,29 +229,72 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     fixed: optional [n_cam, 8] bool mask of parameters held at their values (gauge_mask;
     sfm_ba_fix_params after every linearisation).
 
+    shard (multi-GPU; needs an initialised torch.distributed group): every rank
+    takes the points of its `shard_points` range with their observations; the camera blocks
+    U / g_c are all-reduced after each linearisation, the Schur-complement PCG runs sharded
+    (sfm_ba_solve_sharded: one 8·n_cam fp64 all-reduce per CG iteration), the trial cost is
+    all-reduced and the points are gathered at the end.  Every rank returns the same result,
+    equal to the unsharded one up to the fp64 summation order.
+
     Returns (cams [n_cam,8], pts [n_pt,3], history [(cost, λ, accepted, cg_iterations)])."""
     import torch
     n_cam, n_pt = len(cams), len(pts)
-    prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device)
+    allreduce = None
+    if shard:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            allreduce = make_allreduce(group)
+            rank, world = dist.get_rank(group), dist.get_world_size(group)
+    lo, hi = 0, n_pt
+    if allreduce is not None:
+        cam_idx = np.asarray(cam_idx, np.int32)
+        pt_idx = np.asarray(pt_idx, np.int32)
+        uv = np.asarray(uv, np.float64)
+        order = np.argsort(pt_idx, kind="stable")
+        cam_idx, pt_idx, uv = cam_idx[order], pt_idx[order], uv[order]
+        pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
+        lo, hi = shard_points(pt_ptr, rank, world)
+        o0, o1 = int(pt_ptr[lo]), int(pt_ptr[hi])
+        cam_idx, pt_idx, uv = cam_idx[o0:o1], pt_idx[o0:o1] - lo, uv[o0:o1]
+    prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, hi - lo, device)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(prob.dev)
-    cams_d, pts_d = T(cams), T(pts)
+    cams_d, pts_d = T(cams), T(np.asarray(pts, np.float64)[lo:hi])
     fixed_d = None
     if fixed is not None and np.any(fixed):
         fixed_d = torch.from_numpy(np.ascontiguousarray(fixed, np.uint8).reshape(n_cam, 8)).to(prob.dev)
 
     def linearize(c, p):
         lin = prob.linearize(c, p, loss_s)
+        if allreduce is not None:   # global camera blocks before the gauge is applied
+            nu_, ng = lin["U"].numel(), lin["gc"].numel()
+            buf = torch.cat([lin["U"].reshape(-1), lin["gc"].reshape(-1)])
+            allreduce(buf)
+            lin["U"].copy_(buf[:nu_].view_as(lin["U"]))
+            lin["gc"].copy_(buf[nu_:nu_ + ng].view_as(lin["gc"]))
         if fixed_d is not None:
             prob.ctx.ba_fix_params(lin, prob.cam_idx, fixed_d)
         return lin
+
+    def cost(c, p):
+        t = prob.cost(c, p, loss_s)
+        if allreduce is not None:
+            allreduce(t)
+        return t
+
+    def solve(lin, lam):
+        if allreduce is None:
+            return prob.solve(lin, lam, max_cg, cg_tol)
+        return prob.ctx.ba_solve_sharded(lin, prob.cam_idx, prob.pt_idx, prob.pt_ptr,
+                                         prob.cam_ptr, prob.cam_obs, lam, allreduce,
+                                         max_iter=max_cg, tol=cg_tol)
     lam, nu = lam0, 2.0
     hist = []
-    old = float(prob.cost(cams_d, pts_d, loss_s).item())
+    old = float(cost(cams_d, pts_d).item())
     lin = linearize(cams_d, pts_d)
     for _ in range(max_iter):
-        dc, dp, info = prob.solve(lin, lam, max_cg, cg_tol)
+        dc, dp, info = solve(lin, lam)
         c2, p2 = prob.update(cams_d, dc, pts_d, dp)
-        new_t = prob.cost(c2, p2, loss_s)
+        new_t = cost(c2, p2)
         vals = torch.cat([info, new_t]).cpu().numpy()       # the one host sync of the step
         it, gd, q, new = int(vals[0]), float(vals[2]), float(vals[3]), float(vals[5])
         pred = -(gd + 0.5 * q)
@@ -256,4 +315,9 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             hist.append((old, lam, False, it))
             if lam > 1e16:
                 break
+    if allreduce is not None:   # gather the point shards: one all-reduce of the zero-padded set
+        full = torch.zeros((n_pt, 3), dtype=torch.float64, device=prob.dev)
+        full[lo:hi] = pts_d
+        allreduce(full.view(-1))
+        pts_d = full
     return cams_d.cpu().numpy(), pts_d.cpu().numpy(), hist

@@ -45,7 +45,9 @@ def _worker(rank, world, port, out_dir):
     U, gc = torch.from_numpy(o["U"]), torch.from_numpy(o["gc"])
     cost = torch.tensor([o["cost"]], dtype=torch.float64)
     reconstruction.allreduce_camera_blocks(U, gc, cost)
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), U=U.numpy(), gc=gc.numpy(),
+    ar = torch.arange(6, dtype=torch.float64) * (rank + 1)   # the sharded solve's hook (gloo path)
+    reconstruction.make_allreduce()(ar[1:5])
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), U=U.numpy(), gc=gc.numpy(), ar=ar.numpy(),
              cost=cost.numpy(), V=o["V"], W=o["W"], res=o["res"], lo=lo, hi=hi, o0=o0, o1=o1)
     dist.barrier()
     dist.destroy_process_group()
@@ -77,3 +79,4 @@ def test_ba_allreduce_gloo_world2(tmp_path):
         np.testing.assert_array_equal(r[k]["V"], full["V"][lo:hi])
         np.testing.assert_array_equal(r[k]["W"], full["W"][o0:o1])
         np.testing.assert_array_equal(r[k]["res"], full["res"][o0:o1])
+        np.testing.assert_array_equal(r[k]["ar"], [0, 3, 6, 9, 12, 5 * (k + 1)])

@@ -1,0 +1,120 @@
+"""GPU: the point-sharded bundle-adjustment step —
+sfm_ba_solve_sharded and reconstruction.bundle_adjust(shard=True).
+
+Tolerances (fp64; sharding re-associates the camera-space sums over observations):
+  world-size-1 RCCL group: δ bit-identical to sfm_ba_solve (the phases split the same sums), the
+    LM model terms to 1e-12 relative (one extra fixed-order reduction), the LM end state to 1e-9;
+  two ranks (gloo, one GPU): every rank returns the same bits; δ within 1e-8 of max|δ| of the
+    unsharded solve, the LM end cost within 1e-9 relative, cameras within 1e-7 relative.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import reconstruction as R
+import sfmcore
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def problem():
+    return synth.make_ba_problem(9, 300, obs_per_pt=4, seed=17, perturb=3e-3)
+
+
+def shard_solve(prob, rank, world, allreduce, lam=1e-3):
+    """One sharded solve from the initial linearisation of `prob` on this rank's point shard."""
+    import torch
+    n_cam, n_pt = len(prob["cams"]), len(prob["pts"])
+    pt_ptr, _ = sfmcore.csr_by(prob["pt_idx"], n_pt)
+    lo, hi = R.shard_points(pt_ptr, rank, world)
+    o0, o1 = int(pt_ptr[lo]), int(pt_ptr[hi])
+    P = R.BAProblem(prob["pp"], prob["cam_idx"][o0:o1], prob["pt_idx"][o0:o1] - lo,
+                    prob["uv"][o0:o1], n_cam, hi - lo)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()
+    lin = P.linearize(T(prob["cams"]), T(prob["pts"][lo:hi]), 2.0)
+    allreduce(lin["U"].view(-1))
+    allreduce(lin["gc"].view(-1))
+    dc, dp, info = P.ctx.ba_solve_sharded(lin, P.cam_idx, P.pt_idx, P.pt_ptr, P.cam_ptr,
+                                          P.cam_obs, lam, allreduce, max_iter=500, tol=1e-12)
+    return dc.cpu().numpy(), dp.cpu().numpy(), info.cpu().numpy(), lo, hi
+
+
+def _reference_solve(prob, lam=1e-3):
+    import torch
+    P = R.BAProblem(prob["pp"], prob["cam_idx"], prob["pt_idx"], prob["uv"], len(prob["cams"]),
+                    len(prob["pts"]))
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()
+    lin = P.linearize(T(prob["cams"]), T(prob["pts"]), 2.0)
+    return tuple(t.cpu().numpy() for t in P.solve(lin, lam, max_iter=500, tol=1e-12))
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_ba_sharded_world1_rccl():
+    """World-size-1 `nccl` group: the sharded solve runs its RCCL all-reduces and reproduces the
+    unsharded solve; the sharded LM matches the unsharded LM."""
+    import torch
+    import torch.distributed as dist
+    assert not dist.is_initialized()
+    prob = problem()
+    rdc, rdp, rinfo = _reference_solve(prob)
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
+    rcams, rpts, rhist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        dc, dp, info, lo, hi = shard_solve(prob, 0, 1, R.make_allreduce())
+        assert (lo, hi) == (0, len(prob["pts"]))
+        np.testing.assert_array_equal(dc, rdc)
+        np.testing.assert_array_equal(dp, rdp)
+        assert info[0] == rinfo[0] and info[1] == rinfo[1] and info[4] == rinfo[4]
+        np.testing.assert_allclose(info[2:4], rinfo[2:4], rtol=1e-12)
+        cams, pts, hist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed, shard=True)
+        assert abs(hist[-1][0] - rhist[-1][0]) <= 1e-9 * rhist[-1][0]
+        np.testing.assert_allclose(cams, rcams, rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(pts, rpts, rtol=1e-9, atol=1e-12)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ba_sharded_two_ranks(tmp_path):
+    """Two ranks (torch.distributed.run, gloo, both on GPU 0) shard the points: the ranks agree
+    bit for bit, and the sharded solve / LM match the single-process ones to fp64 reassociation."""
+    import subprocess
+    import sys
+    prob = problem()
+    rdc, rdp, rinfo = _reference_solve(prob)
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
+    rcams, rpts, rhist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "ba")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "tests", "dist_ba_worker.py"), out]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = [np.load(f"{out}.rank{k}.npz") for k in range(2)]
+    for key in ("cams", "pts", "hist", "dc", "info"):
+        np.testing.assert_array_equal(d[0][key], d[1][key])
+    assert int(d[0]["hi"]) == int(d[1]["lo"]) and 0 < int(d[0]["hi"]) < len(prob["pts"])
+    np.testing.assert_allclose(d[0]["dc"], rdc, rtol=0, atol=1e-8 * np.abs(rdc).max())
+    dp = np.concatenate([d[k]["dp"] for k in range(2)])
+    np.testing.assert_allclose(dp, rdp, rtol=0, atol=1e-8 * np.abs(rdp).max())
+    assert d[0]["info"][0] > 0 and d[0]["info"][1] <= 1e-12 and d[0]["info"][4] == 0
+    np.testing.assert_allclose(d[0]["info"][2:4], rinfo[2:4], rtol=1e-8)
+    hist = d[0]["hist"]
+    assert abs(hist[-1][0] - rhist[-1][0]) <= 1e-9 * rhist[-1][0]
+    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-7, atol=1e-10)
+    np.testing.assert_allclose(d[0]["pts"], rpts, rtol=1e-7, atol=1e-10)
+    np.testing.assert_array_equal(d[0]["cams"][fixed], prob["cams"][fixed])
