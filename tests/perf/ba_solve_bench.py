@@ -78,6 +78,36 @@ def main():
         "default_lm_step": {"max_cg": 200, "cg_tol": 1e-10, "cg_iters": it10,
                             "ms_poll_every_8": t_def, "ms_no_poll_all_launches": t_def_async},
     }
+    # the sharded solve (sfm_ba_solve_sharded) in a world-size-1 RCCL group: the cost of its
+    # split camera passes and of one all-reduce per CG iteration (at N ranks each rank's point
+    # pass shrinks to 1/N; the camera-side all-reduce of 8 n_cam doubles stays)
+    import socket
+    import torch.distributed as dist
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    ar = R.make_allreduce()
+    shs = lambda it: P.ctx.ba_solve_sharded(lin, P.cam_idx, P.pt_idx, P.pt_ptr, P.cam_ptr,
+                                            P.cam_obs, lam, ar, max_iter=it, tol=0.0)
+    s0 = timed(lambda: shs(0), 10)
+    sn = timed(lambda: shs(cg), 5)
+    sh_it = (sn - s0) / cg
+    fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    import time
+    tw = time.perf_counter()
+    _, _, h1 = R.bundle_adjust(*args, max_iter=5, fixed=fixed)
+    t_un = time.perf_counter() - tw
+    tw = time.perf_counter()
+    _, _, h2 = R.bundle_adjust(*args, max_iter=5, fixed=fixed, shard=True)
+    t_sh = time.perf_counter() - tw
+    dist.destroy_process_group()
+    out["sharded_world1_rccl"] = {
+        "cg_iter_ms": sh_it, "setup_backsub_ms": s0, "cg_iter_overhead_ms": sh_it - per_it,
+        "bundle_adjust_5_steps_s": {"unsharded": t_un, "sharded": t_sh},
+        "final_cost_rel_diff": abs(h1[-1][0] - h2[-1][0]) / h1[-1][0]}
     print(json.dumps(out))
 
 
