@@ -544,7 +544,7 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
     const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
-    unsigned long long* __restrict__ colpart) {
+    unsigned long long* __restrict__ colpart, int col_atomic) {
     constexpr int QT = Geo<D>::QT, QB = mu_qb<D>(), CHUNK = MU_CHUNK_BYTES / D, NK = Geo<D>::NK;
     constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32, NTHR = 64 * MU_WAVES;
     constexpr int PIECES = CHUNK * D / 1024 / MU_WAVES, RPP = 1024 / D;
@@ -703,8 +703,18 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
             if (h == 0 && q < na) rowres[(size_t)p * k_pad + q] = make_int4(e1, e2, 0, 0);
         }
     }
-    unsigned long long* dst = colpart + ((size_t)p * n_qblk + qb) * k_pad;
-    for (int j = tid; j < k_pad; j += NTHR) dst[j] = lds_col[j];
+    if (col_atomic) {
+        // merged across the pair's query blocks in place (zeroed before the launch; the grid
+        // keeps every pair's blocks on one XCD, so the merge happens in that XCD's L2)
+        unsigned long long* dst = colpart + (size_t)p * k_pad;
+        for (int j = tid; j < k_pad; j += NTHR) {
+            const unsigned long long v = lds_col[j];
+            if (v != 0ull) atomicMax(dst + j, v);
+        }
+    } else {
+        unsigned long long* dst = colpart + ((size_t)p * n_qblk + qb) * k_pad;
+        for (int j = tid; j < k_pad; j += NTHR) dst[j] = lds_col[j];
+    }
 #ifdef MU_CLOCK
     __syncthreads();
     if (tid == 0 && blockIdx.x < MU_CLOCK_SLOTS)
@@ -1033,7 +1043,17 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
     int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
     const int n_blk = n_pairs * n_qblk;
-    const int grid = 8 * ((n_blk + 7) / 8);
+    // column winners merged by atomics (default) or as per-query-block partials the finalize
+    // reduces (SFM_MU_COLPART=1); DESIGN.md 4.1
+    static const int col_atomic = [] {
+        const char* e = getenv("SFM_MU_COLPART");
+        return (e && e[0] == '1') ? 0 : 1;
+    }();
+    // whole pairs per XCD (blocks of one pair never straddle two XCDs' ranges)
+    const int grid = 8 * ((n_pairs + 7) / 8) * n_qblk;
+    const int fin_qblk = col_atomic ? 1 : n_qblk;
+    if (col_atomic)
+        SFM_HIP_CHECK(hipMemsetAsync(colpart, 0, sizeof(unsigned long long) * (size_t)n_pairs * k_pad, st));
     hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
                        pairs, n_pairs, n_img, pair_order, pair_order + n_pairs);
     SFM_HIP_CHECK(hipGetLastError());
@@ -1050,7 +1070,7 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(64 * MU_WAVES),             \
                        (size_t)k_pad * 8, st, desc_i8, n_kp,                                      \
                        k_max, k_pad, norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk,     \
-                       rowres, colpart)
+                       rowres, colpart, col_atomic)
     if (l2 && rows) SFM_MU_SCAN(128, true);
     else if (l2) SFM_MU_SCAN(128, false);
     else if (rows) SFM_MU_SCAN(256, true);
@@ -1061,16 +1081,16 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
         if (l2)
             hipLaunchKernelGGL(mutual_finalize_kernel<128>, dim3(n_pairs), dim3(MU_FT),
                                (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
-                               n_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
+                               fin_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
                                (long long)prm->max_dist, out_count, out_match, out_dist);
         else
             hipLaunchKernelGGL(mutual_finalize_kernel<256>, dim3(n_pairs), dim3(MU_FT),
                                (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
-                               n_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
+                               fin_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
                                (long long)prm->max_dist, out_count, out_match, out_dist);
     } else {
         hipLaunchKernelGGL(opencv_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st,
-                           n_kp, k_max, k_pad, norm, pairs, n_qblk, colpart,
+                           n_kp, k_max, k_pad, norm, pairs, fin_qblk, colpart,
                            (long long)prm->max_dist, out_count, out_match, out_dist);
     }
     SFM_HIP_CHECK(hipGetLastError());
