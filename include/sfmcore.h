@@ -177,23 +177,35 @@ int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
                  const double* W, const double* gc, const double* gp,
                  const sfm_ba_solve_params* prm, double* dc, double* dp, double* info);
 /* Multi-GPU form of sfm_ba_solve (observations sharded by point, one process per
- * GPU).  V, W, gp, dp, pt_ptr and the observation arrays are this rank's point shard (point and
- * observation indices local to it); U and gc are the GLOBAL camera blocks (sfm_ba_jtj on the
- * shard, then an all-reduce of U/gc, then sfm_ba_fix_params).  Every camera-space sum over
- * observations is written to the caller's device buffer comm (>= 44 * n_cam doubles) and
- * `allreduce(user, comm, n)` must sum comm[0, n) over all ranks in place, ordered on the
- * context's stream (e.g. an RCCL all-reduce enqueued on it), and return 0: once per solve with
- * n = 44 n_cam, once per CG iteration with n = 8 n_cam, once with n = 2.  All camera-space
- * state is then replicated, so every rank takes the same CG decisions and returns the same
- * dc and info; dp is the shard's.  Same result as sfm_ba_solve on the whole problem up to the
- * summation order (fp64).  No counterpart in the reference (its BA module is empty). */
-typedef int (*sfm_allreduce_fn)(void* user, double* buf, int64_t n);
-int sfm_ba_solve_sharded(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
-                         const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
-                         const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
-                         const double* V, const double* W, const double* gc, const double* gp,
-                         const sfm_ba_solve_params* prm, sfm_allreduce_fn allreduce, void* user,
-                         double* comm, double* dc, double* dp, double* info);
+ * GPU), as caller-driven stages so that no callback crosses the ABI: the caller all-reduces
+ * (sums over all ranks, in place) the device buffer comm (>= 44 * n_cam doubles) between the
+ * stage that fills it and the next one, ordered on the context's stream (e.g. an RCCL all-reduce
+ * enqueued on it).  V, W, gp, dp, pt_ptr and the observation arrays are this rank's point shard
+ * (indices local to it); U and gc are the GLOBAL camera blocks (sfm_ba_jtj on the shard, an
+ * all-reduce of U / gc, then sfm_ba_fix_params).  Sequence (prm / arrays identical in every call;
+ * no other sfm_* call on this context in between — the stages share its workspace):
+ *   SETUP           -> all-reduce comm[0, 44 n_cam)  -> SETUP_FINISH
+ *   for k = 0 .. max_iter-1:
+ *     [every prm->poll (0: 8) iterations, k > 0: POLL -> *done (host int32); stop if 1]
+ *     ITER(k)       -> all-reduce comm[0, 8 n_cam)   -> ITER_FINISH(k)
+ *   BACKSUB         -> all-reduce comm[0, 2)         -> MODEL   (dc, dp, info as sfm_ba_solve)
+ * After each all-reduce every camera-space value is replicated, so every rank takes the same CG
+ * decisions (POLL included) and issues the same collectives; dc and info are the same on every
+ * rank, dp is the shard's.  Equal to sfm_ba_solve on the whole problem up to the fp64 summation
+ * order.  No counterpart in the reference (its BA module is empty). */
+#define SFM_BA_STAGE_SETUP 0
+#define SFM_BA_STAGE_SETUP_FINISH 1
+#define SFM_BA_STAGE_ITER 2
+#define SFM_BA_STAGE_ITER_FINISH 3
+#define SFM_BA_STAGE_BACKSUB 4
+#define SFM_BA_STAGE_MODEL 5
+#define SFM_BA_STAGE_POLL 6
+int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_t n_cam, int32_t n_pt,
+                       int32_t n_obs, const int32_t* cam_idx, const int32_t* pt_idx,
+                       const int32_t* pt_ptr, const int32_t* cam_ptr, const int32_t* cam_obs,
+                       const double* U, const double* V, const double* W, const double* gc,
+                       const double* gp, const sfm_ba_solve_params* prm, double* comm, double* dc,
+                       double* dp, double* info, int32_t* done);
 /* Fixed parameters (the gauge: the reference camera's pose and one translation coordinate of a
  * second camera; known intrinsics f, k1): in place on sfm_ba_jtj's U [n_cam][8][8], W [n_obs][8][3]
  * and g_c [n_cam][8], the rows/columns of the parameters marked in fixed [n_cam][8] (u8, 1 =

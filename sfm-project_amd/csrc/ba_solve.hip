@@ -699,132 +699,95 @@ __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const d
 
 }  // namespace
 
-// The solve; `allreduce` == nullptr: unsharded.  Otherwise the points (V, gp, dp, pt_ptr and the
-// observations) are this rank's shard, the camera blocks (U, gc) are the all-reduced global ones,
-// and every camera-space partial that sums over observations goes through comm + allreduce:
-// the 44 setup sums per camera once, Σ_o W_o t_p (8 per camera) per CG iteration, and the 2
-// point-side LM model terms.  Everything downstream of an all-reduce is computed from replicated
-// values, so every rank takes the same CG decisions (the convergence poll included) and calls
-// `allreduce` the same number of times.
-static int ba_solve_impl(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
-                         const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
-                         const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
-                         const double* V, const double* W, const double* gc, const double* gp,
-                         const sfm_ba_solve_params* prm, sfm_allreduce_fn allreduce, void* user,
-                         double* comm, double* dc, double* dp, double* info) {
-    const bool sharded = allreduce != nullptr;
-    SFM_REQUIRE(!sharded || comm != nullptr, "sfm_ba_solve_sharded: comm is NULL");
-#define SFM_ALLREDUCE(n)                                                                       \
-    do {                                                                                       \
-        SFM_HIP_CHECK(hipGetLastError());                                                      \
-        if (allreduce(user, comm, (int64_t)(n)) != 0) {                                        \
-            sfm::set_error("sfm_ba_solve_sharded: the all-reduce callback failed");            \
-            return SFM_ERR_INVALID;                                                            \
-        }                                                                                      \
-    } while (0)
-    SFM_REQUIRE(ctx != nullptr && prm != nullptr, "sfm_ba_solve: ctx/prm is NULL");
-    SFM_REQUIRE(n_cam > 0 && n_pt >= 0 && n_obs >= 0, "sfm_ba_solve: bad size");
-    SFM_REQUIRE(prm->max_iter >= 0 && prm->lambda >= 0.0 && prm->tol >= 0.0,
-                "sfm_ba_solve: max_iter, lambda and tol must be >= 0");
-    // per-observation arrays may be NULL without observations, per-point ones without points
-    SFM_REQUIRE(cam_ptr && U && gc && dc && info && (n_obs == 0 || (cam_idx && pt_idx && cam_obs && W)) &&
-                    (n_pt == 0 || (pt_ptr && V && gp && dp)),
-                "sfm_ba_solve: NULL array");
-    SFM_HIP_CHECK(hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
-    const int pblk = std::max(1, (n_pt + 255) / 256);
+// Device workspace of a solve (one carve for the unsharded solve and every stage of the sharded
+// one: the same sizes give the same pointers, so state persists across the stage calls).
+struct SolveWs {
+    double *Vinv, *vg, *t, *Ud, *Mc, *r, *z, *pv, *q, *rzc, *rrc, *pq, *mpart, *Wp, *Wc;
+    PcgState* state;
+    int32_t* bad;
+    int32_t* ptc;
+    int pblk, gblk, vblk;
+};
+
+static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, SolveWs& w) {
     // workspace: Vinv 9 | vg 3 | t 3 per point; Ud 64 | M 64 | r z p q 8 each | rz, rr partials
     // (2 parity slots each) | p·q per camera; backsub partials; state; bad flag
+    w.pblk = std::max(1, (n_pt + 255) / 256);
     const size_t np = (size_t)std::max(n_pt, 1), nc = (size_t)n_cam;
     const size_t b_pt = sfm::align_up(sizeof(double) * 15 * np, 256);
     const size_t b_cam = sfm::align_up(sizeof(double) * (128 + 32 + 5) * nc, 256);
-    const int gblk = std::max(1, (n_pt + 256 / PG - 1) / (256 / PG));  // PG lanes per point
-    const size_t b_part = sfm::align_up(sizeof(double) * 2 * (size_t)gblk, 256);
+    w.gblk = std::max(1, (n_pt + 256 / PG - 1) / (256 / PG));  // PG lanes per point
+    const size_t b_part = sfm::align_up(sizeof(double) * 2 * (size_t)w.gblk, 256);
     const size_t no = (size_t)std::max(n_obs, 1);
     const size_t b_soa = sfm::align_up(sizeof(double) * 48 * no + sizeof(int32_t) * no, 256);
     char* ws = (char*)sfm::workspace(ctx, b_pt + b_cam + b_part + 512 + b_soa);
     if (!ws) return SFM_ERR_NOMEM;
-    double* Vinv = (double*)ws;
-    double* vg = Vinv + 9 * np;
-    double* t = vg + 3 * np;
-    double* Ud = (double*)(ws + b_pt);
-    double* Mc = Ud + 64 * nc;
-    double* r = Mc + 64 * nc;
-    double* z = r + 8 * nc;
-    double* pv = z + 8 * nc;
-    double* q = pv + 8 * nc;
-    double* rzc = q + 8 * nc;   // [2][n_cam]
-    double* rrc = rzc + 2 * nc; // [2][n_cam]
-    double* pq = rrc + 2 * nc;
-    double* mpart = (double*)(ws + b_pt + b_cam);
-    PcgState* state = (PcgState*)(ws + b_pt + b_cam + b_part);
-    int32_t* bad = (int32_t*)(ws + b_pt + b_cam + b_part + 256);
-    double* Wp = (double*)(ws + b_pt + b_cam + b_part + 512);
-    double* Wc = Wp + 24 * no;
-    int32_t* ptc = (int32_t*)(Wc + 24 * no);
-    const double lam = prm->lambda, tol = prm->tol;
-    SFM_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int32_t), st));
+    w.Vinv = (double*)ws;
+    w.vg = w.Vinv + 9 * np;
+    w.t = w.vg + 3 * np;
+    w.Ud = (double*)(ws + b_pt);
+    w.Mc = w.Ud + 64 * nc;
+    w.r = w.Mc + 64 * nc;
+    w.z = w.r + 8 * nc;
+    w.pv = w.z + 8 * nc;
+    w.q = w.pv + 8 * nc;
+    w.rzc = w.q + 8 * nc;    // [2][n_cam]
+    w.rrc = w.rzc + 2 * nc;  // [2][n_cam]
+    w.pq = w.rrc + 2 * nc;
+    w.mpart = (double*)(ws + b_pt + b_cam);
+    w.state = (PcgState*)(ws + b_pt + b_cam + b_part);
+    w.bad = (int32_t*)(ws + b_pt + b_cam + b_part + 256);
+    w.Wp = (double*)(ws + b_pt + b_cam + b_part + 512);
+    w.Wc = w.Wp + 24 * no;
+    w.ptc = (int32_t*)(w.Wc + 24 * no);
+    w.vblk = (8 * n_cam + 255) / 256;
+    return SFM_OK;
+}
+
+// Point setup, SoA W and the camera setup (phase 0: whole; 1: partial sums -> comm).
+static int solve_setup(hipStream_t st, const SolveWs& w, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+                       const int32_t* pt_idx, const int32_t* pt_ptr, const int32_t* cam_ptr,
+                       const int32_t* cam_obs, const double* U, const double* V, const double* W,
+                       const double* gc, const double* gp, double lam, double* dc, int phase,
+                       double* comm) {
+    SFM_HIP_CHECK(hipMemsetAsync(w.bad, 0, sizeof(int32_t), st));
     if (n_pt > 0) {
-        hipLaunchKernelGGL(bas_point_setup, dim3(pblk), dim3(256), 0, st, n_pt, pt_ptr, V, gp, lam,
-                           Vinv, vg);
+        hipLaunchKernelGGL(bas_point_setup, dim3(w.pblk), dim3(256), 0, st, n_pt, pt_ptr, V, gp,
+                           lam, w.Vinv, w.vg);
         SFM_HIP_CHECK(hipGetLastError());
     }
     if (n_obs > 0) {
         hipLaunchKernelGGL(bas_soa, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs, cam_obs,
-                           pt_idx, W, Wp, Wc, ptc);
+                           pt_idx, W, w.Wp, w.Wc, w.ptc);
         SFM_HIP_CHECK(hipGetLastError());
     }
-    if (sharded) {
-        hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
-                           ptc, U, Wc, Vinv, vg, gc, lam, Ud, Mc, dc, r, z, pv, rzc, rrc, bad, 1,
-                           comm);
-        SFM_ALLREDUCE(44 * (size_t)n_cam);
-    }
-    hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr, ptc,
-                       U, Wc, Vinv, vg, gc, lam, Ud, Mc, dc, r, z, pv, rzc, rrc, bad,
-                       sharded ? 2 : 0, comm);
-    SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, rrc, state);
-    SFM_HIP_CHECK(hipGetLastError());
-    const int vblk = (8 * n_cam + 255) / 256;
-    const int poll = prm->poll == 0 ? 8 : prm->poll;
-    if (poll > 0 && !ctx->pinned)
-        SFM_HIP_CHECK(hipHostMalloc((void**)&ctx->pinned, 64, hipHostMallocDefault));
-    for (int k = 0; k < prm->max_iter; ++k) {
-        // state->done is set by bas_pcg_point of the first iteration after convergence: once it
-        // reads 1, every later iteration would exit at once, so stop enqueueing them
-        if (poll > 0 && k > 0 && k % poll == 0) {
-            SFM_HIP_CHECK(hipMemcpyAsync(ctx->pinned, &state->done, sizeof(int32_t),
-                                         hipMemcpyDeviceToHost, st));
-            SFM_HIP_CHECK(hipStreamSynchronize(st));
-            if (ctx->pinned[0] != 0) break;
-        }
-        hipLaunchKernelGGL(bas_pcg_point, dim3(gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
-                           pt_ptr, cam_idx, Wp, Vinv, z, pv, rzc, rrc, tol, state, t);
-        if (sharded) {
-            hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs,
-                               cam_ptr, ptc, Wc, t, Ud, z, pv, state, q, pq, 1, comm);
-            SFM_ALLREDUCE(8 * (size_t)n_cam);
-        }
-        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
-                           ptc, Wc, t, Ud, z, pv, state, q, pq, sharded ? 2 : 0, comm);
-        hipLaunchKernelGGL(bas_pcg_vec, dim3(vblk), dim3(256), 0, st, k, n_cam, Mc, dc, r, z, pv, q,
-                           pq, rzc, rrc, state);
-    }
-    SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bas_backsub, dim3(gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr, cam_idx, Wp, V,
-                       Vinv, vg, gp, dc, dp, mpart);
-    SFM_HIP_CHECK(hipGetLastError());
-    if (sharded) {
-        hipLaunchKernelGGL(bas_mpart_total, dim3(1), dim3(1024), 0, st, gblk, mpart, comm);
-        SFM_ALLREDUCE(2);
-    }
-    hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, sharded ? 1 : gblk, U, gc, dc,
-                       sharded ? comm : mpart, rrc, state, bad, info);
+    hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
+                       w.ptc, U, w.Wc, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
+                       w.rzc, w.rrc, w.bad, phase, comm);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
-#undef SFM_ALLREDUCE
 }
+
+static int solve_poll(sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int32_t* done) {
+    if (!ctx->pinned)
+        SFM_HIP_CHECK(hipHostMalloc((void**)&ctx->pinned, 64, hipHostMallocDefault));
+    SFM_HIP_CHECK(hipMemcpyAsync(ctx->pinned, &w.state->done, sizeof(int32_t),
+                                 hipMemcpyDeviceToHost, st));
+    SFM_HIP_CHECK(hipStreamSynchronize(st));
+    *done = ctx->pinned[0];
+    return SFM_OK;
+}
+
+#define SFM_SOLVE_ARGS_CHECK(NAME)                                                                \
+    SFM_REQUIRE(ctx != nullptr && prm != nullptr, NAME ": ctx/prm is NULL");                     \
+    SFM_REQUIRE(n_cam > 0 && n_pt >= 0 && n_obs >= 0, NAME ": bad size");                        \
+    SFM_REQUIRE(prm->max_iter >= 0 && prm->lambda >= 0.0 && prm->tol >= 0.0,                      \
+                NAME ": max_iter, lambda and tol must be >= 0");                                  \
+    /* per-observation arrays may be NULL without observations, per-point ones without points */ \
+    SFM_REQUIRE(cam_ptr && U && gc && dc && info &&                                               \
+                    (n_obs == 0 || (cam_idx && pt_idx && cam_obs && W)) &&                        \
+                    (n_pt == 0 || (pt_ptr && V && gp && dp)),                                     \
+                NAME ": NULL array")
 
 extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
                             const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,
@@ -832,22 +795,110 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
                             const double* V, const double* W, const double* gc, const double* gp,
                             const sfm_ba_solve_params* prm, double* dc, double* dp,
                             double* info) {
-    return ba_solve_impl(ctx, n_cam, n_pt, n_obs, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
-                         W, gc, gp, prm, nullptr, nullptr, nullptr, dc, dp, info);
+    SFM_SOLVE_ARGS_CHECK("sfm_ba_solve");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    SolveWs w;
+    if (solve_ws(ctx, n_cam, n_pt, n_obs, w) != SFM_OK) return SFM_ERR_NOMEM;
+    const double lam = prm->lambda, tol = prm->tol;
+    const int rc = solve_setup(st, w, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
+                               W, gc, gp, lam, dc, 0, nullptr);
+    if (rc != SFM_OK) return rc;
+    hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
+    SFM_HIP_CHECK(hipGetLastError());
+    const int poll = prm->poll == 0 ? 8 : prm->poll;
+    for (int k = 0; k < prm->max_iter; ++k) {
+        // state->done is set by bas_pcg_point of the first iteration after convergence: once it
+        // reads 1, every later iteration would exit at once, so stop enqueueing them
+        if (poll > 0 && k > 0 && k % poll == 0) {
+            int32_t done = 0;
+            const int prc = solve_poll(ctx, st, w, &done);
+            if (prc != SFM_OK) return prc;
+            if (done) break;
+        }
+        hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
+                           pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol, w.state,
+                           w.t);
+        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
+                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 0, nullptr);
+        hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
+                           w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);
+    }
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bas_backsub, dim3(w.gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr, cam_idx,
+                       w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, w.gblk, U, gc, dc, w.mpart,
+                       w.rrc, w.state, w.bad, info);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
 }
 
-extern "C" int sfm_ba_solve_sharded(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
-                                    const int32_t* cam_idx, const int32_t* pt_idx,
-                                    const int32_t* pt_ptr, const int32_t* cam_ptr,
-                                    const int32_t* cam_obs, const double* U, const double* V,
-                                    const double* W, const double* gc, const double* gp,
-                                    const sfm_ba_solve_params* prm, sfm_allreduce_fn allreduce,
-                                    void* user, double* comm, double* dc, double* dp,
-                                    double* info) {
-    SFM_REQUIRE(allreduce != nullptr, "sfm_ba_solve_sharded: allreduce callback is NULL");
-    return ba_solve_impl(ctx, n_cam, n_pt, n_obs, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
-                         W, gc, gp, prm, allreduce, user, comm, dc, dp, info);
+// The sharded solve as caller-driven stages (no callbacks across the ABI): the caller all-reduces
+// comm between the stages that produce partial sums and the ones that consume them.  Every stage
+// after an all-reduce works on replicated camera-space values, so all ranks take the same CG
+// decisions and issue the same collectives.
+extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_t n_cam,
+                                  int32_t n_pt, int32_t n_obs, const int32_t* cam_idx,
+                                  const int32_t* pt_idx, const int32_t* pt_ptr,
+                                  const int32_t* cam_ptr, const int32_t* cam_obs, const double* U,
+                                  const double* V, const double* W, const double* gc,
+                                  const double* gp, const sfm_ba_solve_params* prm, double* comm,
+                                  double* dc, double* dp, double* info, int32_t* done) {
+    SFM_SOLVE_ARGS_CHECK("sfm_ba_solve_stage");
+    SFM_REQUIRE(comm != nullptr, "sfm_ba_solve_stage: comm is NULL");
+    SFM_REQUIRE(stage >= SFM_BA_STAGE_SETUP && stage <= SFM_BA_STAGE_POLL,
+                "sfm_ba_solve_stage: unknown stage");
+    SFM_REQUIRE(stage != SFM_BA_STAGE_POLL || done != nullptr, "sfm_ba_solve_stage: done is NULL");
+    SFM_REQUIRE(k >= 0, "sfm_ba_solve_stage: k must be >= 0");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    SolveWs w;
+    if (solve_ws(ctx, n_cam, n_pt, n_obs, w) != SFM_OK) return SFM_ERR_NOMEM;
+    const double lam = prm->lambda, tol = prm->tol;
+    switch (stage) {
+    case SFM_BA_STAGE_SETUP:  // -> comm[0, 44 n_cam)
+        return solve_setup(st, w, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V, W,
+                           gc, gp, lam, dc, 1, comm);
+    case SFM_BA_STAGE_SETUP_FINISH:
+        hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
+                           w.ptc, U, w.Wc, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
+                           w.rzc, w.rrc, w.bad, 2, comm);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
+        break;
+    case SFM_BA_STAGE_ITER:  // -> comm[0, 8 n_cam)
+        hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
+                           pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol, w.state,
+                           w.t);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
+                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 1, comm);
+        break;
+    case SFM_BA_STAGE_ITER_FINISH:
+        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
+                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 2, comm);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
+                           w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);
+        break;
+    case SFM_BA_STAGE_BACKSUB:  // -> comm[0, 2)
+        hipLaunchKernelGGL(bas_backsub, dim3(w.gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr,
+                           cam_idx, w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(bas_mpart_total, dim3(1), dim3(1024), 0, st, w.gblk, w.mpart, comm);
+        break;
+    case SFM_BA_STAGE_MODEL:
+        hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, 1, U, gc, dc, comm,
+                           w.rrc, w.state, w.bad, info);
+        break;
+    case SFM_BA_STAGE_POLL:
+        return solve_poll(ctx, st, w, done);
+    }
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
 }
+#undef SFM_SOLVE_ARGS_CHECK
 
 // ---- fixed parameters (gauge / known intrinsics) ------------------------------------------------
 //

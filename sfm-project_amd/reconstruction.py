@@ -232,7 +232,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     shard (multi-GPU; needs an initialised torch.distributed group): every rank
     takes the points of its `shard_points` range with their observations; the camera blocks
     U / g_c are all-reduced after each linearisation, the Schur-complement PCG runs sharded
-    (sfm_ba_solve_sharded: one 8·n_cam fp64 all-reduce per CG iteration), the trial cost is
+    (sfm_ba_solve_stage: one 8·n_cam fp64 all-reduce per CG iteration), the trial cost is
     all-reduced and the points are gathered at the end.  Every rank returns the same result,
     equal to the unsharded one up to the fp64 summation order.
 

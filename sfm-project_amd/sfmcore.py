@@ -24,7 +24,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
-            "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_sharded"]
+            "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage"]
 
 
 class SfmCoreError(RuntimeError):
@@ -56,8 +56,9 @@ class RansacParams(C.Structure):
                 ("_pad", C.c_int32), ("seed", C.c_uint64)]
 
 
-# int (*sfm_allreduce_fn)(void* user, double* buf, int64_t n)
-ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64)
+# stages of sfm_ba_solve_stage (include/sfmcore.h)
+(BA_STAGE_SETUP, BA_STAGE_SETUP_FINISH, BA_STAGE_ITER, BA_STAGE_ITER_FINISH, BA_STAGE_BACKSUB,
+ BA_STAGE_MODEL, BA_STAGE_POLL) = range(7)
 
 _lib = None
 _lock = threading.Lock()
@@ -96,9 +97,8 @@ def load_library(path: str = LIB_PATH):
                                  vp, vp, vp, vp, vp, vp]
         L.sfm_ba_solve.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                    C.POINTER(BaSolveParams), vp, vp, vp]
-        L.sfm_ba_solve_sharded.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
-                                           vp, C.POINTER(BaSolveParams), ALLREDUCE_FN, vp, vp, vp,
-                                           vp, vp]
+        L.sfm_ba_solve_stage.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp,
+                                         vp, vp, vp, C.POINTER(BaSolveParams), vp, vp, vp, vp, vp]
         L.sfm_ba_cost.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp]
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
         L.sfm_ba_fix_params.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp]
@@ -370,8 +370,9 @@ class Context:
     def ba_solve_sharded(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, allreduce,
                          max_iter=100, tol=1e-10, out=None, poll=0):
         """ba_solve on this rank's point shard (lin: ba_jtj of the shard with U / gc already
-        all-reduced).  allreduce(t): sums the f64 device tensor t over all ranks in place, ordered
-        on the current stream (reconstruction.make_allreduce).  Returns (dc, dp, info)."""
+        all-reduced), driving sfm_ba_solve_stage: allreduce(t) sums the f64 device tensor t over
+        all ranks in place, ordered on the current stream (reconstruction.make_allreduce).
+        Returns (dc, dp, info) like ba_solve."""
         torch = self.torch
         U = lin["U"]
         dev = U.device
@@ -383,26 +384,31 @@ class Context:
                    torch.empty(5, dtype=f64, device=dev))
         dc, dp, info = out
         comm = torch.empty(44 * nc, dtype=torch.float64, device=dev)
-        err = []
-
-        def cb(_user, _buf, n):
-            try:
-                allreduce(comm[:n])
-                return 0
-            except Exception as e:  # reported through sfm_last_error's caller below
-                err.append(e)
-                return 1
-        fn = ALLREDUCE_FN(cb)
         prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll))
+        done = C.c_int32(0)
+        args = (nc, npt, no, _ptr(cam_idx), _ptr(pt_idx), _ptr(pt_ptr), _ptr(cam_ptr),
+                _ptr(cam_obs), _ptr(U), _ptr(lin["V"]), _ptr(lin["W"]), _ptr(lin["gc"]),
+                _ptr(lin["gp"]), C.byref(prm), _ptr(comm), _ptr(dc), _ptr(dp), _ptr(info),
+                C.byref(done))
         self._bind_stream()
-        rc = self.lib.sfm_ba_solve_sharded(self.handle, nc, npt, no, _ptr(cam_idx), _ptr(pt_idx),
-                                           _ptr(pt_ptr), _ptr(cam_ptr), _ptr(cam_obs), _ptr(U),
-                                           _ptr(lin["V"]), _ptr(lin["W"]), _ptr(lin["gc"]),
-                                           _ptr(lin["gp"]), C.byref(prm), fn, None, _ptr(comm),
-                                           _ptr(dc), _ptr(dp), _ptr(info))
-        if err:
-            raise err[0]
-        _check(rc)
+
+        def stage(s, k=0):
+            _check(self.lib.sfm_ba_solve_stage(self.handle, s, k, *args))
+        stage(BA_STAGE_SETUP)
+        allreduce(comm[:44 * nc])
+        stage(BA_STAGE_SETUP_FINISH)
+        every = 8 if poll == 0 else poll
+        for k in range(max_iter):
+            if every > 0 and k > 0 and k % every == 0:
+                stage(BA_STAGE_POLL)   # the same decision on every rank (replicated state)
+                if done.value:
+                    break
+            stage(BA_STAGE_ITER, k)
+            allreduce(comm[:8 * nc])
+            stage(BA_STAGE_ITER_FINISH, k)
+        stage(BA_STAGE_BACKSUB)
+        allreduce(comm[:2])
+        stage(BA_STAGE_MODEL)
         return dc, dp, info
 
     def ba_fix_params(self, lin, cam_idx, fixed):

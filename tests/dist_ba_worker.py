@@ -1,7 +1,7 @@
 """Worker of tests/test_gpu_ba_sharded.py::test_ba_sharded_two_ranks: one rank of a
 torch.distributed.run job (gloo, every rank on GPU 0 — RCCL cannot share a device).  Each rank runs
 the point-sharded bundle adjustment (reconstruction.bundle_adjust(shard=True): camera-block
-all-reduce, sfm_ba_solve_sharded with one all-reduce per CG iteration, all-reduced trial cost,
+all-reduce, sfm_ba_solve_stage with one all-reduce per CG iteration, all-reduced trial cost,
 gathered points) and one sharded solve from the initial linearisation; it writes OUT.rank<r>.npz.
 Usage: python -m torch.distributed.run --nproc-per-node N ... dist_ba_worker.py OUT"""
 import os

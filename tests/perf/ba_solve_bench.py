@@ -78,7 +78,7 @@ def main():
         "default_lm_step": {"max_cg": 200, "cg_tol": 1e-10, "cg_iters": it10,
                             "ms_poll_every_8": t_def, "ms_no_poll_all_launches": t_def_async},
     }
-    # the sharded solve (sfm_ba_solve_sharded) in a world-size-1 RCCL group: the cost of its
+    # the sharded solve (sfm_ba_solve_stage) in a world-size-1 RCCL group: the cost of its
     # split camera passes and of one all-reduce per CG iteration (at N ranks each rank's point
     # pass shrinks to 1/N; the camera-side all-reduce of 8 n_cam doubles stays)
     import socket

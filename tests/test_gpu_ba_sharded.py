@@ -1,5 +1,5 @@
 """GPU: the point-sharded bundle-adjustment step —
-sfm_ba_solve_sharded and reconstruction.bundle_adjust(shard=True).
+sfm_ba_solve_stage and reconstruction.bundle_adjust(shard=True).
 
 Tolerances (fp64; sharding re-associates the camera-space sums over observations):
   world-size-1 RCCL group: δ bit-identical to sfm_ba_solve (the phases split the same sums), the
