@@ -3,7 +3,8 @@ torch.distributed.run job (gloo, every rank on GPU 0 — RCCL cannot share a dev
 the point-sharded bundle adjustment (reconstruction.bundle_adjust(shard=True): camera-block
 all-reduce, sfm_ba_solve_stage with one all-reduce per CG iteration, all-reduced trial cost,
 gathered points) and one sharded solve from the initial linearisation; it writes OUT.rank<r>.npz.
-Usage: python -m torch.distributed.run --nproc-per-node N ... dist_ba_worker.py OUT"""
+A second argument `tiny` uses a 2-point problem (with 3 ranks one shard is empty).
+Usage: python -m torch.distributed.run --nproc-per-node N ... dist_ba_worker.py OUT [tiny]"""
 import os
 import sys
 
@@ -17,7 +18,7 @@ import torch.distributed as dist
 import reconstruction as R
 import sfmcore
 import synth
-from test_gpu_ba_sharded import problem, shard_solve
+from test_gpu_ba_sharded import problem, shard_solve, tiny_problem
 
 
 def main():
@@ -25,7 +26,7 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    prob = problem()
+    prob = tiny_problem() if len(sys.argv) > 2 and sys.argv[2] == "tiny" else problem()
     args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
     fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
     cams, pts, hist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed, shard=True)

@@ -23,6 +23,10 @@ def problem():
     return synth.make_ba_problem(9, 300, obs_per_pt=4, seed=17, perturb=3e-3)
 
 
+def tiny_problem():
+    return synth.make_ba_problem(4, 2, obs_per_pt=3, seed=5, perturb=1e-3)
+
+
 def shard_solve(prob, rank, world, allreduce, lam=1e-3):
     """One sharded solve from the initial linearisation of `prob` on this rank's point shard."""
     import torch
@@ -86,25 +90,54 @@ def test_ba_sharded_world1_rccl():
         dist.destroy_process_group()
 
 
+def _run_ranks(tmp_path, n, *extra):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "ba")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "tests", "dist_ba_worker.py"), out, *extra]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return [np.load(f"{out}.rank{k}.npz") for k in range(n)]
+
+
+def test_ba_sharded_three_ranks_with_an_empty_shard(tmp_path):
+    """Three ranks on a 2-point problem: one rank owns no point and no observation, and still
+    takes part in every collective; all ranks agree bit for bit and match the single process."""
+    prob = tiny_problem()
+    pt_ptr, _ = sfmcore.csr_by(prob["pt_idx"], len(prob["pts"]))
+    assert min(h - l for l, h in (R.shard_points(pt_ptr, r, 3) for r in range(3))) == 0
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
+    rcams, rpts, rhist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
+    rdc, rdp, _ = _reference_solve(prob)
+    d = _run_ranks(tmp_path, 3, "tiny")
+    for k in (1, 2):
+        for key in ("cams", "pts", "hist", "dc", "info"):
+            np.testing.assert_array_equal(d[0][key], d[k][key])
+    # a 2-point problem is under-determined (the LM damping regularises it), so the tolerances
+    # against the single process are looser than the 300-point test's
+    np.testing.assert_allclose(d[0]["dc"], rdc, rtol=0, atol=1e-6 * np.abs(rdc).max())
+    np.testing.assert_allclose(np.concatenate([d[k]["dp"] for k in range(3)]), rdp, rtol=0,
+                               atol=1e-6 * np.abs(rdp).max())
+    assert abs(d[0]["hist"][-1][0] - rhist[-1][0]) <= 1e-6 * rhist[-1][0] + 1e-20
+    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(d[0]["pts"], rpts, rtol=1e-5, atol=1e-8)
+    assert len(d[2]["dp"]) == 0
+
+
 def test_ba_sharded_two_ranks(tmp_path):
     """Two ranks (torch.distributed.run, gloo, both on GPU 0) shard the points: the ranks agree
     bit for bit, and the sharded solve / LM match the single-process ones to fp64 reassociation."""
-    import subprocess
-    import sys
     prob = problem()
     rdc, rdp, rinfo = _reference_solve(prob)
     args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
     fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
     rcams, rpts, rhist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = str(tmp_path / "ba")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(root, "tests", "dist_ba_worker.py"), out]
-    env = dict(os.environ, OMP_NUM_THREADS="4")
-    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    d = [np.load(f"{out}.rank{k}.npz") for k in range(2)]
+    d = _run_ranks(tmp_path, 2)
     for key in ("cams", "pts", "hist", "dc", "info"):
         np.testing.assert_array_equal(d[0][key], d[1][key])
     assert int(d[0]["hi"]) == int(d[1]["lo"]) and 0 < int(d[0]["hi"]) < len(prob["pts"])
