@@ -86,6 +86,11 @@ constexpr int NU = 36 + 8;  // upper triangle of U_c (8x8) + g_c
 #define CAM_MLP 2  // observations whose gathers a camera-wave lane keeps in flight (2: 196 VGPRs,
                    // 60.3 us vs 61-62 with 4 at 220 VGPRs, profiles/r02/k3_ba_ab.txt)
 #endif
+#ifndef BA_CAM_HALVES
+#define BA_CAM_HALVES 1  // 2: two waves per camera, each accumulating half of the 44 sums
+#endif
+constexpr int CH = BA_CAM_HALVES, NUH = NU / CH;  // waves per camera, sums per wave
+static_assert(NU % CH == 0, "camera halves");
 #ifndef BA_SPLIT_TARGET
 #define BA_SPLIT_TARGET 256
 #endif
@@ -229,6 +234,46 @@ __device__ __forceinline__ void obs_block(
 // splits == 1, else as partials for ba_final_kernel.  One camera per WAVE (four per block): the
 // camera work holds a quarter of the block slots it held as block-per-camera, so the observation
 // blocks of the same launch stream underneath it from the start.
+// Sums t in [H*NUH, H*NUH + NUH) of one observation into acc[t - H*NUH] (compile-time indices).
+template <int H>
+__device__ __forceinline__ void cam_accum_half(double (&acc)[NU], const ObsLin& L) {
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = i; j < 8; ++j) {
+            if (t >= H * NUH && t < H * NUH + NUH)
+                acc[t - H * NUH] += L.w * (L.Jc[i] * L.Jc[j] + L.Jc[8 + i] * L.Jc[8 + j]);
+            ++t;
+        }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (t >= H * NUH && t < H * NUH + NUH)
+            acc[t - H * NUH] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
+        ++t;
+    }
+}
+
+// U_c (both triangles) and g_c entries t in [T0, T0 + N) from acc[t - T0].
+template <int T0, int N>
+__device__ __forceinline__ void cam_store(const double (&acc)[NU], double* __restrict__ Uc,
+                                          double* __restrict__ g) {
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = i; j < 8; ++j) {
+            if (t >= T0 && t < T0 + N) {
+                Uc[8 * i + j] = acc[t - T0];
+                Uc[8 * j + i] = acc[t - T0];
+            }
+            ++t;
+        }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (36 + i >= T0 && 36 + i < T0 + N) g[i] = acc[36 + i - T0];
+}
+
 __device__ __forceinline__ void camera_wave(
     int cw, const double* __restrict__ cams, const double* __restrict__ pp,
     const double* __restrict__ pts, const int32_t* __restrict__ pt_idx,
@@ -236,8 +281,10 @@ __device__ __forceinline__ void camera_wave(
     const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
     double* __restrict__ U, double* __restrict__ gc) {
     const int lane = threadIdx.x & 63;
+    const int hw = cw % CH;  // which NUH of the 44 sums this wave accumulates (wave-uniform)
+    cw /= CH;
     const int c = cw / splits, s = cw - c * splits;
-    double acc[NU];
+    double acc[NU];  // entries outside [hw*NUH, hw*NUH + NUH) are dead when CH > 1
 #pragma unroll
     for (int i = 0; i < NU; ++i) acc[i] = 0.0;
     const double* cam = cams + 8 * (size_t)c;
@@ -278,19 +325,26 @@ __device__ __forceinline__ void camera_wave(
             if (o[q] < 0) break;
             ObsLin L;
             linearize(R, cam, pp + 2 * (size_t)c, X[q], u[q], v[q], loss_s, false, L);
-            int t = 0;
+            if (CH == 1) {
+                int t = 0;
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+                for (int i = 0; i < 8; ++i)
 #pragma unroll
-                for (int j = i; j < 8; ++j)
-                    acc[t++] += L.w * (L.Jc[i] * L.Jc[j] + L.Jc[8 + i] * L.Jc[8 + j]);
+                    for (int j = i; j < 8; ++j)
+                        acc[t++] += L.w * (L.Jc[i] * L.Jc[j] + L.Jc[8 + i] * L.Jc[8 + j]);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) acc[36 + i] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
+                for (int i = 0; i < 8; ++i) acc[36 + i] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
+            } else {
+                // the same expressions, sum t of this wave's half into acc[t - hw*NUH]
+                if (hw == 0) cam_accum_half<0>(acc, L);
+                else cam_accum_half<1>(acc, L);
+            }
         }
     }
+    constexpr int NR = CH == 1 ? NU : NUH;  // live sums of this wave
 #ifndef BA_ABL_NORED  // ablation (timing only): no cross-lane reduction
 #pragma unroll
-    for (int i = 0; i < NU; ++i) {
+    for (int i = 0; i < NR; ++i) {
         double v = acc[i];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
@@ -298,24 +352,15 @@ __device__ __forceinline__ void camera_wave(
     }
 #endif
     if (lane != 0) return;
+    const int t0 = CH == 1 ? 0 : hw * NUH;  // sum index of acc[0]
     if (splits > 1) {
-        double* o = part + ((size_t)c * splits + s) * NU;
+        double* o = part + ((size_t)c * splits + s) * NU + t0;
 #pragma unroll
-        for (int i = 0; i < NU; ++i) o[i] = acc[i];
+        for (int i = 0; i < NR; ++i) o[i] = acc[i];
         return;
     }
-    double* Uc = U + 64 * (size_t)c;
-    int t = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = i; j < 8; ++j) {
-            Uc[8 * i + j] = acc[t];
-            Uc[8 * j + i] = acc[t];
-            ++t;
-        }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) gc[8 * (size_t)c + i] = acc[36 + i];
+    if (CH == 1 || hw == 0) cam_store<0, NR>(acc, U + 64 * (size_t)c, gc + 8 * (size_t)c);
+    else cam_store<NUH, NR>(acc, U + 64 * (size_t)c, gc + 8 * (size_t)c);
 }
 
 // One launch for both independent halves of the linearisation: blocks [0, n_camb) are the
@@ -324,7 +369,12 @@ __device__ __forceinline__ void camera_wave(
 // stream instead of after it.  The finish blocks (which read the observation blocks' segment
 // records) are a second launch.  (Measured alternative: the camera kernel on a forked
 // high-priority stream — the cross-queue join left ~18 us idle per call)
-__global__ __launch_bounds__(256) void ba_jtj_kernel(
+#ifdef BA_MINW  // build knob: minimum waves per SIMD for the merged kernel (caps its VGPRs)
+#define BA_JTJ_ATTR __attribute__((amdgpu_waves_per_eu(BA_MINW, 8)))
+#else
+#define BA_JTJ_ATTR
+#endif
+__global__ __launch_bounds__(256) BA_JTJ_ATTR void ba_jtj_kernel(
     int n_camb, int n_camw, int n_obs, const double* __restrict__ cams,
     const double* __restrict__ pp, const double* __restrict__ pts,
     const int32_t* __restrict__ cam_idx, const int32_t* __restrict__ pt_idx,
@@ -586,7 +636,7 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     double* cost_blk = (double*)(ws + sb + ib);
     double* part = (double*)(ws + sb + ib + cb);
     // camera waves (four per block) + observation blocks in one launch, then the finish blocks
-    const int n_camw = n_cam * splits;
+    const int n_camw = n_cam * splits * CH;
     const int n_camb = (n_camw + 3) / 4;
 #ifdef BA_ABL_CAMONLY  // ablation (timing only): camera waves alone
     const int n_ob_launch = 0;
