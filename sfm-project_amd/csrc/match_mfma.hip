@@ -538,6 +538,9 @@ constexpr int MU_CLOCK_W = 8;  // per block: loop memtime/realtime start+end, en
 __device__ unsigned long long g_mu_clock[MU_CLOCK_W * MU_CLOCK_SLOTS];
 #endif
 
+#ifndef MU_ROW_I4
+#define MU_ROW_I4 0  // 1: the round-1 16-B row records (A/B only)
+#endif
 template <int D, bool ROWS>
 __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
@@ -700,7 +703,11 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
             const int e1 = max(tb[c], P1);
             const int e2 = max(min(tb[c], P1), max(ts[c], P2));
             const int q = qbase + c * 32 + r32;
+#if MU_ROW_I4
             if (h == 0 && q < na) rowres[(size_t)p * k_pad + q] = make_int4(e1, e2, 0, 0);
+#else  // 8-B row records (e1, e2): half the row bytes of the 16-B layout
+            if (h == 0 && q < na) ((int2*)rowres)[(size_t)p * k_pad + q] = make_int2(e1, e2);
+#endif
         }
     }
     if (col_atomic) {
@@ -799,7 +806,11 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
         long long d1 = 0;
         if (tid == 0) nslow = 0;
         if (i < na) {
+#if MU_ROW_I4
             const int4 r = rowres[(size_t)p * k_pad + i];
+#else
+            const int2 r = ((const int2*)rowres)[(size_t)p * k_pad + i];
+#endif
             const long long A = na_norm[i];
             const unsigned long long e = lds_best[i];
             const long long Dp = e != ~0ull ? (long long)(e >> 32) : sfm::DIST_INF;  // best proposal
