@@ -338,7 +338,11 @@ __device__ __forceinline__ bool xcd_pair_block(int n_pairs, int n_hb, int gp, in
 static inline unsigned xcd_grid(int n_pairs, int n_hb) { return 8u * (unsigned)((n_pairs + 7) >> 3) * (unsigned)n_hb; }
 
 constexpr int CH = 16;         // matches per scalar-load chunk (4 x s_load_dwordx16)
-constexpr int PRUNE_EVERY = 64;
+#ifndef RANSAC_PRUNE_EVERY
+#define RANSAC_PRUNE_EVERY 32  // K2 at cfg4 vs 32: 16 and 64 +0.8 %, 128 +2.5 % (ransac_prune_every_ab.txt)
+#endif
+constexpr int PRUNE_EVERY = RANSAC_PRUNE_EVERY;  // matches between bound checks (multiple of CH)
+static_assert(PRUNE_EVERY % CH == 0, "prune period");
 
 // One lane = one hypothesis; see the file comment.  The scoring coordinates are wave-uniform, so
 // they come through the scalar cache into SGPRs (no LDS traffic; the packed FMAs take them as
