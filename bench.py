@@ -268,7 +268,7 @@ def main():
                        "flops_per_step": r_alg,
                        "note": "algorithmic = every hypothesis scored on every match; the exact "
                                "pruning skips part of it (executed_frac_estimate: PMC-measured "
-                               "on a cfg4 pair sample, profiles/r02/pmc_ransac_exec_cfg4.txt)",
+                               "on a cfg4 pair sample, profiles/r02/pmc_ransac_exec_cfg4_pe32.txt)",
                        "executed_frac_estimate": r_exec,
                        "practical_peak": PRACTICAL_F32_VALU_TFLOPS,
                        "executed_frac_of_practical":
@@ -315,9 +315,9 @@ def graph_checksum(torch, graph):
 
 def ransac_flops(run, n_hyp):
     """Algorithmic K2 flops per step (every hypothesis on every match of pairs with >= 8
-    matches) and the executed fraction of the scoring: 0.586 measured on a 2048-pair stride sample
+    matches) and the executed fraction of the scoring: 0.580 measured on a 2048-pair stride sample
     of the cfg4 scene (SQ_INSTS_VALU of the pruned vs the unpruned score kernel,
-    tools/pmc_ransac_exec.sh, profiles/r02/pmc_ransac_exec_cfg4.txt); 0.59 in the cfg3 pruning
+    tools/pmc_ransac_exec.sh, profiles/r02/pmc_ransac_exec_cfg4_pe32.txt); 0.59 in the cfg3 pruning
     simulation."""
     import numpy as np
     cnt = np.concatenate([run.gb._buffers(pt.shape[0])["match"][0].cpu().numpy()
@@ -327,7 +327,7 @@ def ransac_flops(run, n_hyp):
     n_pairs = sum(pt.shape[0] for _, pt in run.chunks)
     m = np.where(cnt >= 8, cnt, 0).astype(np.float64)
     per_pair = n_hyp * float(np.mean(m * RANSAC_FLOP_PER_EVAL + (m > 0) * RANSAC_FLOP_PER_FIT))
-    return per_pair * n_pairs, 0.586
+    return per_pair * n_pairs, 0.580
 
 
 def cpu_baseline(scene, pairs, lo, hi, graph, gb, seconds, n_hyp):
