@@ -465,7 +465,12 @@ __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[
     return true;
 }
 
-__global__ __launch_bounds__(256) void ransac_fit_kernel(
+#ifdef RANSAC_FIT_MINW  // build knob: minimum waves per SIMD for the fit kernel (caps its VGPRs)
+#define RANSAC_FIT_ATTR __attribute__((amdgpu_waves_per_eu(RANSAC_FIT_MINW, 8)))
+#else
+#define RANSAC_FIT_ATTR
+#endif
+__global__ __launch_bounds__(256) RANSAC_FIT_ATTR void ransac_fit_kernel(
     int n_pairs, int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
     const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
     int n_hyp, int gp, float* __restrict__ hypG, int32_t* __restrict__ prev) {
