@@ -748,7 +748,7 @@ __device__ __forceinline__ int mu_dot(const uint4* x, const uint4* y) {
 // A wide block: every pass over the trains / queries is one global round trip, so fewer passes
 // (2 at k = 2048) is what makes this latency-bound kernel fast.
 #ifndef MU_FT_THREADS
-#define MU_FT_THREADS 256
+#define MU_FT_THREADS 512  // 256: +0.5 % K1 at cfg4 (k1_variants_ab.txt)
 #endif
 constexpr int MU_FT = MU_FT_THREADS;
 template <int D>
