@@ -6,10 +6,11 @@
  * defaults nfeatures 500, scaleFactor 1.2, nlevels 8, edgeThreshold 31, patchSize 31, FAST
  * threshold 20, HARRIS_SCORE, WTA_K 2).  OpenCV is absent here, so this is the
  * published ORB algorithm (Rublee et al. 2011; OpenCV's documented pipeline) written as an
- * integer-exact spec — PARITY UNPINNED against OpenCV itself.  Deviations that are deliberate
- * (DESIGN.md §4.10): the BRIEF test pattern is generated from a seeded RNG (BRIEF's G II
- * sampling) instead of OpenCV's learned bit_pattern_31_ table; pyramid, blur and Harris are
- * defined in fixed-point / integer arithmetic; ties are broken in raster order.
+ * integer-exact spec — PARITY UNPINNED against OpenCV itself.  The BRIEF tests are OpenCV's
+ * learned bit_pattern_31_ table (generated header orb_bit_pattern_31.h).  Deviations that are
+ * deliberate: pyramid, blur and Harris are defined in fixed-point / integer
+ * arithmetic; the rotated test points are rounded exactly from the intensity centroid instead of
+ * from a float angle; ties are broken in raster order.
  *
  * Per image (u8 [H][W]):
  *   levels      l = 0..L-1, sc_l = 1.2^l (repeated multiplication), W_l = lround(W / sc_l);
@@ -32,6 +33,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include "orb_bit_pattern_31.h"
 
 #define ORB_EDGE 31
 #define ORB_MAXC 32768
@@ -65,32 +68,11 @@ void oracle_orb_levels(int W, int H, int nlevels, double scale, int nfeat, int32
     nl[nlevels - 1] = nfeat - sum > 0 ? nfeat - sum : 0;
 }
 
-static uint64_t sm_next(uint64_t* s) {
-    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-static int pattern_coord(uint64_t* s) {
-    double g = 0.0;
-    for (int i = 0; i < 12; ++i) g += (double)(sm_next(s) >> 11) * (1.0 / 9007199254740992.0);
-    g -= 6.0;
-    long v = lround(6.2 * g);
-    return (int)(v < -13 ? -13 : (v > 13 ? 13 : v));
-}
-
-/* 256 tests (x1, y1, x2, y2), BRIEF G II: i.i.d. ~N(0, (31/5)^2) clipped to [-13, 13]. */
+/* 256 tests (x1, y1, x2, y2): OpenCV's learned bit_pattern_31_ (the table cv2.ORB_create() uses
+ * at patchSize 31), from the generated header (tools/gen_orb_pattern.py: scikit-image's copy of the
+ * same table, with its sha256). */
 void oracle_orb_pattern(int32_t* pat) {
-    uint64_t s = 0x5EED0B5EULL;
-    for (int t = 0; t < 256; ++t) {
-        int x1 = pattern_coord(&s), y1 = pattern_coord(&s), x2, y2;
-        do {
-            x2 = pattern_coord(&s);
-            y2 = pattern_coord(&s);
-        } while (x2 == x1 && y2 == y1);
-        pat[4 * t] = x1; pat[4 * t + 1] = y1; pat[4 * t + 2] = x2; pat[4 * t + 3] = y2;
-    }
+    for (int k = 0; k < 256 * 4; ++k) pat[k] = SFM_ORB_BIT_PATTERN_31[k];
 }
 
 /* resample map of one axis: n_out entries (i0, i1, w) */

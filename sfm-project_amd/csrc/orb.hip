@@ -25,6 +25,7 @@
 #include <cstring>
 #include <vector>
 
+#include "orb_bit_pattern_31.h"
 #include "sfm_internal.h"
 
 namespace {
@@ -637,32 +638,9 @@ __global__ __launch_bounds__(256) void orb_pack_kernel(OrbLevels L, int nfeat,
 
 // ---- host-side tables (mirrored by oracle/sfm_oracle_orb.c) ------------------------------------
 
-uint64_t sm_next(uint64_t& s) {
-    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-int pattern_coord(uint64_t& s) {
-    double g = 0.0;
-    for (int i = 0; i < 12; ++i) g += (double)(sm_next(s) >> 11) * (1.0 / 9007199254740992.0);
-    g -= 6.0;
-    const long v = lround(6.2 * g);
-    return (int)std::min(13L, std::max(-13L, v));
-}
-
+// OpenCV's learned pattern (generated header, tools/gen_orb_pattern.py).
 void make_pattern(int32_t* pat) {
-    uint64_t s = 0x5EED0B5EULL;
-    for (int t = 0; t < 256; ++t) {
-        const int x1 = pattern_coord(s), y1 = pattern_coord(s);
-        int x2, y2;
-        do {
-            x2 = pattern_coord(s);
-            y2 = pattern_coord(s);
-        } while (x2 == x1 && y2 == y1);
-        pat[4 * t] = x1; pat[4 * t + 1] = y1; pat[4 * t + 2] = x2; pat[4 * t + 3] = y2;
-    }
+    for (int k = 0; k < 256 * 4; ++k) pat[k] = SFM_ORB_BIT_PATTERN_31[k];
 }
 
 void axis_map(int n_in, int n_out, int32_t* map) {
