@@ -42,7 +42,8 @@ def main():
     ms = ev[0].elapsed_time(ev[1]) / 20
     qb = 512                                      # MU_WAVES (4) x QT (4) x 32 queries per block
     n_blk = len(pairs) * ((K + qb - 1) // qb)
-    grid = 8 * ((n_blk + 7) // 8)
+    persist = os.environ.get("SFM_MU_PERSIST", "1") != "0"
+    grid = 512 if persist else 8 * ((n_blk + 7) // 8)  # persistent: 2 blocks per CU x 256 CUs
     W = 8
     buf = np.zeros(W * grid, np.uint64)
     L = sfmcore.load_library()
@@ -54,8 +55,10 @@ def main():
     cyc = st[:, 2] - st[:, 0]
     wall = (st[:, 3] - st[:, 1]) / 100e6
     clk = cyc / wall
-    tiles = K // 32                               # per wave: every train tile of the pair
-    res = {"workload": f"{len(pairs)} pairs x {K}", "launches": n, "launch_ms": ms,
+    # per wave: every train tile of the pair (one block per item), or the block's share of all
+    # units x 4 tiles (persistent schedule)
+    tiles = (n_blk * (K // 128) / grid * 4) if persist else K // 32
+    res = {"workload": f"{len(pairs)} pairs x {K}", "persistent": persist, "launches": n, "launch_ms": ms,
            "blocks": int(len(st)), "clock_GHz_median": float(np.median(clk) / 1e9),
            "clock_GHz_p10_p90": [float(np.percentile(clk, 10) / 1e9),
                                  float(np.percentile(clk, 90) / 1e9)],
@@ -68,6 +71,11 @@ def main():
     cu = ((raw[:, 7].astype(np.int64) & 15) << 8) | ((raw[:, 6].astype(np.int64) >> 8) & 255)
     life = (t_out - t_in) / 100.0  # us
     res["block_life_us_median"] = float(np.median(life))
+    res["block_life_us_p10_p90_max"] = [float(np.percentile(life, 10)), float(np.percentile(life, 90)),
+                                        float(life.max())]
+    xcc = raw[:, 7].astype(np.int64) & 15
+    res["block_life_us_mean_by_xcc"] = [float(life[xcc == x].mean()) if (xcc == x).any() else None
+                                        for x in range(8)]
     res["prologue_us_median"] = float(np.median((l0 - t_in) / 100.0))
     res["epilogue_us_median"] = float(np.median((t_out - l1) / 100.0))
     span = (t_out.max() - t_in.min()) / 100.0
