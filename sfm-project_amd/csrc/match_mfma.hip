@@ -729,314 +729,6 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
 #endif
 }
 
-// ---- Persistent schedule of the column-winner kernel (round 3) -----------------
-//
-// The one-block-per-(pair, query block) grid ran 9.5 rounds of 76-us blocks on 512 slots at cfg3:
-// 14 % of the launch was block prologues/epilogues and the partial last round (k1_clock, profiles/
-// r03/k1_variants_ab.txt).  Here a fixed grid of G blocks (2 per CU) splits the launch's units —
-// (pair rank r in pair_order, query block `it`, 128-train chunk c), rank-major — into G contiguous
-// ranges of equal length (XCD x takes the x-th eighth, so its L2 streams a contiguous run of the
-// train-sorted pairs).  A block walks its range chunk by chunk with the same double-buffered
-// LDS-DMA stages (the next chunk may belong to the next item); a maximal run of one item is a
-// segment: queries are (re)loaded at a segment start, the row top-2 is written at its end —
-// rowres[p][q] when the segment is the whole item, else ovf[block][first ? 0 : 1][q - it QB],
-// which the finalize merges (mu_row_record).  The LDS column table spans all items of a pair
-// processed by the block and is merged into the pair's row by atomicMax when the pair changes.
-__device__ __forceinline__ int mu_unit_block(long long u, long long U, int G) {
-    return (int)(((u + 1) * G - 1) / U);  // the block whose range [kU/G, (k+1)U/G) holds unit u
-}
-
-// Units per pair rank and their exclusive prefix (one block): uoff[r] for r = 0..n_pairs;
-// rank_of[p] = r.  A pair with no keypoints on either side has no units.
-__global__ __launch_bounds__(1024) void mu_units_kernel(const int32_t* __restrict__ pairs,
-                                                        const int32_t* __restrict__ n_kp,
-                                                        const int32_t* __restrict__ order,
-                                                        int n_pairs, int qb, int chunk,
-                                                        int32_t* __restrict__ uoff,
-                                                        int32_t* __restrict__ rank_of) {
-    __shared__ int part[1024];
-    const int tid = threadIdx.x;
-    const int per = (n_pairs + 1023) / 1024, r0 = tid * per, r1 = min(n_pairs, r0 + per);
-    auto units = [&](int r) {
-        const int p = order[r];
-        const int na = n_kp[pairs[2 * p]], nb = n_kp[pairs[2 * p + 1]];
-        return (na > 0 && nb > 0) ? ((na + qb - 1) / qb) * ((nb + chunk - 1) / chunk) : 0;
-    };
-    int sum = 0;
-    for (int r = r0; r < r1; ++r) sum += units(r);
-    part[tid] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
-        const int v = tid >= off ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    int run = part[tid] - sum;
-    for (int r = r0; r < r1; ++r) {
-        uoff[r] = run;
-        run += units(r);
-        rank_of[order[r]] = r;
-    }
-    if (tid == 1023) uoff[n_pairs] = part[1023];
-}
-
-template <int D, bool ROWS>
-__global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_pk_kernel(
-    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
-    const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
-    const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_pairs,
-    const int32_t* __restrict__ pair_order, const int32_t* __restrict__ uoff,
-    int2* __restrict__ rowres, int2* __restrict__ ovf, unsigned long long* __restrict__ colrow) {
-    constexpr int QT = Geo<D>::QT, QB = mu_qb<D>(), CHUNK = MU_CHUNK_BYTES / D, NK = Geo<D>::NK;
-    constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32, NTHR = 64 * MU_WAVES;
-    constexpr int PIECES = CHUNK * D / 1024 / MU_WAVES, RPP = 1024 / D;
-    static_assert(PIECES >= 1 && CHUNK % 32 == 0 && CHUNK / 4 <= 64, "stage geometry");
-    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
-    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
-    extern __shared__ unsigned long long lds_col[];  // [k_pad], dynamic
-
-#ifdef MU_CLOCK
-    const unsigned long long tin = __builtin_amdgcn_s_memrealtime();
-#endif
-    const int G = (int)gridDim.x;
-    const int sblk = (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
-    const long long U = uoff[n_pairs];
-    const int u0 = (int)((long long)sblk * U / G), u1 = (int)((long long)(sblk + 1) * U / G);
-    if (u0 >= u1) return;  // block-uniform, before any barrier
-    const int S = u1 - u0;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
-    for (int j = tid; j < k_pad; j += NTHR) lds_col[j] = 0ull;
-
-    // position of a unit: pair rank, pair, images, item, chunk.  Along the range it advances by
-    // arithmetic (chunk, then item); the next pair's position is loaded once per pair, one pair
-    // ahead (a chain of dependent global loads per chunk would stall the staging).
-    struct Pos { int r, p, a, b, na, nb, it, c, nch, nit; };
-    auto pair_pos = [&](int r, int w) {  // unit w of rank r (uoff[r] <= uoff[r] + w < uoff[r + 1])
-        Pos x;
-        x.r = r;
-        x.p = pair_order[r];
-        x.a = pairs[2 * x.p];
-        x.b = pairs[2 * x.p + 1];
-        x.na = n_kp[x.a];
-        x.nb = n_kp[x.b];
-        x.nch = (x.nb + CHUNK - 1) / CHUNK;
-        x.nit = (x.na + QB - 1) / QB;
-        x.it = w / x.nch;
-        x.c = w - x.it * x.nch;
-        return x;
-    };
-    auto next_pair = [&](int r) {  // first unit of the next rank that has units (r + 1 < n_pairs)
-        int q = r + 1;
-        while (q + 1 < n_pairs && uoff[q + 1] == uoff[q]) ++q;
-        return pair_pos(q, 0);
-    };
-    int r_lo = 0, r_hi = n_pairs - 1;  // first rank of the range: uoff[r] <= u0 < uoff[r + 1]
-    while (r_lo < r_hi) {
-        const int m = (r_lo + r_hi + 1) >> 1;
-        if (uoff[m] <= u0) r_lo = m; else r_hi = m - 1;
-    }
-    Pos cur = pair_pos(r_lo, u0 - uoff[r_lo]);
-    Pos np = cur;
-    if (u1 > uoff[r_lo + 1]) np = next_pair(r_lo);  // the range reaches into the next pair
-    auto advance = [&](const Pos& x) {
-        Pos y = x;
-        if (++y.c == y.nch) {
-            y.c = 0;
-            if (++y.it == y.nit) y = np;
-        }
-        return y;
-    };
-
-    auto stage = [&](const Pos& x, unsigned char* dst) {
-        const uint8_t* db = desc + (size_t)x.b * k_max * D;
-        const int32_t* cib = cinit + (size_t)x.b * k_pad;
-#pragma unroll
-        for (int i = 0; i < PIECES; ++i) {
-            const int piece = wave * PIECES + i;
-            const int row = piece * RPP + lane / SLOTS;
-            const int slot = (lane % SLOTS) ^ swz<D>(row);
-            const int j = x.c * CHUNK + row;
-            const uint8_t* src = (j < x.nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
-        }
-        if (wave == 0 && lane < CHUNK / 4) {
-            const int32_t* src = cib + x.c * CHUNK + lane * 4;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D), 16, 0, 0);
-        }
-    };
-
-    v4i bq[QT][NK];
-    int ccol[QT], tb[QT], ts[QT];
-    int qbase = 0;
-    bool active = false;
-    auto seg_begin = [&](const Pos& x) {  // the item's queries -> registers, row state reset
-        qbase = x.it * QB + wave * QT * 32;
-        active = qbase < x.na;  // wave-uniform
-        const uint8_t* da = desc + (size_t)x.a * k_max * D;
-#pragma unroll
-        for (int c = 0; c < QT; ++c) {
-            const int q = qbase + c * 32 + r32;
-            const v4i* src = (const v4i*)((q < x.na) ? da + (size_t)q * D + (D / 2) * h : zero_row + (D / 2) * h);
-#pragma unroll
-            for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
-            ccol[c] = (q < x.na) ? (-128 * norm[(size_t)x.a * k_pad + q] + 127 - (c * 32 + r32)) : MU_COL_PAD;
-            tb[c] = INT_MIN; ts[c] = INT_MIN;
-        }
-    };
-    const int rr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 + ((lane >> 3) & 1) * 2 +
-                   ((lane >> 4) & 1);
-    const int rowoff = (rr & 3) + 8 * (rr >> 2) + 4 * h;
-
-    auto process = [&](const Pos& x, const unsigned char* cur_buf) {
-        const int nt = min(NT, (x.nb - x.c * CHUNK + 31) >> 5);
-        if (!active) return;
-        const unsigned char* A = cur_buf;
-        const int* Ci = (const int*)(cur_buf + CHUNK * D);
-        for (int tt = 0; tt < nt; ++tt) {
-            const int row = tt * 32 + r32;
-            const int sw = swz<D>(row);
-            v4i af[NK];
-#pragma unroll
-            for (int s = 0; s < NK; ++s)
-                af[s] = *(const v4i*)(A + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
-            v16i init;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
-                init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
-                init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
-            }
-            int colacc[16];
-#pragma unroll
-            for (int c = 0; c < QT; c += 2) {
-                v16i acc0 = init, acc1 = init;
-#pragma unroll
-                for (int s = 0; s < NK; ++s) {
-                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
-                }
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) {
-                    if constexpr (ROWS) {
-                        mu_top2(tb[c], ts[c], acc0[r], acc0[r + 1]);
-                        mu_top2(tb[c + 1], ts[c + 1], acc1[r], acc1[r + 1]);
-                    }
-                    const int a0 = (int)(((unsigned)acc0[r] << 8) + (unsigned)ccol[c]);
-                    const int a1 = (int)(((unsigned)acc1[r] << 8) + (unsigned)ccol[c + 1]);
-                    const int b0 = (int)(((unsigned)acc0[r + 1] << 8) + (unsigned)ccol[c]);
-                    const int b1 = (int)(((unsigned)acc1[r + 1] << 8) + (unsigned)ccol[c + 1]);
-                    colacc[r] = (c == 0) ? max(a0, a1) : vmax3(colacc[r], a0, a1);
-                    colacc[r + 1] = (c == 0) ? max(b0, b1) : vmax3(colacc[r + 1], b0, b1);
-                }
-            }
-            const int key = transpose_max16(colacc, lane);
-            const int j = x.c * CHUNK + tt * 32 + rowoff;
-            if (!(lane & 1) && j < x.nb) {
-                const int nd = key >> 7;  // 2e - |x'_q|^2 = -d^2 - p_j
-                const unsigned gq = (unsigned)(qbase + 127 - (key & 127));
-                lds_max_u64(&lds_col[j], ((unsigned long long)((unsigned)nd ^ 0x80000000u) << 32) |
-                                             (unsigned long long)(0xFFFFFFFFu - gq));
-            }
-        }
-    };
-
-    int seg_c0 = cur.c;    // chunk at which the current segment started
-    bool first_seg = true;  // the segment that starts at u0
-    auto seg_end = [&](const Pos& x) {
-        if (!(ROWS && active)) return;
-        const bool whole = seg_c0 == 0 && x.c == x.nch - 1;
-        int2* dst = whole ? rowres + (size_t)x.p * k_pad + x.it * QB
-                          : ovf + ((size_t)sblk * 2 + (first_seg ? 0 : 1)) * QB;
-#pragma unroll
-        for (int c = 0; c < QT; ++c) {
-            const int P1 = __shfl_xor(tb[c], 32), P2 = __shfl_xor(ts[c], 32);
-            const int e1 = max(tb[c], P1);
-            const int e2 = max(min(tb[c], P1), max(ts[c], P2));
-            const int ql = wave * QT * 32 + c * 32 + r32;
-            if (h == 0 && x.it * QB + ql < x.na) dst[ql] = make_int2(e1, e2);
-        }
-    };
-    auto pair_end = [&](const Pos& x) {  // block table -> the pair's column row; table zeroed
-        __syncthreads();
-        unsigned long long* dst = colrow + (size_t)x.p * k_pad;
-        for (int j = tid; j < k_pad; j += NTHR) {
-            const unsigned long long v = lds_col[j];
-            if (v != 0ull) {
-                atomicMax(dst + j, v);
-                lds_col[j] = 0ull;
-            }
-        }
-    };
-    // one unit: stage the next, scan this chunk, close the segment / pair when it ends there
-    auto step = [&](int k, const unsigned char* cbuf, unsigned char* nbuf) {
-        const bool has_next = k + 1 < S;
-        Pos nx = cur;
-        if (has_next) {
-            nx = advance(cur);
-            stage(nx, nbuf);
-        }
-        process(cur, cbuf);
-        const bool new_pair = !has_next || nx.r != cur.r;
-        const bool new_seg = new_pair || nx.it != cur.it;
-        if (new_seg) seg_end(cur);
-        if (new_pair) pair_end(cur);
-        __syncthreads();  // the next chunk landed (vmcnt drained); everyone is done with cbuf
-        if (has_next && new_seg) {
-            seg_begin(nx);
-            seg_c0 = nx.c;
-            first_seg = false;
-        }
-        if (has_next && new_pair && u0 + k + 1 + (nx.nit * nx.nch) < u1)
-            np = next_pair(nx.r);  // the range reaches past this new pair too
-        cur = nx;
-    };
-#ifdef MU_CLOCK
-    const unsigned long long t0c = __builtin_amdgcn_s_memtime(), t0r = __builtin_amdgcn_s_memrealtime();
-#endif
-    stage(cur, lds0);
-    seg_begin(cur);
-    __syncthreads();
-    for (int k = 0; k < S; k += 2) {
-        step(k, lds0, lds1);
-        if (k + 1 < S) step(k + 1, lds1, lds0);
-    }
-#ifdef MU_CLOCK
-    {
-        const unsigned long long t1c = __builtin_amdgcn_s_memtime(), t1r = __builtin_amdgcn_s_memrealtime();
-        if (tid == 0 && blockIdx.x < MU_CLOCK_SLOTS) {
-            unsigned long long* d = g_mu_clock + MU_CLOCK_W * (size_t)blockIdx.x;
-            d[0] = t0c; d[1] = t0r; d[2] = t1c; d[3] = t1r; d[4] = tin;
-            d[5] = __builtin_amdgcn_s_memrealtime();
-            d[6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-            d[7] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
-        }
-    }
-#endif
-}
-
-// Row record (e1, e2) of query i of pair p under the persistent schedule: the item's segments
-// merged (top-2 of the segments' top-2s).  QB queries per item, CHUNK trains per unit.
-template <int QB, int CHUNK>
-__device__ __forceinline__ int2 mu_row_record(const int2* __restrict__ rowres,
-                                              const int2* __restrict__ ovf,
-                                              const int32_t* __restrict__ uoff, int r, int p,
-                                              int k_pad, int nb, int i, long long U, int G) {
-    const int nch = (nb + CHUNK - 1) / CHUNK, it = i / QB;
-    const long long i0 = uoff[r] + (long long)it * nch, i1 = i0 + nch;
-    const int k0 = mu_unit_block(i0, U, G), k1 = mu_unit_block(i1 - 1, U, G);
-    if (k0 == k1) return rowres[(size_t)p * k_pad + i];
-    int e1 = INT_MIN, e2 = INT_MIN;
-    for (int k = k0; k <= k1; ++k) {
-        const long long us = (long long)k * U / G;
-        if ((long long)(k + 1) * U / G == us) continue;  // a block with no units (U < G)
-        const int2 v = ovf[((size_t)k * 2 + (i0 > us ? 1 : 0)) * QB + (i - it * QB)];
-        e2 = max(max(e2, v.y), min(e1, v.x));
-        e1 = max(e1, v.x);
-    }
-    return make_int2(e1, e2);
-}
-
 // Exact dot product of two D-byte i8 rows (v_dot4_i32_i8).
 template <int D>
 __device__ __forceinline__ int mu_dot(const uint4* x, const uint4* y) {
@@ -1065,8 +757,7 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
     const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs, int n_qblk,
     const int4* __restrict__ rowres, const unsigned long long* __restrict__ colpart, int rnum,
     int rden, long long max_dist, int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
-    int32_t* __restrict__ out_dist, const int2* __restrict__ ovf, const int32_t* __restrict__ uoff,
-    const int32_t* __restrict__ rank_of, int pk_grid, int n_pairs) {
+    int32_t* __restrict__ out_dist) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
     __shared__ int wsum[MU_FT / 64], slow[MU_FT], nslow;
     __shared__ long long rb1[MU_FT], rb2[MU_FT];
@@ -1118,10 +809,7 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
 #if MU_ROW_I4
             const int4 r = rowres[(size_t)p * k_pad + i];
 #else
-            const int2 r = pk_grid ? mu_row_record<mu_qb<D>(), MU_CHUNK_BYTES / D>(
-                                         (const int2*)rowres, ovf, uoff, rank_of[p], p, k_pad, nb, i,
-                                         (long long)uoff[n_pairs], pk_grid)
-                                   : ((const int2*)rowres)[(size_t)p * k_pad + i];
+            const int2 r = ((const int2*)rowres)[(size_t)p * k_pad + i];
 #endif
             const long long A = na_norm[i];
             const unsigned long long e = lds_best[i];
@@ -1337,10 +1025,6 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
                              (const void*)mfma_mutual_kernel<128, false>,
                              (const void*)mfma_mutual_kernel<256, true>,
                              (const void*)mfma_mutual_kernel<256, false>,
-                             (const void*)mfma_mutual_pk_kernel<128, true>,
-                             (const void*)mfma_mutual_pk_kernel<128, false>,
-                             (const void*)mfma_mutual_pk_kernel<256, true>,
-                             (const void*)mfma_mutual_pk_kernel<256, false>,
                              (const void*)mutual_finalize_kernel<128>,
                              (const void*)mutual_finalize_kernel<256>,
                              (const void*)opencv_finalize_kernel};
@@ -1348,29 +1032,12 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
             SFM_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, want));
     }
     const int n_qblk = (k_max + QB - 1) / QB;
-    // persistent balanced-range schedule (default, round 3) or one block per (pair, query block)
-    // (SFM_MU_PERSIST=0)
-    static const bool persist = [] {  // measured slower (profiles/r03/k1_variants_ab.txt): opt-in
-        const char* e = getenv("SFM_MU_PERSIST");
-        return e && e[0] == '1';
-    }();
-    // column winners merged by atomics (default) or as per-query-block partials the finalize
-    // reduces (SFM_MU_COLPART=1, one-block-per-item schedule only); DESIGN.md 4.1
-    static const int col_atomic_env = [] {
-        const char* e = getenv("SFM_MU_COLPART");
-        return (e && e[0] == '1') ? 0 : 1;
-    }();
-    const int col_atomic = persist ? 1 : col_atomic_env;
-    const int blk_per_cu = std::max(1, 4 * MU_MINW / MU_WAVES);
-    const int G = 8 * std::max(1, (ctx->n_cu * blk_per_cu) / 8);
     const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
-    const size_t rowb = sfm::align_up((size_t)n_pairs * k_pad * sizeof(int4), 256);
-    const size_t colb = (size_t)n_pairs * (col_atomic ? 1 : n_qblk) * k_pad * sizeof(unsigned long long);
+    const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
+    const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
     const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
     const size_t ordb = sfm::align_up(sizeof(int32_t) * ((size_t)n_pairs + n_img), 256);
-    const size_t pkb = sfm::align_up(sizeof(int32_t) * (2 * (size_t)n_pairs + 1), 256);
-    const size_t ovfb = sfm::align_up((size_t)G * 2 * QB * sizeof(int2), 256);
-    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + pkb + ovfb + 1024);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     uint8_t* zero_row = (uint8_t*)ws;
     int32_t* norm = (int32_t*)(ws + 256);
@@ -1379,10 +1046,13 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
     uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
     int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
-    int32_t* uoff = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb + ordb);
-    int32_t* rank_of = uoff + n_pairs + 1;
-    int2* ovf = (int2*)(ws + 256 + 2 * tab + rowb + colb + descb + ordb + pkb);
     const int n_blk = n_pairs * n_qblk;
+    // column winners merged by atomics (default) or as per-query-block partials the finalize
+    // reduces (SFM_MU_COLPART=1); DESIGN.md 4.1
+    static const int col_atomic = [] {
+        const char* e = getenv("SFM_MU_COLPART");
+        return (e && e[0] == '1') ? 0 : 1;
+    }();
     // whole pairs per XCD (blocks of one pair never straddle two XCDs' ranges)
     const int grid = 8 * ((n_pairs + 7) / 8) * n_qblk;
     const int fin_qblk = col_atomic ? 1 : n_qblk;
@@ -1400,47 +1070,28 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
                            dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row,
                            (uint4*)desc_i8);
     SFM_HIP_CHECK(hipGetLastError());
-    if (persist) {
-        hipLaunchKernelGGL(mu_units_kernel, dim3(1), dim3(1024), 0, st, pairs, n_kp, pair_order,
-                           n_pairs, QB, (l2 ? MU_CHUNK_BYTES / 128 : MU_CHUNK_BYTES / 256), uoff,
-                           rank_of);
-        SFM_HIP_CHECK(hipGetLastError());
 #define SFM_MU_SCAN(DD, RR)                                                                       \
-        hipLaunchKernelGGL((mfma_mutual_pk_kernel<DD, RR>), dim3(G), dim3(64 * MU_WAVES),         \
-                           (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, cinit,       \
-                           zero_row, pairs, n_pairs, pair_order, uoff, (int2*)rowres, ovf,        \
-                           colpart)
-        if (l2 && rows) SFM_MU_SCAN(128, true);
-        else if (l2) SFM_MU_SCAN(128, false);
-        else if (rows) SFM_MU_SCAN(256, true);
-        else SFM_MU_SCAN(256, false);
+    hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(64 * MU_WAVES),             \
+                       (size_t)k_pad * 8, st, desc_i8, n_kp,                                      \
+                       k_max, k_pad, norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk,     \
+                       rowres, colpart, col_atomic)
+    if (l2 && rows) SFM_MU_SCAN(128, true);
+    else if (l2) SFM_MU_SCAN(128, false);
+    else if (rows) SFM_MU_SCAN(256, true);
+    else SFM_MU_SCAN(256, false);
 #undef SFM_MU_SCAN
-    } else {
-#define SFM_MU_SCAN(DD, RR)                                                                       \
-        hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(64 * MU_WAVES),         \
-                           (size_t)k_pad * 8, st, desc_i8, n_kp,                                  \
-                           k_max, k_pad, norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk, \
-                           rowres, colpart, col_atomic)
-        if (l2 && rows) SFM_MU_SCAN(128, true);
-        else if (l2) SFM_MU_SCAN(128, false);
-        else if (rows) SFM_MU_SCAN(256, true);
-        else SFM_MU_SCAN(256, false);
-#undef SFM_MU_SCAN
-    }
     SFM_HIP_CHECK(hipGetLastError());
     if (rows) {
         if (l2)
             hipLaunchKernelGGL(mutual_finalize_kernel<128>, dim3(n_pairs), dim3(MU_FT),
                                (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
                                fin_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
-                               (long long)prm->max_dist, out_count, out_match, out_dist, ovf, uoff,
-                               rank_of, persist ? G : 0, n_pairs);
+                               (long long)prm->max_dist, out_count, out_match, out_dist);
         else
             hipLaunchKernelGGL(mutual_finalize_kernel<256>, dim3(n_pairs), dim3(MU_FT),
                                (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
                                fin_qblk, rowres, colpart, prm->ratio_num, prm->ratio_den,
-                               (long long)prm->max_dist, out_count, out_match, out_dist, ovf, uoff,
-                               rank_of, persist ? G : 0, n_pairs);
+                               (long long)prm->max_dist, out_count, out_match, out_dist);
     } else {
         hipLaunchKernelGGL(opencv_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st,
                            n_kp, k_max, k_pad, norm, pairs, fin_qblk, colpart,
