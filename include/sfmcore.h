@@ -103,13 +103,24 @@ int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_
 
 /* Diagnostic companion of sfm_ransac_f_batch: the inlier count of EVERY hypothesis (no pruning),
  * out_counts [n_pairs][n_hyp] i32 (-1: degenerate sample or fewer than 8 matches), computed by the
- * score kernel of sfm_ransac_f_batch with pruning off; out_norm as above.  The exhaustive parity
- * tests compare it with the oracle's per-hypothesis counts.
+ * score kernel of sfm_ransac_f_batch with pruning off; out_norm as above.  Optional (NULL: not
+ * written): out_hyp_F [n_pairs][n_hyp][9] f32, every hypothesis's F in normalised coordinates;
+ * out_hyp_mask [n_pairs][n_hyp][k_max] u8, every hypothesis's inlier decision per match.  The
+ * exhaustive parity tests compare them with the oracle's and with scikit-image's estimates.
  */
 int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
                       const int32_t* pairs, int32_t n_pairs, const int32_t* match_count,
                       const int32_t* matches, const sfm_ransac_params* prm, int32_t* out_counts,
-                      float* out_norm);
+                      float* out_norm, float* out_hyp_F, uint8_t* out_hyp_mask);
+
+/* Execution statistics of sfm_ransac_f_batch (measurement, default off).  enable != 0: every later
+ * batch on ctx adds its Sampson evaluations to device counters (one u32 store per score wave + a
+ * small reduction kernel on the context's stream).  out != NULL: synchronises the stream, writes
+ * (executed evaluations, algorithmic evaluations = n_hyp x M summed over pairs with M >= 8, number
+ * of such pairs) and resets the counters.  executed / algorithmic is the share of the Sampson work
+ * the exact pruning did not skip.
+ */
+int sfm_ransac_stats(sfm_ctx* ctx, int32_t enable, uint64_t* out);
 
 /* ---- verified match graph -------------------------------------------------------------------
  * Replaces the pair_matches list of code/pipeline.py:42-47 (Pair(img_inx_1, img_inx_2, matches)

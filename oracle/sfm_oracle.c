@@ -209,11 +209,17 @@ void oracle_normalize(const float* xy, int M, float* nxy, float* cx, float* cy, 
 
 /*
  * Fundamental matrix from 8 normalised correspondences (Householder QR null space of the 8x9
- * epipolar system, then rank-2 by removing the smallest eigen-direction of F^T F, found by
- * RANK2_ITERS power iterations on adj(F^T F)).
+ * epipolar system, then rank-2 by removing the smallest eigen-direction of F^T F: the dominant
+ * eigenvector of adj(F^T F), taken as the max-diagonal column of adj(F^T F)^(2^RANK2_SQUARINGS)
+ * after RANK2_SQUARINGS exactly rescaled squarings).
  * p1/p2: [8][2] normalised points.  Returns 0 on success, -1 if degenerate.  F row-major.
+ *
+ * Round 3: the rank-2 step was 4 power iterations on adj(F^T F) (error ~ (s3/s2)^8 in the removed
+ * direction, s = singular values of the 8-point solution), which left the projection visibly
+ * different from the exact SVD truncation (scikit-image FundamentalMatrixTransform) for about
+ * 2 % of the hypotheses of noisy cfg3 pairs; squaring reaches the power 2^8 = 256 ((s3/s2)^512).
  */
-#define RANK2_ITERS 4
+#define RANK2_SQUARINGS 8
 
 /* adjugate of a symmetric 3x3 (itself symmetric) */
 static void adj3_sym(const float G[3][3], float A[3][3]) {
@@ -233,6 +239,25 @@ static void rescale3_pow2(float v[3]) {
         frexpf(m, &e);
         for (int i = 0; i < 3; ++i) v[i] = ldexpf(v[i], -e);
     }
+}
+
+/* symmetric A <- (2^-e A)^2, e the exponent of max|A_ij| (upper triangle, fixed fma order) */
+static void square3_sym(float A[3][3]) {
+    const float m = fmaxf(fmaxf(fmaxf(fabsf(A[0][0]), fabsf(A[1][1])), fmaxf(fabsf(A[2][2]), fabsf(A[0][1]))),
+                          fmaxf(fabsf(A[0][2]), fabsf(A[1][2])));
+    float a00 = A[0][0], a11 = A[1][1], a22 = A[2][2], a01 = A[0][1], a02 = A[0][2], a12 = A[1][2];
+    if (m > 0.0f && isfinite(m)) {
+        int e;
+        frexpf(m, &e);
+        a00 = ldexpf(a00, -e); a11 = ldexpf(a11, -e); a22 = ldexpf(a22, -e);
+        a01 = ldexpf(a01, -e); a02 = ldexpf(a02, -e); a12 = ldexpf(a12, -e);
+    }
+    A[0][0] = fmaf(a02, a02, fmaf(a01, a01, a00 * a00));
+    A[1][1] = fmaf(a12, a12, fmaf(a11, a11, a01 * a01));
+    A[2][2] = fmaf(a22, a22, fmaf(a12, a12, a02 * a02));
+    A[0][1] = A[1][0] = fmaf(a02, a12, fmaf(a01, a11, a00 * a01));
+    A[0][2] = A[2][0] = fmaf(a02, a22, fmaf(a01, a12, a00 * a02));
+    A[1][2] = A[2][1] = fmaf(a12, a22, fmaf(a11, a12, a01 * a02));
 }
 
 int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
@@ -272,9 +297,9 @@ int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
         float f = beta[k] * dot;
         for (int r = k; r < 9; ++r) z[r] = fmaf(-f, V[k][r], z[r]);
     }
-    /* rank 2: smallest eigen-direction v of G = F^T F by power iteration on adj(G) (its dominant
-       eigenvector; ratio lambda_min/lambda_mid per step), exact power-of-two rescaling, then
-       F' = F - (F v) v^T */
+    /* rank 2: smallest eigen-direction v of G = F^T F = the dominant eigenvector of adj(G)
+       (ratio (s3/s2)^2 per power), from RANK2_SQUARINGS rescaled squarings of adj(G) and its
+       max-diagonal column; then F' = F - (F v) v^T */
     float G[3][3];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
@@ -284,16 +309,11 @@ int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
         }
     float A[3][3];
     adj3_sym(G, A);
+    for (int it = 0; it < RANK2_SQUARINGS; ++it) square3_sym(A);
     int kk = 0;
     if (A[1][1] > A[kk][kk]) kk = 1;
     if (A[2][2] > A[kk][kk]) kk = 2;
     float v[3] = {A[0][kk], A[1][kk], A[2][kk]};
-    for (int it = 0; it < RANK2_ITERS; ++it) {
-        rescale3_pow2(v);
-        float w[3];
-        for (int i = 0; i < 3; ++i) w[i] = fmaf(A[i][2], v[2], fmaf(A[i][1], v[1], A[i][0] * v[0]));
-        v[0] = w[0]; v[1] = w[1]; v[2] = w[2];
-    }
     rescale3_pow2(v);
     const float n2 = fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0]));
     if (n2 > 0.0f) {

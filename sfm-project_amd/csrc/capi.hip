@@ -71,6 +71,8 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->rs_wave) (void)hipFree(ctx->rs_wave);
+    if (ctx->rs_acc) (void)hipFree(ctx->rs_acc);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return SFM_OK;

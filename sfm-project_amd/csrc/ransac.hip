@@ -12,7 +12,7 @@
 //                 (scoring, X = k * x_normalised, k = 1/(s*sqrt(thr))), plus (cx,cy,s) per side.
 //   ransac_hyp    one LANE per hypothesis (256 per block): counter-based Philox sample of 8 distinct
 //                 matches (Floyd), Householder-QR null space of the 8x9 epipolar system, rank-2
-//                 projection (power iteration on adj(F^T F)), then a sweep over all M matches counting
+//                 projection (squarings of adj(F^T F)), then a sweep over all M matches counting
 //                 Sampson inliers (17 flops + compare per match).  The match coordinates are
 //                 wave-uniform, so they are read with scalar loads into SGPRs and fed to packed
 //                 FMAs as SGPR-pair operands.  Exact pruning: every 64 matches a wave reads
@@ -31,7 +31,7 @@
 
 namespace {
 
-constexpr int RANK2_ITERS = 4;  // oracle_fit_f8
+constexpr int RANK2_SQUARINGS = 8;  // oracle_fit_f8 (round 3; was 4 power iterations)
 
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1, uint32_t out[4]) {
@@ -137,27 +137,41 @@ __device__ __forceinline__ bool fit_f8(const float4 s[8], float F[9]) {
     A[0][1] = A[1][0] = fmaf(G[0][2], G[1][2], -(G[0][1] * G[2][2]));
     A[0][2] = A[2][0] = fmaf(G[0][1], G[1][2], -(G[0][2] * G[1][1]));
     A[1][2] = A[2][1] = fmaf(G[0][1], G[0][2], -(G[0][0] * G[1][2]));
-    int kk = 0;
-    float amax = A[0][0];
-    if (A[1][1] > amax) { kk = 1; amax = A[1][1]; }
-    if (A[2][2] > amax) kk = 2;
-    float v0 = kk == 0 ? A[0][0] : (kk == 1 ? A[0][1] : A[0][2]);
-    float v1 = kk == 0 ? A[1][0] : (kk == 1 ? A[1][1] : A[1][2]);
-    float v2 = kk == 0 ? A[2][0] : (kk == 1 ? A[2][1] : A[2][2]);
+    // rescaled squarings of adj(G) (oracle square3_sym): the max-diagonal column of
+    // adj(G)^(2^RANK2_SQUARINGS) is the removed direction to (s3/s2)^512
+    float a00 = A[0][0], a11 = A[1][1], a22 = A[2][2], a01 = A[0][1], a02 = A[0][2], a12 = A[1][2];
 #pragma unroll
-    for (int it = 0; it <= RANK2_ITERS; ++it) {
-        // exact power-of-two rescale by the exponent of max|v| (oracle rescale3_pow2)
+    for (int it = 0; it < RANK2_SQUARINGS; ++it) {
+        const float m = fmaxf(fmaxf(fmaxf(fabsf(a00), fabsf(a11)), fmaxf(fabsf(a22), fabsf(a01))),
+                              fmaxf(fabsf(a02), fabsf(a12)));
+        if (m > 0.0f && isfinite(m)) {
+            int e;
+            frexpf(m, &e);
+            a00 = ldexpf(a00, -e); a11 = ldexpf(a11, -e); a22 = ldexpf(a22, -e);
+            a01 = ldexpf(a01, -e); a02 = ldexpf(a02, -e); a12 = ldexpf(a12, -e);
+        }
+        const float b00 = fmaf(a02, a02, fmaf(a01, a01, a00 * a00));
+        const float b11 = fmaf(a12, a12, fmaf(a11, a11, a01 * a01));
+        const float b22 = fmaf(a22, a22, fmaf(a12, a12, a02 * a02));
+        const float b01 = fmaf(a02, a12, fmaf(a01, a11, a00 * a01));
+        const float b02 = fmaf(a02, a22, fmaf(a01, a12, a00 * a02));
+        const float b12 = fmaf(a12, a22, fmaf(a11, a12, a01 * a02));
+        a00 = b00; a11 = b11; a22 = b22; a01 = b01; a02 = b02; a12 = b12;
+    }
+    int kk = 0;
+    float amax = a00;
+    if (a11 > amax) { kk = 1; amax = a11; }
+    if (a22 > amax) kk = 2;
+    float v0 = kk == 0 ? a00 : (kk == 1 ? a01 : a02);
+    float v1 = kk == 0 ? a01 : (kk == 1 ? a11 : a12);
+    float v2 = kk == 0 ? a02 : (kk == 1 ? a12 : a22);
+    {   // exact power-of-two rescale by the exponent of max|v| (oracle rescale3_pow2)
         const float m = fmaxf(fabsf(v0), fmaxf(fabsf(v1), fabsf(v2)));
         if (m > 0.0f && isfinite(m)) {
             int e;
             frexpf(m, &e);
             v0 = ldexpf(v0, -e); v1 = ldexpf(v1, -e); v2 = ldexpf(v2, -e);
         }
-        if (it == RANK2_ITERS) break;
-        const float w0 = fmaf(A[0][2], v2, fmaf(A[0][1], v1, A[0][0] * v0));
-        const float w1 = fmaf(A[1][2], v2, fmaf(A[1][1], v1, A[1][0] * v0));
-        const float w2 = fmaf(A[2][2], v2, fmaf(A[2][1], v1, A[2][0] * v0));
-        v0 = w0; v1 = w1; v2 = w2;
     }
     const float n2 = fmaf(v2, v2, fmaf(v1, v1, v0 * v0));
     if (n2 > 0.0f) {
@@ -434,10 +448,12 @@ constexpr int HREC = 12;  // hypothesis record: G[9], preview count (int bits), 
 
 // counts inliers of G over matches [m, mend) into cnt; with PRUNE checks the published bound every
 // PRUNE_EVERY matches and returns false (wave-uniform) when no lane can still win.
+// `mstop` (if given) receives the match index where the wave stopped (mend when it finished).
 template <bool PRUNE, int C = CH>
 __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[9], int m, int mend,
                                               int M, int& cnt,
-                                              const unsigned long long* __restrict__ bestp) {
+                                              const unsigned long long* __restrict__ bestp,
+                                              int* mstop = nullptr) {
     const int mc = m + ((mend - m) & ~(C - 1));
 #pragma unroll 1
     for (; m < mc; m += C) {
@@ -457,11 +473,15 @@ __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[
             const unsigned long long bk =
                 __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int bound = (int)(bk >> 32) - 1;
-            if (__all(cnt + (M - m - C) < bound)) return false;
+            if (__all(cnt + (M - m - C) < bound)) {
+                if (mstop) *mstop = m + C;
+                return false;
+            }
         }
     }
 #pragma unroll 1
     for (; m < mend; ++m) cnt += sampson_inlier(G, S[m], S[kp + m], S[2 * kp + m], S[3 * kp + m]);
+    if (mstop) *mstop = mend;
     return true;
 }
 
@@ -473,7 +493,8 @@ __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[
 __global__ __launch_bounds__(256) RANSAC_FIT_ATTR void ransac_fit_kernel(
     int n_pairs, int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
     const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
-    int n_hyp, int gp, float* __restrict__ hypG, int32_t* __restrict__ prev) {
+    int n_hyp, int gp, float* __restrict__ hypG, int32_t* __restrict__ prev,
+    float* __restrict__ out_hyp_F = nullptr) {
     int p, hb;
     if (!xcd_pair_block(n_pairs, n_hyp >> 8, gp, p, hb)) return;
     const int M = match_count[p];
@@ -501,6 +522,11 @@ __global__ __launch_bounds__(256) RANSAC_FIT_ATTR void ransac_fit_kernel(
 #else
     const bool ok = fit_f8(smp, F);
 #endif
+    if (out_hyp_F) {  // diagnostic (sfm_ransac_counts): F of every hypothesis, normalised frame
+        float* o = out_hyp_F + ((size_t)p * n_hyp + h) * 9;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) o[k] = F[k];
+    }
     sampson_prep(F, k1, k2, G);
     int cnt = 0;
 #ifndef RANSAC_ABL_NOPREVIEW  // ablation: no preview (timing only; order degenerates)
@@ -545,7 +571,8 @@ template <bool PRUNE, bool COUNTS = false>
 __global__ __launch_bounds__(256) void ransac_score_kernel(
     int n_pairs, int k_max, const int32_t* __restrict__ match_count,
     const float* __restrict__ planes, int n_hyp, int gp, const float* __restrict__ hypG,
-    const uint16_t* __restrict__ order, unsigned long long* __restrict__ best, int32_t* __restrict__ out_counts = nullptr) {
+    const uint16_t* __restrict__ order, unsigned long long* __restrict__ best, int32_t* __restrict__ out_counts = nullptr,
+    uint32_t* __restrict__ exec_w = nullptr) {
     int p, hb;
     if (!xcd_pair_block(n_pairs, n_hyp >> 8, gp, p, hb)) return;
     const int M = match_count[p];
@@ -560,7 +587,11 @@ __global__ __launch_bounds__(256) void ransac_score_kernel(
     const float G[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
     const int pc = __float_as_int(r2.y);
     int cnt = max(pc, 0);
-    if (M > PV && !score_matches<PRUNE>(S, kp, G, PV, M, M, cnt, best + p)) return;
+    int mstop = PV;
+    const bool alive = M <= PV || score_matches<PRUNE>(S, kp, G, PV, M, M, cnt, best + p, &mstop);
+    if (exec_w && (threadIdx.x & 63) == 0)  // sfm_ransac_stats: matches this wave scored past the preview
+        exec_w[(size_t)p * (n_hyp >> 6) + hb * 4 + (threadIdx.x >> 6)] = (uint32_t)max(mstop - PV, 0);
+    if (!alive) return;
     if (pc < 0) cnt = -1;
     if (COUNTS) {
         out_counts[(size_t)p * n_hyp + h] = cnt;
@@ -623,6 +654,58 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
         out_best_h[p] = (int)h;
     }
     if (tid < 9) out_F[p * 9 + tid] = ok ? F[tid] : 0.0f;
+}
+
+// Diagnostic (sfm_ransac_counts out_hyp_mask): every hypothesis's inlier decision on every match,
+// lane per hypothesis, from the fit kernel's G record (the same scalar Sampson test).
+__global__ __launch_bounds__(256) void ransac_hyp_mask_kernel(
+    int k_max, const int32_t* __restrict__ match_count, const float* __restrict__ planes, int n_hyp,
+    const float* __restrict__ hypG, uint8_t* __restrict__ out_mask) {
+    const int p = blockIdx.x;
+    const int M = match_count[p];
+    if (M < 8) return;
+    const int h = blockIdx.y * 256 + threadIdx.x;
+    const int kp = plane_len(k_max);
+    const float* S = planes + (size_t)p * 8 * kp + 4 * kp;
+    const float4* rec = (const float4*)(hypG + ((size_t)p * n_hyp + h) * HREC);
+    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+    const float G[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+    uint8_t* o = out_mask + ((size_t)p * n_hyp + h) * k_max;
+    for (int m = 0; m < M; ++m)
+        o[m] = (uint8_t)sampson_inlier(G, S[m], S[kp + m], S[2 * kp + m], S[3 * kp + m]);
+}
+
+// sfm_ransac_stats: (executed, algorithmic) Sampson evaluations of a batch and its pairs with >= 8
+// matches.  executed = every hypothesis's preview (min(PV, M)) + 64 x the matches each score wave
+// scored past the preview + the final kernel's M; algorithmic = H x M.
+__global__ __launch_bounds__(256) void ransac_stats_kernel(int n_pairs, int n_hyp,
+                                                           const int32_t* __restrict__ match_count,
+                                                           const uint32_t* __restrict__ exec_w,
+                                                           unsigned long long* __restrict__ acc) {
+    __shared__ unsigned long long se[4], sa[4], sn[4];
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    unsigned long long ex = 0, al = 0, np = 0;
+    if (p < n_pairs) {
+        const int M = match_count[p];
+        if (M >= 8) {
+            const int nw = n_hyp >> 6;
+            for (int w = lane; w < nw; w += 64) ex += 64ull * exec_w[(size_t)p * nw + w];
+            if (lane == 0) {
+                ex += (unsigned long long)n_hyp * (unsigned)min(PV, M) + (unsigned)M;
+                al = (unsigned long long)n_hyp * (unsigned)M;
+                np = 1;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ex += __shfl_xor(ex, off, 64);
+    if (lane == 0) { se[threadIdx.x >> 6] = ex; sa[threadIdx.x >> 6] = al; sn[threadIdx.x >> 6] = np; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(acc, se[0] + se[1] + se[2] + se[3]);
+        atomicAdd(acc + 1, sa[0] + sa[1] + sa[2] + sa[3]);
+        atomicAdd(acc + 2, sn[0] + sn[1] + sn[2] + sn[3]);
+    }
 }
 
 }  // namespace
@@ -709,17 +792,35 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
                        match_count, matches, prm->thr, w.planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 grid(n_pairs, H / 256);
+    uint32_t* exec_w = nullptr;  // sfm_ransac_stats (ordered schedule only)
+    if (ctx->ransac_stats && ordered) {
+        const size_t need = (size_t)n_pairs * (H / 64);
+        if (need > ctx->rs_wave_n) {
+            if (ctx->rs_wave) SFM_HIP_CHECK(hipFree(ctx->rs_wave));
+            ctx->rs_wave = nullptr;
+            SFM_HIP_CHECK(hipMalloc(&ctx->rs_wave, need * sizeof(uint32_t)));
+            ctx->rs_wave_n = need;
+        }
+        exec_w = ctx->rs_wave;
+    }
     if (ordered) {
         const dim3 xgrid(xcd_grid(n_pairs, H / 256));
         const int gp = ransac_group(n_pairs);
         hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
-                           match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG, w.prev);
+                           match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG,
+                           w.prev, (float*)nullptr);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                            w.prev, w.order);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(ransac_score_kernel<true>, xgrid, dim3(256), 0, st, n_pairs, k_max,
-                           match_count, w.planes, H, gp, w.hypG, w.order, w.best);
+                           match_count, w.planes, H, gp, w.hypG, w.order, w.best,
+                           (int32_t*)nullptr, exec_w);
+        if (exec_w) {
+            SFM_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(ransac_stats_kernel, dim3((n_pairs + 3) / 4), dim3(256), 0, st,
+                               n_pairs, H, match_count, exec_w, ctx->rs_acc);
+        }
     } else if (mode == 1) {
         hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
                            match_count, w.planes, out_norm, prm->seed, prm->thr, w.best);
@@ -738,7 +839,8 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
 extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
                                  const int32_t* pairs, int32_t n_pairs, const int32_t* match_count,
                                  const int32_t* matches, const sfm_ransac_params* prm,
-                                 int32_t* out_counts, float* out_norm) {
+                                 int32_t* out_counts, float* out_norm, float* out_hyp_F,
+                                 uint8_t* out_hyp_mask) {
     RANSAC_CHECK_ARGS("sfm_ransac_counts");
     SFM_REQUIRE(out_counts && out_norm, "sfm_ransac_counts: NULL output");
     SFM_REQUIRE(prm->n_hyp <= 65536, "sfm_ransac_counts: n_hyp > 65536");
@@ -757,13 +859,38 @@ extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, 
     const dim3 xgrid(xcd_grid(n_pairs, H / 256));
     const int gp = ransac_group(n_pairs);
     hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
-                       match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG, w.prev);
+                       match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG, w.prev,
+                       out_hyp_F);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                        w.prev, w.order);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL((ransac_score_kernel<false, true>), xgrid, dim3(256), 0, st, n_pairs, k_max,
-                       match_count, w.planes, H, gp, w.hypG, w.order, w.best, out_counts);
+                       match_count, w.planes, H, gp, w.hypG, w.order, w.best, out_counts,
+                       (uint32_t*)nullptr);
     SFM_HIP_CHECK(hipGetLastError());
+    if (out_hyp_mask) {
+        hipLaunchKernelGGL(ransac_hyp_mask_kernel, dim3(n_pairs, H / 256), dim3(256), 0, st, k_max,
+                           match_count, w.planes, H, w.hypG, out_hyp_mask);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
+    return SFM_OK;
+}
+
+extern "C" int sfm_ransac_stats(sfm_ctx* ctx, int32_t enable, uint64_t* out) {
+    SFM_REQUIRE(ctx, "sfm_ransac_stats: ctx is NULL");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    if (!ctx->rs_acc) {
+        SFM_HIP_CHECK(hipMalloc(&ctx->rs_acc, 3 * sizeof(unsigned long long)));
+        SFM_HIP_CHECK(hipMemsetAsync(ctx->rs_acc, 0, 3 * sizeof(unsigned long long), ctx->stream));
+    }
+    if (out) {  // read and reset the counters (synchronises the context's stream)
+        unsigned long long h[3];
+        SFM_HIP_CHECK(hipMemcpyAsync(h, ctx->rs_acc, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+        SFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        out[0] = h[0]; out[1] = h[1]; out[2] = h[2];
+        SFM_HIP_CHECK(hipMemsetAsync(ctx->rs_acc, 0, 3 * sizeof(unsigned long long), ctx->stream));
+    }
+    ctx->ransac_stats = enable ? 1 : 0;
     return SFM_OK;
 }

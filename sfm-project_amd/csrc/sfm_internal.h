@@ -15,6 +15,12 @@ struct sfm_ctx {
     hipEvent_t handoff = nullptr;  // orders the workspace across sfm_ctx_set_stream switches
     int32_t* pinned = nullptr;     // small pinned host buffer (device -> host flag reads)
     int n_cu = 256;
+    // RANSAC execution statistics (sfm_ransac_stats): per-wave scored-match counts of the last
+    // batch and the accumulated (executed, algorithmic, pairs) evaluation counters
+    int ransac_stats = 0;
+    uint32_t* rs_wave = nullptr;
+    size_t rs_wave_n = 0;
+    unsigned long long* rs_acc = nullptr;
 };
 
 namespace sfm {

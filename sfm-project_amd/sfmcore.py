@@ -24,7 +24,8 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_last_error", "sfm_version", "sfm_match_batch", "sfm_ransac_f_batch",
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
-            "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage"]
+            "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
+            "sfm_ransac_stats"]
 
 
 class SfmCoreError(RuntimeError):
@@ -92,7 +93,8 @@ def load_library(path: str = LIB_PATH):
         L.sfm_ransac_f_batch.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
                                          C.POINTER(RansacParams), vp, vp, vp, vp, vp]
         L.sfm_ransac_counts.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
-                                        C.POINTER(RansacParams), vp, vp]
+                                        C.POINTER(RansacParams), vp, vp, vp, vp]
+        L.sfm_ransac_stats.argtypes = [vp, i32, vp]
         L.sfm_ba_jtj.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp,
                                  vp, vp, vp, vp, vp, vp]
         L.sfm_ba_solve.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -229,10 +231,13 @@ class Context:
                                            _ptr(out["mask"]), _ptr(out["F"]), _ptr(out["norm"])))
         return out
 
-    def ransac_counts(self, kps, pairs, count, match, n_hyp=4096, seed=42, thr=1.0):
+    def ransac_counts(self, kps, pairs, count, match, n_hyp=4096, seed=42, thr=1.0,
+                      hyp_F=False, hyp_mask=False):
         """Diagnostic: the inlier count of every hypothesis ([P, n_hyp] i32 device tensor, -1 for
         degenerate samples / pairs with < 8 matches) and norm [P,6], by the same score path as
-        ransac_batch (sfm_ransac_counts)."""
+        ransac_batch (sfm_ransac_counts); with hyp_F also every hypothesis's F [P, n_hyp, 9] f32
+        (normalised coordinates), with hyp_mask every hypothesis's decisions [P, n_hyp, k_max] u8.
+        Returns (counts, norm) or (counts, norm, F, mask) (None for what was not asked)."""
         torch = self.torch
         n_img, k_max, _ = kps.shape
         P = pairs.shape[0]
@@ -241,12 +246,24 @@ class Context:
             raise SfmCoreError("ransac_counts: kps must be contiguous float32")
         counts = torch.empty((P, n_hyp), dtype=torch.int32, device=dev)
         norm = torch.empty((P, 6), dtype=torch.float32, device=dev)
+        F = torch.empty((P, n_hyp, 9), dtype=torch.float32, device=dev) if hyp_F else None
+        mk = torch.zeros((P, n_hyp, k_max), dtype=torch.uint8, device=dev) if hyp_mask else None
         prm = RansacParams(int(n_hyp), 0, float(thr), 0, int(seed))
         self._bind_stream()
         _check(self.lib.sfm_ransac_counts(self.handle, _ptr(kps), n_img, k_max, _ptr(pairs), P,
                                           _ptr(count), _ptr(match), C.byref(prm), _ptr(counts),
-                                          _ptr(norm)))
-        return counts, norm
+                                          _ptr(norm), _ptr(F) if hyp_F else None,
+                                          _ptr(mk) if hyp_mask else None))
+        return (counts, norm, F, mk) if (hyp_F or hyp_mask) else (counts, norm)
+
+    def ransac_stats(self, enable=True, read=False):
+        """sfm_ransac_stats: enable / disable the execution counters of ransac_batch; with read,
+        returns and resets (executed Sampson evaluations, algorithmic = n_hyp x M over pairs with
+        M >= 8, number of such pairs) — synchronises the stream."""
+        out = (C.c_uint64 * 3)()
+        self._bind_stream()
+        _check(self.lib.sfm_ransac_stats(self.handle, 1 if enable else 0, out if read else None))
+        return (int(out[0]), int(out[1]), int(out[2])) if read else None
 
     # ---- verified match graph --------------------------------------------------------------
     def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15,

@@ -6,7 +6,9 @@
    `FundamentalMatrixTransform`).  The reference itself cannot run here (no cv2),
    so these pin the SEMANTICS (mutual cross check, lowest-index ties, Lowe ratio on unsquared
    distances, Hartley 8-point + rank 2), not the reference's outputs: parity stays "unpinned".
-2. oracle_fixtures.npz — inputs and the CPU oracle's outputs (match lists, RANSAC winner, inlier
+2. skimage_ransac_fixtures.npz — 4 noisy cfg3 pairs x 256 hypotheses: the sampled indices (the
+   build's Philox sampler), scikit-image's 8-point F and Sampson decisions per hypothesis.
+3. oracle_fixtures.npz — inputs and the CPU oracle's outputs (match lists, RANSAC winner, inlier
    mask, F bits) for small seeded cases; the GPU tests compare against these stored vectors.
 
 Usage:  python tests/golden/make_golden.py      (system python 3.10; calls python3.9 for skimage)
@@ -74,6 +76,82 @@ def skimage_fixtures():
     return {k: v.shape for k, v in outs.items()}
 
 
+# Per-hypothesis 8-point estimates of scikit-image's FundamentalMatrixTransform on the same
+# samples the build's Philox sampler draws.  skimage normalises each 8-point sample on its own
+# (RMS variant of Hartley); the build normalises once per pair (mean-distance variant, DESIGN
+# 4.2).  The 8x9 null space (F before the rank-2 step) does not depend on the normalisation, but
+# the rank-2 truncation does, so skimage's _center_and_normalize_points is given the build's
+# pair-level transform for the estimate: the comparison is of the arithmetic (null space + rank
+# 2), in the same frame.  Residuals are skimage's own Sampson distances in pixels.
+SKIMAGE_RANSAC_SCRIPT = r"""
+import sys, numpy as np
+from skimage.transform import _geometric as g
+from skimage.transform import FundamentalMatrixTransform
+d = np.load(sys.argv[1]); out = {}
+for i in range(int(d["n_pairs"])):
+    x1 = d[f"p{i}_x1"].astype(np.float64); x2 = d[f"p{i}_x2"].astype(np.float64)
+    nm = d[f"p{i}_norm"].astype(np.float64)
+    mk = lambda cx, cy, s: np.array([[s, 0, -s * cx], [0, s, -s * cy], [0, 0, 1.0]])
+    T = {"src": mk(*nm[:3]), "dst": mk(*nm[3:])}
+    Fs, R, C = [], [], []
+    orig = g._center_and_normalize_points
+    for ix in d[f"p{i}_idx"]:
+        seq = iter(["src", "dst"])
+        def pair_frame(points, _seq=seq):
+            m = T[next(_seq)]
+            return m, (m @ np.row_stack([points.T, np.ones(points.shape[0])])).T[:, :2]
+        g._center_and_normalize_points = pair_frame
+        t = FundamentalMatrixTransform()
+        assert t.estimate(x1[ix], x2[ix])
+        g._center_and_normalize_points = orig
+        Fs.append((t.params / np.linalg.norm(t.params)).ravel())
+        R.append(t.residuals(x1, x2))
+        n1 = (T["src"] @ np.row_stack([x1[ix].T, np.ones(8)])).T
+        n2 = (T["dst"] @ np.row_stack([x2[ix].T, np.ones(8)])).T
+        A = np.ones((8, 9)); A[:, :2] = n1[:, :2]; A[:, :3] *= n2[:, 0:1]
+        A[:, 3:5] = n1[:, :2]; A[:, 3:6] *= n2[:, 1:2]; A[:, 6:8] = n1[:, :2]
+        sv = np.linalg.svd(A, compute_uv=False)
+        C.append(sv[-1] / sv[0])
+    out[f"p{i}_F"] = np.array(Fs); out[f"p{i}_res2"] = np.array(R) ** 2; out[f"p{i}_cond"] = np.array(C)
+np.savez(sys.argv[2], **out)
+"""
+RANSAC_PAIRS = [(0, 1), (5, 6), (12, 30), (40, 41)]  # cfg3 scene (50 x 2048, seed 0)
+RANSAC_H = 256
+RANSAC_BAND = 1e-5  # decisions may differ only where |res^2 / thr - 1| < RANSAC_BAND
+
+
+def skimage_ransac_fixtures():
+    import oracle as O
+    import synth
+    s = synth.make_scene(50, 2048, seed=0)
+    inp = {"n_pairs": np.int32(len(RANSAC_PAIRS)), "pairs": np.array(RANSAC_PAIRS, np.int32),
+           "seed": np.uint64(42), "thr": np.float32(1.0), "band": np.float64(RANSAC_BAND)}
+    for i, (a, b) in enumerate(RANSAC_PAIRS):
+        q, t, _ = O.match(s["desc"][a], s["desc"][b], 0, 1, (4, 5))   # the bench rule's matches
+        x1 = s["kps"][a][q].astype(np.float32)
+        x2 = s["kps"][b][t].astype(np.float32)
+        _, cx1, cy1, s1 = O.normalize(x1)
+        _, cx2, cy2, s2 = O.normalize(x2)
+        inp[f"p{i}_x1"], inp[f"p{i}_x2"] = x1, x2
+        inp[f"p{i}_norm"] = np.array([cx1, cy1, s1, cx2, cy2, s2], np.float32)
+        inp[f"p{i}_idx"] = np.stack([O.sample8(42, a, b, h, len(q)) for h in range(RANSAC_H)])
+    with tempfile.TemporaryDirectory() as td:
+        fi, fo = os.path.join(td, "in.npz"), os.path.join(td, "out.npz")
+        np.savez(fi, **inp)
+        subprocess.run([SKIMAGE_PY, "-c", SKIMAGE_RANSAC_SCRIPT, fi, fo], check=True,
+                       stderr=subprocess.DEVNULL)
+        out = dict(np.load(fo))
+    fx = dict(inp)
+    for i in range(len(RANSAC_PAIRS)):
+        r2 = out[f"p{i}_res2"] / 1.0
+        fx[f"p{i}_expect_F"] = out[f"p{i}_F"]
+        fx[f"p{i}_expect_cond"] = out[f"p{i}_cond"]
+        fx[f"p{i}_expect_mask"] = np.packbits(r2 < 1.0, axis=1)
+        fx[f"p{i}_band"] = np.packbits(np.abs(r2 - 1.0) < RANSAC_BAND, axis=1)
+    np.savez_compressed(os.path.join(HERE, "skimage_ransac_fixtures.npz"), **fx)
+    return sum(v.nbytes for v in fx.values())
+
+
 def oracle_fixtures():
     import oracle as O
     import synth
@@ -111,4 +189,5 @@ def oracle_fixtures():
 
 if __name__ == "__main__":
     print("skimage:", skimage_fixtures())
+    print("skimage ransac bytes:", skimage_ransac_fixtures())
     print("oracle entries:", oracle_fixtures())

@@ -42,7 +42,7 @@ def main():
     ms = ev[0].elapsed_time(ev[1]) / 20
     qb = 512                                      # MU_WAVES (4) x QT (4) x 32 queries per block
     n_blk = len(pairs) * ((K + qb - 1) // qb)
-    persist = os.environ.get("SFM_MU_PERSIST", "1") != "0"
+    persist = os.environ.get("SFM_MU_PERSIST", "0") == "1"
     grid = 512 if persist else 8 * ((n_blk + 7) // 8)  # persistent: 2 blocks per CU x 256 CUs
     W = 8
     buf = np.zeros(W * grid, np.uint64)

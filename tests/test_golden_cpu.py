@@ -77,3 +77,51 @@ def test_oracle_regression_pin(orc):
     q, t, d = O.match(orc["orb_desc"][0], orc["orb_desc"][1], 1, 2, None, 26)
     np.testing.assert_array_equal(np.stack([q, t], 1), orc["orb_match"])
     np.testing.assert_array_equal(d, orc["orb_dist"])
+
+
+# ---- per-hypothesis 8-point F vs scikit-image (tests/golden/skimage_ransac_fixtures.npz) ----------
+F_TOL, F_TOL_ILL, COND_MIN = 1e-4, 1e-3, 5e-3
+
+
+def pixel_frame_F(Fn, norm):
+    """F of the normalised frame (9 f32) -> unit-norm pixel-frame F (T2^T F T1)."""
+    cx1, cy1, s1, cx2, cy2, s2 = (float(v) for v in norm)
+    T1 = np.array([[s1, 0, -s1 * cx1], [0, s1, -s1 * cy1], [0, 0, 1.0]])
+    T2 = np.array([[s2, 0, -s2 * cx2], [0, s2, -s2 * cy2], [0, 0, 1.0]])
+    F = T2.T @ np.asarray(Fn, np.float64).reshape(3, 3) @ T1
+    return F / np.linalg.norm(F)
+
+
+def check_hypotheses_vs_skimage(fx, i, F_norm_frame, masks, norm):
+    """Shared by the CPU (oracle) and GPU tests: every hypothesis's F within F_TOL of skimage's
+    (up to sign; F_TOL_ILL where the 8x9 system's sigma_8/sigma_1 < COND_MIN), and identical
+    inlier decisions except within the stated band |res^2/thr - 1| < band."""
+    M = fx[f"p{i}_x1"].shape[0]
+    E = fx[f"p{i}_expect_F"]
+    cond = fx[f"p{i}_expect_cond"]
+    err = np.array([min(np.abs(pixel_frame_F(F_norm_frame[h], norm) - E[h].reshape(3, 3)).max(),
+                        np.abs(pixel_frame_F(F_norm_frame[h], norm) + E[h].reshape(3, 3)).max())
+                    for h in range(E.shape[0])])
+    well = cond >= COND_MIN
+    assert err[well].max() < F_TOL, (i, err[well].max())
+    assert err.max() < F_TOL_ILL, (i, err.max())
+    exp = np.unpackbits(fx[f"p{i}_expect_mask"], axis=1)[:, :M].astype(bool)
+    band = np.unpackbits(fx[f"p{i}_band"], axis=1)[:, :M].astype(bool)
+    diff = (np.asarray(masks)[:, :M].astype(bool) != exp)
+    assert not (diff & ~band).any(), (i, np.argwhere(diff & ~band)[:5])
+    return int(well.sum()), int(diff.sum())
+
+
+def test_ransac_hypotheses_vs_skimage():
+    fx = dict(np.load(os.path.join(G, "skimage_ransac_fixtures.npz")))
+    H = fx["p0_expect_F"].shape[0]
+    for i, (a, b) in enumerate(fx["pairs"]):
+        x1, x2 = fx[f"p{i}_x1"], fx[f"p{i}_x2"]
+        n1, cx1, cy1, s1 = O.normalize(x1)
+        n2, cx2, cy2, s2 = O.normalize(x2)
+        norm = np.array([cx1, cy1, s1, cx2, cy2, s2], np.float32)
+        np.testing.assert_array_equal(norm.view(np.uint32), fx[f"p{i}_norm"].view(np.uint32))
+        masks, idx, ok = O.ransac_masks(x1, x2, H=H, seed=42, pa=int(a), pb=int(b), thr=1.0)
+        np.testing.assert_array_equal(idx, fx[f"p{i}_idx"])
+        Fn = np.stack([O.fit_f8(n1[ix], n2[ix])[1] for ix in idx])
+        check_hypotheses_vs_skimage(fx, i, Fn, masks, norm)

@@ -40,3 +40,68 @@ def test_gpu_matches_golden_vectors(ctx):
     k = int(c2.cpu()[0])
     np.testing.assert_array_equal(m2.cpu().numpy()[0, :k], f["orb_match"])
     np.testing.assert_array_equal(d2.cpu().numpy()[0, :k], f["orb_dist"])
+
+
+# ---- the GPU directly on scikit-image's vectors (tests/golden/skimage_fixtures.npz) -------------
+SK_L2 = [("l2_mutual_r08", 1, (4, 5), -1), ("l2_none_r08", 0, (4, 5), -1), ("l2_mutual", 1, None, -1),
+         ("l2_mutual_maxd180", 1, None, 180 * 180)]  # L2 max_dist on d^2: d < 180 <=> d^2 < 32400
+SK_HAM = [("ham_mutual", -1), ("ham_mutual_max26", 26)]  # d < 25.5/256 of the bits <=> d < 26
+
+
+def _gpu_pair(ctx, A, B, **kw):
+    import torch
+    k = max(A.shape[0], B.shape[0])
+    desc = np.zeros((2, k, A.shape[1]), np.uint8)
+    desc[0, :A.shape[0]] = A
+    desc[1, :B.shape[0]] = B
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    cnt, mt, _ = ctx.match_batch(T(desc), T(np.array([A.shape[0], B.shape[0]], np.int32)),
+                                 T(np.array([[0, 1]], np.int32)), **kw)
+    torch.cuda.synchronize()
+    n = int(cnt.cpu()[0])
+    return mt.cpu().numpy()[0, :n].astype(np.int64)
+
+
+@pytest.mark.parametrize("key,xc,ratio,md", SK_L2)
+def test_gpu_l2_vs_skimage(ctx, key, xc, ratio, md):
+    sk = np.load(os.path.join(G, "skimage_fixtures.npz"))
+    got = _gpu_pair(ctx, sk["l2_A"], sk["l2_B"], metric=0, cross_check=xc, ratio=ratio,
+                    max_dist=md)
+    np.testing.assert_array_equal(got, sk["expect_" + key].astype(np.int64))
+
+
+@pytest.mark.parametrize("key,md", SK_HAM)
+def test_gpu_hamming_vs_skimage(ctx, key, md):
+    sk = np.load(os.path.join(G, "skimage_fixtures.npz"))
+    got = _gpu_pair(ctx, sk["ham_A"], sk["ham_B"], metric=1, cross_check=1, max_dist=md)
+    np.testing.assert_array_equal(got, sk["expect_" + key].astype(np.int64))
+
+
+def test_gpu_ransac_hypotheses_vs_skimage(ctx):
+    """Every hypothesis of 4 noisy cfg3 pairs (256 each, the GPU's own Philox samples): F within
+    1e-4 of scikit-image's FundamentalMatrixTransform (1e-3 for the ill-conditioned 8x9 systems),
+    identical inlier decisions outside the stated band (test_golden_cpu.check_hypotheses_vs_skimage)."""
+    import torch
+    from test_golden_cpu import check_hypotheses_vs_skimage
+    fx = dict(np.load(os.path.join(G, "skimage_ransac_fixtures.npz")))
+    pairs = fx["pairs"].astype(np.int32)
+    Ms = [fx[f"p{i}_x1"].shape[0] for i in range(len(pairs))]
+    k_max = max(Ms)
+    kps = np.zeros((int(pairs.max()) + 1, k_max, 2), np.float32)
+    match = np.zeros((len(pairs), k_max, 2), np.int32)
+    for i, (a, b) in enumerate(pairs):
+        kps[a, :Ms[i]] = fx[f"p{i}_x1"]
+        kps[b, :Ms[i]] = fx[f"p{i}_x2"]
+        match[i, :Ms[i]] = np.arange(Ms[i])[:, None]
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    H = fx["p0_expect_F"].shape[0]
+    counts, norm, F, mk = ctx.ransac_counts(T(kps), T(pairs), T(np.array(Ms, np.int32)), T(match),
+                                            n_hyp=H, seed=int(fx["seed"]), thr=float(fx["thr"]),
+                                            hyp_F=True, hyp_mask=True)
+    torch.cuda.synchronize()
+    counts, norm, F, mk = (t.cpu().numpy() for t in (counts, norm, F, mk))
+    for i in range(len(pairs)):
+        np.testing.assert_array_equal(norm[i].view(np.uint32), fx[f"p{i}_norm"].view(np.uint32))
+        ok = counts[i] >= 0  # -1: degenerate sample
+        np.testing.assert_array_equal(mk[i][ok, :Ms[i]].sum(1), counts[i][ok])
+        check_hypotheses_vs_skimage(fx, i, F[i], mk[i], norm[i])
