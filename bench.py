@@ -99,6 +99,7 @@ class Runner:
         self.gb = match_graph.GraphBuilder(scene["desc"], scene["kps"], scene["n_kp"],
                                            device=local, ratio=(4, 5), n_hyp=n_hyp, seed=42,
                                            thr=1.0, min_inliers=15)
+        self.ctx = self.gb.ctx
         self.lo, self.hi = lo, hi
         shard = pairs[lo:hi]
         self.chunks = []
@@ -201,6 +202,9 @@ def main():
     for _ in range(args.warmup):
         run.step(xr)
     torch.cuda.synchronize()
+    # K2's executed share, measured in the timed steps themselves (sfm_ransac_stats: one u32 store
+    # per score wave + one small reduction kernel per launch, ~10 us at cfg4)
+    run.ctx.ransac_stats(enable=True, read=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -220,11 +224,12 @@ def main():
 
     verified_per_step = int(graph.shape[0])
     checksum = graph_checksum(torch, graph)  # after the timed region
+    r_alg, r_exec, r_evals = ransac_flops(run.ctx.ransac_stats(enable=False, read=True),
+                                          args.n_hyp, args.steps)
     st = [Runner.stage_ms(e) for e in evs]
     match_ms = float(np.mean([s[0] for s in st]))
     ransac_ms = float(np.mean([s[1] for s in st]))
     k1_tops = run.k1_ops / (match_ms * 1e-3) / 1e12
-    r_alg, r_exec = ransac_flops(run, args.n_hyp)
     value = verified_per_step * args.steps / elapsed
     result = {
         "metric": "verified matches/sec (match+RANSAC)",
@@ -263,15 +268,19 @@ def main():
                    "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,
                    "ransac_roofline": {
                        "bound": "f32 VALU", "peak": PEAK_F32_VALU_TFLOPS, "unit": "TFLOP/s",
-                       "achieved": r_alg / (ransac_ms * 1e-3) / 1e12,
-                       "frac": r_alg / (ransac_ms * 1e-3) / 1e12 / PEAK_F32_VALU_TFLOPS,
-                       "flops_per_step": r_alg,
-                       "note": "algorithmic = every hypothesis scored on every match; the exact "
-                               "pruning skips part of it (executed_frac_estimate: PMC-measured "
-                               "on a cfg4 pair sample, profiles/r02/pmc_ransac_exec_cfg4_pe32.txt)",
-                       "executed_frac_estimate": r_exec,
+                       "achieved": r_alg * r_exec / (ransac_ms * 1e-3) / 1e12,
+                       "frac": r_alg * r_exec / (ransac_ms * 1e-3) / 1e12 / PEAK_F32_VALU_TFLOPS,
+                       "executed_flops_per_step": r_alg * r_exec,
+                       "algorithmic_flops_per_step": r_alg,
+                       "executed_frac": r_exec,
+                       "evaluations_per_step": r_evals,
+                       "note": "achieved / frac count the EXECUTED work (the exact pruning skips "
+                               "the rest): Sampson evaluations counted by the score waves in the "
+                               "timed steps (sfm_ransac_stats) x 33 flop + 1400 flop per fitted "
+                               "hypothesis; algorithmic = every hypothesis on every match "
+                               "(pairs with >= 8 matches); executed_frac = executed / algorithmic",
                        "practical_peak": PRACTICAL_F32_VALU_TFLOPS,
-                       "executed_frac_of_practical":
+                       "frac_of_practical":
                            r_alg * r_exec / (ransac_ms * 1e-3) / 1e12 / PRACTICAL_F32_VALU_TFLOPS}},
     }
     # step-level fraction = sum of the stages' roofline times / measured step time
@@ -283,7 +292,7 @@ def main():
         "frac": (t_k1 + t_k2) / step_s, "k1_ideal_ms": t_k1 * 1e3, "k2_ideal_ms": t_k2 * 1e3,
         "step_ms": step_s * 1e3,
         "note": "sum of stage roofline times / measured step; K2 ideal on the executed "
-                "(pruned) share of the algorithmic flops"}
+                "(pruned) share of the algorithmic flops (measured in the timed steps)"}
 
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
@@ -313,21 +322,17 @@ def graph_checksum(torch, graph):
     return int(((v * w) % P).sum().item() % P)
 
 
-def ransac_flops(run, n_hyp):
-    """Algorithmic K2 flops per step (every hypothesis on every match of pairs with >= 8
-    matches) and the executed fraction of the scoring: 0.580 measured on a 2048-pair stride sample
-    of the cfg4 scene (SQ_INSTS_VALU of the pruned vs the unpruned score kernel,
-    tools/pmc_ransac_exec.sh, profiles/r02/pmc_ransac_exec_cfg4_pe32.txt); 0.59 in the cfg3 pruning
-    simulation."""
-    import numpy as np
-    cnt = np.concatenate([run.gb._buffers(pt.shape[0])["match"][0].cpu().numpy()
-                          for _, pt in run.chunks[-1:]])
-    # the tentative counts of the last chunk stand for the chunk mix (strong-scaling chunks are
-    # drawn from one scene); scale to the whole shard
-    n_pairs = sum(pt.shape[0] for _, pt in run.chunks)
-    m = np.where(cnt >= 8, cnt, 0).astype(np.float64)
-    per_pair = n_hyp * float(np.mean(m * RANSAC_FLOP_PER_EVAL + (m > 0) * RANSAC_FLOP_PER_FIT))
-    return per_pair * n_pairs, 0.580
+def ransac_flops(stats, n_hyp, steps):
+    """K2 flops per step from the device counters of the timed steps (sfm_ransac_stats):
+    stats = (executed Sampson evaluations, algorithmic evaluations = n_hyp x M over pairs with
+    M >= 8, number of such pairs), summed over `steps`.  Returns (algorithmic flops per step,
+    executed fraction, evaluation counts per step)."""
+    ex, al, npairs = (v / steps for v in stats)
+    fit = RANSAC_FLOP_PER_FIT * n_hyp * npairs
+    alg = RANSAC_FLOP_PER_EVAL * al + fit
+    exe = RANSAC_FLOP_PER_EVAL * ex + fit
+    return alg, (exe / alg if alg > 0 else 0.0), {"executed": ex, "algorithmic": al,
+                                                   "pairs_ge8": npairs}
 
 
 def cpu_baseline(scene, pairs, lo, hi, graph, gb, seconds, n_hyp):
@@ -337,10 +342,8 @@ def cpu_baseline(scene, pairs, lo, hi, graph, gb, seconds, n_hyp):
     import numpy as np
     import torch
     import oracle as O
-    aff = len(os.sched_getaffinity(0))
-    # the GPU box gives one GPU slot a 16-CPU share of the host (OMP_NUM_THREADS is set to it);
-    # here, without the variable, every CPU in the affinity mask
-    threads = min(aff, int(os.environ.get("OMP_NUM_THREADS") or aff))
+    share = cpu_share()
+    aff, threads = share["cpus_in_affinity"], share["threads"]
     O.set_threads(threads)
     shard = pairs[lo:hi]
     cal = np.ascontiguousarray(shard[:: max(1, len(shard) // threads)][:threads])
@@ -390,13 +393,54 @@ def cpu_baseline(scene, pairs, lo, hi, graph, gb, seconds, n_hyp):
     return {"value": tot / dt, "unit": "verified matches/s", "cores": threads, "kind": "port",
             "sample": (f"{len(sample)} of {len(shard)} pairs (stride {stride}), full K1+K2 per "
                        f"pair, OpenMP over pairs, {dt:.1f} s wall on {model_str(aff)}"),
-            "host_cpus_in_affinity": aff, "cpu_model": cpu_model(),
+            "host_cpus_in_affinity": aff, "cpu_share": share, "cpu_model": cpu_model(),
             "per_pair_core_ms": dt * 1e3 * threads / len(sample),
             "parity": {"pairs": int(len(sample)), "match_counts": ok_cnt,
                        "match_indices": bool(ok_idx),
                        "inlier_masks_best_h_counts": bool(ok_mask),
                        "graph_rows_of_timed_step": ok_rows},
             "inlier_parity_with_gpu": bool(ok_cnt and ok_idx and ok_mask and ok_rows)}
+
+
+def cpu_share():
+    """The CPUs this process may use: the affinity mask, the cgroup CPU quota (v2 cpu.max or v1
+    cpu.cfs_quota_us / cpu.cfs_period_us) and OMP_NUM_THREADS (the GPU box sets it to the one-GPU
+    slot's 16-CPU share and asks that worker pools be sized to it).  threads = the smallest."""
+    aff = len(os.sched_getaffinity(0))
+    info = {"cpus_in_affinity": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    quota = None
+    for path, kind in (("/sys/fs/cgroup/cpu.max", "v2"),
+                       ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "v1")):
+        try:
+            raw = open(path).read().strip()
+        except OSError:
+            continue
+        info["cgroup_" + kind] = raw
+        try:
+            if kind == "v2":
+                q, per = raw.split()
+                if q != "max":
+                    quota = float(q) / float(per)
+            else:
+                q = float(raw)
+                per = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                if q > 0:
+                    quota = q / per
+        except (OSError, ValueError):
+            pass
+        break
+    info["cgroup_cpu_quota"] = quota
+    lim = [aff]
+    if quota:
+        lim.append(max(1, int(math.ceil(quota))))
+    if info["omp_num_threads"]:
+        lim.append(int(info["omp_num_threads"]))
+    info["threads"] = min(lim)
+    info["limited_by"] = ("cgroup quota" if quota and info["threads"] == int(math.ceil(quota))
+                          else "OMP_NUM_THREADS (the box's per-GPU CPU share)"
+                          if info["omp_num_threads"] and info["threads"] == int(info["omp_num_threads"])
+                          else "affinity mask")
+    return info
 
 
 def model_str(aff):
