@@ -101,6 +101,18 @@ int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_
                        int32_t* out_inl_count, int32_t* out_best_h, uint8_t* out_mask,
                        float* out_F, float* out_norm);
 
+/* fp64 mode of sfm_ransac_f_batch (SURVEY.md §8b's f64 coordinates / F): the same spec, sampler,
+ * schedule and outputs with every floating-point operation of normalisation, 8-point fit, rank-2
+ * step and Sampson test in double (the oracle's *_f64 restatement is bit-identical).  kps
+ * [n_img][k_max][2] f64; out_F [n_pairs][9] f64; out_norm [n_pairs][6] f64; the ordered schedule
+ * only (SFM_RANSAC_MODE is ignored).
+ */
+int sfm_ransac_f_batch_f64(sfm_ctx* ctx, const double* kps, int32_t n_img, int32_t k_max,
+                           const int32_t* pairs, int32_t n_pairs, const int32_t* match_count,
+                           const int32_t* matches, const sfm_ransac_params* prm,
+                           int32_t* out_inl_count, int32_t* out_best_h, uint8_t* out_mask,
+                           double* out_F, double* out_norm);
+
 /* Diagnostic companion of sfm_ransac_f_batch: the inlier count of EVERY hypothesis (no pruning),
  * out_counts [n_pairs][n_hyp] i32 (-1: degenerate sample or fewer than 8 matches), computed by the
  * score kernel of sfm_ransac_f_batch with pruning off; out_norm as above.  Optional (NULL: not
@@ -175,11 +187,12 @@ typedef struct sfm_ba_solve_params {
     double lambda;    /* Marquardt damping λ (>= 0) */
     double tol;       /* relative CG residual |r|/|b| */
     int32_t max_iter; /* CG iteration cap */
-    int32_t poll;     /* convergence poll: every `poll` CG iterations (0 = every 8) the host reads
-                         the device's convergence flag (one 4-byte copy + stream sync) and stops
-                         enqueueing once it is set; < 0 = never (fully asynchronous: all max_iter
+    int32_t poll;     /* convergence poll: every `poll` > 0 CG iterations the host reads the
+                         device's convergence flag (one 4-byte copy + a hipStreamSynchronize) and
+                         stops enqueueing once it is set; <= 0 (the zero-initialised default) =
+                         never: fully asynchronous, capturable in a hip graph (all max_iter
                          iterations are enqueued, the converged ones exit at once).  Results are
-                         identical either way. */
+                         identical either way; sfmcore.py / reconstruction.py poll every 8. */
 } sfm_ba_solve_params;
 
 int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
@@ -197,7 +210,7 @@ int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
  * no other sfm_* call on this context in between — the stages share its workspace):
  *   SETUP           -> all-reduce comm[0, 44 n_cam)  -> SETUP_FINISH
  *   for k = 0 .. max_iter-1:
- *     [every prm->poll (0: 8) iterations, k > 0: POLL -> *done (host int32); stop if 1]
+ *     [every prm->poll > 0 iterations, k > 0: POLL -> *done (host int32); stop if 1]
  *     ITER(k)       -> all-reduce comm[0, 8 n_cam)   -> ITER_FINISH(k)
  *   BACKSUB         -> all-reduce comm[0, 2)         -> MODEL   (dc, dp, info as sfm_ba_solve)
  * After each all-reduce every camera-space value is replicated, so every rank takes the same CG

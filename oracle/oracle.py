@@ -58,6 +58,16 @@ def _bind(L):
     L.oracle_match_verify_batch.argtypes = [vp, vp, i32, i32, i32, vp, i32, i32, i32, i64, i32,
                                             u64, f32, i32, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_match_verify_batch.restype = C.c_longlong
+    # fp64 mode of the same spec (sfm_oracle_ransac.inc with R = double)
+    L.oracle_normalize_f64.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.oracle_fit_f8_f64.argtypes = [vp, vp, vp]
+    L.oracle_fit_f8_f64.restype = i32
+    L.oracle_ransac_f_f64.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp, vp, vp, vp]
+    L.oracle_ransac_f_f64.restype = i32
+    L.oracle_ransac_counts_f64.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp]
+    L.oracle_ransac_masks_f64.argtypes = [vp, vp, i32, i32, u64, u32, u32, f32, vp, vp, vp]
+    L.oracle_match_verify_batch_f64.argtypes = L.oracle_match_verify_batch.argtypes
+    L.oracle_match_verify_batch_f64.restype = C.c_longlong
     L.oracle_set_threads.argtypes = [i32]
     L.oracle_get_threads.restype = i32
     L.oracle_ba_obs.argtypes = [vp, vp, vp, vp, f64, vp, vp, vp, vp, vp]
@@ -140,48 +150,59 @@ def fit_f8(p1, p2):
     return ok, F
 
 
-def ransac_f(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
-    """Returns dict(count, best_h, F (normalised, 9 f32), norm (6 f32), mask (u8 [M]))."""
-    xy1 = np.ascontiguousarray(xy1, np.float32)
-    xy2 = np.ascontiguousarray(xy2, np.float32)
+def _rt(f64):
+    return (np.float64, "_f64") if f64 else (np.float32, "")
+
+
+def ransac_f(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0, f64=False):
+    """Returns dict(count, best_h, F (normalised, 9), norm (6), mask (u8 [M])); f32 spec, or the
+    fp64 mode of the same spec with f64=True (coordinates, F and norm in float64)."""
+    dt, sfx = _rt(f64)
+    xy1 = np.ascontiguousarray(xy1, dt)
+    xy2 = np.ascontiguousarray(xy2, dt)
     M = xy1.shape[0]
     bh = np.zeros(1, np.int32)
-    F = np.zeros(9, np.float32)
-    nrm = np.zeros(6, np.float32)
+    F = np.zeros(9, dt)
+    nrm = np.zeros(6, dt)
     mask = np.zeros(max(M, 1), np.uint8)
-    c = lib().oracle_ransac_f(_p(xy1), _p(xy2), M, H, seed, pa, pb, thr, _p(bh), _p(F), _p(nrm),
-                              _p(mask))
+    c = getattr(lib(), "oracle_ransac_f" + sfx)(_p(xy1), _p(xy2), M, H, seed, pa, pb, thr, _p(bh),
+                                               _p(F), _p(nrm), _p(mask))
     return dict(count=c, best_h=int(bh[0]), F=F, norm=nrm, mask=mask[:M])
 
 
-def ransac_counts(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
-    xy1 = np.ascontiguousarray(xy1, np.float32)
-    xy2 = np.ascontiguousarray(xy2, np.float32)
+def ransac_counts(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0, f64=False):
+    dt, sfx = _rt(f64)
+    xy1 = np.ascontiguousarray(xy1, dt)
+    xy2 = np.ascontiguousarray(xy2, dt)
     counts = np.zeros(H, np.int32)
-    lib().oracle_ransac_counts(_p(xy1), _p(xy2), xy1.shape[0], H, seed, pa, pb, thr, _p(counts))
+    getattr(lib(), "oracle_ransac_counts" + sfx)(_p(xy1), _p(xy2), xy1.shape[0], H, seed, pa, pb,
+                                                 thr, _p(counts))
     return counts
 
 
-def ransac_masks(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0):
-    """Per-hypothesis f32-spec decisions: (masks [H,M] u8, idx [H,8] i32, ok [H] bool)."""
-    xy1 = np.ascontiguousarray(xy1, np.float32)
-    xy2 = np.ascontiguousarray(xy2, np.float32)
+def ransac_masks(xy1, xy2, H=4096, seed=42, pa=0, pb=1, thr=1.0, f64=False):
+    """Per-hypothesis decisions: (masks [H,M] u8, idx [H,8] i32, ok [H] bool)."""
+    dt, sfx = _rt(f64)
+    xy1 = np.ascontiguousarray(xy1, dt)
+    xy2 = np.ascontiguousarray(xy2, dt)
     M = xy1.shape[0]
     masks = np.zeros((H, max(M, 1)), np.uint8)
     idx = np.zeros((H, 8), np.int32)
     ok = np.zeros(H, np.int32)
-    lib().oracle_ransac_masks(_p(xy1), _p(xy2), M, H, seed, pa, pb, thr, _p(masks), _p(idx), _p(ok))
+    getattr(lib(), "oracle_ransac_masks" + sfx)(_p(xy1), _p(xy2), M, H, seed, pa, pb, thr,
+                                                _p(masks), _p(idx), _p(ok))
     return masks[:, :M], idx, ok.astype(bool)
 
 
 def match_verify_batch(desc, kps, pairs, ratio=(4, 5), max_dist=-1, H=4096, seed=42, thr=1.0,
-                       min_inl=15, full=False):
+                       min_inl=15, full=False, f64=False):
     """K1 (mutual + ratio) + K2 per pair, OpenMP over pairs.  Returns (total verified inliers,
     n_match [P], n_inl [P]); full=True adds a dict with match [P,K,2] (queryIdx, trainIdx),
     mask [P,K] u8, dist [P,K] i32 (d^2), best_h [P] and F [P,9] f32 (entries past n_match[p]
     are zero; F and best_h are meaningful for pairs with >= 8 matches)."""
+    dt, sfx = _rt(f64)
     desc = np.ascontiguousarray(desc, np.uint8)
-    kps = np.ascontiguousarray(kps, np.float32)
+    kps = np.ascontiguousarray(kps, dt)
     pairs = np.ascontiguousarray(pairs, np.int32)
     P, K = pairs.shape[0], desc.shape[1]
     nm = np.zeros(P, np.int32)
@@ -190,9 +211,9 @@ def match_verify_batch(desc, kps, pairs, ratio=(4, 5), max_dist=-1, H=4096, seed
     mk = np.zeros((P, K), np.uint8) if full else None
     bh = np.zeros(P, np.int32) if full else None
     dd = np.zeros((P, K), np.int32) if full else None
-    FF = np.zeros((P, 9), np.float32) if full else None
+    FF = np.zeros((P, 9), dt) if full else None
     nul = C.c_void_p(None)
-    tot = lib().oracle_match_verify_batch(_p(desc), _p(kps), desc.shape[0], desc.shape[1],
+    tot = getattr(lib(), "oracle_match_verify_batch" + sfx)(_p(desc), _p(kps), desc.shape[0], desc.shape[1],
                                           desc.shape[2], _p(pairs), P, ratio[0], ratio[1],
                                           max_dist, H, seed, thr, min_inl, _p(nm), _p(ni),
                                           _p(mt) if full else nul, _p(mk) if full else nul,

@@ -168,410 +168,42 @@ void oracle_sample8(uint64_t seed, uint32_t pa, uint32_t pb, uint32_t h, int M, 
     }
 }
 
-/* Fixed-order fp32 sum: 64 lane partials (lane l sums m = l, l+64, ... in order), then a
- * halving tree (off = 32..1: p[l] += p[l+off]).  Mirrors the GPU wave reduction exactly. */
-static float fixed_sum(const float* v, int M) {
-    float p[64];
-    for (int l = 0; l < 64; ++l) {
-        float s = 0.0f;
-        for (int m = l; m < M; m += 64) s = s + v[m];
-        p[l] = s;
-    }
-    for (int off = 32; off >= 1; off >>= 1)
-        for (int l = 0; l < off; ++l) p[l] = p[l] + p[l + off];
-    return p[0];
-}
+#define R float
+#define NAME(x) x
+#define FMA fmaf
+#define SQRT sqrtf
+#define FABS fabsf
+#define FMAX fmaxf
+#define FREXP frexpf
+#define LDEXP ldexpf
+#include "sfm_oracle_ransac.inc"
+#undef R
+#undef NAME
+#undef FMA
+#undef SQRT
+#undef FABS
+#undef FMAX
+#undef FREXP
+#undef LDEXP
 
-/* Hartley isotropic normalisation of one image side: returns cx, cy, s and writes normalised xy. */
-void oracle_normalize(const float* xy, int M, float* nxy, float* cx, float* cy, float* s) {
-    float* tmp = (float*)malloc(sizeof(float) * (M > 0 ? M : 1));
-    for (int m = 0; m < M; ++m) tmp[m] = xy[2 * m];
-    float sx = fixed_sum(tmp, M);
-    for (int m = 0; m < M; ++m) tmp[m] = xy[2 * m + 1];
-    float sy = fixed_sum(tmp, M);
-    float mx = sx / (float)M, my = sy / (float)M;
-    for (int m = 0; m < M; ++m) {
-        float dx = xy[2 * m] - mx, dy = xy[2 * m + 1] - my;
-        float q = dx * dx;
-        q = fmaf(dy, dy, q);
-        tmp[m] = sqrtf(q);
-    }
-    float sd = fixed_sum(tmp, M);
-    float mean = sd / (float)M;
-    float sc = (mean > 0.0f) ? (1.41421356237309515f / mean) : 1.0f;
-    for (int m = 0; m < M; ++m) {
-        nxy[2 * m] = (xy[2 * m] - mx) * sc;
-        nxy[2 * m + 1] = (xy[2 * m + 1] - my) * sc;
-    }
-    *cx = mx; *cy = my; *s = sc;
-    free(tmp);
-}
-
-/*
- * Fundamental matrix from 8 normalised correspondences (Householder QR null space of the 8x9
- * epipolar system, then rank-2 by removing the smallest eigen-direction of F^T F: the dominant
- * eigenvector of adj(F^T F), taken as the max-diagonal column of adj(F^T F)^(2^RANK2_SQUARINGS)
- * after RANK2_SQUARINGS exactly rescaled squarings).
- * p1/p2: [8][2] normalised points.  Returns 0 on success, -1 if degenerate.  F row-major.
- *
- * Round 3: the rank-2 step was 4 power iterations on adj(F^T F) (error ~ (s3/s2)^8 in the removed
- * direction, s = singular values of the 8-point solution), which left the projection visibly
- * different from the exact SVD truncation (scikit-image FundamentalMatrixTransform) for about
- * 2 % of the hypotheses of noisy cfg3 pairs; squaring reaches the power 2^8 = 256 ((s3/s2)^512).
- */
-#define RANK2_SQUARINGS 8
-
-/* adjugate of a symmetric 3x3 (itself symmetric) */
-static void adj3_sym(const float G[3][3], float A[3][3]) {
-    A[0][0] = fmaf(G[1][1], G[2][2], -(G[1][2] * G[1][2]));
-    A[1][1] = fmaf(G[0][0], G[2][2], -(G[0][2] * G[0][2]));
-    A[2][2] = fmaf(G[0][0], G[1][1], -(G[0][1] * G[0][1]));
-    A[0][1] = A[1][0] = fmaf(G[0][2], G[1][2], -(G[0][1] * G[2][2]));
-    A[0][2] = A[2][0] = fmaf(G[0][1], G[1][2], -(G[0][2] * G[1][1]));
-    A[1][2] = A[2][1] = fmaf(G[0][1], G[0][2], -(G[0][0] * G[1][2]));
-}
-
-/* v *= 2^-e with e the exponent of max|v_i| (exact; keeps the iteration away from under/overflow) */
-static void rescale3_pow2(float v[3]) {
-    const float m = fmaxf(fabsf(v[0]), fmaxf(fabsf(v[1]), fabsf(v[2])));
-    if (m > 0.0f && isfinite(m)) {
-        int e;
-        frexpf(m, &e);
-        for (int i = 0; i < 3; ++i) v[i] = ldexpf(v[i], -e);
-    }
-}
-
-/* symmetric A <- (2^-e A)^2, e the exponent of max|A_ij| (upper triangle, fixed fma order) */
-static void square3_sym(float A[3][3]) {
-    const float m = fmaxf(fmaxf(fmaxf(fabsf(A[0][0]), fabsf(A[1][1])), fmaxf(fabsf(A[2][2]), fabsf(A[0][1]))),
-                          fmaxf(fabsf(A[0][2]), fabsf(A[1][2])));
-    float a00 = A[0][0], a11 = A[1][1], a22 = A[2][2], a01 = A[0][1], a02 = A[0][2], a12 = A[1][2];
-    if (m > 0.0f && isfinite(m)) {
-        int e;
-        frexpf(m, &e);
-        a00 = ldexpf(a00, -e); a11 = ldexpf(a11, -e); a22 = ldexpf(a22, -e);
-        a01 = ldexpf(a01, -e); a02 = ldexpf(a02, -e); a12 = ldexpf(a12, -e);
-    }
-    A[0][0] = fmaf(a02, a02, fmaf(a01, a01, a00 * a00));
-    A[1][1] = fmaf(a12, a12, fmaf(a11, a11, a01 * a01));
-    A[2][2] = fmaf(a22, a22, fmaf(a12, a12, a02 * a02));
-    A[0][1] = A[1][0] = fmaf(a02, a12, fmaf(a01, a11, a00 * a01));
-    A[0][2] = A[2][0] = fmaf(a02, a22, fmaf(a01, a12, a00 * a02));
-    A[1][2] = A[2][1] = fmaf(a12, a22, fmaf(a11, a12, a01 * a02));
-}
-
-int oracle_fit_f8(const float* p1, const float* p2, float F[9]) {
-    float Mt[9][8]; /* Mt = A^T, column k = epipolar row of sample k */
-    for (int k = 0; k < 8; ++k) {
-        float x1 = p1[2 * k], y1 = p1[2 * k + 1], x2 = p2[2 * k], y2 = p2[2 * k + 1];
-        Mt[0][k] = x2 * x1; Mt[1][k] = x2 * y1; Mt[2][k] = x2;
-        Mt[3][k] = y2 * x1; Mt[4][k] = y2 * y1; Mt[5][k] = y2;
-        Mt[6][k] = x1;      Mt[7][k] = y1;      Mt[8][k] = 1.0f;
-    }
-    float V[8][9];
-    float beta[8];
-    for (int k = 0; k < 8; ++k) {
-        float nrm2 = 0.0f;
-        for (int r = k; r < 9; ++r) nrm2 = fmaf(Mt[r][k], Mt[r][k], nrm2);
-        if (!(nrm2 > 0.0f)) return -1;
-        float nrm = sqrtf(nrm2);
-        float alpha = (Mt[k][k] > 0.0f) ? -nrm : nrm;
-        for (int r = k; r < 9; ++r) V[k][r] = Mt[r][k];
-        V[k][k] = Mt[k][k] - alpha;
-        float vn2 = 0.0f;
-        for (int r = k; r < 9; ++r) vn2 = fmaf(V[k][r], V[k][r], vn2);
-        if (!(vn2 > 0.0f)) return -1;
-        beta[k] = 2.0f / vn2;
-        Mt[k][k] = alpha;
-        for (int c = k + 1; c < 8; ++c) {
-            float dot = 0.0f;
-            for (int r = k; r < 9; ++r) dot = fmaf(V[k][r], Mt[r][c], dot);
-            float f = beta[k] * dot;
-            for (int r = k; r < 9; ++r) Mt[r][c] = fmaf(-f, V[k][r], Mt[r][c]);
-        }
-    }
-    float z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 1.0f};
-    for (int k = 7; k >= 0; --k) {
-        float dot = 0.0f;
-        for (int r = k; r < 9; ++r) dot = fmaf(V[k][r], z[r], dot);
-        float f = beta[k] * dot;
-        for (int r = k; r < 9; ++r) z[r] = fmaf(-f, V[k][r], z[r]);
-    }
-    /* rank 2: smallest eigen-direction v of G = F^T F = the dominant eigenvector of adj(G)
-       (ratio (s3/s2)^2 per power), from RANK2_SQUARINGS rescaled squarings of adj(G) and its
-       max-diagonal column; then F' = F - (F v) v^T */
-    float G[3][3];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            float g = 0.0f;
-            for (int r = 0; r < 3; ++r) g = fmaf(z[3 * r + i], z[3 * r + j], g);
-            G[i][j] = g;
-        }
-    float A[3][3];
-    adj3_sym(G, A);
-    for (int it = 0; it < RANK2_SQUARINGS; ++it) square3_sym(A);
-    int kk = 0;
-    if (A[1][1] > A[kk][kk]) kk = 1;
-    if (A[2][2] > A[kk][kk]) kk = 2;
-    float v[3] = {A[0][kk], A[1][kk], A[2][kk]};
-    rescale3_pow2(v);
-    const float n2 = fmaf(v[2], v[2], fmaf(v[1], v[1], v[0] * v[0]));
-    if (n2 > 0.0f) {
-        const float inv = 1.0f / sqrtf(n2);
-        const float v0 = v[0] * inv, v1 = v[1] * inv, v2 = v[2] * inv;
-        for (int r = 0; r < 3; ++r) {
-            float w = fmaf(z[3 * r + 2], v2, fmaf(z[3 * r + 1], v1, z[3 * r] * v0));
-            F[3 * r + 0] = fmaf(-w, v0, z[3 * r + 0]);
-            F[3 * r + 1] = fmaf(-w, v1, z[3 * r + 1]);
-            F[3 * r + 2] = fmaf(-w, v2, z[3 * r + 2]);
-        }
-    } else {
-        for (int i = 0; i < 9; ++i) F[i] = z[i];
-    }
-    return 0;
-}
-
-/* Sampson inlier test in pixel units.  With t1 = thr*s1^2, t2 = thr*s2^2
- * (s = normalisation scales) the test is  t2*|(F x1)_{0,1}|^2 + t1*|(F^T x2)_{0,1}|^2 > (x2^T F x1)^2.
- * Scaling the homogeneous points x1 -> k1*(x1, y1, 1), x2 -> k2*(x2, y2, 1) with
- * k = 1/(s*sqrt(thr)) turns both weights into 1, so the test becomes
- *   |a|^2 + |b|^2 - r^2 > 0,  a = (G X1)_{0,1}, b = (G^T X2)_{0,1}, r = X2^T G X1
- * on pre-scaled coordinates X = k * x_normalised and the per-hypothesis matrix G = F with the
- * homogeneous column / row folded in (sampson_prep).  This op sequence is the spec. */
-static inline void sampson_scales(float s1, float s2, float thr, float* k1, float* k2) {
-    const float rt = sqrtf(thr);
-    *k1 = 1.0f / (s1 * rt);
-    *k2 = 1.0f / (s2 * rt);
-}
-
-static inline void sampson_prep(const float F[9], float k1, float k2, float G[9]) {
-    for (int i = 0; i < 9; ++i) G[i] = F[i];
-    G[2] = F[2] * k1;
-    G[5] = F[5] * k1;
-    G[6] = F[6] * k2;
-    G[7] = F[7] * k2;
-    G[8] = (F[8] * k1) * k2;
-}
-
-static inline int sampson_inlier(const float G[9], float x1, float y1, float x2, float y2) {
-    float a0 = fmaf(G[0], x1, fmaf(G[1], y1, G[2]));
-    float a1 = fmaf(G[3], x1, fmaf(G[4], y1, G[5]));
-    float c2 = fmaf(G[6], x1, fmaf(G[7], y1, G[8]));
-    float b0 = fmaf(G[0], x2, fmaf(G[3], y2, G[6]));
-    float b1 = fmaf(G[1], x2, fmaf(G[4], y2, G[7]));
-    float r = fmaf(x2, a0, fmaf(y2, a1, c2));
-    float den = fmaf(a0, a0, fmaf(a1, a1, fmaf(b0, b0, b1 * b1)));
-    float e = fmaf(-r, r, den);
-    return e > 0.0f;
-}
-
-/* scoring coordinates: X = k * x_normalised, planar per side */
-static void sampson_coords(const float* n, int M, float k, float* X) {
-    for (int m = 0; m < M; ++m) {
-        X[2 * m] = n[2 * m] * k;
-        X[2 * m + 1] = n[2 * m + 1] * k;
-    }
-}
-
-/*
- * RANSAC over one pair.  xy1/xy2: [M][2] pixel coordinates of the tentative matches (in match
- * order).  Returns the best inlier count (-1 if M < 8); writes best hypothesis id, the normalised
- * F (row-major) and the normalisation (cx1, cy1, s1, cx2, cy2, s2), and the inlier mask.
- */
-int oracle_ransac_f(const float* xy1, const float* xy2, int M, int H, uint64_t seed,
-                    uint32_t pa, uint32_t pb, float thr, int32_t* best_h, float Fout[9],
-                    float norm[6], uint8_t* mask) {
-    if (M < 8) {
-        *best_h = -1;
-        for (int i = 0; i < 9; ++i) Fout[i] = 0.0f;
-        for (int i = 0; i < 6; ++i) norm[i] = 0.0f;
-        for (int m = 0; m < M; ++m) mask[m] = 0;
-        return -1;
-    }
-    float* n1 = (float*)malloc(sizeof(float) * 2 * M);
-    float* n2 = (float*)malloc(sizeof(float) * 2 * M);
-    float cx1, cy1, s1, cx2, cy2, s2;
-    oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
-    oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
-    float k1, k2;
-    sampson_scales(s1, s2, thr, &k1, &k2);
-    float* X1 = (float*)malloc(sizeof(float) * 2 * M);
-    float* X2 = (float*)malloc(sizeof(float) * 2 * M);
-    sampson_coords(n1, M, k1, X1);
-    sampson_coords(n2, M, k2, X2);
-    int bestc = -2, besth = -1;
-    for (int h = 0; h < H; ++h) {
-        int32_t idx[8];
-        oracle_sample8(seed, pa, pb, (uint32_t)h, M, idx);
-        float p1[16], p2[16], F[9];
-        for (int k = 0; k < 8; ++k) {
-            p1[2 * k] = n1[2 * idx[k]]; p1[2 * k + 1] = n1[2 * idx[k] + 1];
-            p2[2 * k] = n2[2 * idx[k]]; p2[2 * k + 1] = n2[2 * idx[k] + 1];
-        }
-        int cnt = -1;
-        if (oracle_fit_f8(p1, p2, F) == 0) {
-            float G[9];
-            sampson_prep(F, k1, k2, G);
-            cnt = 0;
-            for (int m = 0; m < M; ++m)
-                cnt += sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m], X2[2 * m + 1]);
-        }
-        if (cnt > bestc) { bestc = cnt; besth = h; }
-    }
-    int32_t idx[8];
-    oracle_sample8(seed, pa, pb, (uint32_t)besth, M, idx);
-    float p1[16], p2[16], F[9];
-    for (int k = 0; k < 8; ++k) {
-        p1[2 * k] = n1[2 * idx[k]]; p1[2 * k + 1] = n1[2 * idx[k] + 1];
-        p2[2 * k] = n2[2 * idx[k]]; p2[2 * k + 1] = n2[2 * idx[k] + 1];
-    }
-    int ok = oracle_fit_f8(p1, p2, F);
-    float G[9];
-    sampson_prep(F, k1, k2, G);
-    int cnt = 0;
-    for (int m = 0; m < M; ++m) {
-        int in = (ok == 0) ? sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m],
-                                            X2[2 * m + 1]) : 0;
-        mask[m] = (uint8_t)in;
-        cnt += in;
-    }
-    for (int i = 0; i < 9; ++i) Fout[i] = (ok == 0) ? F[i] : 0.0f;
-    norm[0] = cx1; norm[1] = cy1; norm[2] = s1; norm[3] = cx2; norm[4] = cy2; norm[5] = s2;
-    *best_h = besth;
-    free(n1); free(n2); free(X1); free(X2);
-    return cnt;
-}
-
-/* Inlier count of every hypothesis (for fine-grained parity tests). */
-void oracle_ransac_counts(const float* xy1, const float* xy2, int M, int H, uint64_t seed,
-                          uint32_t pa, uint32_t pb, float thr, int32_t* counts) {
-    float* n1 = (float*)malloc(sizeof(float) * 2 * M);
-    float* n2 = (float*)malloc(sizeof(float) * 2 * M);
-    float cx1, cy1, s1, cx2, cy2, s2;
-    oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
-    oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
-    float k1, k2;
-    sampson_scales(s1, s2, thr, &k1, &k2);
-    float* X1 = (float*)malloc(sizeof(float) * 2 * M);
-    float* X2 = (float*)malloc(sizeof(float) * 2 * M);
-    sampson_coords(n1, M, k1, X1);
-    sampson_coords(n2, M, k2, X2);
-    for (int h = 0; h < H; ++h) {
-        int32_t idx[8];
-        oracle_sample8(seed, pa, pb, (uint32_t)h, M, idx);
-        float p1[16], p2[16], F[9];
-        for (int k = 0; k < 8; ++k) {
-            p1[2 * k] = n1[2 * idx[k]]; p1[2 * k + 1] = n1[2 * idx[k] + 1];
-            p2[2 * k] = n2[2 * idx[k]]; p2[2 * k + 1] = n2[2 * idx[k] + 1];
-        }
-        int cnt = -1;
-        if (oracle_fit_f8(p1, p2, F) == 0) {
-            float G[9];
-            sampson_prep(F, k1, k2, G);
-            cnt = 0;
-            for (int m = 0; m < M; ++m)
-                cnt += sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m], X2[2 * m + 1]);
-        }
-        counts[h] = cnt;
-    }
-    free(n1); free(n2); free(X1); free(X2);
-}
-
-/* Per-hypothesis decisions of the f32 spec (tests/perf/ransac_fp64_study.py compares them with an
- * fp64 evaluation of the same samples): masks [H][M] (1 = inlier; all 0 for a degenerate fit),
- * idx [H][8] the sample, ok [H] (1 = fit succeeded). */
-void oracle_ransac_masks(const float* xy1, const float* xy2, int M, int H, uint64_t seed,
-                         uint32_t pa, uint32_t pb, float thr, uint8_t* masks, int32_t* idx,
-                         int32_t* ok) {
-    float* n1 = (float*)malloc(sizeof(float) * 2 * M);
-    float* n2 = (float*)malloc(sizeof(float) * 2 * M);
-    float cx1, cy1, s1, cx2, cy2, s2;
-    oracle_normalize(xy1, M, n1, &cx1, &cy1, &s1);
-    oracle_normalize(xy2, M, n2, &cx2, &cy2, &s2);
-    float k1, k2;
-    sampson_scales(s1, s2, thr, &k1, &k2);
-    float* X1 = (float*)malloc(sizeof(float) * 2 * M);
-    float* X2 = (float*)malloc(sizeof(float) * 2 * M);
-    sampson_coords(n1, M, k1, X1);
-    sampson_coords(n2, M, k2, X2);
-    for (int h = 0; h < H; ++h) {
-        int32_t* id = idx + (size_t)h * 8;
-        oracle_sample8(seed, pa, pb, (uint32_t)h, M, id);
-        float p1[16], p2[16], F[9];
-        for (int k = 0; k < 8; ++k) {
-            p1[2 * k] = n1[2 * id[k]]; p1[2 * k + 1] = n1[2 * id[k] + 1];
-            p2[2 * k] = n2[2 * id[k]]; p2[2 * k + 1] = n2[2 * id[k] + 1];
-        }
-        uint8_t* mk = masks + (size_t)h * M;
-        ok[h] = oracle_fit_f8(p1, p2, F) == 0;
-        if (ok[h]) {
-            float G[9];
-            sampson_prep(F, k1, k2, G);
-            for (int m = 0; m < M; ++m)
-                mk[m] = (uint8_t)sampson_inlier(G, X1[2 * m], X1[2 * m + 1], X2[2 * m], X2[2 * m + 1]);
-        } else {
-            memset(mk, 0, (size_t)M);
-        }
-    }
-    free(n1); free(n2); free(X1); free(X2);
-}
-
-/* ------------------------------------------------------------------------------------------ */
-/* Batched match + verify over a pair list (the CPU baseline bench.py times; OpenMP over pairs). */
-/* ------------------------------------------------------------------------------------------ */
-/* desc [n_img][K][D], kps [n_img][K][2]; pairs [P][2].  Per pair: L2 + mutual cross-check + ratio,
- * then RANSAC on the tentative matches.  Writes n_match[P], n_inl[P]; returns the number of
- * verified matches (sum of inlier counts over pairs with n_inl >= min_inl). */
-long long oracle_match_verify_batch(const uint8_t* desc, const float* kps, int n_img, int K,
-                                    int D, const int32_t* pairs, int P, int ratio_num,
-                                    int ratio_den, int64_t max_dist, int H, uint64_t seed,
-                                    float thr, int min_inl, int32_t* n_match, int32_t* n_inl,
-                                    int32_t* out_match, uint8_t* out_mask, int32_t* out_best_h,
-                                    int32_t* out_dist, float* out_F) {
-    /* Per pair: K1 (mutual cross check + ratio, code/feature_matching.py:48-58 restated) then K2.
-     * Optional outputs (NULL = not wanted): out_match [P][K][2] (queryIdx, trainIdx) of the
-     * tentative matches, out_mask [P][K] their inlier mask, out_best_h [P] the winning
-     * hypothesis, out_dist [P][K] the matches' d^2, out_F [P][9] the winner's F (normalised
- * coordinates) -- the full per-pair result bench.py / the tests compare the GPU's against. */
-    long long total = 0;
-    (void)n_img;
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
-    for (int p = 0; p < P; ++p) {
-        int a = pairs[2 * p], b = pairs[2 * p + 1];
-        int32_t* q = (int32_t*)malloc(sizeof(int32_t) * K);
-        int32_t* t = (int32_t*)malloc(sizeof(int32_t) * K);
-        int64_t* d = (int64_t*)malloc(sizeof(int64_t) * K);
-        float* x1 = (float*)malloc(sizeof(float) * 2 * K);
-        float* x2 = (float*)malloc(sizeof(float) * 2 * K);
-        uint8_t* mask = (uint8_t*)calloc((size_t)K + 1, 1);
-        int M = oracle_match(desc + (size_t)a * K * D, K, desc + (size_t)b * K * D, K, D, 0,
-                             SFM_XC_MUTUAL, ratio_num, ratio_den, max_dist, q, t, d);
-        for (int m = 0; m < M; ++m) {
-            x1[2 * m] = kps[((size_t)a * K + q[m]) * 2];
-            x1[2 * m + 1] = kps[((size_t)a * K + q[m]) * 2 + 1];
-            x2[2 * m] = kps[((size_t)b * K + t[m]) * 2];
-            x2[2 * m + 1] = kps[((size_t)b * K + t[m]) * 2 + 1];
-        }
-        int32_t bh = -1;
-        float F[9], nrm[6];
-        int c = oracle_ransac_f(x1, x2, M, H, seed, (uint32_t)a, (uint32_t)b, thr, &bh, F, nrm,
-                                mask);
-        n_match[p] = M;
-        n_inl[p] = c < 0 ? 0 : c;
-        if (c >= min_inl) total += c;
-        if (out_match) {
-            int32_t* o = out_match + (size_t)p * K * 2;
-            for (int m = 0; m < M; ++m) { o[2 * m] = q[m]; o[2 * m + 1] = t[m]; }
-        }
-        if (out_mask) memcpy(out_mask + (size_t)p * K, mask, (size_t)M);
-        if (out_best_h) out_best_h[p] = bh;
-        if (out_dist)
-            for (int m = 0; m < M; ++m) out_dist[(size_t)p * K + m] = (int32_t)d[m];
-        if (out_F) memcpy(out_F + (size_t)p * 9, F, sizeof(F));
-        free(q); free(t); free(d); free(x1); free(x2); free(mask);
-    }
-    return total;
-}
+/* fp64 mode (sfm_ransac_f_batch_f64): the same spec in double, names *_f64 */
+#define R double
+#define NAME(x) x##_f64
+#define FMA fma
+#define SQRT sqrt
+#define FABS fabs
+#define FMAX fmax
+#define FREXP frexp
+#define LDEXP ldexp
+#include "sfm_oracle_ransac.inc"
+#undef R
+#undef NAME
+#undef FMA
+#undef SQRT
+#undef FABS
+#undef FMAX
+#undef FREXP
+#undef LDEXP
 
 /* Thread control for the timed CPU baseline (bench.py reports the count it used). */
 #ifdef _OPENMP

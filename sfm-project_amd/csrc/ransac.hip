@@ -48,10 +48,33 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+// Scalar-type helpers: the f32 spec (default) and its fp64 mode (sfm_ransac_f_batch_f64) run the
+// same op sequence; these pick the fmaf / fma families (oracle/sfm_oracle_ransac.inc).
+__device__ __forceinline__ float fmaT(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double fmaT(double a, double b, double c) { return fma(a, b, c); }
+__device__ __forceinline__ float sqrtT(float a) { return sqrtf(a); }
+__device__ __forceinline__ double sqrtT(double a) { return sqrt(a); }
+__device__ __forceinline__ float fabsT(float a) { return fabsf(a); }
+__device__ __forceinline__ double fabsT(double a) { return fabs(a); }
+__device__ __forceinline__ float fmaxT(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ double fmaxT(double a, double b) { return fmax(a, b); }
+__device__ __forceinline__ float frexpT(float a, int* e) { return frexpf(a, e); }
+__device__ __forceinline__ double frexpT(double a, int* e) { return frexp(a, e); }
+__device__ __forceinline__ float ldexpT(float a, int e) { return ldexpf(a, e); }
+__device__ __forceinline__ double ldexpT(double a, int e) { return ldexp(a, e); }
+template <typename T> struct V4 { T x, y, z, w; };
+template <typename T> struct alignas(2 * sizeof(T)) V2 { T x, y; };
+// the preview count rides in a record slot of the scalar type (its bit pattern)
+__device__ __forceinline__ float pc_bits(int pc, float) { return __int_as_float(pc); }
+__device__ __forceinline__ double pc_bits(int pc, double) { return __longlong_as_double((long long)pc); }
+__device__ __forceinline__ int pc_of(float v) { return __float_as_int(v); }
+__device__ __forceinline__ int pc_of(double v) { return (int)__double_as_longlong(v); }
+
 // pl[i] through a 32-bit byte offset (the plane block of a pair is < 4 GB): the load takes the
 // pair's uniform base in SGPRs and no per-lane 64-bit address arithmetic
-__device__ __forceinline__ float ldf(const float* __restrict__ pl, int i) {
-    return *(const float*)((const char*)pl + ((uint32_t)i << 2));
+template <typename T>
+__device__ __forceinline__ T ldT(const T* __restrict__ pl, int i) {
+    return *(const T*)((const char*)pl + (uint32_t)i * (uint32_t)sizeof(T));
 }
 
 __device__ __forceinline__ void sample8(uint64_t seed, uint32_t pa, uint32_t pb, uint32_t h, int M,
@@ -71,118 +94,119 @@ __device__ __forceinline__ void sample8(uint64_t seed, uint32_t pa, uint32_t pb,
 }
 
 // Mirrors oracle_fit_f8.  Returns false if degenerate.  V[k][r] (r > k) lives in Mt[r][k].
-__device__ __forceinline__ bool fit_f8(const float4 s[8], float F[9]) {
-    float Mt[9][8];
+template <typename T>
+__device__ __forceinline__ bool fit_f8(const V4<T> s[8], T F[9]) {
+    T Mt[9][8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const float x1 = s[k].x, y1 = s[k].y, x2 = s[k].z, y2 = s[k].w;
+        const T x1 = s[k].x, y1 = s[k].y, x2 = s[k].z, y2 = s[k].w;
         Mt[0][k] = x2 * x1; Mt[1][k] = x2 * y1; Mt[2][k] = x2;
         Mt[3][k] = y2 * x1; Mt[4][k] = y2 * y1; Mt[5][k] = y2;
-        Mt[6][k] = x1;      Mt[7][k] = y1;      Mt[8][k] = 1.0f;
+        Mt[6][k] = x1;      Mt[7][k] = y1;      Mt[8][k] = T(1.0);
     }
-    float vkk[8], beta[8];
+    T vkk[8], beta[8];
     bool ok = true;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        float nrm2 = 0.0f;
+        T nrm2 = T(0.0);
 #pragma unroll
-        for (int r = k; r < 9; ++r) nrm2 = fmaf(Mt[r][k], Mt[r][k], nrm2);
-        ok = ok && (nrm2 > 0.0f);
-        const float nrm = sqrtf(nrm2);
-        const float alpha = (Mt[k][k] > 0.0f) ? -nrm : nrm;
+        for (int r = k; r < 9; ++r) nrm2 = fmaT(Mt[r][k], Mt[r][k], nrm2);
+        ok = ok && (nrm2 > T(0.0));
+        const T nrm = sqrtT(nrm2);
+        const T alpha = (Mt[k][k] > T(0.0)) ? -nrm : nrm;
         vkk[k] = Mt[k][k] - alpha;
-        float vn2 = fmaf(vkk[k], vkk[k], 0.0f);
+        T vn2 = fmaT(vkk[k], vkk[k], T(0.0));
 #pragma unroll
-        for (int r = k + 1; r < 9; ++r) vn2 = fmaf(Mt[r][k], Mt[r][k], vn2);
-        ok = ok && (vn2 > 0.0f);
-        beta[k] = 2.0f / vn2;
+        for (int r = k + 1; r < 9; ++r) vn2 = fmaT(Mt[r][k], Mt[r][k], vn2);
+        ok = ok && (vn2 > T(0.0));
+        beta[k] = T(2.0) / vn2;
         Mt[k][k] = alpha;
 #pragma unroll
         for (int c = k + 1; c < 8; ++c) {
-            float dot = fmaf(vkk[k], Mt[k][c], 0.0f);
+            T dot = fmaT(vkk[k], Mt[k][c], T(0.0));
 #pragma unroll
-            for (int r = k + 1; r < 9; ++r) dot = fmaf(Mt[r][k], Mt[r][c], dot);
-            const float f = beta[k] * dot;
-            Mt[k][c] = fmaf(-f, vkk[k], Mt[k][c]);
+            for (int r = k + 1; r < 9; ++r) dot = fmaT(Mt[r][k], Mt[r][c], dot);
+            const T f = beta[k] * dot;
+            Mt[k][c] = fmaT(-f, vkk[k], Mt[k][c]);
 #pragma unroll
-            for (int r = k + 1; r < 9; ++r) Mt[r][c] = fmaf(-f, Mt[r][k], Mt[r][c]);
+            for (int r = k + 1; r < 9; ++r) Mt[r][c] = fmaT(-f, Mt[r][k], Mt[r][c]);
         }
     }
-    float z[9] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 1.0f};
+    T z[9] = {T(0.0), T(0.0), T(0.0), T(0.0), T(0.0), T(0.0), T(0.0), T(0.0), T(1.0)};
 #pragma unroll
     for (int k = 7; k >= 0; --k) {
-        float dot = fmaf(vkk[k], z[k], 0.0f);
+        T dot = fmaT(vkk[k], z[k], T(0.0));
 #pragma unroll
-        for (int r = k + 1; r < 9; ++r) dot = fmaf(Mt[r][k], z[r], dot);
-        const float f = beta[k] * dot;
-        z[k] = fmaf(-f, vkk[k], z[k]);
+        for (int r = k + 1; r < 9; ++r) dot = fmaT(Mt[r][k], z[r], dot);
+        const T f = beta[k] * dot;
+        z[k] = fmaT(-f, vkk[k], z[k]);
 #pragma unroll
-        for (int r = k + 1; r < 9; ++r) z[r] = fmaf(-f, Mt[r][k], z[r]);
+        for (int r = k + 1; r < 9; ++r) z[r] = fmaT(-f, Mt[r][k], z[r]);
     }
     // rank 2 (oracle_fit_f8): smallest eigen-direction of G = F^T F by power iteration on adj(G)
-    float G[3][3];
+    T G[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            float g = 0.0f;
+            T g = T(0.0);
 #pragma unroll
-            for (int r = 0; r < 3; ++r) g = fmaf(z[3 * r + i], z[3 * r + j], g);
+            for (int r = 0; r < 3; ++r) g = fmaT(z[3 * r + i], z[3 * r + j], g);
             G[i][j] = g;
         }
-    float A[3][3];
-    A[0][0] = fmaf(G[1][1], G[2][2], -(G[1][2] * G[1][2]));
-    A[1][1] = fmaf(G[0][0], G[2][2], -(G[0][2] * G[0][2]));
-    A[2][2] = fmaf(G[0][0], G[1][1], -(G[0][1] * G[0][1]));
-    A[0][1] = A[1][0] = fmaf(G[0][2], G[1][2], -(G[0][1] * G[2][2]));
-    A[0][2] = A[2][0] = fmaf(G[0][1], G[1][2], -(G[0][2] * G[1][1]));
-    A[1][2] = A[2][1] = fmaf(G[0][1], G[0][2], -(G[0][0] * G[1][2]));
+    T A[3][3];
+    A[0][0] = fmaT(G[1][1], G[2][2], -(G[1][2] * G[1][2]));
+    A[1][1] = fmaT(G[0][0], G[2][2], -(G[0][2] * G[0][2]));
+    A[2][2] = fmaT(G[0][0], G[1][1], -(G[0][1] * G[0][1]));
+    A[0][1] = A[1][0] = fmaT(G[0][2], G[1][2], -(G[0][1] * G[2][2]));
+    A[0][2] = A[2][0] = fmaT(G[0][1], G[1][2], -(G[0][2] * G[1][1]));
+    A[1][2] = A[2][1] = fmaT(G[0][1], G[0][2], -(G[0][0] * G[1][2]));
     // rescaled squarings of adj(G) (oracle square3_sym): the max-diagonal column of
     // adj(G)^(2^RANK2_SQUARINGS) is the removed direction to (s3/s2)^512
-    float a00 = A[0][0], a11 = A[1][1], a22 = A[2][2], a01 = A[0][1], a02 = A[0][2], a12 = A[1][2];
+    T a00 = A[0][0], a11 = A[1][1], a22 = A[2][2], a01 = A[0][1], a02 = A[0][2], a12 = A[1][2];
 #pragma unroll
     for (int it = 0; it < RANK2_SQUARINGS; ++it) {
-        const float m = fmaxf(fmaxf(fmaxf(fabsf(a00), fabsf(a11)), fmaxf(fabsf(a22), fabsf(a01))),
-                              fmaxf(fabsf(a02), fabsf(a12)));
-        if (m > 0.0f && isfinite(m)) {
+        const T m = fmaxT(fmaxT(fmaxT(fabsT(a00), fabsT(a11)), fmaxT(fabsT(a22), fabsT(a01))),
+                              fmaxT(fabsT(a02), fabsT(a12)));
+        if (m > T(0.0) && isfinite(m)) {
             int e;
-            frexpf(m, &e);
-            a00 = ldexpf(a00, -e); a11 = ldexpf(a11, -e); a22 = ldexpf(a22, -e);
-            a01 = ldexpf(a01, -e); a02 = ldexpf(a02, -e); a12 = ldexpf(a12, -e);
+            frexpT(m, &e);
+            a00 = ldexpT(a00, -e); a11 = ldexpT(a11, -e); a22 = ldexpT(a22, -e);
+            a01 = ldexpT(a01, -e); a02 = ldexpT(a02, -e); a12 = ldexpT(a12, -e);
         }
-        const float b00 = fmaf(a02, a02, fmaf(a01, a01, a00 * a00));
-        const float b11 = fmaf(a12, a12, fmaf(a11, a11, a01 * a01));
-        const float b22 = fmaf(a22, a22, fmaf(a12, a12, a02 * a02));
-        const float b01 = fmaf(a02, a12, fmaf(a01, a11, a00 * a01));
-        const float b02 = fmaf(a02, a22, fmaf(a01, a12, a00 * a02));
-        const float b12 = fmaf(a12, a22, fmaf(a11, a12, a01 * a02));
+        const T b00 = fmaT(a02, a02, fmaT(a01, a01, a00 * a00));
+        const T b11 = fmaT(a12, a12, fmaT(a11, a11, a01 * a01));
+        const T b22 = fmaT(a22, a22, fmaT(a12, a12, a02 * a02));
+        const T b01 = fmaT(a02, a12, fmaT(a01, a11, a00 * a01));
+        const T b02 = fmaT(a02, a22, fmaT(a01, a12, a00 * a02));
+        const T b12 = fmaT(a12, a22, fmaT(a11, a12, a01 * a02));
         a00 = b00; a11 = b11; a22 = b22; a01 = b01; a02 = b02; a12 = b12;
     }
     int kk = 0;
-    float amax = a00;
+    T amax = a00;
     if (a11 > amax) { kk = 1; amax = a11; }
     if (a22 > amax) kk = 2;
-    float v0 = kk == 0 ? a00 : (kk == 1 ? a01 : a02);
-    float v1 = kk == 0 ? a01 : (kk == 1 ? a11 : a12);
-    float v2 = kk == 0 ? a02 : (kk == 1 ? a12 : a22);
+    T v0 = kk == 0 ? a00 : (kk == 1 ? a01 : a02);
+    T v1 = kk == 0 ? a01 : (kk == 1 ? a11 : a12);
+    T v2 = kk == 0 ? a02 : (kk == 1 ? a12 : a22);
     {   // exact power-of-two rescale by the exponent of max|v| (oracle rescale3_pow2)
-        const float m = fmaxf(fabsf(v0), fmaxf(fabsf(v1), fabsf(v2)));
-        if (m > 0.0f && isfinite(m)) {
+        const T m = fmaxT(fabsT(v0), fmaxT(fabsT(v1), fabsT(v2)));
+        if (m > T(0.0) && isfinite(m)) {
             int e;
-            frexpf(m, &e);
-            v0 = ldexpf(v0, -e); v1 = ldexpf(v1, -e); v2 = ldexpf(v2, -e);
+            frexpT(m, &e);
+            v0 = ldexpT(v0, -e); v1 = ldexpT(v1, -e); v2 = ldexpT(v2, -e);
         }
     }
-    const float n2 = fmaf(v2, v2, fmaf(v1, v1, v0 * v0));
-    if (n2 > 0.0f) {
-        const float inv = 1.0f / sqrtf(n2);
+    const T n2 = fmaT(v2, v2, fmaT(v1, v1, v0 * v0));
+    if (n2 > T(0.0)) {
+        const T inv = T(1.0) / sqrtT(n2);
         v0 = v0 * inv; v1 = v1 * inv; v2 = v2 * inv;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-            const float w = fmaf(z[3 * r + 2], v2, fmaf(z[3 * r + 1], v1, z[3 * r] * v0));
-            F[3 * r + 0] = fmaf(-w, v0, z[3 * r + 0]);
-            F[3 * r + 1] = fmaf(-w, v1, z[3 * r + 1]);
-            F[3 * r + 2] = fmaf(-w, v2, z[3 * r + 2]);
+            const T w = fmaT(z[3 * r + 2], v2, fmaT(z[3 * r + 1], v1, z[3 * r] * v0));
+            F[3 * r + 0] = fmaT(-w, v0, z[3 * r + 0]);
+            F[3 * r + 1] = fmaT(-w, v1, z[3 * r + 1]);
+            F[3 * r + 2] = fmaT(-w, v2, z[3 * r + 2]);
         }
     } else {
 #pragma unroll
@@ -193,7 +217,8 @@ __device__ __forceinline__ bool fit_f8(const float4 s[8], float F[9]) {
 
 // Sampson inlier test, oracle/sfm_oracle.c sampson_prep / sampson_inlier: G = F with the
 // homogeneous scales folded in, coordinates pre-scaled; inlier iff |a|^2 + |b|^2 - r^2 > 0.
-__device__ __forceinline__ void sampson_prep(const float F[9], float k1, float k2, float G[9]) {
+template <typename T>
+__device__ __forceinline__ void sampson_prep(const T F[9], T k1, T k2, T G[9]) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) G[i] = F[i];
     G[2] = F[2] * k1;
@@ -203,29 +228,30 @@ __device__ __forceinline__ void sampson_prep(const float F[9], float k1, float k
     G[8] = (F[8] * k1) * k2;
 }
 
-__device__ __forceinline__ int sampson_inlier(const float G[9], float x1, float y1, float x2,
-                                              float y2) {
-    const float a0 = fmaf(G[0], x1, fmaf(G[1], y1, G[2]));
-    const float a1 = fmaf(G[3], x1, fmaf(G[4], y1, G[5]));
-    const float c2 = fmaf(G[6], x1, fmaf(G[7], y1, G[8]));
-    const float b0 = fmaf(G[0], x2, fmaf(G[3], y2, G[6]));
-    const float b1 = fmaf(G[1], x2, fmaf(G[4], y2, G[7]));
-    const float r = fmaf(x2, a0, fmaf(y2, a1, c2));
-    const float den = fmaf(a0, a0, fmaf(a1, a1, fmaf(b0, b0, b1 * b1)));
-    const float e = fmaf(-r, r, den);
-    return e > 0.0f ? 1 : 0;
+template <typename T>
+__device__ __forceinline__ int sampson_inlier(const T G[9], T x1, T y1, T x2, T y2) {
+    const T a0 = fmaT(G[0], x1, fmaT(G[1], y1, G[2]));
+    const T a1 = fmaT(G[3], x1, fmaT(G[4], y1, G[5]));
+    const T c2 = fmaT(G[6], x1, fmaT(G[7], y1, G[8]));
+    const T b0 = fmaT(G[0], x2, fmaT(G[3], y2, G[6]));
+    const T b1 = fmaT(G[1], x2, fmaT(G[4], y2, G[7]));
+    const T r = fmaT(x2, a0, fmaT(y2, a1, c2));
+    const T den = fmaT(a0, a0, fmaT(a1, a1, fmaT(b0, b0, b1 * b1)));
+    const T e = fmaT(-r, r, den);
+    return e > T(0.0) ? 1 : 0;
 }
 
 // per-pair scales of the scoring coordinates (oracle sampson_scales)
-__device__ __forceinline__ void sampson_scales(float s1, float s2, float thr, float& k1,
-                                               float& k2) {
-    const float rt = sqrtf(thr);
-    k1 = 1.0f / (s1 * rt);
-    k2 = 1.0f / (s2 * rt);
+template <typename T>
+__device__ __forceinline__ void sampson_scales(T s1, T s2, T thr, T& k1, T& k2) {
+    const T rt = sqrtT(thr);
+    k1 = T(1.0) / (s1 * rt);
+    k2 = T(1.0) / (s2 * rt);
 }
 
 // fixed-order sum: lane l accumulates m = l, l+64, ... then a halving tree (oracle fixed_sum)
-__device__ __forceinline__ float wave_fixed_sum(float partial) {
+template <typename T>
+__device__ __forceinline__ T wave_fixed_sum(T partial) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) partial = partial + __shfl_down(partial, off, 64);
     return __shfl(partial, 0, 64);
@@ -234,25 +260,26 @@ __device__ __forceinline__ float wave_fixed_sum(float partial) {
 // plane stride per pair: 8 planes of k_pl floats (k_pl multiple of 16: 64-B aligned planes)
 __host__ __device__ __forceinline__ int plane_len(int k_max) { return (k_max + 15) & ~15; }
 
+template <typename T>
 __global__ __launch_bounds__(64) void ransac_prep_kernel(
-    const float* __restrict__ kps, int k_max, const int32_t* __restrict__ pairs,
-    const int32_t* __restrict__ match_count, const int32_t* __restrict__ matches, float thr,
-    float* __restrict__ planes, float* __restrict__ out_norm) {
+    const T* __restrict__ kps, int k_max, const int32_t* __restrict__ pairs,
+    const int32_t* __restrict__ match_count, const int32_t* __restrict__ matches, T thr,
+    T* __restrict__ planes, T* __restrict__ out_norm) {
     const int p = blockIdx.x, l = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int M = match_count[p];
     const int32_t* mt = matches + (size_t)p * k_max * 2;
     const int kp = plane_len(k_max);
-    float* X1 = planes + (size_t)p * 8 * kp;  // normalised x1 | y1 | x2 | y2
-    float* Y1 = X1 + kp;
-    float* X2 = Y1 + kp;
-    float* Y2 = X2 + kp;
-    float* S = Y2 + kp;                        // scaled X1 | Y1 | X2 | Y2
+    T* X1 = planes + (size_t)p * 8 * kp;  // normalised x1 | y1 | x2 | y2
+    T* Y1 = X1 + kp;
+    T* X2 = Y1 + kp;
+    T* Y2 = X2 + kp;
+    T* S = Y2 + kp;                        // scaled X1 | Y1 | X2 | Y2
     if (M < 8) {
-        if (l < 6) out_norm[p * 6 + l] = 0.0f;
+        if (l < 6) out_norm[p * 6 + l] = T(0.0);
         return;
     }
-    float sx1 = 0.f, sy1 = 0.f, sx2 = 0.f, sy2 = 0.f;
+    T sx1 = 0.f, sy1 = 0.f, sx2 = 0.f, sy2 = 0.f;
     // four matches per lane in flight (index loads, then the coordinate gathers): one wave per
     // pair is latency-bound; the sums still accumulate in m order
     for (int m0 = l; m0 < M; m0 += 256) {
@@ -262,11 +289,11 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
             const int m = m0 + 64 * t;
             id[t] = m < M ? *(const int2*)(mt + 2 * m) : make_int2(0, 0);
         }
-        float2 u[4], v[4];
+        V2<T> u[4], v[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            u[t] = *(const float2*)(kps + ((size_t)a * k_max + id[t].x) * 2);
-            v[t] = *(const float2*)(kps + ((size_t)b * k_max + id[t].y) * 2);
+            u[t] = *(const V2<T>*)(kps + ((size_t)a * k_max + id[t].x) * 2);
+            v[t] = *(const V2<T>*)(kps + ((size_t)b * k_max + id[t].y) * 2);
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -277,31 +304,31 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
             }
         }
     }
-    const float fM = (float)M;
-    const float mx1 = wave_fixed_sum(sx1) / fM, my1 = wave_fixed_sum(sy1) / fM;
-    const float mx2 = wave_fixed_sum(sx2) / fM, my2 = wave_fixed_sum(sy2) / fM;
-    float sd1 = 0.f, sd2 = 0.f;
+    const T fM = (T)M;
+    const T mx1 = wave_fixed_sum(sx1) / fM, my1 = wave_fixed_sum(sy1) / fM;
+    const T mx2 = wave_fixed_sum(sx2) / fM, my2 = wave_fixed_sum(sy2) / fM;
+    T sd1 = 0.f, sd2 = 0.f;
 #pragma unroll 4
     for (int m = l; m < M; m += 64) {
-        const float4 w = make_float4(X1[m], Y1[m], X2[m], Y2[m]);
-        float dx = w.x - mx1, dy = w.y - my1;
-        float q = dx * dx;
-        q = fmaf(dy, dy, q);
-        sd1 = sd1 + sqrtf(q);
+        const V4<T> w = {X1[m], Y1[m], X2[m], Y2[m]};
+        T dx = w.x - mx1, dy = w.y - my1;
+        T q = dx * dx;
+        q = fmaT(dy, dy, q);
+        sd1 = sd1 + sqrtT(q);
         dx = w.z - mx2; dy = w.w - my2;
         q = dx * dx;
-        q = fmaf(dy, dy, q);
-        sd2 = sd2 + sqrtf(q);
+        q = fmaT(dy, dy, q);
+        sd2 = sd2 + sqrtT(q);
     }
-    const float mean1 = wave_fixed_sum(sd1) / fM, mean2 = wave_fixed_sum(sd2) / fM;
-    const float s1 = (mean1 > 0.0f) ? (1.41421356237309515f / mean1) : 1.0f;
-    const float s2 = (mean2 > 0.0f) ? (1.41421356237309515f / mean2) : 1.0f;
-    float k1, k2;
+    const T mean1 = wave_fixed_sum(sd1) / fM, mean2 = wave_fixed_sum(sd2) / fM;
+    const T s1 = (mean1 > T(0.0)) ? (T(1.41421356237309515) / mean1) : T(1.0);
+    const T s2 = (mean2 > T(0.0)) ? (T(1.41421356237309515) / mean2) : T(1.0);
+    T k1, k2;
     sampson_scales(s1, s2, thr, k1, k2);
 #pragma unroll 4
     for (int m = l; m < M; m += 64) {
-        const float x1 = (X1[m] - mx1) * s1, y1 = (Y1[m] - my1) * s1;
-        const float x2 = (X2[m] - mx2) * s2, y2 = (Y2[m] - my2) * s2;
+        const T x1 = (X1[m] - mx1) * s1, y1 = (Y1[m] - my1) * s1;
+        const T x2 = (X2[m] - mx2) * s2, y2 = (Y2[m] - my2) * s2;
         X1[m] = x1; Y1[m] = y1; X2[m] = x2; Y2[m] = y2;
         S[m] = x1 * k1;
         S[kp + m] = y1 * k1;
@@ -309,12 +336,15 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
         S[3 * kp + m] = y2 * k2;
     }
     if (l == 0) {
-        float* o = out_norm + p * 6;
+        T* o = out_norm + p * 6;
         o[0] = mx1; o[1] = my1; o[2] = s1; o[3] = mx2; o[4] = my2; o[5] = s2;
     }
 }
 
 typedef const __attribute__((address_space(4))) float* cfloat_p;  // scalar (constant) loads
+typedef const __attribute__((address_space(4))) double* cdouble_p;
+template <typename T> struct CPtr { typedef cfloat_p type; };
+template <> struct CPtr<double> { typedef cdouble_p type; };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -381,11 +411,11 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
     const uint32_t h = blockIdx.y * 256 + tid;
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
-    float4 smp[8];
+    V4<float> smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        smp[k] = make_float4(ldf(pl, idx[k]), ldf(pl, kp + idx[k]), ldf(pl, 2 * kp + idx[k]),
-                             ldf(pl, 3 * kp + idx[k]));
+        smp[k] = {ldT(pl, idx[k]), ldT(pl, kp + idx[k]), ldT(pl, 2 * kp + idx[k]),
+                  ldT(pl, 3 * kp + idx[k])};
     float F[9], G[9];
     const bool ok = fit_f8(smp, F);
     sampson_prep(F, k1, k2, G);
@@ -449,15 +479,16 @@ constexpr int HREC = 12;  // hypothesis record: G[9], preview count (int bits), 
 // counts inliers of G over matches [m, mend) into cnt; with PRUNE checks the published bound every
 // PRUNE_EVERY matches and returns false (wave-uniform) when no lane can still win.
 // `mstop` (if given) receives the match index where the wave stopped (mend when it finished).
-template <bool PRUNE, int C = CH>
-__device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[9], int m, int mend,
-                                              int M, int& cnt,
+// f32: two matches per packed op (sampson_inlier2); fp64: the scalar test per match.
+template <bool PRUNE, int C = CH, typename T = float>
+__device__ __forceinline__ bool score_matches(typename CPtr<T>::type S, int kp, const T G[9], int m,
+                                              int mend, int M, int& cnt,
                                               const unsigned long long* __restrict__ bestp,
                                               int* mstop = nullptr) {
     const int mc = m + ((mend - m) & ~(C - 1));
 #pragma unroll 1
     for (; m < mc; m += C) {
-        float x1[C], y1[C], x2[C], y2[C];
+        T x1[C], y1[C], x2[C], y2[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) {
             x1[j] = S[m + j];
@@ -465,10 +496,15 @@ __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[
             x2[j] = S[2 * kp + m + j];
             y2[j] = S[3 * kp + m + j];
         }
+        if constexpr (sizeof(T) == 4) {
 #pragma unroll
-        for (int j = 0; j < C; j += 2)
-            cnt += sampson_inlier2(G, f2{x1[j], x1[j + 1]}, f2{y1[j], y1[j + 1]},
-                                   f2{x2[j], x2[j + 1]}, f2{y2[j], y2[j + 1]});
+            for (int j = 0; j < C; j += 2)
+                cnt += sampson_inlier2(G, f2{x1[j], x1[j + 1]}, f2{y1[j], y1[j + 1]},
+                                       f2{x2[j], x2[j + 1]}, f2{y2[j], y2[j + 1]});
+        } else {
+#pragma unroll
+            for (int j = 0; j < C; ++j) cnt += sampson_inlier(G, x1[j], y1[j], x2[j], y2[j]);
+        }
         if (PRUNE && ((m + C) % PRUNE_EVERY) == 0) {
             const unsigned long long bk =
                 __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -490,53 +526,54 @@ __device__ __forceinline__ bool score_matches(cfloat_p S, int kp, const float G[
 #else
 #define RANSAC_FIT_ATTR
 #endif
+template <typename T>
 __global__ __launch_bounds__(256) RANSAC_FIT_ATTR void ransac_fit_kernel(
     int n_pairs, int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
-    const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
-    int n_hyp, int gp, float* __restrict__ hypG, int32_t* __restrict__ prev,
+    const T* __restrict__ planes, const T* __restrict__ norm, uint64_t seed, T thr,
+    int n_hyp, int gp, T* __restrict__ hypG, int32_t* __restrict__ prev,
     float* __restrict__ out_hyp_F = nullptr) {
     int p, hb;
     if (!xcd_pair_block(n_pairs, n_hyp >> 8, gp, p, hb)) return;
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int kp = plane_len(k_max);
-    const float* pl = planes + (size_t)p * 8 * kp;
-    const cfloat_p S = (cfloat_p)(pl + 4 * kp);
+    const T* pl = planes + (size_t)p * 8 * kp;
+    const typename CPtr<T>::type S = (typename CPtr<T>::type)(pl + 4 * kp);
     const uint32_t pa = (uint32_t)pairs[2 * p], pb = (uint32_t)pairs[2 * p + 1];
-    const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
-    float k1, k2;
+    const T s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
+    T k1, k2;
     sampson_scales(s1, s2, thr, k1, k2);
     const uint32_t h = hb * 256 + threadIdx.x;
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
-    float4 smp[8];
+    V4<T> smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        smp[k] = make_float4(ldf(pl, idx[k]), ldf(pl, kp + idx[k]), ldf(pl, 2 * kp + idx[k]),
-                             ldf(pl, 3 * kp + idx[k]));
-    float F[9], G[9];
+        smp[k] = {ldT(pl, idx[k]), ldT(pl, kp + idx[k]), ldT(pl, 2 * kp + idx[k]),
+                  ldT(pl, 3 * kp + idx[k])};
+    T F[9], G[9];
 #ifdef RANSAC_ABL_NOFIT  // ablation: no 8-point fit (timing only; results invalid)
     const bool ok = true;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) F[k] = smp[k & 7].x * (float)(k + 1) + smp[(k + 3) & 7].w;
+    for (int k = 0; k < 9; ++k) F[k] = smp[k & 7].x * (T)(k + 1) + smp[(k + 3) & 7].w;
 #else
     const bool ok = fit_f8(smp, F);
 #endif
     if (out_hyp_F) {  // diagnostic (sfm_ransac_counts): F of every hypothesis, normalised frame
         float* o = out_hyp_F + ((size_t)p * n_hyp + h) * 9;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) o[k] = F[k];
+        for (int k = 0; k < 9; ++k) o[k] = (float)F[k];
     }
     sampson_prep(F, k1, k2, G);
     int cnt = 0;
 #ifndef RANSAC_ABL_NOPREVIEW  // ablation: no preview (timing only; order degenerates)
-    score_matches<false, 8>(S, kp, G, 0, min(PV, M), M, cnt, nullptr);  // 8-match chunks: fewer VGPRs beside the fit
+    score_matches<false, 8, T>(S, kp, G, 0, min(PV, M), M, cnt, nullptr);  // 8-match chunks: fewer VGPRs beside the fit
 #endif
     const int pc = ok ? cnt : -1;
-    float4* rec = (float4*)(hypG + ((size_t)p * n_hyp + h) * HREC);
-    rec[0] = make_float4(G[0], G[1], G[2], G[3]);
-    rec[1] = make_float4(G[4], G[5], G[6], G[7]);
-    rec[2] = make_float4(G[8], __int_as_float(pc), 0.0f, 0.0f);
+    V4<T>* rec = (V4<T>*)(hypG + ((size_t)p * n_hyp + h) * HREC);
+    rec[0] = {G[0], G[1], G[2], G[3]};
+    rec[1] = {G[4], G[5], G[6], G[7]};
+    rec[2] = {G[8], pc_bits(pc, T(0)), T(0), T(0)};
     prev[(size_t)p * n_hyp + h] = pc;  // also dense, for the order kernel's coalesced read
 }
 
@@ -567,10 +604,10 @@ __global__ __launch_bounds__(256) void ransac_order_kernel(int n_hyp,
 }
 
 // COUNTS: no pruning; every hypothesis's count to out_counts[p][h] (sfm_ransac_counts)
-template <bool PRUNE, bool COUNTS = false>
+template <typename T, bool PRUNE, bool COUNTS = false>
 __global__ __launch_bounds__(256) void ransac_score_kernel(
     int n_pairs, int k_max, const int32_t* __restrict__ match_count,
-    const float* __restrict__ planes, int n_hyp, int gp, const float* __restrict__ hypG,
+    const T* __restrict__ planes, int n_hyp, int gp, const T* __restrict__ hypG,
     const uint16_t* __restrict__ order, unsigned long long* __restrict__ best, int32_t* __restrict__ out_counts = nullptr,
     uint32_t* __restrict__ exec_w = nullptr) {
     int p, hb;
@@ -578,17 +615,17 @@ __global__ __launch_bounds__(256) void ransac_score_kernel(
     const int M = match_count[p];
     if (M < 8) return;  // block-uniform
     const int kp = plane_len(k_max);
-    const cfloat_p S = (cfloat_p)(planes + (size_t)p * 8 * kp + 4 * kp);
+    const typename CPtr<T>::type S = (typename CPtr<T>::type)(planes + (size_t)p * 8 * kp + 4 * kp);
     const uint32_t h = order[(size_t)p * n_hyp + hb * 256 + threadIdx.x];
     // h is a permutation of the pair's hypotheses: one 48-byte record per hypothesis keeps the
     // lane's fetch to 1-2 cache lines (a [9][H] table scattered it over 9; PMC)
-    const float4* rec = (const float4*)(hypG + ((size_t)p * n_hyp + h) * HREC);
-    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
-    const float G[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
-    const int pc = __float_as_int(r2.y);
+    const V4<T>* rec = (const V4<T>*)(hypG + ((size_t)p * n_hyp + h) * HREC);
+    const V4<T> r0 = rec[0], r1 = rec[1], r2 = rec[2];
+    const T G[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+    const int pc = pc_of(r2.y);
     int cnt = max(pc, 0);
     int mstop = PV;
-    const bool alive = M <= PV || score_matches<PRUNE>(S, kp, G, PV, M, M, cnt, best + p, &mstop);
+    const bool alive = M <= PV || score_matches<PRUNE, CH, T>(S, kp, G, PV, M, M, cnt, best + p, &mstop);
     if (exec_w && (threadIdx.x & 63) == 0)  // sfm_ransac_stats: matches this wave scored past the preview
         exec_w[(size_t)p * (n_hyp >> 6) + hb * 4 + (threadIdx.x >> 6)] = (uint32_t)max(mstop - PV, 0);
     if (!alive) return;
@@ -606,37 +643,38 @@ __global__ __launch_bounds__(256) void ransac_score_kernel(
     if ((threadIdx.x & 63) == 0) atomicMax(&best[p], key);
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void ransac_final_kernel(
     int k_max, const int32_t* __restrict__ pairs, const int32_t* __restrict__ match_count,
-    const float* __restrict__ planes, const float* __restrict__ norm, uint64_t seed, float thr,
+    const T* __restrict__ planes, const T* __restrict__ norm, uint64_t seed, T thr,
     const unsigned long long* __restrict__ best, int32_t* __restrict__ out_inl_count,
-    int32_t* __restrict__ out_best_h, uint8_t* __restrict__ out_mask, float* __restrict__ out_F) {
+    int32_t* __restrict__ out_best_h, uint8_t* __restrict__ out_mask, T* __restrict__ out_F) {
     __shared__ int wsum[4];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int M = match_count[p];
     uint8_t* mask = out_mask + (size_t)p * k_max;
     if (M < 8) {
         for (int m = tid; m < M; m += 256) mask[m] = 0;
-        if (tid < 9) out_F[p * 9 + tid] = 0.0f;
+        if (tid < 9) out_F[p * 9 + tid] = T(0);
         if (tid == 0) { out_inl_count[p] = -1; out_best_h[p] = -1; }
         return;
     }
     const uint32_t pa = (uint32_t)pairs[2 * p], pb = (uint32_t)pairs[2 * p + 1];
     const uint32_t h = 0xFFFFFFFFu - (uint32_t)best[p];
     const int kp = plane_len(k_max);
-    const float* pl = planes + (size_t)p * 8 * kp;
-    const float* S = pl + 4 * kp;
-    const float s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
-    float k1, k2;
+    const T* pl = planes + (size_t)p * 8 * kp;
+    const T* S = pl + 4 * kp;
+    const T s1 = norm[p * 6 + 2], s2 = norm[p * 6 + 5];
+    T k1, k2;
     sampson_scales(s1, s2, thr, k1, k2);
     int idx[8];
     sample8(seed, pa, pb, h, M, idx);
-    float4 smp[8];
+    V4<T> smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        smp[k] = make_float4(ldf(pl, idx[k]), ldf(pl, kp + idx[k]), ldf(pl, 2 * kp + idx[k]),
-                             ldf(pl, 3 * kp + idx[k]));
-    float F[9], G[9];
+        smp[k] = {ldT(pl, idx[k]), ldT(pl, kp + idx[k]), ldT(pl, 2 * kp + idx[k]),
+                  ldT(pl, 3 * kp + idx[k])};
+    T F[9], G[9];
     const bool ok = fit_f8(smp, F);
     sampson_prep(F, k1, k2, G);
     int cnt = 0;
@@ -653,7 +691,7 @@ __global__ __launch_bounds__(256) void ransac_final_kernel(
         out_inl_count[p] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
         out_best_h[p] = (int)h;
     }
-    if (tid < 9) out_F[p * 9 + tid] = ok ? F[tid] : 0.0f;
+    if (tid < 9) out_F[p * 9 + tid] = ok ? F[tid] : T(0);
 }
 
 // Diagnostic (sfm_ransac_counts out_hyp_mask): every hypothesis's inlier decision on every match,
@@ -733,24 +771,25 @@ static int ransac_group(int n_pairs) {
 
 namespace {
 struct RansacWs {
-    float* planes;
+    void* planes;
     unsigned long long* best;
-    float* hypG;
+    void* hypG;
     int32_t* prev;
     uint16_t* order;
 };
-// Workspace of one batch.  ordered: hypothesis table, previews, order.
-int ransac_ws(sfm_ctx* ctx, int n_pairs, int kp, int H, bool ordered, RansacWs& w) {
-    const size_t plb = sfm::align_up((size_t)n_pairs * 8 * kp * sizeof(float), 256);
+// Workspace of one batch (scalar size `rs`: 4 = f32 spec, 8 = fp64 mode).  ordered: hypothesis
+// table, previews, order.
+int ransac_ws(sfm_ctx* ctx, int n_pairs, int kp, int H, bool ordered, RansacWs& w, size_t rs = 4) {
+    const size_t plb = sfm::align_up((size_t)n_pairs * 8 * kp * rs, 256);
     const size_t bb = sfm::align_up((size_t)n_pairs * sizeof(unsigned long long), 256);
-    const size_t gb = ordered ? sfm::align_up((size_t)n_pairs * HREC * H * sizeof(float), 256) : 0;
+    const size_t gb = ordered ? sfm::align_up((size_t)n_pairs * HREC * H * rs, 256) : 0;
     const size_t vb = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(int32_t), 256) : 0;
     const size_t ob = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(uint16_t), 256) : 0;
     char* ws = (char*)sfm::workspace(ctx, plb + bb + gb + vb + ob + 1024);
     if (!ws) return SFM_ERR_NOMEM;
-    w.planes = (float*)ws;
+    w.planes = (void*)ws;
     w.best = (unsigned long long*)(ws + plb);
-    w.hypG = (float*)(ws + plb + bb);
+    w.hypG = (void*)(ws + plb + bb);
     w.prev = (int32_t*)(ws + plb + bb + gb);
     w.order = (uint16_t*)(ws + plb + bb + gb + vb);
     return SFM_OK;
@@ -768,28 +807,29 @@ int ransac_ws(sfm_ctx* ctx, int n_pairs, int kp, int H, bool ordered, RansacWs& 
     SFM_REQUIRE(k_max <= 8192, NAME ": k_max > 8192 not supported");                               \
     SFM_REQUIRE(prm->n_hyp / 256 <= 65535, NAME ": n_hyp too large")
 
-extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
-                                  const int32_t* pairs, int32_t n_pairs,
-                                  const int32_t* match_count, const int32_t* matches,
-                                  const sfm_ransac_params* prm, int32_t* out_inl_count,
-                                  int32_t* out_best_h, uint8_t* out_mask, float* out_F,
-                                  float* out_norm) {
-    RANSAC_CHECK_ARGS("sfm_ransac_f_batch");
-    SFM_REQUIRE(out_inl_count && out_best_h && out_mask && out_F && out_norm,
-                "sfm_ransac_f_batch: NULL output");
+// One batch in the scalar type T: f32 (the spec; every schedule) or f64 (the fp64 mode; the
+// ordered schedule).
+template <typename T>
+static int ransac_batch(sfm_ctx* ctx, const T* kps, int32_t k_max, const int32_t* pairs,
+                        int32_t n_pairs, const int32_t* match_count, const int32_t* matches,
+                        const sfm_ransac_params* prm, int32_t* out_inl_count, int32_t* out_best_h,
+                        uint8_t* out_mask, T* out_F, T* out_norm) {
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int kp = plane_len(std::max(k_max, 1));
     const int H = prm->n_hyp;
-    const int mode = ransac_mode();
+    const int mode = sizeof(T) == 4 ? ransac_mode() : 0;
     const bool ordered = mode == 0;
     SFM_REQUIRE(!ordered || H <= 65536, "sfm_ransac_f_batch: n_hyp > 65536");
+    const T thr = (T)prm->thr;
     RansacWs w;
-    const int rc = ransac_ws(ctx, n_pairs, kp, H, ordered, w);
+    const int rc = ransac_ws(ctx, n_pairs, kp, H, ordered, w, sizeof(T));
     if (rc != SFM_OK) return rc;
+    T* planes = (T*)w.planes;
+    T* hypG = (T*)w.hypG;
     SFM_HIP_CHECK(hipMemsetAsync(w.best, 0, (size_t)n_pairs * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(ransac_prep_kernel, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
-                       match_count, matches, prm->thr, w.planes, out_norm);
+    hipLaunchKernelGGL(ransac_prep_kernel<T>, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
+                       match_count, matches, thr, planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 grid(n_pairs, H / 256);
     uint32_t* exec_w = nullptr;  // sfm_ransac_stats (ordered schedule only)
@@ -806,34 +846,61 @@ extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img,
     if (ordered) {
         const dim3 xgrid(xcd_grid(n_pairs, H / 256));
         const int gp = ransac_group(n_pairs);
-        hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
-                           match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG,
-                           w.prev, (float*)nullptr);
+        hipLaunchKernelGGL(ransac_fit_kernel<T>, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
+                           match_count, planes, out_norm, prm->seed, thr, H, gp, hypG, w.prev,
+                           (float*)nullptr);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                            w.prev, w.order);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(ransac_score_kernel<true>, xgrid, dim3(256), 0, st, n_pairs, k_max,
-                           match_count, w.planes, H, gp, w.hypG, w.order, w.best,
-                           (int32_t*)nullptr, exec_w);
+        hipLaunchKernelGGL((ransac_score_kernel<T, true>), xgrid, dim3(256), 0, st, n_pairs, k_max,
+                           match_count, planes, H, gp, hypG, w.order, w.best, (int32_t*)nullptr,
+                           exec_w);
         if (exec_w) {
             SFM_HIP_CHECK(hipGetLastError());
             hipLaunchKernelGGL(ransac_stats_kernel, dim3((n_pairs + 3) / 4), dim3(256), 0, st,
                                n_pairs, H, match_count, exec_w, ctx->rs_acc);
         }
-    } else if (mode == 1) {
-        hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
-                           match_count, w.planes, out_norm, prm->seed, prm->thr, w.best);
-    } else {
-        hipLaunchKernelGGL(ransac_hyp_kernel<false>, grid, dim3(256), 0, st, k_max, pairs,
-                           match_count, w.planes, out_norm, prm->seed, prm->thr, w.best);
+    } else if constexpr (sizeof(T) == 4) {
+        if (mode == 1)
+            hipLaunchKernelGGL(ransac_hyp_kernel<true>, grid, dim3(256), 0, st, k_max, pairs,
+                               match_count, planes, out_norm, prm->seed, prm->thr, w.best);
+        else
+            hipLaunchKernelGGL(ransac_hyp_kernel<false>, grid, dim3(256), 0, st, k_max, pairs,
+                               match_count, planes, out_norm, prm->seed, prm->thr, w.best);
     }
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ransac_final_kernel, dim3(n_pairs), dim3(256), 0, st, k_max, pairs,
-                       match_count, w.planes, out_norm, prm->seed, prm->thr, w.best, out_inl_count,
+    hipLaunchKernelGGL(ransac_final_kernel<T>, dim3(n_pairs), dim3(256), 0, st, k_max, pairs,
+                       match_count, planes, out_norm, prm->seed, thr, w.best, out_inl_count,
                        out_best_h, out_mask, out_F);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
+}
+
+extern "C" int sfm_ransac_f_batch(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
+                                  const int32_t* pairs, int32_t n_pairs,
+                                  const int32_t* match_count, const int32_t* matches,
+                                  const sfm_ransac_params* prm, int32_t* out_inl_count,
+                                  int32_t* out_best_h, uint8_t* out_mask, float* out_F,
+                                  float* out_norm) {
+    RANSAC_CHECK_ARGS("sfm_ransac_f_batch");
+    SFM_REQUIRE(out_inl_count && out_best_h && out_mask && out_F && out_norm,
+                "sfm_ransac_f_batch: NULL output");
+    return ransac_batch<float>(ctx, kps, k_max, pairs, n_pairs, match_count, matches, prm,
+                               out_inl_count, out_best_h, out_mask, out_F, out_norm);
+}
+
+extern "C" int sfm_ransac_f_batch_f64(sfm_ctx* ctx, const double* kps, int32_t n_img,
+                                      int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                                      const int32_t* match_count, const int32_t* matches,
+                                      const sfm_ransac_params* prm, int32_t* out_inl_count,
+                                      int32_t* out_best_h, uint8_t* out_mask, double* out_F,
+                                      double* out_norm) {
+    RANSAC_CHECK_ARGS("sfm_ransac_f_batch_f64");
+    SFM_REQUIRE(out_inl_count && out_best_h && out_mask && out_F && out_norm,
+                "sfm_ransac_f_batch_f64: NULL output");
+    return ransac_batch<double>(ctx, kps, k_max, pairs, n_pairs, match_count, matches, prm,
+                                out_inl_count, out_best_h, out_mask, out_F, out_norm);
 }
 
 extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_max,
@@ -853,25 +920,27 @@ extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, 
     if (rc != SFM_OK) return rc;
     // pairs with fewer than 8 matches: every count -1
     SFM_HIP_CHECK(hipMemsetAsync(out_counts, 0xFF, (size_t)n_pairs * H * sizeof(int32_t), st));
-    hipLaunchKernelGGL(ransac_prep_kernel, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
-                       match_count, matches, prm->thr, w.planes, out_norm);
+    float* planes = (float*)w.planes;
+    float* hypG = (float*)w.hypG;
+    hipLaunchKernelGGL(ransac_prep_kernel<float>, dim3(n_pairs), dim3(64), 0, st, kps, k_max,
+                       pairs, match_count, matches, prm->thr, planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 xgrid(xcd_grid(n_pairs, H / 256));
     const int gp = ransac_group(n_pairs);
-    hipLaunchKernelGGL(ransac_fit_kernel, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
-                       match_count, w.planes, out_norm, prm->seed, prm->thr, H, gp, w.hypG, w.prev,
+    hipLaunchKernelGGL(ransac_fit_kernel<float>, xgrid, dim3(256), 0, st, n_pairs, k_max, pairs,
+                       match_count, planes, out_norm, prm->seed, prm->thr, H, gp, hypG, w.prev,
                        out_hyp_F);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(ransac_order_kernel, dim3(n_pairs), dim3(256), 0, st, H, match_count,
                        w.prev, w.order);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((ransac_score_kernel<false, true>), xgrid, dim3(256), 0, st, n_pairs, k_max,
-                       match_count, w.planes, H, gp, w.hypG, w.order, w.best, out_counts,
-                       (uint32_t*)nullptr);
+    hipLaunchKernelGGL((ransac_score_kernel<float, false, true>), xgrid, dim3(256), 0, st,
+                       n_pairs, k_max, match_count, planes, H, gp, hypG, w.order, w.best,
+                       out_counts, (uint32_t*)nullptr);
     SFM_HIP_CHECK(hipGetLastError());
     if (out_hyp_mask) {
         hipLaunchKernelGGL(ransac_hyp_mask_kernel, dim3(n_pairs, H / 256), dim3(256), 0, st, k_max,
-                           match_count, w.planes, H, w.hypG, out_hyp_mask);
+                           match_count, planes, H, hypG, out_hyp_mask);
         SFM_HIP_CHECK(hipGetLastError());
     }
     return SFM_OK;

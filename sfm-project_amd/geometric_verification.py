@@ -37,10 +37,7 @@ def verify_pair(kp1, kp2, matches, pair=(0, 1), n_hyp=DEFAULT_HYPOTHESES, seed=D
     Returns dict(F [3,3] pixel F, inliers [n] match indices (ascending), count, verified,
     best_h)."""
     import torch
-    if len(matches) and hasattr(matches[0], "queryIdx"):
-        mt = np.array([[m.queryIdx, m.trainIdx] for m in matches], np.int32)
-    else:
-        mt = np.asarray(matches, np.int32).reshape(-1, 2)
+    mt = _match_array(matches)
     k1, k2 = np.asarray(kp1, np.float32), np.asarray(kp2, np.float32)
     k_max = max(len(k1), len(k2), len(mt), 1)
     kps = np.zeros((2, k_max, 2), np.float32)
@@ -68,16 +65,49 @@ def verify_pair(kp1, kp2, matches, pair=(0, 1), n_hyp=DEFAULT_HYPOTHESES, seed=D
                 verified=cnt >= min_inliers, best_h=int(out["best_h"].cpu()[0]))
 
 
-def verify_pairs(pair_matches, keypoints, **kw):
+def _match_array(matches) -> np.ndarray:
+    if len(matches) and hasattr(matches[0], "queryIdx"):
+        return np.array([[m.queryIdx, m.trainIdx] for m in matches], np.int32).reshape(-1, 2)
+    return np.asarray(matches, np.int32).reshape(-1, 2)
+
+
+def verify_pairs(pair_matches, keypoints, n_hyp=DEFAULT_HYPOTHESES, seed=DEFAULT_SEED,
+                 thr=DEFAULT_THRESHOLD, min_inliers=DEFAULT_MIN_INLIERS, device=0):
     """Verifies the reference's pair list (code/pipeline.py:36-47: Pair objects with img_inx_1,
-    img_inx_2, matches); keypoints[i] = [K,2] coordinates of image i.  Returns the verified
-    subset with `.matches` reduced to the inliers and `.F` attached."""
+    img_inx_2, matches; the ordered N(N-1) enumeration or any subset) in ONE batched call:
+    keypoints[i] = [K_i,2] pixel coordinates of image i.  Returns the verified subset (input
+    order) with `.matches` reduced to the inliers (ascending match index) and `.F` (pixel F,
+    unit norm) attached.  Results equal verify_pair on each pair (the RNG is keyed by the pair's
+    image ids, so they do not depend on the batch)."""
+    import torch
+    if not pair_matches:
+        return []
+    mts = [_match_array(pr.matches) for pr in pair_matches]
+    P = len(pair_matches)
+    pairs = np.array([[int(pr.img_inx_1), int(pr.img_inx_2)] for pr in pair_matches], np.int32)
+    n_img = int(pairs.max()) + 1
+    kl = [np.asarray(keypoints[i], np.float32).reshape(-1, 2) for i in range(n_img)]
+    k_max = max([len(k) for k in kl] + [len(m) for m in mts] + [1])
+    kps = np.zeros((n_img, k_max, 2), np.float32)
+    for i, k in enumerate(kl):
+        kps[i, :len(k)] = k
+    counts = np.array([len(m) for m in mts], np.int32)
+    match = np.zeros((P, k_max, 2), np.int32)
+    for p, m in enumerate(mts):
+        match[p, :len(m)] = m
+    dev = torch.device("cuda", device)
+    out = sfmcore.context(device).ransac_batch(
+        torch.from_numpy(kps).to(dev), torch.from_numpy(pairs).to(dev),
+        torch.from_numpy(counts).to(dev), torch.from_numpy(match).to(dev), n_hyp=n_hyp,
+        seed=seed, thr=thr, min_inliers=min_inliers)
+    cnt = out["inl_count"].cpu().numpy()
+    mask = out["mask"].cpu().numpy()
+    Fn, nrm = out["F"].cpu().numpy(), out["norm"].cpu().numpy()
     verified = []
-    for pr in pair_matches:
-        r = verify_pair(keypoints[pr.img_inx_1], keypoints[pr.img_inx_2], pr.matches,
-                        pair=(pr.img_inx_1, pr.img_inx_2), **kw)
-        if r["verified"]:
-            pr.matches = [pr.matches[i] for i in r["inliers"]]
-            pr.F = r["F"]
+    for p, pr in enumerate(pair_matches):
+        if cnt[p] >= min_inliers:
+            keep = np.nonzero(mask[p, :counts[p]])[0]
+            pr.matches = [pr.matches[i] for i in keep]
+            pr.F = denormalize_F(Fn[p], nrm[p])
             verified.append(pr)
     return verified

@@ -145,7 +145,7 @@ class BAProblem:
         return self.ctx.ba_jtj(cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv,
                                self.pt_ptr, self.cam_ptr, self.cam_obs, loss_s=loss_s)
 
-    def solve(self, lin, lam, max_iter=100, tol=1e-10, poll=0):
+    def solve(self, lin, lam, max_iter=100, tol=1e-10, poll=8):
         return self.ctx.ba_solve(lin, self.cam_idx, self.pt_idx, self.pt_ptr, self.cam_ptr,
                                  self.cam_obs, lam, max_iter=max_iter, tol=tol, poll=poll)
 

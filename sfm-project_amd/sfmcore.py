@@ -25,7 +25,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
             "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
-            "sfm_ransac_stats"]
+            "sfm_ransac_stats", "sfm_ransac_f_batch_f64"]
 
 
 class SfmCoreError(RuntimeError):
@@ -92,6 +92,7 @@ def load_library(path: str = LIB_PATH):
                                       vp, vp, vp]
         L.sfm_ransac_f_batch.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
                                          C.POINTER(RansacParams), vp, vp, vp, vp, vp]
+        L.sfm_ransac_f_batch_f64.argtypes = L.sfm_ransac_f_batch.argtypes
         L.sfm_ransac_counts.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
                                         C.POINTER(RansacParams), vp, vp, vp, vp]
         L.sfm_ransac_stats.argtypes = [vp, i32, vp]
@@ -208,24 +209,27 @@ class Context:
     # ---- geometric verification ------------------------------------------------------------
     def ransac_batch(self, kps, pairs, count, match, n_hyp=4096, seed=42, thr=1.0,
                      min_inliers=15, out=None):
-        """kps [n_img,k_max,2] f32 + the outputs of match_batch.  Returns dict of device tensors:
-        inl_count [P] (-1: fewer than 8 matches), best_h [P], mask [P,k_max] u8,
-        F [P,9] f32 (normalised coordinates), norm [P,6] f32 (cx1,cy1,s1,cx2,cy2,s2)."""
+        """kps [n_img,k_max,2] f32 (the spec) or f64 (the fp64 mode, sfm_ransac_f_batch_f64) +
+        the outputs of match_batch.  Returns dict of device tensors: inl_count [P] (-1: fewer
+        than 8 matches), best_h [P], mask [P,k_max] u8, F [P,9] (normalised coordinates),
+        norm [P,6] (cx1,cy1,s1,cx2,cy2,s2); F and norm in the dtype of kps."""
         torch = self.torch
         n_img, k_max, _ = kps.shape
         P = pairs.shape[0]
         dev = kps.device
-        if kps.dtype != torch.float32 or not kps.is_contiguous():
-            raise SfmCoreError("ransac_batch: kps must be contiguous float32")
+        if kps.dtype not in (torch.float32, torch.float64) or not kps.is_contiguous():
+            raise SfmCoreError("ransac_batch: kps must be contiguous float32 or float64")
+        f64 = kps.dtype == torch.float64
         if out is None:
             out = dict(inl_count=torch.empty(P, dtype=torch.int32, device=dev),
                        best_h=torch.empty(P, dtype=torch.int32, device=dev),
                        mask=torch.empty((P, k_max), dtype=torch.uint8, device=dev),
-                       F=torch.empty((P, 9), dtype=torch.float32, device=dev),
-                       norm=torch.empty((P, 6), dtype=torch.float32, device=dev))
+                       F=torch.empty((P, 9), dtype=kps.dtype, device=dev),
+                       norm=torch.empty((P, 6), dtype=kps.dtype, device=dev))
         prm = RansacParams(int(n_hyp), int(min_inliers), float(thr), 0, int(seed))
         self._bind_stream()
-        _check(self.lib.sfm_ransac_f_batch(self.handle, _ptr(kps), n_img, k_max, _ptr(pairs), P,
+        fn = self.lib.sfm_ransac_f_batch_f64 if f64 else self.lib.sfm_ransac_f_batch
+        _check(fn(self.handle, _ptr(kps), n_img, k_max, _ptr(pairs), P,
                                            _ptr(count), _ptr(match), C.byref(prm),
                                            _ptr(out["inl_count"]), _ptr(out["best_h"]),
                                            _ptr(out["mask"]), _ptr(out["F"]), _ptr(out["norm"])))
@@ -361,10 +365,11 @@ class Context:
         return pts, stats
 
     def ba_solve(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, max_iter=100,
-                 tol=1e-10, out=None, poll=0):
+                 tol=1e-10, out=None, poll=8):
         """Damped Schur-complement PCG step from the ba_jtj blocks `lin`; returns
         (dc [n_cam,8], dp [n_pt,3], info [5] f64 device tensor).  poll: convergence poll period
-        in CG iterations (0 = 8; < 0 = none, fully asynchronous), see include/sfmcore.h."""
+        in CG iterations (one host sync each; <= 0 = none, fully asynchronous / graph-capturable),
+        see include/sfmcore.h."""
         torch = self.torch
         U = lin["U"]
         dev = U.device
@@ -385,7 +390,7 @@ class Context:
         return dc, dp, info
 
     def ba_solve_sharded(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, allreduce,
-                         max_iter=100, tol=1e-10, out=None, poll=0):
+                         max_iter=100, tol=1e-10, out=None, poll=8):
         """ba_solve on this rank's point shard (lin: ba_jtj of the shard with U / gc already
         all-reduced), driving sfm_ba_solve_stage: allreduce(t) sums the f64 device tensor t over
         all ranks in place, ordered on the current stream (reconstruction.make_allreduce).
@@ -414,7 +419,7 @@ class Context:
         stage(BA_STAGE_SETUP)
         allreduce(comm[:44 * nc])
         stage(BA_STAGE_SETUP_FINISH)
-        every = 8 if poll == 0 else poll
+        every = poll
         for k in range(max_iter):
             if every > 0 and k > 0 and k % every == 0:
                 stage(BA_STAGE_POLL)   # the same decision on every rank (replicated state)

@@ -63,7 +63,7 @@ def main():
         dc, dp, _ = P.solve(ln, lam, max_iter=200, tol=1e-10, poll=poll)
         c2, p2 = P.update(cams, dc, pts, dp)
         P.cost(c2, p2)
-    t_def = timed(lambda: lm_step_default(0), 5)
+    t_def = timed(lambda: lm_step_default(8), 5)
     t_def_async = timed(lambda: lm_step_default(-1), 5)
     _, _, info = P.solve(lin, lam, max_iter=200, tol=1e-10)
     it10 = int(info[0].item())

@@ -187,3 +187,31 @@ def test_solve_without_observations():
     torch.cuda.synchronize()
     np.testing.assert_allclose(dc.cpu().numpy(), -1.0 / 3.0, rtol=1e-12)
     assert dp.numel() == 0
+
+
+def test_solve_async_default_under_graph_capture():
+    """the zero-initialised poll is fully asynchronous — the solve can be captured in a
+    HIP graph (torch.cuda.CUDAGraph on ROCm) and replayed; the replay equals the eager solve and
+    the polled solve bit for bit."""
+    import torch
+    prob = synth.make_ba_problem(10, 300, obs_per_pt=4, seed=21, perturb=2e-3)
+    P, _, _, lin = _problem(prob)
+    eager = [t.clone() for t in P.solve(lin, 1e-3, max_iter=60, tol=1e-10, poll=0)]
+    polled = [t.clone() for t in P.solve(lin, 1e-3, max_iter=60, tol=1e-10, poll=8)]
+    out = [torch.empty_like(t) for t in eager]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):     # warm-up on the capture stream (workspace already sized)
+        P.ctx.ba_solve(lin, P.cam_idx, P.pt_idx, P.pt_ptr, P.cam_ptr, P.cam_obs, 1e-3,
+                       max_iter=60, tol=1e-10, out=out, poll=0)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    for t in out:
+        t.zero_()
+    with torch.cuda.graph(g, stream=s):  # the context stays bound to s: no cross-stream hand-off
+        P.ctx.ba_solve(lin, P.cam_idx, P.pt_idx, P.pt_ptr, P.cam_ptr, P.cam_obs, 1e-3,
+                       max_iter=60, tol=1e-10, out=out, poll=0)
+    g.replay()
+    torch.cuda.synchronize()
+    for a, b, c in zip(out, eager, polled):
+        assert torch.equal(a, b) and torch.equal(b, c)

@@ -10,6 +10,7 @@ import geometric_verification as gv
 import match_graph
 import oracle as O
 import reconstruction
+import sfmcore
 import synth
 
 pytestmark = pytest.mark.gpu
@@ -181,3 +182,36 @@ def test_match_all_pairs_equals_reference_loop():
     assert [(p.img_inx_1, p.img_inx_2, [(x.queryIdx, x.trainIdx, x.distance) for x in p.matches])
             for p in got] == want
     assert all(p.img_inx_1 != 4 and p.img_inx_2 != 4 for p in got)
+
+
+def test_verify_pairs_batched_equals_per_pair_on_ordered_list():
+    """The reference's ordered N(N-1) Pair list (code/pipeline.py:36-47, match_all_pairs
+    ordered=True) verified in ONE ransac_batch launch equals verify_pair on each pair."""
+    import copy
+    s = synth.make_scene(5, 1024, seed=17)
+    prs = fm.match_all_pairs([s["desc"][i] for i in range(5)], norm="l2", cross_check="mutual",
+                             max_distance=None, ratio=(4, 5), ordered=True, sort=False)
+    assert len(prs) == 20
+    ref = [gv.verify_pair(s["kps"][p.img_inx_1], s["kps"][p.img_inx_2], p.matches,
+                          pair=(p.img_inx_1, p.img_inx_2), n_hyp=1024) for p in prs]
+    calls = []
+    orig = sfmcore.Context.ransac_batch
+
+    def counted(self, *a, **k):
+        calls.append(1)
+        return orig(self, *a, **k)
+
+    sfmcore.Context.ransac_batch = counted
+    try:
+        before = copy.deepcopy(prs)
+        out = gv.verify_pairs(prs, s["kps"], n_hyp=1024)
+    finally:
+        sfmcore.Context.ransac_batch = orig
+    assert len(calls) == 1
+    exp = [(b, r) for b, r in zip(before, ref) if r["verified"]]
+    assert len(out) == len(exp) > 0
+    for o, (b, r) in zip(out, exp):
+        assert (o.img_inx_1, o.img_inx_2) == (b.img_inx_1, b.img_inx_2)
+        assert [(m.queryIdx, m.trainIdx) for m in o.matches] == \
+            [(b.matches[i].queryIdx, b.matches[i].trainIdx) for i in r["inliers"]]
+        np.testing.assert_array_equal(o.F, r["F"])

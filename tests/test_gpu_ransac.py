@@ -222,3 +222,34 @@ def test_ransac_counts_k4096_and_tails(ctx):
         ref = O.ransac_counts(s["kps"][a][mt2[p, :M, 0]], s["kps"][b][mt2[p, :M, 1]], H=256,
                               seed=42, pa=int(a), pb=int(b), thr=1.0)
         np.testing.assert_array_equal(counts[p], ref, err_msg=f"pair {p} (M={M})")
+
+
+def test_ransac_f64_small_pairs_bit_exact(ctx):
+    """fp64 mode on small / ragged pairs (fewer than 8, exactly 8, PV boundaries) vs the oracle."""
+    import torch
+    s = synth.make_scene(4, 700, seed=31)
+    pairs = np.array([[0, 1], [1, 2], [2, 3], [0, 3]], np.int32)
+    n_keep = [700, 8, 5, 65]
+    cnt, mt = [], []
+    k_max = 700
+    match = np.zeros((len(pairs), k_max, 2), np.int32)
+    for p, (a, b) in enumerate(pairs):
+        q, t, _ = O.match(s["desc"][a], s["desc"][b], 0, 1, (4, 5))
+        m = min(len(q), n_keep[p])
+        match[p, :m] = np.c_[q[:m], t[:m]]
+        cnt.append(m)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    rs = ctx.ransac_batch(T(s["kps"].astype(np.float64)), T(pairs), T(np.array(cnt, np.int32)),
+                          T(match), n_hyp=512, seed=7, thr=1.0)
+    torch.cuda.synchronize()
+    rs = {k: v.cpu().numpy() for k, v in rs.items()}
+    for p, (a, b) in enumerate(pairs):
+        m = cnt[p]
+        x1 = s["kps"][a][match[p, :m, 0]].astype(np.float64)
+        x2 = s["kps"][b][match[p, :m, 1]].astype(np.float64)
+        o = O.ransac_f(x1, x2, H=512, seed=7, pa=int(a), pb=int(b), f64=True)
+        assert rs["inl_count"][p] == o["count"] and rs["best_h"][p] == o["best_h"]
+        if m >= 8:
+            np.testing.assert_array_equal(rs["mask"][p, :m], o["mask"])
+            assert rs["F"][p].view(np.uint64).tolist() == o["F"].view(np.uint64).tolist()
+            assert rs["norm"][p].view(np.uint64).tolist() == o["norm"].view(np.uint64).tolist()
