@@ -162,6 +162,7 @@ def main():
                     help="CPU baseline budget (the sample is sized to about this much wall)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 side measurement")
+    ap.add_argument("--no-fp64", action="store_true", help="skip the fp64-K2 side measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: 'gloo' lets N ranks share one GPU (RCCL cannot)")
     ap.add_argument("--device", type=int, default=-1, help="rehearsal only: force this GPU")
@@ -294,6 +295,8 @@ def main():
         "note": "sum of stage roofline times / measured step; K2 ideal on the executed "
                 "(pruned) share of the algorithmic flops (measured in the timed steps)"}
 
+    if rank == 0 and not args.no_fp64:
+        result["k2_fp64"] = fp64_side(run, args.n_hyp)
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(scene, pairs, lo, hi, graph, run.gb,
@@ -307,6 +310,53 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def fp64_side(run, n_hyp, reps=2):
+    """Side measurement (after the timed region): K2 in the fp64 mode (sfm_ransac_f_batch_f64)
+    against the f32 spec on the same tentative matches of this rank's shard, HIP events on the
+    launch stream; plus how many pairs' results differ between the two specs."""
+    import numpy as np
+    torch = run.torch
+    gb = run.gb
+    kps64 = gb.kps.double().contiguous()
+    t32 = t64 = 0.0
+    n_diff = n_ver32 = n_ver64 = inl32 = inl64 = 0
+    for _, pt in run.chunks:
+        count, match, _ = gb.match(pt)
+        out64 = None
+        for impl in ("f32", "f64"):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            for r in range(reps + 1):      # first call untimed (workspace growth)
+                if r == 1:
+                    ev[0].record()
+                if impl == "f32":
+                    rs32 = gb.verify(pt, count, match)
+                else:
+                    out64 = gb.ctx.ransac_batch(kps64, pt, count, match, out=out64,
+                                                **gb.ransac_kw)
+            ev[1].record()
+            torch.cuda.synchronize()
+            ms = ev[0].elapsed_time(ev[1]) / reps
+            if impl == "f32":
+                t32 += ms
+                c32 = rs32["inl_count"].cpu().numpy()
+            else:
+                t64 += ms
+                c64 = out64["inl_count"].cpu().numpy()
+        mi = gb.min_inliers
+        n_diff += int((c32 != c64).sum())
+        n_ver32 += int((c32 >= mi).sum())
+        n_ver64 += int((c64 >= mi).sum())
+        inl32 += int(c32[c32 >= mi].sum())
+        inl64 += int(c64[c64 >= mi].sum())
+    return {"ransac_ms_f32": t32, "ransac_ms_f64": t64, "f64_over_f32": t64 / t32 if t32 else None,
+            "pairs": int(sum(pt.shape[0] for _, pt in run.chunks)),
+            "pairs_with_different_count": n_diff, "verified_pairs_f32": n_ver32,
+            "verified_pairs_f64": n_ver64, "verified_matches_f32": inl32,
+            "verified_matches_f64": inl64,
+            "note": "fp64 verification mode (same sampler, schedule and spec in double, bit-exact "
+                    "vs the fp64 oracle); timed after the main steps on the same matches"}
 
 
 def graph_checksum(torch, graph):
