@@ -19,8 +19,8 @@
  *   budget      n_l = lround(nfeat (1 - 1/s) / (1 - (1/s)^L) (1/s)^l), the last level the rest;
  *   FAST-9      on [31, W_l - 31) x [31, H_l - 31): score = max over the 16 arcs of 9 contiguous
  *               circle pixels of max(min(I_k - p), min(p - I_k)); corner iff score > threshold;
- *   NMS         score strictly greater than all 8 neighbours; candidates in raster order, at
- *               most 32768 per level;
+ *   NMS         score strictly greater than all 8 neighbours; candidates in raster order (all
+ *               of them: round 3 dropped the 32768-per-level cap);
  *   selection   the 2 n_l best by FAST score (ties: raster order), then the n_l best by the
  *               Harris response R = 25 (a b - c^2) - (a + b)^2 (= 25 (det - 0.04 tr^2)) of the
  *               3x3-Sobel structure tensor summed over a 7x7 window (ties: raster order);
@@ -37,7 +37,6 @@
 #include "orb_bit_pattern_31.h"
 
 #define ORB_EDGE 31
-#define ORB_MAXC 32768
 #define ORB_RADIUS 15
 
 static const int FAST_DX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -247,10 +246,12 @@ int oracle_orb(const uint8_t* img, int H, int W, int nfeat, int nlevels, double 
                 const int s = oracle_orb_fast_score(L, w, x, y);
                 S[(size_t)y * w + x] = (uint8_t)(s > fast_thr ? s : 0);
             }
-        orb_cand* c = (orb_cand*)malloc(sizeof(orb_cand) * ORB_MAXC);
+        /* strict 3x3 maxima are never 8-adjacent: at most one per 2x2 block inside the border */
+        const size_t cap = (size_t)((w - 2 * ORB_EDGE + 1) / 2) * (size_t)((h - 2 * ORB_EDGE + 1) / 2);
+        orb_cand* c = (orb_cand*)malloc(sizeof(orb_cand) * (cap > 0 ? cap : 1));
         int nc = 0;
-        for (int y = ORB_EDGE; y < h - ORB_EDGE && nc < ORB_MAXC; ++y)
-            for (int x = ORB_EDGE; x < w - ORB_EDGE && nc < ORB_MAXC; ++x) {
+        for (int y = ORB_EDGE; y < h - ORB_EDGE; ++y)
+            for (int x = ORB_EDGE; x < w - ORB_EDGE; ++x) {
                 const int s = S[(size_t)y * w + x];
                 if (!s) continue;
                 int keep = 1;

@@ -16,7 +16,8 @@
 //                      blur and the kept scores
 //                      and the survivor count of every 64-pixel row segment
 //   orb_scan_kernel    block per (image, level): row positions in raster order
-//   orb_cand_kernel    wave per level row: the raster-order candidate list (x, y, score packed)
+//   orb_cand_kernel    wave per level row: the raster-order candidate list (x, y, score packed),
+//                      every NMS survivor (round 3: no per-level cap)
 //   orb_select_kernel  block per (image, level): FAST-score top 2 n_l by histogram threshold,
 //                      Harris, LDS bitonic sort, orientation and descriptors of the n_l best
 //   orb_pack_kernel    block per image: levels' slots -> one dense list per image
@@ -31,7 +32,6 @@
 namespace {
 
 constexpr int EDGE = 31;
-constexpr int MAXC = 32768;      // candidates per level (raster order)
 constexpr int MAXLEV = 16;
 constexpr int SEL_MAX = 1024;    // 2 n_l per level handled by the select kernel
 constexpr int RADIUS = 15;
@@ -46,6 +46,9 @@ struct OrbLevels {
     int32_t tileoff[MAXLEV + 1];      // first tile of each level (orb_tile_kernel grid x)
     int64_t segoff[MAXLEV + 1];       // first 64-pixel row segment (row-major: y * ntx + tile x)
     int64_t rowoff[MAXLEV + 1];       // first row of each level (row position arrays)
+    int64_t candoff[MAXLEV + 1];      // first candidate slot of each level in an image's list:
+                                      // room for every strict 3x3 maximum inside the border,
+                                      // ceil((W - 62) / 2) x ceil((H - 62) / 2) (no cap)
     double sc[MAXLEV];
 };
 
@@ -347,7 +350,7 @@ __global__ __launch_bounds__(256) void orb_cand_kernel(const uint8_t* __restrict
     }
     const int base = rowpos[img * L.rowoff[L.nlev] + rg];
     const uint8_t* row = nms + img * L.off[L.nlev] + L.off[l] + (size_t)y * L.pitch[l];
-    int32_t* out = cand + (img * L.nlev + l) * (size_t)MAXC;
+    int32_t* out = cand + img * L.candoff[L.nlev] + L.candoff[l];
     for (int t0 = 0; t0 < ntx; t0 += 8) {
         int v[8];
 #pragma unroll
@@ -363,14 +366,15 @@ __global__ __launch_bounds__(256) void orb_cand_kernel(const uint8_t* __restrict
             if (v[j] != 0) {
                 const int k = base + sb + __popcll(m & ((1ull << lane) - 1ull));
                 const int x = (t0 + j) * TW + lane;
-                if (k < MAXC) out[k] = (int32_t)(((unsigned)y << 20) | ((unsigned)x << 8) | (unsigned)v[j]);
+                out[k] = (int32_t)(((unsigned)y << 20) | ((unsigned)x << 8) | (unsigned)v[j]);
             }
         }
     }
 }
 
 // Block per (image, level): row totals (sum of the row's segment counts), exclusive scan over the
-// rows (fixed order) -> row positions, and the level's candidate count (capped at MAXC).
+// rows (fixed order) -> row positions, and the level's candidate count (every survivor: the list
+// has room for all of them, L.candoff).
 __global__ __launch_bounds__(256) void orb_scan_kernel(OrbLevels L, const int32_t* __restrict__ segcnt,
                                                        int32_t* __restrict__ rowpos,
                                                        int32_t* __restrict__ ncand) {
@@ -404,7 +408,7 @@ __global__ __launch_bounds__(256) void orb_scan_kernel(OrbLevels L, const int32_
         if (tid == 255) carry = base + incl;
         __syncthreads();
     }
-    if (tid == 0) ncand[img * L.nlev + l] = min(carry, MAXC);
+    if (tid == 0) ncand[img * L.nlev + l] = carry;
 }
 
 __device__ __forceinline__ bool le_r(long long B, long long A, long long R2) {
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
     if (tid == 0) lvl_count[img * L.nlev + l] = 0;
     if (nl <= 0) return;
     const int nc = ncand[img * L.nlev + l];
-    const int32_t* cd = cand + (img * L.nlev + l) * (size_t)MAXC;
+    const int32_t* cd = cand + img * L.candoff[L.nlev] + L.candoff[l];
     const int64_t tot = L.off[L.nlev];
     const uint8_t* lv = pyr + img * tot + L.off[l];
     const uint8_t* bl = blur + img * tot + L.off[l];
@@ -727,6 +731,12 @@ extern "C" int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img,
     L.tileoff[nlev] = ntile;
     L.segoff[nlev] = nseg;
     L.rowoff[nlev] = nrow;
+    L.candoff[0] = 0;
+    for (int l = 0; l < nlev; ++l) {
+        const int64_t cx = L.W[l] > 2 * EDGE ? (L.W[l] - 2 * EDGE + 1) / 2 : 0;
+        const int64_t cy = L.H[l] > 2 * EDGE ? (L.H[l] - 2 * EDGE + 1) / 2 : 0;
+        L.candoff[l + 1] = L.candoff[l] + cx * cy;
+    }
     std::vector<int32_t> host(3 * (size_t)nmap + 1024);
     for (int l = 1; l < nlev; ++l) {
         axis_map(W, L.W[l], host.data() + 3 * (size_t)L.mapx[l]);
@@ -739,7 +749,7 @@ extern "C" int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img,
     const size_t b_tab = sfm::align_up(sizeof(int32_t) * host.size(), 256);
     const size_t b_img = sfm::align_up(tot * n_img, 256);
     const size_t b_rows = sfm::align_up(sizeof(int32_t) * (size_t)nseg * n_img, 256);  // >= rows
-    const size_t b_cand = sizeof(int32_t) * (size_t)MAXC * nlev * n_img;
+    const size_t b_cand = sfm::align_up(sizeof(int32_t) * (size_t)L.candoff[nlev] * n_img, 256);
     const size_t b_cnt = sfm::align_up(sizeof(int32_t) * (size_t)nlev * n_img, 256);
     const size_t b_skp = sfm::align_up(sizeof(float) * 6 * (size_t)nfeat * n_img, 256);
     const size_t b_sd = sfm::align_up((size_t)32 * nfeat * n_img, 256);

@@ -122,3 +122,19 @@ def test_extract_and_match_draw_without_cv2(monkeypatch):
     ms = fm.extract_and_match_draw(img, sh)
     assert ms == fm.extract_and_match(img, sh) and len(ms) > 100
     assert shown
+
+
+def test_orb_dense_texture_beyond_32768_survivors(ctx):
+    """a heavily textured image whose level 0 has far more than 32768 NMS survivors
+    (uniform noise: a strict 3x3 maximum every few pixels, ~10^5 at 1080p).  Every survivor enters
+    the FAST top-2n_l selection (no per-level cap), so the keypoints cover the whole image instead
+    of the upper rows; GPU == oracle (uncapped too)."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (1, 1080, 1920), dtype=np.uint8)
+    kp, desc, cnt = _gpu_orb(ctx, img)
+    n = _check(img[0], kp[0], desc[0], cnt[0])
+    assert n == 500
+    lvl0 = kp[0, :n][kp[0, :n, 5] == 0]
+    assert len(lvl0) > 50
+    # a 32768 cap in raster order would end around row 31 + 32768 / (~0.1 x 1858) ~ 200
+    assert lvl0[:, 1].max() > 0.8 * 1080 and lvl0[:, 1].min() < 0.2 * 1080
