@@ -16,7 +16,9 @@
 //     bas_pcg_point     8 lanes per point: t_p = V_d⁻¹ Σ_o W_oᵀ p_c     (SoA W, once)
 //     bas_pcg_camera    block per camera: q_c = U_d p_c - Σ_o W_o t_p   (SoA W, once)
 //     bas_pcg_vec       thread per camera component: α, x, r, z = M r, partial r·z, r·r
-//   bas_backsub         8 lanes per point: δp, and the point terms of gᵀδ and δᵀ(JᵀJ)δ
+//   sharded (sfm_ba_solve_stage): bas_pcg_point, bas_pcg_camera phase 1 (-> comm), the caller's
+//     all-reduce, then bas_pcg_finish_vec (q from comm, p·q, α and the vector update in one launch)
+//   bas_backsub        8 lanes per point: δp, and the point terms of gᵀδ and δᵀ(JᵀJ)δ
 //   bas_model           one block: gᵀδ, δᵀ(JᵀJ)δ (LM predicted decrease), iterations, |r|/|b|
 // HBM: a CG iteration reads W twice (2 x 192 B per observation) plus the camera/point vectors;
 // this stage is HBM-bound.
@@ -429,7 +431,8 @@ constexpr int CC = SFM_BA_CC;  // threads per camera block in the CG camera pass
 
 // Block per camera: p_k stored; q_c = U_d p_c - Σ_o W_o t_p; p_c·q_c.
 // Sharded solve: phase 1 writes the local Σ_o W_o t_p to comm[8c..] and stops; after the
-// all-reduce of comm, phase 2 finishes the camera from it (phase 0: unsharded).
+// all-reduce of comm, phase 2 finishes the camera from it (phase 0: unsharded).  Phase 3 (the
+// one-launch finish, bas_pcg_finish_vec): phase 1 plus U_d p_k into q and p_k into pv.
 __global__ __launch_bounds__(CC) void bas_pcg_camera(
     int k, int n_cam, int n_obs, const int32_t* __restrict__ cam_ptr,
     const int32_t* __restrict__ ptc, const double* __restrict__ Wc, const double* __restrict__ t,
@@ -441,6 +444,12 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
     if (st->done) return;
     const double beta = st->beta;
     const int c = blockIdx.x, tid = threadIdx.x;
+    double ur[8];  // U_d row tid (tid < 8), in flight during the observation loop
+    if (tid < 8 && phase != 1) {
+        const double* u = Ud + 64 * (size_t)c + 8 * tid;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ur[j] = u[j];
+    }
     double acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.0;
@@ -472,21 +481,23 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
     }
     __syncthreads();
     if (tid < 8) {
+        const size_t kk = 8 * (size_t)c + tid;
         double wt = 0.0;
 #pragma unroll
         for (int w = 0; w < CC / 64; ++w) wt += red[w][tid];
-        if (phase == 1) {
-            comm[8 * (size_t)c + tid] = wt;
-            return;
-        }
-        if (phase == 2) wt = comm[8 * (size_t)c + tid];
-        const double* u = Ud + 64 * (size_t)c + 8 * tid;
+        if (phase == 1 || phase == 3) comm[kk] = wt;
+        if (phase == 1) return;
+        if (phase == 2) wt = comm[kk];
         double sU = 0.0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sU += u[j] * pc_s[j];
+        for (int j = 0; j < 8; ++j) sU += ur[j] * pc_s[j];
+        pv[kk] = pc_s[tid];
+        if (phase == 3) {
+            q[kk] = sU;
+            return;
+        }
         const double qi = sU - wt;
-        q[8 * (size_t)c + tid] = qi;
-        pv[8 * (size_t)c + tid] = pc_s[tid];
+        q[kk] = qi;
         double v = pc_s[tid] * qi;
         v += __shfl_down(v, 4, 8);
         v += __shfl_down(v, 2, 8);
@@ -543,6 +554,108 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
         }
     }
     if (gi == 0) st->iter = k + 1;
+}
+
+// Largest camera count for which the sharded solve finishes an iteration in one launch
+// (bas_pcg_finish_vec keeps every camera's p·q in LDS and recomputes them in every block:
+// n_cam² · 11 B of L2 reads).  Mirrored by sfmcore.BA_FINISH_VEC_MAX_CAM.
+constexpr int FINISH_VEC_MAX_CAM = 1024;
+constexpr int FV = 512;   // threads per bas_pcg_finish_vec block: 64 cameras per pass
+constexpr int FVR = 8;    // passes per round: 512 cameras' loads in flight at once
+
+// Sharded solve, after the all-reduce of comm = Σ_o W_o t_p over all ranks: bas_pcg_camera's
+// phase 2 and bas_pcg_vec in one launch (thread per camera component).  Phase 3 of the camera
+// pass left p_k (pv) and U_d p_k (su) per camera, so q = su - comm.  Every block forms p·q for
+// ALL cameras (8 lanes each, bas_pcg_camera's shuffle tree, into LDS; 512 cameras' loads per
+// round in flight together), and canon_sum over LDS gives every block the unsharded solve's
+// Σ p·q bit for bit without a second launch.  No block reads z or writes p, so both stay in
+// place.
+__global__ __launch_bounds__(FV) void bas_pcg_finish_vec(
+    int k, int n_cam, const double* __restrict__ su, const double* __restrict__ comm,
+    const double* __restrict__ pv, const double* __restrict__ Mc, double* __restrict__ x,
+    double* __restrict__ r, double* __restrict__ z, double* __restrict__ rzc,
+    double* __restrict__ rrc, PcgState* __restrict__ st) {
+    __shared__ double pq_s[FINISH_VEC_MAX_CAM];
+    __shared__ double red4[4];
+    const int tid = threadIdx.x;
+    const int c = blockIdx.x * (FV / 8) + (tid >> 3), i = tid & 7;
+    const bool valid = c < n_cam;
+    const int s0 = k & 1, s1 = (k + 1) & 1;
+    const size_t kk = 8 * (size_t)(valid ? c : 0) + i;
+    // rounds of FVR passes x FV/8 cameras, straight-line (clamped loads, every lane shuffles) so
+    // a round's loads are in flight together; the first round's loads, this thread's x, r and
+    // preconditioner row are issued before the CG state is read (the latencies overlap)
+    double pj[FVR], sj[FVR], cm[FVR];
+    auto load_round = [&](int c0) {
+#pragma unroll
+        for (int m = 0; m < FVR; ++m) {
+            const int cc = min(c0 + m * (FV / 8) + (tid >> 3), n_cam - 1);
+            const size_t b = 8 * (size_t)cc + i;
+            pj[m] = pv[b];
+            sj[m] = su[b];
+            cm[m] = comm[b];
+        }
+    };
+    load_round(0);
+    const double xk = x[kk], rk = r[kk];
+    double Mr[8];
+    {
+        const double* M = Mc + 64 * (size_t)(valid ? c : 0) + 8 * i;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Mr[j] = M[j];
+    }
+    const bool done = st->done != 0;
+    if (done) {
+        if (valid && i == 0) {
+            rzc[(size_t)s1 * n_cam + c] = rzc[(size_t)s0 * n_cam + c];
+            rrc[(size_t)s1 * n_cam + c] = rrc[(size_t)s0 * n_cam + c];
+        }
+        return;
+    }
+    const double rz_k = st->rz;
+    double pk = 0.0, qi = 0.0;
+    for (int c0 = 0; c0 < n_cam; c0 += FVR * (FV / 8)) {
+        if (c0 > 0) load_round(c0);
+#pragma unroll
+        for (int m = 0; m < FVR; ++m) {
+            const int cc = c0 + m * (FV / 8) + (tid >> 3);
+            const double q = sj[m] - cm[m];
+            double v = pj[m] * q;
+            v += __shfl_down(v, 4, 8);
+            v += __shfl_down(v, 2, 8);
+            v += __shfl_down(v, 1, 8);
+            if (i == 0 && cc < n_cam) pq_s[cc] = v;
+            if (cc == c) {
+                pk = pj[m];
+                qi = q;
+            }
+        }
+    }
+    __syncthreads();
+    const double pqs = canon_sum(pq_s, n_cam, red4);
+    const bool breakdown = !(pqs > 0.0);
+    const double alpha = breakdown ? 0.0 : rz_k / pqs;
+    double ri = 0.0;
+    if (valid) {
+        x[kk] = xk + alpha * pk;
+        ri = rk - alpha * qi;
+        r[kk] = ri;
+    }
+    double zi = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zi += Mr[j] * __shfl(ri, (tid & 63 & ~7) + j, 64);
+    double rz = ri * zi, rr = ri * ri;
+    rz += __shfl_down(rz, 4, 8); rr += __shfl_down(rr, 4, 8);
+    rz += __shfl_down(rz, 2, 8); rr += __shfl_down(rr, 2, 8);
+    rz += __shfl_down(rz, 1, 8); rr += __shfl_down(rr, 1, 8);
+    if (valid) {
+        z[kk] = zi;
+        if (i == 0) {
+            rzc[(size_t)s1 * n_cam + c] = rz;
+            rrc[(size_t)s1 * n_cam + c] = breakdown ? 0.0 : rr;
+        }
+    }
+    if (blockIdx.x == 0 && tid == 0) st->iter += 1;  // k-free: a captured window replays at any k
 }
 
 // One block: |b|^2 (canonical sum of the setup's per-camera shares) and the iteration count.
@@ -856,6 +969,8 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
     SolveWs w;
     if (solve_ws(ctx, n_cam, n_pt, n_obs, w) != SFM_OK) return SFM_ERR_NOMEM;
     const double lam = prm->lambda, tol = prm->tol;
+    // up to FINISH_VEC_MAX_CAM cameras an iteration ends in one launch after the all-reduce
+    const bool fused = n_cam <= FINISH_VEC_MAX_CAM;
     switch (stage) {
     case SFM_BA_STAGE_SETUP:  // -> comm[0, 44 n_cam)
         return solve_setup(st, w, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V, W,
@@ -873,9 +988,16 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
                            w.t);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
-                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 1, comm);
+                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, fused ? 3 : 1,
+                           comm);
         break;
     case SFM_BA_STAGE_ITER_FINISH:
+        if (fused) {
+            hipLaunchKernelGGL(bas_pcg_finish_vec, dim3((8 * n_cam + FV - 1) / FV), dim3(FV), 0, st,
+                               k, n_cam, w.q, comm, w.pv, w.Mc, dc, w.r, w.z, w.rzc, w.rrc,
+                               w.state);
+            break;
+        }
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
                            w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 2, comm);
         SFM_HIP_CHECK(hipGetLastError());

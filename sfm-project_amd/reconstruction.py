@@ -199,19 +199,50 @@ def _rotmat_np(r):
     return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
 
 
-def make_allreduce(group=None):
-    """In-place fp64 sum over the ranks of `group`: RCCL (`nccl`) on the current stream for device
-    tensors; gloo through a host copy (the CPU tests and the same-GPU rehearsals)."""
+_rccl_comms = {}
+
+
+def make_allreduce(group=None, direct: bool = True):
+    """In-place fp64 sum over the ranks of `group`, ordered on the current stream.
+
+    `nccl` groups: by default a direct RCCL communicator (rccl.RcclComm, created once per group
+    and cached: collective, so every rank calls this at the same point) that enqueues
+    ncclAllReduce on the current stream itself, without ProcessGroupNCCL's side stream and its
+    two event waits per call; direct=False goes through torch.distributed.all_reduce.  Both are
+    marked graph_safe (ba_solve_sharded may replay its CG windows as HIP graphs).  Other
+    backends (gloo: the CPU tests and the same-GPU rehearsals) sum through a host copy."""
     import torch.distributed as dist
     if dist.get_backend(group) == "nccl":
-        def allreduce(t):
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        if direct:
+            import rccl
+            key = group if group is not None else dist.group.WORLD
+            comm = _rccl_comms.get(key)
+            if comm is None:
+                comm = _rccl_comms[key] = rccl.RcclComm(group)
+
+            def allreduce(t):
+                comm.allreduce_(t)
+            allreduce.comm = comm
+        else:
+            def allreduce(t):
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        allreduce.graph_safe = True
     else:
         def allreduce(t):
             h = t.cpu()
             dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
             t.copy_(h)
     return allreduce
+
+
+def release_allreduce(group=None):
+    """Destroys the RCCL communicator that make_allreduce opened for `group` (collective; call it
+    on every rank before torch.distributed.destroy_process_group)."""
+    import torch.distributed as dist
+    key = group if group is not None else dist.group.WORLD
+    comm = _rccl_comms.pop(key, None)
+    if comm is not None:
+        comm.close()
 
 
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,

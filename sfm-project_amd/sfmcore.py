@@ -60,6 +60,8 @@ class RansacParams(C.Structure):
 # stages of sfm_ba_solve_stage (include/sfmcore.h)
 (BA_STAGE_SETUP, BA_STAGE_SETUP_FINISH, BA_STAGE_ITER, BA_STAGE_ITER_FINISH, BA_STAGE_BACKSUB,
  BA_STAGE_MODEL, BA_STAGE_POLL) = range(7)
+# up to this many cameras ITER_FINISH is one k-free launch (ba_solve.hip FINISH_VEC_MAX_CAM)
+BA_FINISH_VEC_MAX_CAM = 1024
 
 _lib = None
 _lock = threading.Lock()
@@ -390,11 +392,14 @@ class Context:
         return dc, dp, info
 
     def ba_solve_sharded(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, allreduce,
-                         max_iter=100, tol=1e-10, out=None, poll=8):
+                         max_iter=100, tol=1e-10, out=None, poll=8, graph=False):
         """ba_solve on this rank's point shard (lin: ba_jtj of the shard with U / gc already
         all-reduced), driving sfm_ba_solve_stage: allreduce(t) sums the f64 device tensor t over
         all ranks in place, ordered on the current stream (reconstruction.make_allreduce).
-        Returns (dc, dp, info) like ba_solve."""
+        graph: replay the CG windows between polls as one HIP graph captured on the first
+        window after k = 0 (needs allreduce.graph_safe, i.e. RCCL; the capture costs about as much
+        as the launches it saves within one solve, profiles/r03/ba_sharded_ab.txt, so it is off
+        by default).  Returns (dc, dp, info) like ba_solve."""
         torch = self.torch
         U = lin["U"]
         dev = U.device
@@ -420,14 +425,46 @@ class Context:
         allreduce(comm[:44 * nc])
         stage(BA_STAGE_SETUP_FINISH)
         every = poll
-        for k in range(max_iter):
-            if every > 0 and k > 0 and k % every == 0:
+        # windows of `poll` iterations between host polls.  With a capturable collective (RCCL)
+        # every window after the first replays one HIP graph of its launches and all-reduces:
+        # the iteration kernels depend on k only through its parity and k > 0 (the one-launch
+        # finish counts iterations itself), so a window captured at k = poll replays at any
+        # k = m·poll, poll even.
+        graph = (graph and getattr(allreduce, "graph_safe", False) and every > 0
+                 and every % 2 == 0 and nc <= BA_FINISH_VEC_MAX_CAM)
+        win = every if every > 0 else max(max_iter, 1)
+        g = None
+        k = 0
+        while k < max_iter:
+            if every > 0 and k > 0:
                 stage(BA_STAGE_POLL)   # the same decision on every rank (replicated state)
                 if done.value:
                     break
-            stage(BA_STAGE_ITER, k)
-            allreduce(comm[:8 * nc])
-            stage(BA_STAGE_ITER_FINISH, k)
+            n = min(win, max_iter - k)
+            if graph and k > 0 and n == win:
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    cap = torch.cuda.Stream(dev)
+                    cap.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(cap):
+                        self._bind_stream()
+                        g.capture_begin()
+                        try:
+                            for j in range(n):
+                                stage(BA_STAGE_ITER, k + j)
+                                allreduce(comm[:8 * nc])
+                                stage(BA_STAGE_ITER_FINISH, k + j)
+                        finally:
+                            g.capture_end()
+                    torch.cuda.current_stream(dev).wait_stream(cap)
+                    self._bind_stream()
+                g.replay()
+            else:
+                for j in range(k, k + n):
+                    stage(BA_STAGE_ITER, j)
+                    allreduce(comm[:8 * nc])
+                    stage(BA_STAGE_ITER_FINISH, j)
+            k += n
         stage(BA_STAGE_BACKSUB)
         allreduce(comm[:2])
         stage(BA_STAGE_MODEL)

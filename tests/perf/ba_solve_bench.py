@@ -103,6 +103,7 @@ def main():
     tw = time.perf_counter()
     _, _, h2 = R.bundle_adjust(*args, max_iter=5, fixed=fixed, shard=True)
     t_sh = time.perf_counter() - tw
+    R.release_allreduce()
     dist.destroy_process_group()
     out["sharded_world1_rccl"] = {
         "cg_iter_ms": sh_it, "setup_backsub_ms": s0, "cg_iter_overhead_ms": sh_it - per_it,

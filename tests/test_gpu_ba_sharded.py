@@ -27,7 +27,7 @@ def tiny_problem():
     return synth.make_ba_problem(4, 2, obs_per_pt=3, seed=5, perturb=1e-3)
 
 
-def shard_solve(prob, rank, world, allreduce, lam=1e-3):
+def shard_solve(prob, rank, world, allreduce, lam=1e-3, **kw):
     """One sharded solve from the initial linearisation of `prob` on this rank's point shard."""
     import torch
     n_cam, n_pt = len(prob["cams"]), len(prob["pts"])
@@ -41,17 +41,18 @@ def shard_solve(prob, rank, world, allreduce, lam=1e-3):
     allreduce(lin["U"].view(-1))
     allreduce(lin["gc"].view(-1))
     dc, dp, info = P.ctx.ba_solve_sharded(lin, P.cam_idx, P.pt_idx, P.pt_ptr, P.cam_ptr,
-                                          P.cam_obs, lam, allreduce, max_iter=500, tol=1e-12)
+                                          P.cam_obs, lam, allreduce, **dict(dict(max_iter=500,
+                                                                                 tol=1e-12), **kw))
     return dc.cpu().numpy(), dp.cpu().numpy(), info.cpu().numpy(), lo, hi
 
 
-def _reference_solve(prob, lam=1e-3):
+def _reference_solve(prob, lam=1e-3, max_iter=500, tol=1e-12):
     import torch
     P = R.BAProblem(prob["pp"], prob["cam_idx"], prob["pt_idx"], prob["uv"], len(prob["cams"]),
                     len(prob["pts"]))
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()
     lin = P.linearize(T(prob["cams"]), T(prob["pts"]), 2.0)
-    return tuple(t.cpu().numpy() for t in P.solve(lin, lam, max_iter=500, tol=1e-12))
+    return tuple(t.cpu().numpy() for t in P.solve(lin, lam, max_iter=max_iter, tol=tol))
 
 
 def _free_port():
@@ -87,6 +88,38 @@ def test_ba_sharded_world1_rccl():
         np.testing.assert_allclose(cams, rcams, rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(pts, rpts, rtol=1e-9, atol=1e-12)
     finally:
+        R.release_allreduce()
+        dist.destroy_process_group()
+
+
+def test_ba_sharded_world1_graph_and_launch_modes():
+    """World-size-1 RCCL group: the CG windows replayed as HIP graphs (poll 8 and 4), launched
+    one by one (graph=False; odd poll, where no graph is used), with max_iter ending inside a
+    window, and the two-launch finish above 1024 cameras all reproduce sfm_ba_solve bit for
+    bit."""
+    import torch
+    import torch.distributed as dist
+    assert not dist.is_initialized()
+    prob = problem()
+    big = synth.make_ba_problem(1030, 2500, obs_per_pt=3, seed=3, perturb=1e-3)
+    refs = {(id(p), it): _reference_solve(p, max_iter=it) for p in (prob, big) for it in (500, 21)}
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        ar = R.make_allreduce()
+        assert ar.graph_safe
+        cases = [(prob, 500, dict(graph=True, poll=8)), (prob, 500, dict(graph=True, poll=4)),
+                 (prob, 500, dict(graph=False, poll=8)), (prob, 500, dict(poll=3)),
+                 (prob, 21, dict(graph=True, poll=4)), (prob, 21, dict(poll=0)),
+                 (big, 500, dict(poll=8)), (big, 21, dict(graph=True, poll=4))]
+        for p, it, kw in cases:
+            rdc, rdp, rinfo = refs[(id(p), it)]
+            dc, dp, info, _, _ = shard_solve(p, 0, 1, ar, max_iter=it, **kw)
+            np.testing.assert_array_equal(dc, rdc, err_msg=str((len(p["cams"]), it, kw)))
+            np.testing.assert_array_equal(dp, rdp, err_msg=str((len(p["cams"]), it, kw)))
+            assert info[0] == rinfo[0] and info[4] == rinfo[4], (info, rinfo, kw)
+    finally:
+        R.release_allreduce()
         dist.destroy_process_group()
 
 
