@@ -13,15 +13,15 @@
 //                       observations), its inverse (8x8 Cholesky) = the preconditioner, b, and
 //                       the CG start x = 0, r = b, z = M r, p = z
 //   CG iteration (3 launches, no host synchronisation; converged iterations exit at once):
-//     bas_pcg_point     8 lanes per point: t_p = V_d⁻¹ Σ_o W_oᵀ p_c     (SoA W, once)
-//     bas_pcg_camera    block per camera: q_c = U_d p_c - Σ_o W_o t_p   (SoA W, once)
+//     bas_pcg_point     8 lanes per point: t_p = V_d⁻¹ Σ_o W_oᵀ p_c (SoA W), u_o = W_o t_p
+//     bas_pcg_camera    block per camera: q_c = U_d p_c - Σ_o u_o       (64 B per observation)
 //     bas_pcg_vec       thread per camera component: α, x, r, z = M r, partial r·z, r·r
 //   sharded (sfm_ba_solve_stage): bas_pcg_point, bas_pcg_camera phase 1 (-> comm), the caller's
 //     all-reduce, then bas_pcg_finish_vec (q from comm, p·q, α and the vector update in one launch)
 //   bas_backsub        8 lanes per point: δp, and the point terms of gᵀδ and δᵀ(JᵀJ)δ
 //   bas_model           one block: gᵀδ, δᵀ(JᵀJ)δ (LM predicted decrease), iterations, |r|/|b|
-// HBM: a CG iteration reads W twice (2 x 192 B per observation) plus the camera/point vectors;
-// this stage is HBM-bound.
+// HBM: a CG iteration reads W once (192 B per observation), writes and reads u (2 x 64 B) plus
+// the camera/point vectors; this stage is HBM-bound.
 #include <algorithm>
 
 #include "sfm_internal.h"
@@ -97,15 +97,15 @@ __global__ __launch_bounds__(256) void bas_point_setup(int n_pt, const int32_t* 
     for (int i = 0; i < 3; ++i) g[i] = m[3 * i] * gg[0] + m[3 * i + 1] * gg[1] + m[3 * i + 2] * gg[2];
 }
 
-// Component-major (SoA) copies of W for the CG passes: Wp[24][n_obs] in observation (point-major)
-// order, Wc[24][n_obs] in camera-major order (cam_obs), ptc = pt_idx in camera-major order.  Each
-// pass then reads W with lane-contiguous 8-B loads instead of 192-B rows per lane; the copies
-// cost one read of W and two writes, once per solve.
+// Component-major (SoA) copy of W for the point-major passes: Wp[24][n_obs] in observation
+// (point-major) order, so bas_pcg_point and bas_backsub read W with lane-contiguous 8-B loads
+// instead of 192-B rows per lane; ptc = pt_idx in camera-major order (cam_obs) for the camera
+// setup.  The camera side never needs W again after the setup: the point pass hands it
+// u_o = W_o t_p (bas_pcg_point).
 __global__ __launch_bounds__(256) void bas_soa(int n_obs, const int32_t* __restrict__ cam_obs,
                                                const int32_t* __restrict__ pt_idx,
                                                const double* __restrict__ W,
-                                               double* __restrict__ Wp, double* __restrict__ Wc,
-                                               int32_t* __restrict__ ptc) {
+                                               double* __restrict__ Wp, int32_t* __restrict__ ptc) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n_obs) return;
     const size_t n = (size_t)n_obs;
@@ -116,15 +116,7 @@ __global__ __launch_bounds__(256) void bas_soa(int n_obs, const int32_t* __restr
         Wp[(2 * k) * n + e] = v.x;
         Wp[(2 * k + 1) * n + e] = v.y;
     }
-    const int o = cam_obs[e];
-    ptc[e] = pt_idx[o];
-    const double2* b = (const double2*)(W + 24 * (size_t)o);
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const double2 v = b[k];
-        Wc[(2 * k) * n + e] = v.x;
-        Wc[(2 * k + 1) * n + e] = v.y;
-    }
+    ptc[e] = pt_idx[cam_obs[e]];
 }
 
 // 8x8 SPD inverse via Cholesky (one thread; 500-ish cameras).  Returns false if not SPD.
@@ -168,7 +160,8 @@ __device__ bool inv8_spd(const double (&S)[64], double (&M)[64]) {
 // stops; after the all-reduce of comm, phase 2 takes the sums from comm (phase 0: unsharded).
 __global__ __launch_bounds__(CT) void bas_camera_setup(
     int n_cam, int n_obs, const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ ptc,
-    const double* __restrict__ U, const double* __restrict__ Wc, const double* __restrict__ Vinv,
+    const int32_t* __restrict__ cam_obs, const double* __restrict__ U,
+    const double* __restrict__ W, const double* __restrict__ Vinv,
     const double* __restrict__ vg, const double* __restrict__ gc, double lam,
     double* __restrict__ Ud, double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ pv,
@@ -190,8 +183,13 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
         const double* Vi = Vinv + 9 * (size_t)p;
         const double* g = vg + 3 * (size_t)p;
         double w[24], vi[9];
+        const double2* Wo = (const double2*)(W + 24 * (size_t)cam_obs[e]);  // the row, once per solve
 #pragma unroll
-        for (int k = 0; k < 24; ++k) w[k] = Wc[k * (size_t)n_obs + e];
+        for (int k = 0; k < 12; ++k) {
+            const double2 v = Wo[k];
+            w[2 * k] = v.x;
+            w[2 * k + 1] = v.y;
+        }
 #pragma unroll
         for (int k = 0; k < 9; ++k) vi[k] = Vi[k];
         double wv[24];  // W_o V_d⁻¹ (8x3)
@@ -268,8 +266,8 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
 //
 // Three launches per iteration k and no communication between the blocks of a launch (kernel
 // boundaries are the only grid-wide synchronisation, so no fences or flags):
-//   bas_pcg_point(k)   t = V_d⁻¹ Wᵀ p_k,   p_k = z_k + β_k p_{k-1} formed on the fly
-//   bas_pcg_camera(k)  p_k stored; q = U_d p_k - W t; per-camera p·q
+//   bas_pcg_point(k)   t = V_d⁻¹ Wᵀ p_k (p_k = z_k + β_k p_{k-1} formed on the fly), u_o = W_o t_p
+//   bas_pcg_camera(k)  p_k stored; q = U_d p_k - Σ_o u_o; per-camera p·q
 //   bas_pcg_vec(k)     α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera r·z, r·r
 // The CG scalars are fixed-order sums of the per-camera partials that every block recomputes with
 // the same code (canon_sum), so every block of every kernel sees bit-identical α, β and the same
@@ -351,13 +349,16 @@ __device__ Scalars pcg_scalars(int k, int n_cam, const double* __restrict__ rzc,
 constexpr int PG = SFM_BA_PG;  // lanes per point in the point-major passes
 
 // PG lanes per point: t_p = V_d⁻¹ Σ_o W_oᵀ p_c.  Lane j of a point takes its observations
-// j, j+PG, ... in order; the PG partial sums are combined by a fixed shuffle tree.
+// j, j+PG, ... in order; the PG partial sums are combined by a fixed butterfly (every lane gets
+// the same bits), and each lane then writes u_o = W_o t_p (8 doubles) for its observations: the
+// camera pass sums u_o instead of reading W a second time (64 B instead of 192 + 24 B per
+// observation and CG iteration).
 __global__ __launch_bounds__(256) void bas_pcg_point(
     int k, int n_pt, int n_cam, int n_obs, const int32_t* __restrict__ pt_ptr,
     const int32_t* __restrict__ cam_idx, const double* __restrict__ Wp,
     const double* __restrict__ Vinv, const double* __restrict__ z, const double* __restrict__ pold,
     const double* __restrict__ rzc, const double* __restrict__ rrc, double tol,
-    PcgState* __restrict__ st, double* __restrict__ t) {
+    PcgState* __restrict__ st, double* __restrict__ u) {
     __shared__ double red4[12];
     const int g = blockIdx.x * (blockDim.x / PG) + threadIdx.x / PG;
     const int j = threadIdx.x % PG;
@@ -414,29 +415,40 @@ __global__ __launch_bounds__(256) void bas_pcg_point(
     }
 #pragma unroll
     for (int off = PG / 2; off >= 1; off >>= 1) {
-        s0 += __shfl_down(s0, off, PG);
-        s1 += __shfl_down(s1, off, PG);
-        s2 += __shfl_down(s2, off, PG);
+        s0 += __shfl_xor(s0, off, PG);
+        s1 += __shfl_xor(s1, off, PG);
+        s2 += __shfl_xor(s2, off, PG);
     }
-    if (valid && j == 0) {
-        const double* Vi = Vinv + 9 * (size_t)g;
-        double* tp = t + 3 * (size_t)g;
-        tp[0] = Vi[0] * s0 + Vi[1] * s1 + Vi[2] * s2;
-        tp[1] = Vi[3] * s0 + Vi[4] * s1 + Vi[5] * s2;
-        tp[2] = Vi[6] * s0 + Vi[7] * s1 + Vi[8] * s2;
+    if (!has) return;
+    const double* Vi = Vinv + 9 * (size_t)g;
+    const double t0 = Vi[0] * s0 + Vi[1] * s1 + Vi[2] * s2;
+    const double t1 = Vi[3] * s0 + Vi[4] * s1 + Vi[5] * s2;
+    const double t2 = Vi[6] * s0 + Vi[7] * s1 + Vi[8] * s2;
+    auto put = [&](int o, const double (&wo)[24]) {
+        double uo[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) uo[i] = wo[3 * i] * t0 + wo[3 * i + 1] * t1 + wo[3 * i + 2] * t2;
+        double2* d = (double2*)(u + 8 * (size_t)o);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[i] = make_double2(uo[2 * i], uo[2 * i + 1]);
+    };
+    put(o0, w);
+    for (int o = o0 + PG; o < o1; o += PG) {  // points with more than PG observations
+#pragma unroll
+        for (int m = 0; m < 24; ++m) w[m] = Wp[m * n + o];
+        put(o, w);
     }
 }
 
 constexpr int CC = SFM_BA_CC;  // threads per camera block in the CG camera pass
 
-// Block per camera: p_k stored; q_c = U_d p_c - Σ_o W_o t_p; p_c·q_c.
-// Sharded solve: phase 1 writes the local Σ_o W_o t_p to comm[8c..] and stops; after the
+// Block per camera: p_k stored; q_c = U_d p_c - Σ_o u_o (u_o = W_o t_p, bas_pcg_point); p_c·q_c.
+// Sharded solve: phase 1 writes the local Σ_o u_o to comm[8c..] and stops; after the
 // all-reduce of comm, phase 2 finishes the camera from it (phase 0: unsharded).  Phase 3 (the
 // one-launch finish, bas_pcg_finish_vec): phase 1 plus U_d p_k into q and p_k into pv.
 __global__ __launch_bounds__(CC) void bas_pcg_camera(
-    int k, int n_cam, int n_obs, const int32_t* __restrict__ cam_ptr,
-    const int32_t* __restrict__ ptc, const double* __restrict__ Wc, const double* __restrict__ t,
-    const double* __restrict__ Ud, const double* __restrict__ z, double* __restrict__ pv,
+    int k, int n_cam, const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ cam_obs,
+    const double* __restrict__ u, const double* __restrict__ Ud, const double* __restrict__ z, double* __restrict__ pv,
     const PcgState* __restrict__ st, double* __restrict__ q, double* __restrict__ pq, int phase,
     double* __restrict__ comm) {
     __shared__ double red[CC / 64][8];
@@ -453,15 +465,15 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
     double acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.0;
-    const size_t n = (size_t)n_obs;
     const int e_end = phase == 2 ? 0 : cam_ptr[c + 1];
     for (int e = (phase == 2 ? 0 : cam_ptr[c]) + tid; e < e_end; e += CC) {
-        const double* Wo = Wc + e;
-        const double* tp = t + 3 * (size_t)ptc[e];
-        const double t0 = tp[0], t1 = tp[1], t2 = tp[2];
+        const double2* uo = (const double2*)(u + 8 * (size_t)cam_obs[e]);
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            acc[i] += Wo[(3 * i) * n] * t0 + Wo[(3 * i + 1) * n] * t1 + Wo[(3 * i + 2) * n] * t2;
+        for (int i = 0; i < 4; ++i) {
+            const double2 v = uo[i];
+            acc[2 * i] += v.x;
+            acc[2 * i + 1] += v.y;
+        }
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -815,7 +827,7 @@ __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const d
 // Device workspace of a solve (one carve for the unsharded solve and every stage of the sharded
 // one: the same sizes give the same pointers, so state persists across the stage calls).
 struct SolveWs {
-    double *Vinv, *vg, *t, *Ud, *Mc, *r, *z, *pv, *q, *rzc, *rrc, *pq, *mpart, *Wp, *Wc;
+    double *Vinv, *vg, *Ud, *Mc, *r, *z, *pv, *q, *rzc, *rrc, *pq, *mpart, *Wp, *u;
     PcgState* state;
     int32_t* bad;
     int32_t* ptc;
@@ -823,21 +835,21 @@ struct SolveWs {
 };
 
 static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, SolveWs& w) {
-    // workspace: Vinv 9 | vg 3 | t 3 per point; Ud 64 | M 64 | r z p q 8 each | rz, rr partials
-    // (2 parity slots each) | p·q per camera; backsub partials; state; bad flag
+    // workspace: Vinv 9 | vg 3 per point; Ud 64 | M 64 | r z p q 8 each | rz, rr partials
+    // (2 parity slots each) | p·q per camera; backsub partials; state; bad flag; per observation
+    // Wp 24 | u 8 doubles | ptc
     w.pblk = std::max(1, (n_pt + 255) / 256);
     const size_t np = (size_t)std::max(n_pt, 1), nc = (size_t)n_cam;
-    const size_t b_pt = sfm::align_up(sizeof(double) * 15 * np, 256);
+    const size_t b_pt = sfm::align_up(sizeof(double) * 12 * np, 256);
     const size_t b_cam = sfm::align_up(sizeof(double) * (128 + 32 + 5) * nc, 256);
     w.gblk = std::max(1, (n_pt + 256 / PG - 1) / (256 / PG));  // PG lanes per point
     const size_t b_part = sfm::align_up(sizeof(double) * 2 * (size_t)w.gblk, 256);
     const size_t no = (size_t)std::max(n_obs, 1);
-    const size_t b_soa = sfm::align_up(sizeof(double) * 48 * no + sizeof(int32_t) * no, 256);
+    const size_t b_soa = sfm::align_up(sizeof(double) * 32 * no + sizeof(int32_t) * no, 256);
     char* ws = (char*)sfm::workspace(ctx, b_pt + b_cam + b_part + 512 + b_soa);
     if (!ws) return SFM_ERR_NOMEM;
     w.Vinv = (double*)ws;
     w.vg = w.Vinv + 9 * np;
-    w.t = w.vg + 3 * np;
     w.Ud = (double*)(ws + b_pt);
     w.Mc = w.Ud + 64 * nc;
     w.r = w.Mc + 64 * nc;
@@ -851,8 +863,8 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     w.state = (PcgState*)(ws + b_pt + b_cam + b_part);
     w.bad = (int32_t*)(ws + b_pt + b_cam + b_part + 256);
     w.Wp = (double*)(ws + b_pt + b_cam + b_part + 512);
-    w.Wc = w.Wp + 24 * no;
-    w.ptc = (int32_t*)(w.Wc + 24 * no);
+    w.u = w.Wp + 24 * no;
+    w.ptc = (int32_t*)(w.u + 8 * no);
     w.vblk = (8 * n_cam + 255) / 256;
     return SFM_OK;
 }
@@ -871,11 +883,11 @@ static int solve_setup(hipStream_t st, const SolveWs& w, int32_t n_cam, int32_t 
     }
     if (n_obs > 0) {
         hipLaunchKernelGGL(bas_soa, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs, cam_obs,
-                           pt_idx, W, w.Wp, w.Wc, w.ptc);
+                           pt_idx, W, w.Wp, w.ptc);
         SFM_HIP_CHECK(hipGetLastError());
     }
     hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
-                       w.ptc, U, w.Wc, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
+                       w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
                        w.rzc, w.rrc, w.bad, phase, comm);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
@@ -931,9 +943,9 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
         }
         hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
                            pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol, w.state,
-                           w.t);
-        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
-                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 0, nullptr);
+                           w.u);
+        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
+                           cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 0, nullptr);
         hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
                            w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);
     }
@@ -977,18 +989,18 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
                            gc, gp, lam, dc, 1, comm);
     case SFM_BA_STAGE_SETUP_FINISH:
         hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
-                           w.ptc, U, w.Wc, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
-                           w.rzc, w.rrc, w.bad, 2, comm);
+                           w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z,
+                           w.pv, w.rzc, w.rrc, w.bad, 2, comm);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
         break;
     case SFM_BA_STAGE_ITER:  // -> comm[0, 8 n_cam)
         hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
                            pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol, w.state,
-                           w.t);
+                           w.u);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
-                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, fused ? 3 : 1,
+        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
+                           cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, fused ? 3 : 1,
                            comm);
         break;
     case SFM_BA_STAGE_ITER_FINISH:
@@ -998,8 +1010,8 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
                                w.state);
             break;
         }
-        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, n_obs, cam_ptr,
-                           w.ptc, w.Wc, w.t, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 2, comm);
+        hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
+                           cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 2, comm);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
                            w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);

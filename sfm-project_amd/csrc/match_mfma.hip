@@ -655,10 +655,14 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
                             mu_top2(tb[c + 1], ts[c + 1], acc1[r], acc1[r + 1]);
                         }
                         // column keys: 256 e + ccol (wraps only for padded-train rows, never merged)
+#ifdef MU_DIAG_NOKEY  // timing-only bound (wrong results): the column key build costs nothing
+                        const int a0 = acc0[r], a1 = acc1[r], b0 = acc0[r + 1], b1 = acc1[r + 1];
+#else
                         const int a0 = (int)(((unsigned)acc0[r] << 8) + (unsigned)ccol[c]);
                         const int a1 = (int)(((unsigned)acc1[r] << 8) + (unsigned)ccol[c + 1]);
                         const int b0 = (int)(((unsigned)acc0[r + 1] << 8) + (unsigned)ccol[c]);
                         const int b1 = (int)(((unsigned)acc1[r + 1] << 8) + (unsigned)ccol[c + 1]);
+#endif
                         colacc[r] = (c == 0) ? max(a0, a1) : vmax3(colacc[r], a0, a1);
                         colacc[r + 1] = (c == 0) ? max(b0, b1) : vmax3(colacc[r + 1], b0, b1);
                     }
@@ -710,7 +714,11 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
 #endif
         }
     }
+#ifdef MU_DIAG_NOMERGE  // timing-only bound (wrong results): no column-table merge at block end
+    if (false) {
+#else
     if (col_atomic) {
+#endif
         // merged across the pair's query blocks in place (zeroed before the launch; the grid
         // keeps every pair's blocks on one XCD, so the merge happens in that XCD's L2)
         unsigned long long* dst = colpart + (size_t)p * k_pad;

@@ -1,9 +1,10 @@
 """Times the bundle-adjustment step solve (K4) and a full LM step at cfg5 scale on one GPU.
 
 Usage: python tests/perf/ba_solve_bench.py [n_cam n_pt obs_per_pt [cg_iters]]
-Prints one JSON line: per-CG-iteration time and its HBM roofline (algorithmic bytes: W read twice
-= 384 B/obs + indices 12 B/obs + per point V_d⁻¹ 72 B, t 24 B written and read, pt_ptr 4 B),
-setup / back-substitution time, and one LM step (J^TJ + solve + update + trial cost).
+Prints one JSON line: per-CG-iteration time and its HBM roofline (algorithmic bytes: W read once
+= 192 B/obs, u_o = W_o t_p written and read = 128 B/obs, indices 8 B/obs, per point V_d⁻¹ 72 B and
+pt_ptr 4 B, per camera U_d, M and the CG vectors), setup / back-substitution time, and one LM step
+(J^TJ + solve + update + trial cost).
 """
 import json
 import os
@@ -49,7 +50,7 @@ def main():
     per_it = (tn - t0) / cg
     _, _, info = P.solve(lin, lam, max_iter=500, tol=1e-6)
     it6 = int(info[0].item())
-    bytes_it = n_obs * (384 + 12) + n_pt * (72 + 24 + 24 + 4) + n_cam * (64 * 8 + 4 * 8 * 8)
+    bytes_it = n_obs * (192 + 128 + 8) + n_pt * (72 + 4) + n_cam * (64 * 8 + 4 * 8 * 8)
 
     def lm_step():
         ln = P.linearize(cams, pts)
