@@ -397,6 +397,30 @@ __global__ __launch_bounds__(256) BA_JTJ_ATTR void ba_jtj_kernel(
     }
 }
 
+#ifdef BA_SEQ  // A/B variant: the two halves as two launches, each at its own register budget
+__global__ __launch_bounds__(256) void ba_cam_kernel(
+    int n_camw, const double* __restrict__ cams, const double* __restrict__ pp,
+    const double* __restrict__ pts, const int32_t* __restrict__ pt_idx,
+    const double* __restrict__ uv, const int32_t* __restrict__ cam_ptr,
+    const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
+    double* __restrict__ U, double* __restrict__ gc) {
+    const int cw = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (cw < n_camw)
+        camera_wave(cw, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U, gc);
+}
+__global__ __launch_bounds__(256) void ba_obs_kernel(
+    int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
+    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
+    const int32_t* __restrict__ pt_idx, const int32_t* __restrict__ pt_ptr,
+    const double* __restrict__ uv, double loss_s, double* __restrict__ W, double* __restrict__ res,
+    double* __restrict__ V, double* __restrict__ gp, double* __restrict__ seg,
+    int32_t* __restrict__ seg_pt, double* __restrict__ cost_blk) {
+    __shared__ double lds[4 * OBS_LDS];
+    obs_block(blockIdx.x, n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res, V, gp,
+              seg, seg_pt, cost_blk, lds);
+}
+#endif
+
 __device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
                              const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
                              const int32_t* __restrict__ seg_pt, double* __restrict__ V,
@@ -643,9 +667,18 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
 #else
     const int n_ob_launch = n_obsb;
 #endif
+#ifdef BA_SEQ
+    hipLaunchKernelGGL(ba_cam_kernel, dim3(n_camb), dim3(256), 0, st, n_camw, cams, pp, pts, pt_idx,
+                       uv, cam_ptr, cam_obs, loss_s, splits, part, U, gc);
+    if (n_ob_launch > 0)
+        hipLaunchKernelGGL(ba_obs_kernel, dim3(n_ob_launch), dim3(256), 0, st, n_obs, cams, pp, pts,
+                           cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res, V, gp, seg, seg_pt,
+                           cost_blk);
+#else
     hipLaunchKernelGGL(ba_jtj_kernel, dim3(n_camb + n_ob_launch), dim3(256), 0, st, n_camb, n_camw,
                        n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, cam_ptr, cam_obs, loss_s,
                        splits, part, U, gc, W, res, V, gp, seg, seg_pt, cost_blk);
+#endif
     SFM_HIP_CHECK(hipGetLastError());
     const int nw = n_obs > 0 ? n_wave : 0;
     const int n_fin = std::max(std::max((nw + 255) / 256, (n_pt + 255) / 256), 1);
