@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
                                                        uint8_t* __restrict__ nms,
                                                        int32_t* __restrict__ segcnt) {
     __shared__ __attribute__((aligned(16))) uint8_t P[PH][PW];
-    __shared__ int Hb[TH + 6][TW];
+    __shared__ __attribute__((aligned(16))) int Hb[TH + 6][TW];
     __shared__ uint8_t S[TH + 2][TW + 2];
     __shared__ int MX[PW][3], MY[PH][3];
     __shared__ __attribute__((aligned(4))) uint8_t Ob[TH][TW], On[TH][TW];  // blur / nms out
@@ -168,9 +168,13 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
                     const unsigned o0 = (unsigned)MY[r][0], o1 = (unsigned)MY[r][1];
                     const unsigned c0 = (unsigned)MX[c][0], c1 = (unsigned)MX[c][1];
                     const unsigned wx = (unsigned)MX[c][2], wy = (unsigned)MY[r][2];
+#ifdef ORB_ABL_FILL  // timing-only ablation: one source byte per pixel
+                    v[q] = img[o0 + c0] + (int)(wx + wy + o1 + c1) * 0;
+#else
                     const unsigned t0 = __umul24(img[o0 + c0], 2048u - wx) + __umul24(img[o0 + c1], wx);
                     const unsigned t1 = __umul24(img[o1 + c0], 2048u - wx) + __umul24(img[o1 + c1], wx);
                     v[q] = (int)((__umul24(t0, 2048u - wy) + __umul24(t1, wy) + (1u << 21)) >> 22);
+#endif
                 }
             }
         }
@@ -193,24 +197,31 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
             *(uint32_t*)(tpyr + __umul24((unsigned)r, (unsigned)pw) + (unsigned)c4) =
                 *(const uint32_t*)&P[r + 4][c4 + 4];
     }
-    {
-        constexpr int HN = ((TH + 6) * TW + 255) / 256;  // 10 (the last partly)
+    {   // four outputs per thread from three aligned dwords of the pyramid row: the 7 taps as two
+        // v_dot4_u32_u8 over byte windows cut by v_alignbyte (exact integer sums)
+        constexpr int HG = (TH + 6) * TW / 4, HN = (HG + 255) / 256;  // 608 groups, 3 passes
+        constexpr unsigned CA = 18u | 34u << 8 | 49u << 16 | 54u << 24;  // taps 0-3
+        constexpr unsigned CB = 49u | 34u << 8 | 18u << 16;              // taps 4-6 (+ 0)
 #pragma unroll
-        for (int q0 = 0; q0 < HN; q0 += 5) {
-            int v[5][7];
-#pragma unroll
-            for (int q = 0; q < 5; ++q) {
-                const int k = min(tid + (q0 + q) * 256, (TH + 6) * TW - 1);
-                const int r = k / TW, c = k - r * TW;
-#pragma unroll
-                for (int j = 0; j < 7; ++j) v[q][j] = P[r + 1][c + 1 + j];  // pixel (y0-3+r, x0+c-3+j)
-            }
-#pragma unroll
-            for (int q = 0; q < 5; ++q) {
-                const int k = tid + (q0 + q) * 256;
-                if (q0 + q < HN && k < (TH + 6) * TW)
-                    Hb[k / TW][k % TW] = 18 * v[q][0] + 34 * v[q][1] + 49 * v[q][2] + 54 * v[q][3] +
-                                         49 * v[q][4] + 34 * v[q][5] + 18 * v[q][6];
+        for (int q = 0; q < HN; ++q) {
+            const int g = tid + q * 256;
+            if (g < HG) {
+                const int r = g >> 4, c4 = (g & 15) * 4;  // output row r = pixel row y0-3+r
+                const uint32_t* pr = (const uint32_t*)&P[r + 1][c4];  // P cols c4 .. c4+11
+                const uint32_t d0 = pr[0], d1 = pr[1], d2 = pr[2];
+#ifdef ORB_ABL_HBLUR  // timing-only ablation: one tap
+                const int4 o = make_int4(d0 & 255, d1 & 255, d2 & 255, d0 >> 24);
+#else
+                int4 o;
+                o.x = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), CA,
+                          __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), CB, 0, false), false);
+                o.y = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), CA,
+                          __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), CB, 0, false), false);
+                o.z = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), CA,
+                          __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), CB, 0, false), false);
+                o.w = (int)__builtin_amdgcn_udot4(d1, CA, __builtin_amdgcn_udot4(d2, CB, 0, false), false);
+#endif
+                *(int4*)&Hb[r][c4] = o;
             }
         }
     }
@@ -244,7 +255,11 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
             const int nd = (c0 < -thr) + (c4 < -thr) + (c8 < -thr) + (c12 < -thr);
             const bool inside = gx >= EDGE && gx < w - EDGE && gy >= EDGE && gy < h - EDGE;
             S[r][c] = 0;
+#ifdef ORB_ABL_FAST  // timing-only ablation: no FAST candidates (compass still computed)
+            if (inside && (nb >= 2 || nd >= 2) && thr < 0) flist[atomicAdd(&fcount, 1)] = (uint16_t)k;
+#else
             if (inside && (nb >= 2 || nd >= 2)) flist[atomicAdd(&fcount, 1)] = (uint16_t)k;
+#endif
         }
         __syncthreads();
         const int nf = fcount;
@@ -283,9 +298,21 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
         for (int q = 0; q < 4; ++q) {
             const int r = (tid >> 6) + 4 * (q0 + q), c = lane;
 #pragma unroll
-            for (int j = 0; j < 7; ++j) hv[q][j] = Hb[r + j][c];
+            for (int j = 0; j < 7; ++j) {
+#ifdef ORB_ABL_VBLUR  // timing-only ablation: one tap
+                hv[q][j] = j == 3 ? Hb[r + 3][c] : 0;
+#else
+                hv[q][j] = Hb[r + j][c];
+#endif
+            }
 #pragma unroll
-            for (int j = 0; j < 9; ++j) sv[q][j] = S[r + j / 3][c + j % 3];
+            for (int j = 0; j < 9; ++j) {
+#ifdef ORB_ABL_NMS  // timing-only ablation: no neighbour reads
+                sv[q][j] = j == 4 ? S[r + 1][c + 1] : 0;
+#else
+                sv[q][j] = S[r + j / 3][c + j % 3];
+#endif
+            }
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
