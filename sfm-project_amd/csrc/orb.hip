@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
                                                        int32_t* __restrict__ segcnt) {
     __shared__ __attribute__((aligned(16))) uint8_t P[PH][PW];
     __shared__ __attribute__((aligned(16))) int Hb[TH + 6][TW];
-    __shared__ uint8_t S[TH + 2][TW + 2];
+    __shared__ __attribute__((aligned(4))) uint8_t S[TH + 2][TW + 4];  // 68-B rows: dword reads
     __shared__ int MX[PW][3], MY[PH][3];
     __shared__ __attribute__((aligned(4))) uint8_t Ob[TH][TW], On[TH][TW];  // blur / nms out
     __shared__ uint16_t flist[(TH + 2) * (TW + 2)];                          // FAST candidates
@@ -288,56 +288,55 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
         }
     }
     __syncthreads();
-    // 4. vertical blur and the strict 3x3 maximum of the tile; wave = one 64-pixel row segment
-    //    per step (lane = column): its survivors are counted for the candidate scatter
-    const int lane = tid & 63;
+    // 4. vertical blur and the strict 3x3 maximum, four columns per thread (16 threads per 64-pixel
+    //    row segment, 16 rows per pass): 7 int4 reads of the horizontal sums and two aligned dwords
+    //    of each of 3 score rows; the segment's survivors are counted for the candidate scatter
 #pragma unroll
-    for (int q0 = 0; q0 < TH / 4; q0 += 4) {
-        int hv[4][7], sv[4][9];
+    for (int q = 0; q < TH / 16; ++q) {
+        const int r = (tid >> 4) + 16 * q, c4 = (tid & 15) * 4;
+        int4 hv[7];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = (tid >> 6) + 4 * (q0 + q), c = lane;
+        for (int j = 0; j < 7; ++j) hv[j] = *(const int4*)&Hb[r + j][c4];
+        uint32_t sw[3][2];  // S row r+i, S cols c4 .. c4+7 = tile cols c4-1 .. c4+6
 #pragma unroll
-            for (int j = 0; j < 7; ++j) {
+        for (int i = 0; i < 3; ++i) {
+            sw[i][0] = *(const uint32_t*)&S[r + i][c4];
+            sw[i][1] = *(const uint32_t*)&S[r + i][c4 + 4];
+        }
+        int sb[3][6];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) sb[i][j] = (int)((sw[i][j >> 2] >> (8 * (j & 3))) & 255u);
+        uint32_t ob = 0, on = 0;
+        int cnt = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int hm[7] = {hv[0][m], hv[1][m], hv[2][m], hv[3][m], hv[4][m], hv[5][m], hv[6][m]};
 #ifdef ORB_ABL_VBLUR  // timing-only ablation: one tap
-                hv[q][j] = j == 3 ? Hb[r + 3][c] : 0;
+            const unsigned acc = __umul24((unsigned)hm[3], 256u);
 #else
-                hv[q][j] = Hb[r + j][c];
+            // hv <= 255 * 256: 24-bit products, the sum < 2^24 (exact)
+            const unsigned acc =
+                __umul24((unsigned)hm[0], 18u) + __umul24((unsigned)hm[1], 34u) +
+                __umul24((unsigned)hm[2], 49u) + __umul24((unsigned)hm[3], 54u) +
+                __umul24((unsigned)hm[4], 49u) + __umul24((unsigned)hm[5], 34u) +
+                __umul24((unsigned)hm[6], 18u);
 #endif
-            }
-#pragma unroll
-            for (int j = 0; j < 9; ++j) {
-#ifdef ORB_ABL_NMS  // timing-only ablation: no neighbour reads
-                sv[q][j] = j == 4 ? S[r + 1][c + 1] : 0;
-#else
-                sv[q][j] = S[r + j / 3][c + j % 3];
-#endif
-            }
+            ob |= ((acc + 32768u) >> 16) << (8 * m);
+            const int s0 = sb[1][m + 1];
+            const int nmax = max(max(max(sb[0][m], sb[0][m + 1]), max(sb[0][m + 2], sb[1][m])),
+                                 max(max(sb[1][m + 2], sb[2][m]), max(sb[2][m + 1], sb[2][m + 2])));
+            // strict maximum (a kept score is nonzero: only inside the EDGE border)
+            const bool keep = y0 + r < h && x0 + c4 + m < w && s0 != 0 && s0 > nmax;
+            on |= (keep ? (uint32_t)s0 : 0u) << (8 * m);
+            cnt += keep ? 1 : 0;
         }
+        *(uint32_t*)&Ob[r][c4] = ob;
+        *(uint32_t*)&On[r][c4] = on;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = (tid >> 6) + 4 * (q0 + q), c = lane;
-            const bool in = y0 + r < h && x0 + c < w;
-            bool keep = false;
-            if (in) {
-                // hv <= 255 * 256: 24-bit products, the sum < 2^24 (exact)
-                const unsigned acc =
-                    __umul24((unsigned)hv[q][0], 18u) + __umul24((unsigned)hv[q][1], 34u) +
-                    __umul24((unsigned)hv[q][2], 49u) + __umul24((unsigned)hv[q][3], 54u) +
-                    __umul24((unsigned)hv[q][4], 49u) + __umul24((unsigned)hv[q][5], 34u) +
-                    __umul24((unsigned)hv[q][6], 18u);
-                Ob[r][c] = (uint8_t)((acc + 32768u) >> 16);
-                const int s0 = sv[q][4];
-                keep = s0 != 0;  // nonzero only inside the EDGE border
-#pragma unroll
-                for (int j = 0; j < 9; ++j)
-                    if (j != 4 && sv[q][j] >= s0) keep = false;
-            }
-            On[r][c] = keep ? (uint8_t)sv[q][4] : (uint8_t)0;
-            const unsigned long long m = __ballot(keep);
-            if (lane == 0 && y0 + r < h)
-                tseg[__umul24((unsigned)r, (unsigned)L.ntx[l])] = __popcll(m);
-        }
+        for (int off = 8; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 16);
+        if ((tid & 15) == 0 && y0 + r < h) tseg[__umul24((unsigned)r, (unsigned)L.ntx[l])] = cnt;
     }
     __syncthreads();
 #pragma unroll
