@@ -72,6 +72,7 @@ constexpr int PW = TW + 8, PH = TH + 8;  // pyramid tile + 4-pixel halo (FAST 3 
 // circle differences: best over the 16 arcs of 9 of max(min d, min -d), with the arc minima by
 // min of three 3-runs — exactly the spec's arc loop (integer min/max, |d| <= 255).
 typedef short s2 __attribute__((ext_vector_type(2)));
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s2 smin(s2 a, s2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ s2 fast_score2(const s2 (&d)[16]) {
@@ -103,7 +104,8 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
     __shared__ __attribute__((aligned(16))) uint8_t P[PH][PW];
     __shared__ __attribute__((aligned(16))) int Hb[TH + 6][TW];
     __shared__ __attribute__((aligned(4))) uint8_t S[TH + 2][TW + 4];  // 68-B rows: dword reads
-    __shared__ int MX[PW][3], MY[PH][3];
+    __shared__ int MX[PW][3], MY[PH][3], GB[PW / 4];
+    __shared__ uint32_t MXs[PW][2];  // v_perm selectors of each column's two taps (fast fill)
     __shared__ __attribute__((aligned(4))) uint8_t Ob[TH][TW], On[TH][TW];  // blur / nms out
     __shared__ uint16_t flist[(TH + 2) * (TW + 2)];                          // FAST candidates
     __shared__ int fcount;
@@ -123,13 +125,35 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
     uint8_t* tpyr = pyr + tb;
     int32_t* tseg = segcnt + (size_t)blockIdx.y * L.segoff[L.nlev] + L.segoff[l] +
                     (int64_t)y0 * L.ntx[l] + tx0;
-    // 1. pyramid tile with halo (clamped coordinates)
+    // 1. pyramid tile with halo (clamped coordinates), four columns per thread: 720 groups of
+    //    4 pixels (18 per row).  Level 0: one dword load per group away from the image border.
+    //    Levels >= 1: the group's bilinear taps lie in a 16-byte window of each of its two source
+    //    rows (window start GB: its first column's c0, dword-aligned, at most W - 16), so a group
+    //    is two 16-byte loads; each pixel's two taps are cut from a window by two v_perm_b32 (the
+    //    per-column selectors, lo/hi 8 bytes, set up once per tile) into u16 lanes and weighted
+    //    by one v_dot2_u32_u16 - the same integer sum as the per-tap formula.  Tiles whose window
+    //    does not hold every tap (large scale factors) or images with W % 4 != 0 take the per-byte
+    //    path.
+    constexpr int NG = PH * PW / 4, GPR = PW / 4;  // 720 groups, 18 per row
+    const bool wal = (W & 3) == 0 && W >= 16;      // dword-aligned rows, a 16-byte window fits
+    int slow = 0;
     if (l > 0) {
+        int bad = 0;
         for (int k = tid; k < PW + PH; k += 256) {
             if (k < PW) {
                 const int cx = min(max(x0 - 4 + k, 0), w - 1);
                 const int32_t* m = maps + 3 * (L.mapx[l] + cx);
-                MX[k][0] = m[0]; MX[k][1] = m[1]; MX[k][2] = m[2];
+                const int c0 = m[0], c1 = m[1], wx = m[2];
+                MX[k][0] = c0; MX[k][1] = c1; MX[k][2] = wx;
+                const int cg = min(max(x0 - 4 + (k & ~3), 0), w - 1);
+                const int base = min(maps[3 * (L.mapx[l] + cg)] & ~3, W - 16);
+                const int k0 = c0 - base, k1 = c1 - base;
+                bad |= (k0 < 0 || k1 > 15) ? 1 : 0;
+                const unsigned lo0 = k0 < 8 ? k0 : 12, lo1 = k1 < 8 ? k1 : 12;  // 12: byte 0x00
+                const unsigned hi0 = k0 >= 8 ? k0 - 8 : 12, hi1 = k1 >= 8 ? k1 - 8 : 12;
+                MXs[k][0] = lo0 | 12u << 8 | lo1 << 16 | 12u << 24;
+                MXs[k][1] = hi0 | 12u << 8 | hi1 << 16 | 12u << 24;
+                if ((k & 3) == 0) GB[k >> 2] = base;
             } else {  // source rows as byte offsets (< 4095 * 4095 < 2^24)
                 const int r = k - PW, cy = min(max(y0 - 4 + r, 0), h - 1);
                 const int32_t* m = maps + 3 * (L.mapy[l] + cy);
@@ -138,9 +162,71 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
                 MY[r][2] = m[2];
             }
         }
-        __syncthreads();
+        slow = __syncthreads_or(bad) || !wal;
     }
-    {   // every load of the thread issued before any is used (the fill is latency-bound)
+    if (l > 0 && !slow) {
+        uint32_t A[3][4], B[3][4];
+        int gr[3], gcl[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {  // every load issued before any is used
+            const int g = min(tid + q * 256, NG - 1);
+            gr[q] = g / GPR;
+            gcl[q] = g - gr[q] * GPR;
+            const uint32_t* pa = (const uint32_t*)(img + (unsigned)MY[gr[q]][0] + (unsigned)GB[gcl[q]]);
+            const uint32_t* pb = (const uint32_t*)(img + (unsigned)MY[gr[q]][1] + (unsigned)GB[gcl[q]]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { A[q][i] = pa[i]; B[q][i] = pb[i]; }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if (tid + q * 256 >= NG) continue;
+            const unsigned wy = (unsigned)MY[gr[q]][2];
+            uint32_t out = 0;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int col = gcl[q] * 4 + m;
+                const uint32_t sl = MXs[col][0], sh = MXs[col][1], wx = (uint32_t)MX[col][2];
+                const uint32_t ta = __builtin_amdgcn_perm(A[q][1], A[q][0], sl) |
+                                    __builtin_amdgcn_perm(A[q][3], A[q][2], sh);
+                const uint32_t tb2 = __builtin_amdgcn_perm(B[q][1], B[q][0], sl) |
+                                     __builtin_amdgcn_perm(B[q][3], B[q][2], sh);
+                const uint32_t wv = (wx << 16) | (2048u - wx);
+                const unsigned t0 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, ta),
+                                                           __builtin_bit_cast(ushort2_t, wv), 0u, false);
+                const unsigned t1 = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, tb2),
+                                                           __builtin_bit_cast(ushort2_t, wv), 0u, false);
+#ifdef ORB_ABL_FILL  // timing-only ablation
+                const unsigned v = (t0 + t1) & 255u;
+#else
+                const unsigned v = (__umul24(t0, 2048u - wy) + __umul24(t1, wy) + (1u << 21)) >> 22;
+#endif
+                out |= v << (8 * m);
+            }
+            *(uint32_t*)&P[gr[q]][gcl[q] * 4] = out;
+        }
+    } else if (l == 0) {
+        uint32_t v[3];
+        int gr[3], gcl[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int g = min(tid + q * 256, NG - 1);
+            gr[q] = g / GPR;
+            gcl[q] = g - gr[q] * GPR;
+            const int cy = min(max(y0 - 4 + gr[q], 0), h - 1), cx = x0 - 4 + gcl[q] * 4;
+            const unsigned ro = __umul24((unsigned)cy, (unsigned)W);
+            if (wal && cx >= 0 && cx + 3 < w) {
+                v[q] = *(const uint32_t*)(img + ro + (unsigned)cx);
+            } else {
+                v[q] = 0;
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    v[q] |= (uint32_t)img[ro + (unsigned)min(max(cx + m, 0), w - 1)] << (8 * m);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            if (tid + q * 256 < NG) *(uint32_t*)&P[gr[q]][gcl[q] * 4] = v[q];
+    } else {  // per-byte bilinear (windows that do not fit, or W % 4 != 0)
         constexpr int PN = (PH * PW + 255) / 256;
         int v[PN], rr[PN], cc[PN];
         // (row, column) of k = tid + 256 q stepped without divisions: 256 = 3 PW + 40
@@ -159,23 +245,13 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
             v[q] = 0;
             if (k < PH * PW) {
                 const int r = rr[q], c = cc[q];
-                // 32-bit offsets off the image's uniform base (SGPR-base loads, no 64-bit
-                // address math per pixel); 24-bit products (every operand < 2^24: exact)
-                if (l == 0) {
-                    const int cy = min(max(y0 - 4 + r, 0), h - 1), cx = min(max(x0 - 4 + c, 0), w - 1);
-                    v[q] = img[__umul24((unsigned)cy, (unsigned)W) + (unsigned)cx];
-                } else {
-                    const unsigned o0 = (unsigned)MY[r][0], o1 = (unsigned)MY[r][1];
-                    const unsigned c0 = (unsigned)MX[c][0], c1 = (unsigned)MX[c][1];
-                    const unsigned wx = (unsigned)MX[c][2], wy = (unsigned)MY[r][2];
-#ifdef ORB_ABL_FILL  // timing-only ablation: one source byte per pixel
-                    v[q] = img[o0 + c0] + (int)(wx + wy + o1 + c1) * 0;
-#else
-                    const unsigned t0 = __umul24(img[o0 + c0], 2048u - wx) + __umul24(img[o0 + c1], wx);
-                    const unsigned t1 = __umul24(img[o1 + c0], 2048u - wx) + __umul24(img[o1 + c1], wx);
-                    v[q] = (int)((__umul24(t0, 2048u - wy) + __umul24(t1, wy) + (1u << 21)) >> 22);
-#endif
-                }
+                // 32-bit offsets off the image's uniform base; 24-bit products (exact)
+                const unsigned o0 = (unsigned)MY[r][0], o1 = (unsigned)MY[r][1];
+                const unsigned c0 = (unsigned)MX[c][0], c1 = (unsigned)MX[c][1];
+                const unsigned wx = (unsigned)MX[c][2], wy = (unsigned)MY[r][2];
+                const unsigned t0 = __umul24(img[o0 + c0], 2048u - wx) + __umul24(img[o0 + c1], wx);
+                const unsigned t1 = __umul24(img[o1 + c0], 2048u - wx) + __umul24(img[o1 + c1], wx);
+                v[q] = (int)((__umul24(t0, 2048u - wy) + __umul24(t1, wy) + (1u << 21)) >> 22);
             }
         }
 #pragma unroll
@@ -248,6 +324,10 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
             const int r = fr, c = fc;
             const int gy = y0 - 1 + r, gx = x0 - 1 + c;
             const int py = r + 3, px = c + 3;  // P coordinates of the pixel
+#ifdef ORB_ABL_COMPASS  // timing-only ablation: no compass test
+            S[r][c] = 0;
+            if (thr >= 0) continue;
+#endif
             const int cv = P[py][px];
             const int c0 = (int)P[py + 3][px] - cv, c4 = (int)P[py][px + 3] - cv;
             const int c8 = (int)P[py - 3][px] - cv, c12 = (int)P[py][px - 3] - cv;
