@@ -102,12 +102,15 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
                                                        uint8_t* __restrict__ nms,
                                                        int32_t* __restrict__ segcnt) {
     __shared__ __attribute__((aligned(16))) uint8_t P[PH][PW];
-    __shared__ __attribute__((aligned(16))) int Hb[TH + 6][TW];
+    __shared__ __attribute__((aligned(16))) uint16_t Hb[TH + 6][TW];  // horizontal sums <= 65280
     __shared__ __attribute__((aligned(4))) uint8_t S[TH + 2][TW + 4];  // 68-B rows: dword reads
     __shared__ int MX[PW][3], MY[PH][3], GB[PW / 4];
     __shared__ uint32_t MXs[PW][2];  // v_perm selectors of each column's two taps (fast fill)
-    __shared__ __attribute__((aligned(4))) uint8_t Ob[TH][TW], On[TH][TW];  // blur / nms out
-    __shared__ uint16_t flist[(TH + 2) * (TW + 2)];                          // FAST candidates
+    // FAST candidate list (phase 3), then the blur / nms output rows (phase 4) in the same bytes
+    __shared__ __attribute__((aligned(16))) uint16_t flist[(TH + 2) * (TW + 2)];
+    static_assert(sizeof(flist) >= 2 * TH * TW, "blur / nms rows alias the candidate list");
+    uint8_t (*Ob)[TW] = (uint8_t (*)[TW])flist;
+    uint8_t (*On)[TW] = (uint8_t (*)[TW])((uint8_t*)flist + TH * TW);
     __shared__ int fcount;
     const int tid = threadIdx.x;
     const int t = blockIdx.x;
@@ -286,18 +289,18 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
                 const uint32_t* pr = (const uint32_t*)&P[r + 1][c4];  // P cols c4 .. c4+11
                 const uint32_t d0 = pr[0], d1 = pr[1], d2 = pr[2];
 #ifdef ORB_ABL_HBLUR  // timing-only ablation: one tap
-                const int4 o = make_int4(d0 & 255, d1 & 255, d2 & 255, d0 >> 24);
+                const uint4 o = make_uint4(d0 & 255, d1 & 255, d2 & 255, d0 >> 24);
 #else
-                int4 o;
-                o.x = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), CA,
+                uint4 o;
+                o.x = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), CA,
                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), CB, 0, false), false);
-                o.y = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), CA,
+                o.y = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), CA,
                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), CB, 0, false), false);
-                o.z = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), CA,
+                o.z = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), CA,
                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), CB, 0, false), false);
-                o.w = (int)__builtin_amdgcn_udot4(d1, CA, __builtin_amdgcn_udot4(d2, CB, 0, false), false);
+                o.w = __builtin_amdgcn_udot4(d1, CA, __builtin_amdgcn_udot4(d2, CB, 0, false), false);
 #endif
-                *(int4*)&Hb[r][c4] = o;
+                *(uint2*)&Hb[r][c4] = make_uint2(o.x | o.y << 16, o.z | o.w << 16);
             }
         }
     }
@@ -307,39 +310,64 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
     //    but in most waves) are appended to an LDS list and scored densely, two per lane in the
     //    i16 halves of a register.
     {
-        constexpr int FT = (TH + 2) * (TW + 2), FN = (FT + 255) / 256;  // 9
+        // four pixels per thread (17 groups per ring row; the last group's columns 66, 67 lie
+        // outside the ring and never pass): 7 aligned dword reads cover the centres and the four
+        // compass points, cut by v_alignbyte; the tests run on i16 pairs (v_pk_sub_i16)
+        constexpr int GR = (TW + 4) / 4, FG = (TH + 2) * GR;  // 17, 578
         if (tid == 0) fcount = 0;
         __syncthreads();
-        int fr = tid / (TW + 2), fc = tid - fr * (TW + 2);  // stepped as in the fill
+        const s2 tp1 = {(short)(thr + 1), (short)(thr + 1)};
 #pragma unroll
-        for (int q = 0; q < FN; ++q) {
-            const int k = tid + q * 256;
-            if (q > 0) {
-                fc += 256 - (256 / (TW + 2)) * (TW + 2);
-                const bool wrap = fc >= TW + 2;
-                fc = wrap ? fc - (TW + 2) : fc;
-                fr += 256 / (TW + 2) + (wrap ? 1 : 0);
-            }
-            if (k >= FT) continue;
-            const int r = fr, c = fc;
-            const int gy = y0 - 1 + r, gx = x0 - 1 + c;
-            const int py = r + 3, px = c + 3;  // P coordinates of the pixel
+        for (int q = 0; q < (FG + 255) / 256; ++q) {
+            const int g = tid + q * 256;
+            if (g >= FG) continue;
+            const int r = g / GR, c4 = (g - r * GR) * 4;
+            const int py = r + 3;  // P row of the pixels; P cols c4+3 .. c4+6
+            const uint32_t* rc = (const uint32_t*)&P[py][c4];
+            const uint32_t* ru = (const uint32_t*)&P[py - 3][c4];
+            const uint32_t* rd = (const uint32_t*)&P[py + 3][c4];
+            const uint32_t d0 = rc[0], d1 = rc[1], d2 = rc[2];
+            const uint32_t u0 = ru[0], u1 = ru[1], w0 = rd[0], w1 = rd[1];
+            *(uint32_t*)&S[r][c4] = 0u;
 #ifdef ORB_ABL_COMPASS  // timing-only ablation: no compass test
-            S[r][c] = 0;
             if (thr >= 0) continue;
 #endif
-            const int cv = P[py][px];
-            const int c0 = (int)P[py + 3][px] - cv, c4 = (int)P[py][px + 3] - cv;
-            const int c8 = (int)P[py - 3][px] - cv, c12 = (int)P[py][px - 3] - cv;
-            const int nb = (c0 > thr) + (c4 > thr) + (c8 > thr) + (c12 > thr);
-            const int nd = (c0 < -thr) + (c4 < -thr) + (c8 < -thr) + (c12 < -thr);
-            const bool inside = gx >= EDGE && gx < w - EDGE && gy >= EDGE && gy < h - EDGE;
-            S[r][c] = 0;
+            const uint32_t cen = __builtin_amdgcn_alignbyte(d1, d0, 3);
+            const uint32_t nbr[4] = {__builtin_amdgcn_alignbyte(w1, w0, 3),   // point 0: row + 3
+                                     __builtin_amdgcn_alignbyte(d2, d1, 2),   // point 4: col + 3
+                                     __builtin_amdgcn_alignbyte(u1, u0, 3),   // point 8: row - 3
+                                     d0};                                     // point 12: col - 3
+            unsigned bits = 0;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {  // pixels (2 hf, 2 hf + 1) in the i16 lanes
+                const unsigned sel = hf ? 0x0c030c02u : 0x0c010c00u;
+                const s2 cv = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, cen, sel));
+                const s2 cb = cv + tp1, cd = cv - tp1;
+                s2 nb = {0, 0}, nd = {0, 0};  // number of compass points NOT brighter / darker
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const s2 nv = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, nbr[e], sel));
+                    nb += __builtin_bit_cast(s2, __builtin_bit_cast(ushort2_t, nv - cb) >> 15);
+                    nd += __builtin_bit_cast(s2, __builtin_bit_cast(ushort2_t, cd - nv) >> 15);
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int c = c4 + 2 * hf + m;  // ring column of the pixel
+                    const int gy = y0 - 1 + r, gx = x0 - 1 + c;
+                    const bool inside = c < TW + 2 && gx >= EDGE && gx < w - EDGE &&
+                                        gy >= EDGE && gy < h - EDGE;
+                    if (inside && (nb[m] <= 2 || nd[m] <= 2)) bits |= 1u << (2 * hf + m);
+                }
+            }
 #ifdef ORB_ABL_FAST  // timing-only ablation: no FAST candidates (compass still computed)
-            if (inside && (nb >= 2 || nd >= 2) && thr < 0) flist[atomicAdd(&fcount, 1)] = (uint16_t)k;
-#else
-            if (inside && (nb >= 2 || nd >= 2)) flist[atomicAdd(&fcount, 1)] = (uint16_t)k;
+            if (thr >= 0) bits = 0;
 #endif
+            if (bits) {
+                int o = atomicAdd(&fcount, __popc(bits));
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if (bits & (1u << m)) flist[o++] = (uint16_t)(r * (TW + 2) + c4 + m);
+            }
         }
         __syncthreads();
         const int nf = fcount;
@@ -374,9 +402,9 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
 #pragma unroll
     for (int q = 0; q < TH / 16; ++q) {
         const int r = (tid >> 4) + 16 * q, c4 = (tid & 15) * 4;
-        int4 hv[7];
+        uint2 hp[7];
 #pragma unroll
-        for (int j = 0; j < 7; ++j) hv[j] = *(const int4*)&Hb[r + j][c4];
+        for (int j = 0; j < 7; ++j) hp[j] = *(const uint2*)&Hb[r + j][c4];
         uint32_t sw[3][2];  // S row r+i, S cols c4 .. c4+7 = tile cols c4-1 .. c4+6
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -392,7 +420,9 @@ __global__ __launch_bounds__(256) void orb_tile_kernel(const uint8_t* __restrict
         int cnt = 0;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            const int hm[7] = {hv[0][m], hv[1][m], hv[2][m], hv[3][m], hv[4][m], hv[5][m], hv[6][m]};
+            int hm[7];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) hm[j] = (int)(((m < 2 ? hp[j].x : hp[j].y) >> (16 * (m & 1))) & 0xFFFFu);
 #ifdef ORB_ABL_VBLUR  // timing-only ablation: one tap
             const unsigned acc = __umul24((unsigned)hm[3], 256u);
 #else
