@@ -562,15 +562,17 @@ __device__ __forceinline__ int round_div(long long n, long long R2) {
     return (int)k;
 }
 
-// Block per (image, level), 256 threads.
-__global__ __launch_bounds__(256) void orb_select_kernel(
+// Block per (image, level), SELT threads: the grid is only (levels x images) blocks, so each
+// block is one CU's worth of waves — every phase is latency-bound per wave and runs 16-wide.
+constexpr int SELT = 1024, SELW = SELT / 64;
+__global__ __launch_bounds__(SELT) void orb_select_kernel(
     const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur, OrbLevels L,
     const int32_t* __restrict__ cand, const int32_t* __restrict__ ncand,
     const int32_t* __restrict__ pattern, int nfeat, float* __restrict__ slot_kp,
     uint8_t* __restrict__ slot_desc, int32_t* __restrict__ lvl_count) {
     __shared__ int hist[256];
     __shared__ int s_T, s_above, s_sel, s_ties;
-    __shared__ int wcnt[4][2];
+    __shared__ int wcnt[SELW][2];
     __shared__ unsigned sel_c[SEL_MAX];
     __shared__ long long sel_r[SEL_MAX];
     __shared__ int sel_i[SEL_MAX];
@@ -586,11 +588,11 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
     const int64_t tot = L.off[L.nlev];
     const uint8_t* lv = pyr + img * tot + L.off[l];
     const uint8_t* bl = blur + img * tot + L.off[l];
-    for (int k = tid; k < 1024; k += 256) s_pat[k] = pattern[k];
+    for (int k = tid; k < 1024; k += SELT) s_pat[k] = pattern[k];
     // ---- the 2 n_l best FAST scores: histogram threshold, ties in raster order ----
-    hist[tid] = 0;
+    if (tid < 256) hist[tid] = 0;
     __syncthreads();
-    for (int k = tid; k < nc; k += 256) atomicAdd(&hist[cd[k] & 255], 1);
+    for (int k = tid; k < nc; k += SELT) atomicAdd(&hist[cd[k] & 255], 1);
     __syncthreads();
     const int a = 2 * nl;
     if (tid == 0) {
@@ -606,7 +608,7 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
     __syncthreads();
     const int T = s_T, quota = a - s_above;
     const bool all = nc <= a;
-    for (int k0 = 0; k0 < nc; k0 += 256) {
+    for (int k0 = 0; k0 < nc; k0 += SELT) {
         const int k = k0 + tid;
         const int sc = k < nc ? (cd[k] & 255) : -1;
         const bool gt = k < nc && (all || sc > T);
@@ -630,8 +632,10 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
         }
         __syncthreads();
         if (tid == 0) {
-            s_ties += wcnt[0][0] + wcnt[1][0] + wcnt[2][0] + wcnt[3][0];
-            s_sel += wcnt[0][1] + wcnt[1][1] + wcnt[2][1] + wcnt[3][1];
+            int te = 0, ts = 0;
+            for (int q = 0; q < SELW; ++q) { te += wcnt[q][0]; ts += wcnt[q][1]; }
+            s_ties += te;
+            s_sel += ts;
         }
         __syncthreads();
     }
@@ -640,11 +644,11 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
     //      (the integer sums are order-free) ----
     int np2 = 1;
     while (np2 < n1) np2 <<= 1;
-    for (int k = n1 + tid; k < np2; k += 256) {
+    for (int k = n1 + tid; k < np2; k += SELT) {
         sel_r[k] = LLONG_MIN;
         sel_i[k] = k;
     }
-    for (int k = wv; k < n1; k += 4) {
+    for (int k = wv; k < n1; k += SELW) {
         const unsigned c = sel_c[k];
         const int y = (int)(c >> 20), x = (int)((c >> 8) & 4095u);
         int A = 0, B = 0, C = 0;  // |ix|, |iy| <= 1020: 49 squares < 2^31
@@ -671,7 +675,7 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
     // ---- bitonic sort: R descending, raster index ascending ----
     for (int size = 2; size <= np2; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int k = tid; k < np2; k += 256) {
+            for (int k = tid; k < np2; k += SELT) {
                 const int j = k ^ stride;
                 if (j > k) {
                     const bool up = (k & size) == 0;  // first element should precede
@@ -689,7 +693,7 @@ __global__ __launch_bounds__(256) void orb_select_kernel(
     const int n2 = min(n1, nl);
     // ---- orientation and descriptor of the n_l best: wave per keypoint (lanes over the disk,
     //      then over the 256 tests: four ballots give the eight descriptor words) ----
-    for (int k = wv; k < n2; k += 4) {
+    for (int k = wv; k < n2; k += SELW) {
         const unsigned c = sel_c[sel_i[k]];
         const int y = (int)(c >> 20), x = (int)((c >> 8) & 4095u);
         int a10 = 0, a01 = 0;  // |sum| <= 709 * 15 * 255 < 2^31
@@ -916,7 +920,7 @@ extern "C" int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img,
     hipLaunchKernelGGL(orb_cand_kernel, dim3((unsigned)((nrow + 3) / 4), (unsigned)n_img), dim3(256),
                        0, st, nms, L, segcnt, rowpos, cand);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(orb_select_kernel, dim3(nlev, n_img), dim3(256), 0, st, pyr, blur, L,
+    hipLaunchKernelGGL(orb_select_kernel, dim3(nlev, n_img), dim3(SELT), 0, st, pyr, blur, L,
                        cand, ncand, pattern, nfeat, skp, sdesc, lvl);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(orb_pack_kernel, dim3(n_img), dim3(256), 0, st, L, nfeat, skp, sdesc, lvl,

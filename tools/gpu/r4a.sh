@@ -1,0 +1,14 @@
+#!/bin/bash
+# ORB: select kernel with 1024-thread blocks (16 waves per (image, level)): ORB GPU
+# tests, then tile-kernel time (rocprofv3 stats, 32 images 1080p) interleaved with the previous build.
+set -o pipefail
+mkdir -p gpurun_out/r4a
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_orb.py > gpurun_out/r4a_pytest.log 2>&1 || exit 1
+for r in 1 2; do
+  for v in orbprev base; do
+    L=$PWD/sfm-project_amd/lib/libsfmcore_$v.so; [ $v = base ] && L=$PWD/sfm-project_amd/lib/libsfmcore.so
+    SFMCORE_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4a/${v}_$r -o run -- python3 tests/perf/orb_bench.py 32 > gpurun_out/r4a/${v}_$r.log 2>&1 || exit 1
+    python3 tools/orb_kstats.py gpurun_out/r4a/${v}_$r $v
+  done
+done
