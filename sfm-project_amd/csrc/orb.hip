@@ -562,6 +562,17 @@ __device__ __forceinline__ int round_div(long long n, long long R2) {
     return (int)k;
 }
 
+// The same value through a reciprocal root computed once per keypoint: |n / sqrt(R2)| <= 18.4 for
+// the pattern's points, so n * rinv + 1/2 is within 1e-13 of the exact value; when its fractional
+// part is farther than 1e-9 from an integer the floor is already exact, otherwise (rare) the
+// integer comparisons decide.
+__device__ __forceinline__ int round_div_fast(long long n, long long R2, double rinv) {
+    const double t = (double)n * rinv + 0.5;
+    const double fl = floor(t), f = t - fl;
+    if (f > 1e-9 && f < 1.0 - 1e-9) return (int)fl;
+    return round_div(n, R2);
+}
+
 // Block per (image, level), SELT threads: the grid is only (levels x images) blocks, so each
 // block is one CU's worth of waves — every phase is latency-bound per wave and runs 16-wide.
 constexpr int SELT = 1024, SELW = SELT / 64;
@@ -723,6 +734,7 @@ __global__ __launch_bounds__(SELT) void orb_select_kernel(
             kp[4] = (float)((double)sel_r[k] / 25.0);
             kp[5] = (float)l;
         }
+        const double rinv = R2 == 0 ? 0.0 : 1.0 / sqrt((double)R2);
         unsigned words[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -735,8 +747,8 @@ __global__ __launch_bounds__(SELT) void orb_select_kernel(
                     q[2 * e] = (int)px;
                     q[2 * e + 1] = (int)py;
                 } else {
-                    q[2 * e] = round_div(px * m10 - py * m01, R2);
-                    q[2 * e + 1] = round_div(px * m01 + py * m10, R2);
+                    q[2 * e] = round_div_fast(px * m10 - py * m01, R2, rinv);
+                    q[2 * e + 1] = round_div_fast(px * m01 + py * m10, R2, rinv);
                 }
             }
             const int i1 = bl[(size_t)(y + q[1]) * pw + x + q[0]];
