@@ -720,18 +720,20 @@ __global__ __launch_bounds__(256) void ransac_stats_kernel(int n_pairs, int n_hy
                                                            const int32_t* __restrict__ match_count,
                                                            const uint32_t* __restrict__ exec_w,
                                                            unsigned long long* __restrict__ acc) {
+    // wave per pair, grid-stride over the pairs (a few hundred blocks: three 64-bit atomics per
+    // block instead of per four pairs, which serialised on one L2 line)
     __shared__ unsigned long long se[4], sa[4], sn[4];
-    const int p = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63;
     unsigned long long ex = 0, al = 0, np = 0;
-    if (p < n_pairs) {
+    for (int p = blockIdx.x * 4 + (threadIdx.x >> 6); p < n_pairs; p += gridDim.x * 4) {
         const int M = match_count[p];
         if (M >= 8) {
             const int nw = n_hyp >> 6;
             for (int w = lane; w < nw; w += 64) ex += 64ull * exec_w[(size_t)p * nw + w];
             if (lane == 0) {
                 ex += (unsigned long long)n_hyp * (unsigned)min(PV, M) + (unsigned)M;
-                al = (unsigned long long)n_hyp * (unsigned)M;
-                np = 1;
+                al += (unsigned long long)n_hyp * (unsigned)M;
+                np += 1;
             }
         }
     }
@@ -858,8 +860,8 @@ static int ransac_batch(sfm_ctx* ctx, const T* kps, int32_t k_max, const int32_t
                            exec_w);
         if (exec_w) {
             SFM_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(ransac_stats_kernel, dim3((n_pairs + 3) / 4), dim3(256), 0, st,
-                               n_pairs, H, match_count, exec_w, ctx->rs_acc);
+            hipLaunchKernelGGL(ransac_stats_kernel, dim3(std::min((n_pairs + 3) / 4, 512)),
+                               dim3(256), 0, st, n_pairs, H, match_count, exec_w, ctx->rs_acc);
         }
     } else if constexpr (sizeof(T) == 4) {
         if (mode == 1)
