@@ -65,13 +65,22 @@ __device__ __forceinline__ void block_sum(double (&a)[N], double (*red)[N], doub
 
 // ---- setup -------------------------------------------------------------------------------------
 
+// Points with more observations than this are handled by a wave each in the CG point pass
+// (long tracks: with 8 lanes per point a wave would wait for its longest point).
+constexpr int LONG_OBS = 64;
+constexpr int LONG_BLOCKS = 64;  // extra point-pass blocks (4 waves each) that take the long points
+
 __global__ __launch_bounds__(256) void bas_point_setup(int n_pt, const int32_t* __restrict__ pt_ptr,
                                                        const double* __restrict__ V,
                                                        const double* __restrict__ gp, double lam,
                                                        double* __restrict__ Vinv,
-                                                       double* __restrict__ vg) {
+                                                       double* __restrict__ vg,
+                                                       int32_t* __restrict__ long_list,
+                                                       int32_t* __restrict__ long_cnt) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pt) return;
+    if (pt_ptr[p + 1] - pt_ptr[p] > LONG_OBS)  // order of the list is irrelevant (points independent)
+        long_list[atomicAdd(long_cnt, 1)] = p;
     double* Vi = Vinv + 9 * (size_t)p;
     double* g = vg + 3 * (size_t)p;
     if (pt_ptr[p + 1] == pt_ptr[p]) {  // unobserved point: δp = 0
@@ -348,19 +357,95 @@ __device__ Scalars pcg_scalars(int k, int n_cam, const double* __restrict__ rzc,
 #endif
 constexpr int PG = SFM_BA_PG;  // lanes per point in the point-major passes
 
+// Wave per long-track point (more than LONG_OBS observations; listed by bas_point_setup): lane j
+// takes observations j, j+64, ... in order, a 64-lane xor butterfly combines them, then the lanes
+// write u_o = W_o t_p for their observations.  The waves of the lb long-track blocks stride over
+// the list; every wave reaches the end of it.
+__device__ __forceinline__ void pcg_point_long(int b, int lb, int n_obs,
+                                               const int32_t* __restrict__ pt_ptr,
+                                               const int32_t* __restrict__ cam_idx,
+                                               const double* __restrict__ Wp,
+                                               const double* __restrict__ Vinv,
+                                               const double* __restrict__ z,
+                                               const double* __restrict__ pold, double beta,
+                                               const int32_t* __restrict__ long_list,
+                                               const int32_t* __restrict__ long_cnt,
+                                               double* __restrict__ u) {
+    const int lane = threadIdx.x & 63;
+    const int nl = *long_cnt;
+    const size_t n = (size_t)n_obs;
+    for (int wv = b * 4 + (threadIdx.x >> 6); wv < nl; wv += lb * 4) {
+        const int g = long_list[wv];
+        const int o0 = pt_ptr[g], o1 = pt_ptr[g + 1];
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        for (int o = o0 + lane; o < o1; o += 64) {
+            const double* Wo = Wp + o;
+            const int c = cam_idx[o];
+            const double* zp = z + 8 * (size_t)c;
+            const double* pp = pold + 8 * (size_t)c;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const double xi = zp[i] + beta * pp[i];  // p_k, as in bas_pcg_point
+                s0 += Wo[(3 * i) * n] * xi;
+                s1 += Wo[(3 * i + 1) * n] * xi;
+                s2 += Wo[(3 * i + 2) * n] * xi;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            s0 += __shfl_xor(s0, off, 64);
+            s1 += __shfl_xor(s1, off, 64);
+            s2 += __shfl_xor(s2, off, 64);
+        }
+        const double* Vi = Vinv + 9 * (size_t)g;
+        const double t0 = Vi[0] * s0 + Vi[1] * s1 + Vi[2] * s2;
+        const double t1 = Vi[3] * s0 + Vi[4] * s1 + Vi[5] * s2;
+        const double t2 = Vi[6] * s0 + Vi[7] * s1 + Vi[8] * s2;
+        for (int o = o0 + lane; o < o1; o += 64) {
+            const double* Wo = Wp + o;
+            double uo[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                uo[i] = Wo[(3 * i) * n] * t0 + Wo[(3 * i + 1) * n] * t1 + Wo[(3 * i + 2) * n] * t2;
+            double2* d = (double2*)(u + 8 * (size_t)o);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d[i] = make_double2(uo[2 * i], uo[2 * i + 1]);
+        }
+    }
+}
+
 // PG lanes per point: t_p = V_d⁻¹ Σ_o W_oᵀ p_c.  Lane j of a point takes its observations
 // j, j+PG, ... in order; the PG partial sums are combined by a fixed butterfly (every lane gets
 // the same bits), and each lane then writes u_o = W_o t_p (8 doubles) for its observations: the
 // camera pass sums u_o instead of reading W a second time (64 B instead of 192 + 24 B per
-// observation and CG iteration).
+// observation and CG iteration).  Points with more than LONG_OBS observations are left to the
+// grid's first n_long_blk blocks, a wave per point (pcg_point_long).
 __global__ __launch_bounds__(256) void bas_pcg_point(
     int k, int n_pt, int n_cam, int n_obs, const int32_t* __restrict__ pt_ptr,
     const int32_t* __restrict__ cam_idx, const double* __restrict__ Wp,
     const double* __restrict__ Vinv, const double* __restrict__ z, const double* __restrict__ pold,
     const double* __restrict__ rzc, const double* __restrict__ rrc, double tol,
-    PcgState* __restrict__ st, double* __restrict__ u) {
+    PcgState* __restrict__ st, double* __restrict__ u, int n_long_blk,
+    const int32_t* __restrict__ long_list, const int32_t* __restrict__ long_cnt) {
     __shared__ double red4[12];
-    const int g = blockIdx.x * (blockDim.x / PG) + threadIdx.x / PG;
+    // every block computes the same CG scalars; block 0 publishes them for the camera and vector
+    // kernels of this iteration (the kernel boundary orders the store before their reads)
+    auto publish = [&](const Scalars& sc) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->beta = sc.beta;
+            st->rz = sc.rz;
+            st->done = sc.done ? 1 : 0;
+        }
+    };
+    if ((int)blockIdx.x < n_long_blk) {  // block-uniform: the long-track blocks, dispatched first
+        const Scalars sc = pcg_scalars(k, n_cam, rzc, rrc, st->bb, tol, red4);
+        publish(sc);
+        if (!sc.done)
+            pcg_point_long(blockIdx.x, n_long_blk, n_obs, pt_ptr, cam_idx, Wp, Vinv, z, pold,
+                           sc.beta, long_list, long_cnt, u);
+        return;
+    }
+    const int g = (blockIdx.x - n_long_blk) * (blockDim.x / PG) + threadIdx.x / PG;
     const int j = threadIdx.x % PG;
     const bool valid = g < n_pt;
     const int o0 = (valid ? pt_ptr[g] : 0) + j;
@@ -382,14 +467,9 @@ __global__ __launch_bounds__(256) void bas_pcg_point(
         }
     }
     const Scalars sc = pcg_scalars(k, n_cam, rzc, rrc, st->bb, tol, red4);
-    // every block computed the same scalars; block 0 publishes them for the camera and vector
-    // kernels of this iteration (the kernel boundary orders the store before their reads)
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->beta = sc.beta;
-        st->rz = sc.rz;
-        st->done = sc.done ? 1 : 0;
-    }
+    publish(sc);
     if (sc.done) return;
+    if (valid && o1 - (o0 - j) > LONG_OBS) return;  // group-uniform: a long-track block's point
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     if (has) {
 #pragma unroll
@@ -830,6 +910,9 @@ struct SolveWs {
     double *Vinv, *vg, *Ud, *Mc, *r, *z, *pv, *q, *rzc, *rrc, *pq, *mpart, *Wp, *u;
     PcgState* state;
     int32_t* bad;
+    int32_t* long_cnt;   // long-track points (bas_point_setup)
+    int32_t* long_list;
+    int lblk;            // long-track blocks ahead of the point pass's point blocks
     int32_t* ptc;
     int pblk, gblk, vblk;
 };
@@ -840,7 +923,7 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     // Wp 24 | u 8 doubles | ptc
     w.pblk = std::max(1, (n_pt + 255) / 256);
     const size_t np = (size_t)std::max(n_pt, 1), nc = (size_t)n_cam;
-    const size_t b_pt = sfm::align_up(sizeof(double) * 12 * np, 256);
+    const size_t b_pt = sfm::align_up(sizeof(double) * 12 * np + sizeof(int32_t) * np, 256);
     const size_t b_cam = sfm::align_up(sizeof(double) * (128 + 32 + 5) * nc, 256);
     w.gblk = std::max(1, (n_pt + 256 / PG - 1) / (256 / PG));  // PG lanes per point
     const size_t b_part = sfm::align_up(sizeof(double) * 2 * (size_t)w.gblk, 256);
@@ -850,6 +933,7 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     if (!ws) return SFM_ERR_NOMEM;
     w.Vinv = (double*)ws;
     w.vg = w.Vinv + 9 * np;
+    w.long_list = (int32_t*)(w.vg + 3 * np);
     w.Ud = (double*)(ws + b_pt);
     w.Mc = w.Ud + 64 * nc;
     w.r = w.Mc + 64 * nc;
@@ -862,6 +946,8 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     w.mpart = (double*)(ws + b_pt + b_cam);
     w.state = (PcgState*)(ws + b_pt + b_cam + b_part);
     w.bad = (int32_t*)(ws + b_pt + b_cam + b_part + 256);
+    w.long_cnt = w.bad + 1;
+    w.lblk = n_obs > LONG_OBS ? LONG_BLOCKS : 0;
     w.Wp = (double*)(ws + b_pt + b_cam + b_part + 512);
     w.u = w.Wp + 24 * no;
     w.ptc = (int32_t*)(w.u + 8 * no);
@@ -875,10 +961,10 @@ static int solve_setup(hipStream_t st, const SolveWs& w, int32_t n_cam, int32_t 
                        const int32_t* cam_obs, const double* U, const double* V, const double* W,
                        const double* gc, const double* gp, double lam, double* dc, int phase,
                        double* comm) {
-    SFM_HIP_CHECK(hipMemsetAsync(w.bad, 0, sizeof(int32_t), st));
+    SFM_HIP_CHECK(hipMemsetAsync(w.bad, 0, 2 * sizeof(int32_t), st));  // bad flag, long count
     if (n_pt > 0) {
         hipLaunchKernelGGL(bas_point_setup, dim3(w.pblk), dim3(256), 0, st, n_pt, pt_ptr, V, gp,
-                           lam, w.Vinv, w.vg);
+                           lam, w.Vinv, w.vg, w.long_list, w.long_cnt);
         SFM_HIP_CHECK(hipGetLastError());
     }
     if (n_obs > 0) {
@@ -941,9 +1027,9 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
             if (prc != SFM_OK) return prc;
             if (done) break;
         }
-        hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
-                           pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol, w.state,
-                           w.u);
+        hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk + w.lblk), dim3(256), 0, st, k, n_pt, n_cam,
+                           n_obs, pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol,
+                           w.state, w.u, w.lblk, w.long_list, w.long_cnt);
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
                            cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 0, nullptr);
         hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
@@ -995,9 +1081,9 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
         hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
         break;
     case SFM_BA_STAGE_ITER:  // -> comm[0, 8 n_cam)
-        hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk), dim3(256), 0, st, k, n_pt, n_cam, n_obs,
-                           pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol, w.state,
-                           w.u);
+        hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk + w.lblk), dim3(256), 0, st, k, n_pt, n_cam,
+                           n_obs, pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol,
+                           w.state, w.u, w.lblk, w.long_list, w.long_cnt);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
                            cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, fused ? 3 : 1,

@@ -147,7 +147,8 @@ def unordered_pairs(n_img: int) -> np.ndarray:
 
 def make_ba_problem(n_cam: int, n_pt: int, obs_per_pt: int = 5, seed: int = 0,
                     noise_px: float = 0.5, perturb: float = 1e-3) -> dict:
-    """Bundle-adjustment observations: each point seen by `obs_per_pt` cameras.
+    """Bundle-adjustment observations: each point seen by `obs_per_pt` cameras
+    (an int, or one count per point).
 
     Observations are grouped by point (point-major), the layout the BA kernels shard on.
     Camera/point parameters are perturbed from the truth so residuals are non-trivial.
@@ -157,11 +158,11 @@ def make_ba_problem(n_cam: int, n_pt: int, obs_per_pt: int = 5, seed: int = 0,
     cams_true = sc["cams"]
     pp = sc["pp"]
     pts_true = rng.uniform(-2.0, 2.0, size=(n_pt, 3))
-    cam_idx = np.empty((n_pt, obs_per_pt), np.int32)
-    for p in range(n_pt):
-        cam_idx[p] = rng.choice(n_cam, size=obs_per_pt, replace=False)
-    cam_idx = np.sort(cam_idx, axis=1).reshape(-1)
-    pt_idx = np.repeat(np.arange(n_pt, dtype=np.int32), obs_per_pt)
+    # obs_per_pt: one count for every point, or a count per point (long and short tracks mixed)
+    counts = np.broadcast_to(np.asarray(obs_per_pt, np.int64), (n_pt,))
+    cam_idx = np.concatenate([np.sort(rng.choice(n_cam, size=int(counts[p]), replace=False))
+                              for p in range(n_pt)] or [np.zeros(0, np.int64)]).astype(np.int32)
+    pt_idx = np.repeat(np.arange(n_pt, dtype=np.int32), counts)
     uv = np.empty((cam_idx.size, 2))
     Rs = [angle_axis_to_rotmat(c[:3]) for c in cams_true]
     for c in range(n_cam):

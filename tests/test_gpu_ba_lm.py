@@ -47,6 +47,28 @@ def test_solve_matches_oracle(lam, loss_s):
     assert abs(info[2] - gd) <= 1e-11 * abs(gd) and abs(info[3] - q) <= 1e-11 * abs(q)
 
 
+def test_solve_long_tracks_match_oracle():
+    """Points with more than 64 observations (taken by the point pass's long-track blocks, a wave
+    per point) mixed with short ones in the same blocks: δ as the oracle's PCG and the dense
+    solve."""
+    counts = np.where(np.arange(90) % 7 == 0, 100 + np.arange(90) % 50, 4)
+    prob = synth.make_ba_problem(160, 90, obs_per_pt=counts, seed=29, perturb=2e-3)
+    assert (np.bincount(prob["pt_idx"]) > 64).sum() == 13
+    P, _, _, lin = _problem(prob, 2.0)
+    dc, dp, info = P.solve(lin, 1e-3, max_iter=500, tol=1e-12)
+    dc, dp, info = dc.cpu().numpy(), dp.cpu().numpy(), info.cpu().numpy()
+    o = O.ba_jtj(prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"],
+                 prob["uv"], 2.0)
+    args = (o["U"], o["V"], o["W"], o["gc"], o["gp"], prob["cam_idx"], prob["pt_idx"])
+    odc, odp, oit, _ = L.schur_pcg(*args, 1e-3, max_iter=500, tol=1e-12)
+    ddc, ddp = L.solve_dense(*args, 1e-3)
+    assert info[1] <= 1e-12 and abs(info[0] - oit) <= 3 and info[4] == 0
+    for a, b in ((dc, odc), (dc, ddc)):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-8 * np.abs(b).max())
+    for a, b in ((dp, odp), (dp, ddp)):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-8 * np.abs(b).max())
+
+
 def test_solve_unobserved_camera_and_point():
     prob = synth.make_ba_problem(5, 60, obs_per_pt=3, seed=5)
     for k in ("cams", "pp", "pts"):

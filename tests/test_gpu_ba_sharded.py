@@ -95,14 +95,17 @@ def test_ba_sharded_world1_rccl():
 def test_ba_sharded_world1_graph_and_launch_modes():
     """World-size-1 RCCL group: the CG windows replayed as HIP graphs (poll 8 and 4), launched
     one by one (graph=False; odd poll, where no graph is used), with max_iter ending inside a
-    window, and the two-launch finish above 1024 cameras all reproduce sfm_ba_solve bit for
-    bit."""
+    window, the two-launch finish above 1024 cameras and long tracks (more than 64 observations
+    per point) all reproduce sfm_ba_solve bit for bit."""
     import torch
     import torch.distributed as dist
     assert not dist.is_initialized()
     prob = problem()
     big = synth.make_ba_problem(1030, 2500, obs_per_pt=3, seed=3, perturb=1e-3)
-    refs = {(id(p), it): _reference_solve(p, max_iter=it) for p in (prob, big) for it in (500, 21)}
+    counts = np.where(np.arange(120) % 9 == 0, 90, 4)  # long tracks: the point pass's wave path
+    mixed = synth.make_ba_problem(140, 120, obs_per_pt=counts, seed=8, perturb=1e-3)
+    refs = {(id(p), it): _reference_solve(p, max_iter=it)
+            for p in (prob, big, mixed) for it in (500, 21)}
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
@@ -111,7 +114,8 @@ def test_ba_sharded_world1_graph_and_launch_modes():
         cases = [(prob, 500, dict(graph=True, poll=8)), (prob, 500, dict(graph=True, poll=4)),
                  (prob, 500, dict(graph=False, poll=8)), (prob, 500, dict(poll=3)),
                  (prob, 21, dict(graph=True, poll=4)), (prob, 21, dict(poll=0)),
-                 (big, 500, dict(poll=8)), (big, 21, dict(graph=True, poll=4))]
+                 (big, 500, dict(poll=8)), (big, 21, dict(graph=True, poll=4)),
+                 (mixed, 500, dict(poll=8)), (mixed, 21, dict(graph=True, poll=4))]
         for p, it, kw in cases:
             rdc, rdp, rinfo = refs[(id(p), it)]
             dc, dp, info, _, _ = shard_solve(p, 0, 1, ar, max_iter=it, **kw)
