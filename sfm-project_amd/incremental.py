@@ -135,7 +135,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     tk = time.perf_counter()
     n_img = len(desc)
     intr = np.asarray(intr, np.float64)
-    pairs = np.array([(a, b) for a in range(n_img) for b in range(a + 1, n_img)], np.int32)
+    pairs = np.stack(np.triu_indices(n_img, 1), axis=1).astype(np.int32)  # (a < b), a-major
     gb = match_graph.GraphBuilder(desc, kps, n_kp, device=device)
     pairs_t = torch.from_numpy(pairs).to(dev)
     rows, inl = _match_graph(gb, pairs, pairs_t, n_kp, group)
