@@ -126,8 +126,9 @@ class Runner:
             if ranges is None:
                 rows_l.append(self.gb.graph_rows(base, count, match, rs))
             else:
-                rows, offs = self.gb.graph_rows(base, count, match, rs, return_offsets=True)
-                c, pk = match_graph.pack_rows(rows, offs)
+                pk, offs = self.gb.graph_rows(base, count, match, rs, return_offsets=True,
+                                              packed=True)
+                c = (offs[1:] - offs[:-1]).to(torch.int32)
                 cnt_l.append(c)
                 pk_l.append(pk)
         if ranges is None:

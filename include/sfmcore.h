@@ -149,6 +149,21 @@ int sfm_graph_rows(sfm_ctx* ctx, int32_t n_pairs, int32_t k_max, int32_t pair_ba
                    const int32_t* match_count, const int32_t* matches, const uint8_t* mask,
                    const int32_t* inl_count, int32_t min_inliers, const int64_t* offsets,
                    int32_t* out_rows);
+/* The multi-GPU exchange form of the same graph (the graph all-gather):
+ *   sfm_graph_rows_packed: out_packed [total] u32 = queryIdx << 16 | trainIdx (k_max <= 65536),
+ *                          same order and offsets as sfm_graph_rows.
+ *   sfm_graph_expand:      rows of n_pairs consecutive pairs back to [total][3] i32: pair p's
+ *                          counts[p] packed rows start at packed[src_offsets[p]] (e.g. inside
+ *                          the padded per-rank slots of an all-gather) and are written at row
+ *                          dst_offsets[p] as (pair_base + p, queryIdx, trainIdx).
+ */
+int sfm_graph_rows_packed(sfm_ctx* ctx, int32_t n_pairs, int32_t k_max,
+                          const int32_t* match_count, const int32_t* matches, const uint8_t* mask,
+                          const int32_t* inl_count, int32_t min_inliers, const int64_t* offsets,
+                          uint32_t* out_packed);
+int sfm_graph_expand(sfm_ctx* ctx, int32_t n_pairs, int32_t pair_base, const int32_t* counts,
+                     const int64_t* src_offsets, const int64_t* dst_offsets,
+                     const uint32_t* packed, int32_t* out_rows);
 
 /* ---- bundle-adjustment linearisation ---------------------------------------------------------
  * Fills the empty code/3d_reconstruction.py (import commented out at code/pipeline.py:4) with the

@@ -5,7 +5,11 @@
 //
 // Two entry points so the caller can size the output between them:
 //   sfm_graph_offsets: one block, exclusive scan of the per-pair verified inlier counts -> [P+1]
-//   sfm_graph_rows:    one block per pair, ordered ballot compaction of the inlier mask.
+//   sfm_graph_rows:    one block per pair, ordered ballot compaction of the inlier mask
+//                      (packed = 1: 4-byte rows queryIdx << 16 | trainIdx, the exchange format).
+// Multi-GPU: every rank writes its rows packed, the ranks all-gather them, and
+//   sfm_graph_expand:  one block per pair turns the gathered packed rows back into [n][3] rows,
+//                      reading each pair's rows at its source offset in the gathered buffer.
 #include "match_common.h"
 #include "sfm_internal.h"
 
@@ -48,7 +52,7 @@ __global__ __launch_bounds__(256) void graph_rows_kernel(
     int k_max, int pair_base, const int32_t* __restrict__ match_count,
     const int32_t* __restrict__ matches, const uint8_t* __restrict__ mask,
     const int32_t* __restrict__ inl, int min_inl, const int64_t* __restrict__ offsets,
-    int32_t* __restrict__ rows) {
+    int32_t* __restrict__ rows, int packed) {
     __shared__ int wsum[4];
     const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (inl[p] < min_inl) return;  // block-uniform
@@ -69,7 +73,9 @@ __global__ __launch_bounds__(256) void graph_rows_kernel(
             off += (w < wave) ? wsum[w] : 0;
             tot += wsum[w];
         }
-        if (keep) {
+        if (keep && packed) {
+            rows[base + off + pre] = (int32_t)(((uint32_t)mt[2 * m] << 16) | (uint32_t)mt[2 * m + 1]);
+        } else if (keep) {
             int32_t* o = rows + (base + off + pre) * 3;
             o[0] = pair_base + p;
             o[1] = mt[2 * m];
@@ -77,6 +83,23 @@ __global__ __launch_bounds__(256) void graph_rows_kernel(
         }
         base += tot;
         __syncthreads();
+    }
+}
+
+// rows[dst[p] + i] = (pair_base + p, v >> 16, v & 0xFFFF), v = packed[src[p] + i], i < count[p]
+__global__ __launch_bounds__(256) void graph_expand_kernel(
+    int pair_base, const int32_t* __restrict__ count, const int64_t* __restrict__ src,
+    const int64_t* __restrict__ dst, const uint32_t* __restrict__ packed,
+    int32_t* __restrict__ rows) {
+    const int p = blockIdx.x;
+    const int n = count[p];
+    const uint32_t* in = packed + src[p];
+    int32_t* out = rows + dst[p] * 3;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const uint32_t v = in[i];
+        out[3 * i] = pair_base + p;
+        out[3 * i + 1] = (int32_t)(v >> 16);
+        out[3 * i + 2] = (int32_t)(v & 0xFFFFu);
     }
 }
 
@@ -94,19 +117,55 @@ extern "C" int sfm_graph_offsets(sfm_ctx* ctx, int32_t n_pairs, const int32_t* i
     return SFM_OK;
 }
 
+static int graph_rows_launch(const char* fn, sfm_ctx* ctx, int32_t n_pairs, int32_t k_max,
+                             int32_t pair_base, const int32_t* match_count,
+                             const int32_t* matches, const uint8_t* mask,
+                             const int32_t* inl_count, int32_t min_inliers,
+                             const int64_t* offsets, int32_t* out, int packed) {
+    SFM_REQUIRE(ctx, std::string(fn) + ": ctx is NULL");
+    SFM_REQUIRE(n_pairs >= 0 && k_max >= 0 && pair_base >= 0, std::string(fn) + ": negative size");
+    SFM_REQUIRE(!packed || k_max <= 65536, std::string(fn) + ": packed rows need k_max <= 65536");
+    if (n_pairs == 0 || k_max == 0) return SFM_OK;
+    SFM_REQUIRE(match_count && matches && mask && inl_count && offsets && out,
+                std::string(fn) + ": NULL array");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(graph_rows_kernel, dim3(n_pairs), dim3(256), 0, ctx->stream, k_max,
+                       pair_base, match_count, matches, mask, inl_count, min_inliers, offsets,
+                       out, packed);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
 extern "C" int sfm_graph_rows(sfm_ctx* ctx, int32_t n_pairs, int32_t k_max, int32_t pair_base,
                               const int32_t* match_count, const int32_t* matches,
                               const uint8_t* mask, const int32_t* inl_count,
                               int32_t min_inliers, const int64_t* offsets, int32_t* out_rows) {
-    SFM_REQUIRE(ctx, "sfm_graph_rows: ctx is NULL");
-    SFM_REQUIRE(n_pairs >= 0 && k_max >= 0 && pair_base >= 0, "sfm_graph_rows: negative size");
-    if (n_pairs == 0 || k_max == 0) return SFM_OK;
-    SFM_REQUIRE(match_count && matches && mask && inl_count && offsets && out_rows,
-                "sfm_graph_rows: NULL array");
+    return graph_rows_launch("sfm_graph_rows", ctx, n_pairs, k_max, pair_base, match_count,
+                             matches, mask, inl_count, min_inliers, offsets, out_rows, 0);
+}
+
+extern "C" int sfm_graph_rows_packed(sfm_ctx* ctx, int32_t n_pairs, int32_t k_max,
+                                     const int32_t* match_count, const int32_t* matches,
+                                     const uint8_t* mask, const int32_t* inl_count,
+                                     int32_t min_inliers, const int64_t* offsets,
+                                     uint32_t* out_packed) {
+    return graph_rows_launch("sfm_graph_rows_packed", ctx, n_pairs, k_max, 0, match_count,
+                             matches, mask, inl_count, min_inliers, offsets,
+                             (int32_t*)out_packed, 1);
+}
+
+extern "C" int sfm_graph_expand(sfm_ctx* ctx, int32_t n_pairs, int32_t pair_base,
+                                const int32_t* counts, const int64_t* src_offsets,
+                                const int64_t* dst_offsets, const uint32_t* packed,
+                                int32_t* out_rows) {
+    SFM_REQUIRE(ctx, "sfm_graph_expand: ctx is NULL");
+    SFM_REQUIRE(n_pairs >= 0 && pair_base >= 0, "sfm_graph_expand: negative size");
+    if (n_pairs == 0) return SFM_OK;
+    SFM_REQUIRE(counts && src_offsets && dst_offsets && packed && out_rows,
+                "sfm_graph_expand: NULL array");
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(graph_rows_kernel, dim3(n_pairs), dim3(256), 0, ctx->stream, k_max,
-                       pair_base, match_count, matches, mask, inl_count, min_inliers, offsets,
-                       out_rows);
+    hipLaunchKernelGGL(graph_expand_kernel, dim3(n_pairs), dim3(256), 0, ctx->stream, pair_base,
+                       counts, src_offsets, dst_offsets, packed, out_rows);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }

@@ -88,8 +88,8 @@ def _match_graph(gb, pairs, pairs_t, n_kp, group):
     dev = pairs_t.device
     if hi > lo:
         count, match, _, rs = gb.run(pairs_t[lo:hi].contiguous())
-        rows, offs = gb.graph_rows(lo, count, match, rs, return_offsets=True)
-        cnt, packed = match_graph.pack_rows(rows, offs)
+        packed, offs = gb.graph_rows(lo, count, match, rs, return_offsets=True, packed=True)
+        cnt = (offs[1:] - offs[:-1]).to(torch.int32)
         inl_loc = rs["inl_count"]
     else:  # more ranks than pairs
         cnt = torch.zeros(0, dtype=torch.int32, device=dev)

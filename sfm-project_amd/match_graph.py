@@ -102,11 +102,13 @@ class GraphBuilder:
         rs = self.verify(pairs_t, count, match)
         return count, match, dist, rs
 
-    def graph_rows(self, pair_base: int, count, match, rs, return_offsets=False):
+    def graph_rows(self, pair_base: int, count, match, rs, return_offsets=False, packed=False):
         """Verified inlier rows [n,3] int32 (global pair index, queryIdx, trainIdx), on device
-        (sfm_graph_offsets + sfm_graph_rows); return_offsets: also the per-pair row offsets."""
+        (sfm_graph_offsets + sfm_graph_rows); return_offsets: also the per-pair row offsets;
+        packed: the exchange form [n] int32 queryIdx << 16 | trainIdx (sfm_graph_rows_packed)."""
         return self.ctx.graph_rows(pair_base, count, match, rs["inl_count"], rs["mask"],
-                                   self.min_inliers, return_offsets=return_offsets)
+                                   self.min_inliers, return_offsets=return_offsets,
+                                   packed=packed)
 
 
 def all_gather_rows(rows, group=None):
@@ -153,13 +155,16 @@ def all_gather_graph(counts, packed, ranges, group=None):
     `ranges` = [(lo, hi)] pair range of every rank (match_graph.shard_range, known to all ranks
     without communication).  Two collectives: the per-pair counts (padded to the longest shard),
     then the packed rows (padded to the largest row count).  No process group: local expansion
-    only (an initialised group of size 1 still runs the collectives)."""
+    only (an initialised group of size 1 still runs the collectives).  Device tensors expand in
+    one kernel straight out of the padded gather buffer (sfm_graph_expand); host tensors (the
+    gloo CPU rehearsals) with the same arithmetic in torch."""
     import torch
     import torch.distributed as dist
     dev = packed.device
     single = not dist.is_available() or not dist.is_initialized()
     if single:
-        all_counts, all_rows = [counts], [packed]
+        world, call, rall, maxn = 1, counts.reshape(1, -1), packed.reshape(1, -1), packed.shape[0]
+        tot = [int(packed.shape[0])]
     else:
         world = dist.get_world_size(group)
         maxp = max(max(hi - lo for lo, hi in ranges), 1)
@@ -171,13 +176,32 @@ def all_gather_graph(counts, packed, ranges, group=None):
         rpad = torch.zeros(maxn, dtype=torch.int32, device=dev)
         rpad[:packed.shape[0]] = packed
         rall = _gather(rpad, world, group)
-        all_counts = [call[r, :hi - lo] for r, (lo, hi) in enumerate(ranges)]
-        all_rows = [rall[r, :tot[r]] for r in range(world)]
+    return expand_gathered(call, rall, tot, ranges[:world], maxn)
+
+
+def expand_gathered(call, rall, tot, ranges, maxn):
+    """[n,3] int32 rows from a gathered packed graph: call [world, >= hi-lo] per-pair counts and
+    rall [world, maxn] packed rows of every rank r (its pairs ranges[r] = (lo, hi), its tot[r]
+    rows first in its slot).  Device tensors: one sfm_graph_expand launch; host tensors: torch."""
+    import torch
+    dev = rall.device
+    world = len(ranges)
+    spans = [(r, hi - lo) for r, (lo, hi) in enumerate(ranges)]
+    if dev.type == "cuda":
+        # pair p of rank r: its rows start at r * maxn + (exclusive scan of rank r's counts)
+        incl = torch.cumsum(call.long(), dim=1)
+        src_all = incl - call.long() + torch.arange(world, device=dev).reshape(-1, 1) * maxn
+        cnt_g = torch.cat([call[r, :n] for r, n in spans]).to(torch.int32).contiguous()
+        src_g = torch.cat([src_all[r, :n] for r, n in spans]).contiguous()
+        dst_g = (torch.cumsum(cnt_g.long(), dim=0) - cnt_g.long()).contiguous()
+        return sfmcore.context(dev.index).graph_expand(ranges[0][0], cnt_g, src_g, dst_g,
+                                                       rall.reshape(-1).contiguous(), sum(tot))
     out = []
-    for (lo, hi), c, pk in zip(ranges, all_counts, all_rows):
+    for (lo, hi), (r, n) in zip(ranges, spans):
+        c, pk = call[r, :n], rall[r, :tot[r]]
         pair = torch.repeat_interleave(torch.arange(lo, hi, device=dev, dtype=torch.int32),
                                        c.long(), output_size=pk.shape[0])
-        out.append(torch.stack([pair, pk >> 16, pk & 0xFFFF], dim=1))
+        out.append(torch.stack([pair, (pk >> 16) & 0xFFFF, pk & 0xFFFF], dim=1))
     return torch.cat(out)
 
 

@@ -25,7 +25,8 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_ba_jtj", "sfm_graph_offsets", "sfm_graph_rows", "sfm_ba_solve", "sfm_ba_cost",
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
             "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
-            "sfm_ransac_stats", "sfm_ransac_f_batch_f64"]
+            "sfm_ransac_stats", "sfm_ransac_f_batch_f64", "sfm_graph_rows_packed",
+            "sfm_graph_expand"]
 
 
 class SfmCoreError(RuntimeError):
@@ -114,6 +115,8 @@ def load_library(path: str = LIB_PATH):
         L.sfm_tracks.argtypes = [vp, i32, vp, i32, vp, i64, vp, i32, vp, vp, vp, vp]
         L.sfm_graph_offsets.argtypes = [vp, i32, vp, i32, vp]
         L.sfm_graph_rows.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, i32, vp, vp]
+        L.sfm_graph_rows_packed.argtypes = [vp, i32, i32, vp, vp, vp, vp, i32, vp, vp]
+        L.sfm_graph_expand.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp]
         for name in EXPORTED:
             getattr(L, name).restype = getattr(L, name).restype or C.c_int
         _lib = L
@@ -273,11 +276,12 @@ class Context:
 
     # ---- verified match graph --------------------------------------------------------------
     def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15,
-                   return_offsets=False):
+                   return_offsets=False, packed=False):
         """Rows [n,3] i32 (pair_base + pair, queryIdx, trainIdx) of the inliers of every verified
         pair (inl_count >= min_inliers), pair-major, ascending match index.  One device->host
         read of the row total sizes the output.  return_offsets: also the [P+1] i64 row offsets
-        per pair."""
+        per pair.  packed: the exchange form instead, [n] i32 rows queryIdx << 16 | trainIdx
+        (sfm_graph_rows_packed; pair_base is then implied by the caller's pair range)."""
         torch = self.torch
         P, k_max = mask.shape
         dev = mask.device
@@ -286,12 +290,30 @@ class Context:
         _check(self.lib.sfm_graph_offsets(self.handle, P, _ptr(inl_count), int(min_inliers),
                                           _ptr(offs)))
         n = int(offs[P].item())
-        rows = torch.empty((n, 3), dtype=torch.int32, device=dev)
-        if n:
+        rows = torch.empty((n,) if packed else (n, 3), dtype=torch.int32, device=dev)
+        if n and packed:
+            _check(self.lib.sfm_graph_rows_packed(self.handle, P, k_max, _ptr(count),
+                                                  _ptr(match), _ptr(mask), _ptr(inl_count),
+                                                  int(min_inliers), _ptr(offs), _ptr(rows)))
+        elif n:
             _check(self.lib.sfm_graph_rows(self.handle, P, k_max, int(pair_base), _ptr(count),
                                            _ptr(match), _ptr(mask), _ptr(inl_count),
                                            int(min_inliers), _ptr(offs), _ptr(rows)))
         return (rows, offs) if return_offsets else rows
+
+    def graph_expand(self, pair_base, counts, src_offsets, dst_offsets, packed, n_rows):
+        """[n_rows,3] i32 rows (pair_base + p, q, t) from packed rows (sfm_graph_expand): pair p's
+        counts[p] rows start at packed[src_offsets[p]] and land at row dst_offsets[p]."""
+        torch = self.torch
+        dev = packed.device
+        rows = torch.empty((n_rows, 3), dtype=torch.int32, device=dev)
+        P = counts.shape[0]
+        if P and n_rows:
+            self._bind_stream()
+            _check(self.lib.sfm_graph_expand(self.handle, P, int(pair_base), _ptr(counts),
+                                             _ptr(src_offsets), _ptr(dst_offsets), _ptr(packed),
+                                             _ptr(rows)))
+        return rows
 
     # ---- bundle adjustment -----------------------------------------------------------------
     def ba_jtj(self, cams, pp, pts, cam_idx, pt_idx, uv, pt_ptr, cam_ptr, cam_obs, loss_s=0.0):

@@ -163,6 +163,44 @@ def test_graph_packed_roundtrip_on_device():
     g = match_graph.all_gather_graph(c, pk, [(0, len(pairs))])
     np.testing.assert_array_equal(g.cpu().numpy(), rows.cpu().numpy())
     assert int(offs[-1]) == rows.shape[0] > 0
+    # the kernel-written exchange form (sfm_graph_rows_packed) is the same packing, same offsets
+    pk2, offs2 = gb.graph_rows(0, count, match, rs, return_offsets=True, packed=True)
+    np.testing.assert_array_equal(offs2.cpu().numpy(), offs.cpu().numpy())
+    np.testing.assert_array_equal(pk2.cpu().numpy(), pk.cpu().numpy())
+    c2 = (offs2[1:] - offs2[:-1]).to(torch.int32)
+    g2 = match_graph.all_gather_graph(c2, pk2, [(0, len(pairs))])
+    np.testing.assert_array_equal(g2.cpu().numpy(), rows.cpu().numpy())
+
+
+def test_graph_expand_kernel_multi_rank_layout():
+    """sfm_graph_expand on a gathered multi-rank layout (padded per-rank slots, ragged shards, an
+    empty shard, empty pairs, indices >= 32768 in both halves of the packed word) equals the
+    host expansion of the same buffers, and a non-zero first pair index carries through."""
+    import torch
+    rng = np.random.default_rng(7)
+    ranges = [(3, 40), (40, 40), (40, 95), (95, 101)]
+    world = len(ranges)
+    maxp = max(hi - lo for lo, hi in ranges)
+    call = np.zeros((world, maxp), np.int32)
+    tot = []
+    for r, (lo, hi) in enumerate(ranges):
+        c = rng.integers(0, 200, hi - lo).astype(np.int32)
+        c[rng.random(hi - lo) < 0.2] = 0
+        call[r, :hi - lo] = c
+        tot.append(int(c.sum()))
+    maxn = max(max(tot), 1)
+    rall = np.full((world, maxn), -7, np.int32)  # padding must never be read
+    for r in range(world):
+        q = rng.integers(0, 65536, tot[r]).astype(np.uint32)
+        t = rng.integers(0, 65536, tot[r]).astype(np.uint32)
+        rall[r, :tot[r]] = ((q << 16) | t).view(np.int32)
+    want = match_graph.expand_gathered(torch.from_numpy(call), torch.from_numpy(rall), tot,
+                                       ranges, maxn)
+    got = match_graph.expand_gathered(torch.from_numpy(call).cuda(),
+                                      torch.from_numpy(rall).cuda(), tot, ranges, maxn)
+    assert got.shape == (sum(tot), 3)
+    np.testing.assert_array_equal(got.cpu().numpy(), want.numpy())
+    assert int(got[0, 0]) == 3 and int(got[:, 1].max()) >= 32768
 
 
 def test_match_all_pairs_equals_reference_loop():
