@@ -260,12 +260,18 @@ __device__ __forceinline__ T wave_fixed_sum(T partial) {
 // plane stride per pair: 8 planes of k_pl floats (k_pl multiple of 16: 64-B aligned planes)
 __host__ __device__ __forceinline__ int plane_len(int k_max) { return (k_max + 15) & ~15; }
 
+// One 256-thread block per pair.  The four waves share the dependent gathers (match index ->
+// keypoint) and the final scaling; wave 0 alone forms the sums, lane l accumulating m = l, l+64,
+// ... in order then the halving tree (the oracle's fixed_sum), so the bits do not depend on the
+// block width.  (One wave per pair spent its life on the gather chain: 28 us at cfg3.)
+constexpr int PREP_T = 256;
 template <typename T>
-__global__ __launch_bounds__(64) void ransac_prep_kernel(
+__global__ __launch_bounds__(PREP_T) void ransac_prep_kernel(
     const T* __restrict__ kps, int k_max, const int32_t* __restrict__ pairs,
     const int32_t* __restrict__ match_count, const int32_t* __restrict__ matches, T thr,
     T* __restrict__ planes, T* __restrict__ out_norm) {
-    const int p = blockIdx.x, l = threadIdx.x;
+    __shared__ T par[8];  // mx1, my1, s1, mx2, my2, s2, k1, k2
+    const int p = blockIdx.x, tid = threadIdx.x, l = tid & 63;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int M = match_count[p];
     const int32_t* mt = matches + (size_t)p * k_max * 2;
@@ -276,17 +282,15 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
     T* Y2 = X2 + kp;
     T* S = Y2 + kp;                        // scaled X1 | Y1 | X2 | Y2
     if (M < 8) {
-        if (l < 6) out_norm[p * 6 + l] = T(0.0);
+        if (tid < 6) out_norm[p * 6 + tid] = T(0.0);
         return;
     }
-    T sx1 = 0.f, sy1 = 0.f, sx2 = 0.f, sy2 = 0.f;
-    // four matches per lane in flight (index loads, then the coordinate gathers): one wave per
-    // pair is latency-bound; the sums still accumulate in m order
-    for (int m0 = l; m0 < M; m0 += 256) {
+    // gathers: four matches per thread in flight, raw coordinates to the planes
+    for (int m0 = tid; m0 < M; m0 += 4 * PREP_T) {
         int2 id[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            const int m = m0 + 64 * t;
+            const int m = m0 + PREP_T * t;
             id[t] = m < M ? *(const int2*)(mt + 2 * m) : make_int2(0, 0);
         }
         V2<T> u[4], v[4];
@@ -297,36 +301,50 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            const int m = m0 + 64 * t;
-            if (m < M) {
-                sx1 = sx1 + u[t].x; sy1 = sy1 + u[t].y; sx2 = sx2 + v[t].x; sy2 = sy2 + v[t].y;
-                X1[m] = u[t].x; Y1[m] = u[t].y; X2[m] = v[t].x; Y2[m] = v[t].y;
-            }
+            const int m = m0 + PREP_T * t;
+            if (m < M) { X1[m] = u[t].x; Y1[m] = u[t].y; X2[m] = v[t].x; Y2[m] = v[t].y; }
         }
     }
-    const T fM = (T)M;
-    const T mx1 = wave_fixed_sum(sx1) / fM, my1 = wave_fixed_sum(sy1) / fM;
-    const T mx2 = wave_fixed_sum(sx2) / fM, my2 = wave_fixed_sum(sy2) / fM;
-    T sd1 = 0.f, sd2 = 0.f;
+    __syncthreads();  // the raw planes are visible to the block
+    if (tid < 64) {
+        T sx1 = 0.f, sy1 = 0.f, sx2 = 0.f, sy2 = 0.f;
 #pragma unroll 4
-    for (int m = l; m < M; m += 64) {
-        const V4<T> w = {X1[m], Y1[m], X2[m], Y2[m]};
-        T dx = w.x - mx1, dy = w.y - my1;
-        T q = dx * dx;
-        q = fmaT(dy, dy, q);
-        sd1 = sd1 + sqrtT(q);
-        dx = w.z - mx2; dy = w.w - my2;
-        q = dx * dx;
-        q = fmaT(dy, dy, q);
-        sd2 = sd2 + sqrtT(q);
+        for (int m = l; m < M; m += 64) {
+            sx1 = sx1 + X1[m]; sy1 = sy1 + Y1[m]; sx2 = sx2 + X2[m]; sy2 = sy2 + Y2[m];
+        }
+        const T fM = (T)M;
+        const T mx1 = wave_fixed_sum(sx1) / fM, my1 = wave_fixed_sum(sy1) / fM;
+        const T mx2 = wave_fixed_sum(sx2) / fM, my2 = wave_fixed_sum(sy2) / fM;
+        T sd1 = 0.f, sd2 = 0.f;
+#pragma unroll 4
+        for (int m = l; m < M; m += 64) {
+            const V4<T> w = {X1[m], Y1[m], X2[m], Y2[m]};
+            T dx = w.x - mx1, dy = w.y - my1;
+            T q = dx * dx;
+            q = fmaT(dy, dy, q);
+            sd1 = sd1 + sqrtT(q);
+            dx = w.z - mx2; dy = w.w - my2;
+            q = dx * dx;
+            q = fmaT(dy, dy, q);
+            sd2 = sd2 + sqrtT(q);
+        }
+        const T mean1 = wave_fixed_sum(sd1) / fM, mean2 = wave_fixed_sum(sd2) / fM;
+        const T s1 = (mean1 > T(0.0)) ? (T(1.41421356237309515) / mean1) : T(1.0);
+        const T s2 = (mean2 > T(0.0)) ? (T(1.41421356237309515) / mean2) : T(1.0);
+        T k1, k2;
+        sampson_scales(s1, s2, thr, k1, k2);
+        if (l == 0) {
+            par[0] = mx1; par[1] = my1; par[2] = s1; par[3] = mx2; par[4] = my2; par[5] = s2;
+            par[6] = k1; par[7] = k2;
+            T* o = out_norm + p * 6;
+            o[0] = mx1; o[1] = my1; o[2] = s1; o[3] = mx2; o[4] = my2; o[5] = s2;
+        }
     }
-    const T mean1 = wave_fixed_sum(sd1) / fM, mean2 = wave_fixed_sum(sd2) / fM;
-    const T s1 = (mean1 > T(0.0)) ? (T(1.41421356237309515) / mean1) : T(1.0);
-    const T s2 = (mean2 > T(0.0)) ? (T(1.41421356237309515) / mean2) : T(1.0);
-    T k1, k2;
-    sampson_scales(s1, s2, thr, k1, k2);
+    __syncthreads();
+    const T mx1 = par[0], my1 = par[1], s1 = par[2], mx2 = par[3], my2 = par[4], s2 = par[5];
+    const T k1 = par[6], k2 = par[7];
 #pragma unroll 4
-    for (int m = l; m < M; m += 64) {
+    for (int m = tid; m < M; m += PREP_T) {
         const T x1 = (X1[m] - mx1) * s1, y1 = (Y1[m] - my1) * s1;
         const T x2 = (X2[m] - mx2) * s2, y2 = (Y2[m] - my2) * s2;
         X1[m] = x1; Y1[m] = y1; X2[m] = x2; Y2[m] = y2;
@@ -334,10 +352,6 @@ __global__ __launch_bounds__(64) void ransac_prep_kernel(
         S[kp + m] = y1 * k1;
         S[2 * kp + m] = x2 * k2;
         S[3 * kp + m] = y2 * k2;
-    }
-    if (l == 0) {
-        T* o = out_norm + p * 6;
-        o[0] = mx1; o[1] = my1; o[2] = s1; o[3] = mx2; o[4] = my2; o[5] = s2;
     }
 }
 
@@ -830,8 +844,8 @@ static int ransac_batch(sfm_ctx* ctx, const T* kps, int32_t k_max, const int32_t
     T* planes = (T*)w.planes;
     T* hypG = (T*)w.hypG;
     SFM_HIP_CHECK(hipMemsetAsync(w.best, 0, (size_t)n_pairs * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(ransac_prep_kernel<T>, dim3(n_pairs), dim3(64), 0, st, kps, k_max, pairs,
-                       match_count, matches, thr, planes, out_norm);
+    hipLaunchKernelGGL(ransac_prep_kernel<T>, dim3(n_pairs), dim3(PREP_T), 0, st, kps, k_max,
+                       pairs, match_count, matches, thr, planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 grid(n_pairs, H / 256);
     uint32_t* exec_w = nullptr;  // sfm_ransac_stats (ordered schedule only)
@@ -924,7 +938,7 @@ extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, 
     SFM_HIP_CHECK(hipMemsetAsync(out_counts, 0xFF, (size_t)n_pairs * H * sizeof(int32_t), st));
     float* planes = (float*)w.planes;
     float* hypG = (float*)w.hypG;
-    hipLaunchKernelGGL(ransac_prep_kernel<float>, dim3(n_pairs), dim3(64), 0, st, kps, k_max,
+    hipLaunchKernelGGL(ransac_prep_kernel<float>, dim3(n_pairs), dim3(PREP_T), 0, st, kps, k_max,
                        pairs, match_count, matches, prm->thr, planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 xgrid(xcd_grid(n_pairs, H / 256));
