@@ -48,6 +48,9 @@ __global__ __launch_bounds__(SCAN_T) void graph_offsets_kernel(int n_pairs,
     if (tid == 0) offsets[n_pairs] = carry;
 }
 
+// (Staging a chunk's [n][3] rows in LDS for consecutive dword stores measured slower here,
+// 847 -> 965 us per cfg4 launch: the extra barrier per chunk costs more than the stores;
+// profiles/r03/graph_lds_ab_r5f.txt.)
 __global__ __launch_bounds__(256) void graph_rows_kernel(
     int k_max, int pair_base, const int32_t* __restrict__ match_count,
     const int32_t* __restrict__ matches, const uint8_t* __restrict__ mask,
@@ -86,20 +89,29 @@ __global__ __launch_bounds__(256) void graph_rows_kernel(
     }
 }
 
-// rows[dst[p] + i] = (pair_base + p, v >> 16, v & 0xFFFF), v = packed[src[p] + i], i < count[p]
+// rows[dst[p] + i] = (pair_base + p, v >> 16, v & 0xFFFF), v = packed[src[p] + i], i < count[p];
+// 256 rows at a time through LDS, stored as consecutive dwords (0.69 -> 0.58 ms at cfg4 size
+// against three 4-B stores at a 12-B lane stride; profiles/r03/graph_lds_ab_r5f.txt)
 __global__ __launch_bounds__(256) void graph_expand_kernel(
     int pair_base, const int32_t* __restrict__ count, const int64_t* __restrict__ src,
     const int64_t* __restrict__ dst, const uint32_t* __restrict__ packed,
     int32_t* __restrict__ rows) {
-    const int p = blockIdx.x;
+    __shared__ int32_t stage[3 * 256];
+    const int p = blockIdx.x, tid = threadIdx.x;
     const int n = count[p];
     const uint32_t* in = packed + src[p];
     int32_t* out = rows + dst[p] * 3;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        const uint32_t v = in[i];
-        out[3 * i] = pair_base + p;
-        out[3 * i + 1] = (int32_t)(v >> 16);
-        out[3 * i + 2] = (int32_t)(v & 0xFFFFu);
+    for (int i0 = 0; i0 < n; i0 += 256) {
+        const int i = i0 + tid, c = min(256, n - i0);
+        if (i < n) {
+            const uint32_t v = in[i];
+            stage[3 * tid] = pair_base + p;
+            stage[3 * tid + 1] = (int32_t)(v >> 16);
+            stage[3 * tid + 2] = (int32_t)(v & 0xFFFFu);
+        }
+        __syncthreads();
+        for (int k = tid; k < 3 * c; k += 256) out[3 * i0 + k] = stage[k];
+        __syncthreads();
     }
 }
 
