@@ -50,6 +50,11 @@ def test_version_and_errors_without_device():
     rp = sfmcore.RansacParams(4096, 15, 1.0, 0, 42)
     assert lib.sfm_ransac_f_batch(None, None, 0, 0, None, 1, None, None, C.byref(rp), None, None,
                                   None, None, None) == -1
+    # the graph exchange entries refuse a NULL context and a packed layout they cannot encode
+    assert lib.sfm_graph_rows_packed(None, 1, 16, None, None, None, None, 15, None, None) == -1
+    assert b"sfm_graph_rows_packed" in lib.sfm_last_error()
+    assert lib.sfm_graph_expand(None, 1, 0, None, None, None, None, None) == -1
+    assert b"sfm_graph_expand" in lib.sfm_last_error()
 
 
 def test_ctx_create_reports_missing_device():
