@@ -3,10 +3,11 @@
 //
 // Nodes are (image, keypoint): node = img_base[image] + keypoint.  Every graph row
 // (pair, queryIdx, trainIdx) is the edge (node(a, q), node(b, t)) with (a, b) = pairs[pair].
-// Connected components by min-label hooking + pointer jumping: the final label of every node is
-// the smallest node id of its component — the unique fixed point, so the result does not depend
-// on thread scheduling (integer atomicMin only).  A track is a component with >= min_len nodes and
-// no two nodes in the same image (COLMAP would split such a component; the build drops it).
+// Connected components by root hooking with compare-and-swap retries (larger root under smaller)
+// + pointer jumping: the final label of every node is the smallest node id of its component — the
+// unique fixed point, so the result does not depend on thread scheduling (integer atomics only).
+// A track is a component with >= min_len nodes and no two nodes in the same image (COLMAP would
+// split such a component; the build drops it).
 // Tracks are ordered by their smallest node id, their nodes ascending (stable radix sort by
 // label), which is exactly what the CPU restatement (tests: union-find) produces.
 #include <hipcub/hipcub.hpp>
@@ -46,10 +47,18 @@ __global__ __launch_bounds__(256) void tk_hook(long long n_rows, const int32_t* 
     if (e >= n_rows) return;
     const int p = rows[3 * e], q = rows[3 * e + 1], t = rows[3 * e + 2];
     const int u = img_base[pairs[2 * p]] + q, v = img_base[pairs[2 * p + 1]] + t;
-    const int ru = root(label, u), rv = root(label, v);
-    if (ru != rv) {
-        atomicMin(&label[max(ru, rv)], min(ru, rv));
-        *changed = 1;
+    int ru = root(label, u), rv = root(label, v);
+    if (ru == rv) return;
+    *changed = 1;
+    // link the larger root under the smaller one; if another edge re-parented it first, follow
+    // both roots again and retry (a root's label only ever moves to a smaller id, so this ends):
+    // one pass joins every edge, and the root of each component is its smallest node id
+    while (ru != rv) {
+        const int hi = max(ru, rv), lo = min(ru, rv);
+        const int old = atomicCAS(&label[hi], hi, lo);
+        if (old == hi) break;
+        ru = root(label, old);
+        rv = root(label, lo);
     }
 }
 
@@ -171,8 +180,9 @@ extern "C" int sfm_tracks(sfm_ctx* ctx, int32_t n_img, const int32_t* img_base, 
     hipLaunchKernelGGL(tk_init, dim3(nb), dim3(256), 0, st, n_nodes, label, iota);
     hipLaunchKernelGGL(tk_node_img, dim3(n_img), dim3(256), 0, st, img_base, node_img);
     SFM_HIP_CHECK(hipGetLastError());
-    // hook + compress until no edge joins two components (each round at least halves the
-    // number of roots an edge can see; 64 rounds is far beyond any real graph)
+    // hook + compress until no edge joins two components: with the CAS retry in tk_hook the first
+    // round already joins every edge and the second one only confirms it (the earlier atomicMin
+    // hook lost concurrent links and needed several rounds)
     if (n_rows > 0) {
         const unsigned eb = (unsigned)((n_rows + 255) / 256);
         int32_t h_changed = 1;
