@@ -143,10 +143,11 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     ptr_t, timg_t, tkp_t = match_graph.build_tracks(rows, pairs_t, n_kp, min_track, device)
     tptr, timg, tkp = (t.cpu().numpy() for t in (ptr_t, timg_t, tkp_t))
     n_tr = len(tptr) - 1
-    kps_np = np.asarray(kps, np.float64)
+    kps_np = np.asarray(kps)  # converted to f64 per gathered row (exact), not as a whole
     obs_track = np.repeat(np.arange(n_tr), np.diff(tptr))
     # one flat row gather (np.take is ~4x faster than the 2-D fancy index at 2 M observations)
-    obs_xy = np.take(kps_np.reshape(-1, 2), timg.astype(np.int64) * kps_np.shape[1] + tkp, axis=0)
+    obs_xy = np.take(kps_np.reshape(-1, 2), timg.astype(np.int64) * kps_np.shape[1] + tkp,
+                     axis=0).astype(np.float64)
     say(f"graph: {len(rows)} verified matches, {n_tr} tracks")
 
     rec = Reconstruction(n_img)
@@ -170,8 +171,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         r = rows[lo:hi].cpu().numpy()
         if len(r) < 50:
             continue
-        xa = _undistort(kps_np[a, r[:, 1]], intr[a])
-        xb = _undistort(kps_np[b, r[:, 2]], intr[b])
+        xa = _undistort(kps_np[a, r[:, 1]].astype(np.float64), intr[a])
+        xb = _undistort(kps_np[b, r[:, 2]].astype(np.float64), intr[b])
         common = np.intersect1d(obs_track[timg == a], obs_track[timg == b])
         best = None
         for R, t in relative_pose(xa, xb):
