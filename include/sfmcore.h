@@ -83,6 +83,17 @@ int sfm_match_batch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int3
                     int32_t k_max, int32_t dim, const int32_t* pairs, int32_t n_pairs,
                     const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
                     int32_t* out_dist);
+/* Both orders of every pair from one distance tile: the reference enumerates ORDERED pairs i != j
+ * (code/pipeline.py:38-41) and matches each with BFMatcher(crossCheck=True)
+ * (code/feature_matching.py:48-50); (a, b) and (b, a) share every distance.  pairs [n_pairs][2]
+ * (a, b); outputs hold 2 * n_pairs results: slot p = sfm_match_batch on (a, b), slot n_pairs + p =
+ * sfm_match_batch on (b, a), bit for bit (out_count [2 n_pairs], out_match [2 n_pairs][k_max][2],
+ * out_dist [2 n_pairs][k_max]).  Any cross_check rule and max_dist; no ratio test (ratio_den
+ * must be 0: the reverse direction's ratio needs its own second-best neighbour); k_max <= 4096. */
+int sfm_match_batch_both(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
+                         int32_t k_max, int32_t dim, const int32_t* pairs, int32_t n_pairs,
+                         const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                         int32_t* out_dist);
 
 /* ---- geometric verification -----------------------------------------------------------------
  * Fills the empty code/geometric_verification.py (placeholder comment at code/pipeline.py:60):
@@ -204,11 +215,13 @@ typedef struct sfm_ba_solve_params {
     int32_t max_iter; /* CG iteration cap */
     int32_t poll;     /* convergence poll: every `poll` > 0 CG iterations the host reads the
                          device's convergence flag (one 4-byte copy + a hipStreamSynchronize) and
-                         stops enqueueing once it is set; <= 0 (the zero-initialised default) =
-                         never: fully asynchronous, capturable in a hip graph (all max_iter
-                         iterations are enqueued, the converged ones exit at once).  Results are
-                         identical either way; sfmcore.py / reconstruction.py poll every 8. */
+                         stops enqueueing once it is set; 0 (the zero-initialised struct) = every
+                         SFM_BA_POLL_DEFAULT (8) iterations; < 0 = never: fully asynchronous,
+                         capturable in a hip graph (all max_iter iterations are enqueued, the
+                         converged ones exit at once).  Results are identical either way.
+                         (sfm_version 1 read 0 as "never"; version 2 restores 0 = poll.) */
 } sfm_ba_solve_params;
+#define SFM_BA_POLL_DEFAULT 8
 
 int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
                  const int32_t* cam_idx, const int32_t* pt_idx, const int32_t* pt_ptr,

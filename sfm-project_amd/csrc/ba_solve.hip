@@ -1017,7 +1017,9 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     if (rc != SFM_OK) return rc;
     hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
     SFM_HIP_CHECK(hipGetLastError());
-    const int poll = prm->poll;  // <= 0: no host synchronisation (the zero-initialised default)
+    // 0 (the zero-initialised struct) = every 8 iterations, the library default; < 0 = never
+    // (no host synchronisation: fully asynchronous, capturable in a hip graph)
+    const int poll = prm->poll == 0 ? SFM_BA_POLL_DEFAULT : prm->poll;
     for (int k = 0; k < prm->max_iter; ++k) {
         // state->done is set by bas_pcg_point of the first iteration after convergence: once it
         // reads 1, every later iteration would exit at once, so stop enqueueing them

@@ -9,6 +9,15 @@ void set_error(const std::string& msg) { g_err = msg; }
 
 void* workspace(sfm_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return ctx->ws;
+    // growing frees and reallocates (a device-wide synchronisation): illegal inside a HIP-graph
+    // capture of the context's stream — the caller runs the call once uncaptured to size it
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(ctx->stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+        set_error("workspace growth to " + std::to_string(bytes) +
+                  " bytes while the context's stream is being captured: run the call once "
+                  "uncaptured first so the workspace is sized");
+        return nullptr;
+    }
     if (ctx->ws) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipFree(ctx->ws);
@@ -29,7 +38,7 @@ extern "C" {
 
 const char* sfm_last_error(void) { return g_err.c_str(); }
 
-int32_t sfm_version(void) { return 1; }
+int32_t sfm_version(void) { return 2; }  // 2: sfm_ba_solve_params.poll 0 = every 8
 
 int sfm_ctx_create(int32_t device, sfm_ctx** out) {
     SFM_REQUIRE(out != nullptr, "sfm_ctx_create: out is NULL");
@@ -71,7 +80,6 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-    if (ctx->rs_wave) (void)hipFree(ctx->rs_wave);
     if (ctx->rs_acc) (void)hipFree(ctx->rs_acc);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -140,6 +148,30 @@ int sfm_match_batch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int3
     }
     sfm::set_error("sfm_match_batch: unknown metric");
     return SFM_ERR_INVALID;
+}
+
+int sfm_match_batch_both(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
+                         int32_t k_max, int32_t dim, const int32_t* pairs, int32_t n_pairs,
+                         const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                         int32_t* out_dist) {
+    SFM_REQUIRE(ctx && prm, "sfm_match_batch_both: ctx/prm is NULL");
+    SFM_REQUIRE(n_pairs >= 0 && n_img >= 0 && k_max >= 0, "sfm_match_batch_both: negative size");
+    if (n_pairs == 0) return SFM_OK;
+    SFM_REQUIRE(desc && n_kp && pairs && out_count && out_match && out_dist,
+                "sfm_match_batch_both: NULL array");
+    SFM_REQUIRE(prm->cross_check >= 0 && prm->cross_check <= 2,
+                "sfm_match_batch_both: bad cross_check");
+    SFM_REQUIRE(prm->ratio_den == 0,
+                "sfm_match_batch_both: no ratio test (it needs the reverse direction's second "
+                "nearest neighbour): match both orders with sfm_match_batch");
+    SFM_REQUIRE(k_max <= 4096, "sfm_match_batch_both: k_max > 4096 not supported");
+    SFM_REQUIRE(prm->metric == SFM_METRIC_L2 || prm->metric == SFM_METRIC_HAMMING,
+                "sfm_match_batch_both: unknown metric");
+    SFM_REQUIRE(dim == (prm->metric == SFM_METRIC_L2 ? 128 : 32),
+                "sfm_match_batch_both: dim must be 128 (L2) or 32 (Hamming)");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    return sfm_match_both_launch(ctx, prm->metric, desc, n_kp, n_img, k_max, pairs, n_pairs, prm,
+                                 out_count, out_match, out_dist);
 }
 
 }  // extern "C"

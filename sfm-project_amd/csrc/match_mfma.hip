@@ -230,7 +230,9 @@ __global__ __launch_bounds__(1024) void pair_order_kernel(const int32_t* __restr
     for (int p = tid; p < n_pairs; p += 1024) order[atomicAdd(&hist[pairs[2 * p + 1]], 1)] = p;
 }
 
-template <int D>
+// TOP2 = false: the row side keeps only (best, argbest) — the second-best value is what the ratio
+// test needs, and the ordered-pair path (sfm_match_batch_both, no ratio) drops its med3 + max.
+template <int D, bool TOP2 = true>
 __global__ __launch_bounds__(512, 2) void mfma_match_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ crow_tab,
@@ -337,11 +339,11 @@ __global__ __launch_bounds__(512, 2) void mfma_match_kernel(
                             // row direction on Kr: running top-2 of the 128-train group
                             const int x0 = mad24(acc0[r], 256, crow[r]);
                             const int y0 = mad24(acc0[r + 1], 256, crow[r + 1]);
-                            ts[c] = max(ts[c], vmed3(tb[c], x0, y0));
+                            if (TOP2) ts[c] = max(ts[c], vmed3(tb[c], x0, y0));
                             tb[c] = vmax3(tb[c], x0, y0);
                             const int x1 = mad24(acc1[r], 256, crow[r]);
                             const int y1 = mad24(acc1[r + 1], 256, crow[r + 1]);
-                            ts[c + 1] = max(ts[c + 1], vmed3(tb[c + 1], x1, y1));
+                            if (TOP2) ts[c + 1] = max(ts[c + 1], vmed3(tb[c + 1], x1, y1));
                             tb[c + 1] = vmax3(tb[c + 1], x1, y1);
                             // column direction on Kc = Kr + ccol (full-rate add)
                             const int a0 = x0 + ccol[c], a1 = x1 + ccol[c + 1];
@@ -942,6 +944,100 @@ __global__ __launch_bounds__(256) void opencv_finalize_kernel(
     if (tid == 0) out_count[p] = base;
 }
 
+// Both directions of an unordered pair (a, b) from ONE fused-key tile (sfm_match_batch_both; the
+// reference enumerates ordered pairs i != j, code/pipeline.py:38-41).  The tile holds, per query i
+// of a, its nearest train J1[i] of b (exact, lowest index) with d1 = n_i - B1, and per train j of b
+// its nearest query of a (exact, lowest index) in colpart.  Forward (a, b) = the usual finalize;
+// reverse (b, a) swaps the roles: the queries are b's rows (the tile's columns), the trains a's.
+//   OpenCV rule:  forward — every train j proposes (d, j) to its nearest query, each query keeps
+//                 the smallest proposal (lowest j on ties);  reverse — every row i proposes
+//                 (d1[i], i) to J1[i] (the train-side NN of the reverse problem), each column j
+//                 keeps the smallest (lowest i on ties): oracle_match cross_check 2 on (b, a).
+//   mutual:       forward keeps i iff colwin(J1[i]) = i;  reverse keeps j iff J1[colwin(j)] = j.
+//   none:         forward (J1[i], d1[i]);  reverse (colwin(j), its d).
+// No ratio test (it needs the reverse problem's second-best; the caller matches both orders).
+// Outputs: pair p's forward result in slot p, its reverse in slot n_pairs + p.
+__global__ __launch_bounds__(256) void both_finalize_kernel(
+    const int32_t* __restrict__ n_kp, int k_max, int k_pad, const int32_t* __restrict__ norm,
+    const int32_t* __restrict__ pairs, int n_pairs, int n_qblk, const int4* __restrict__ rowres,
+    const unsigned long long* __restrict__ colpart, int xc, long long max_dist,
+    int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
+    int32_t* __restrict__ out_dist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
+    __shared__ int wsum[4];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    if (na <= 0 || nb <= 0) {
+        if (tid == 0) { out_count[p] = 0; out_count[n_pairs + p] = 0; }
+        return;
+    }
+    const unsigned long long* cp = colpart + (size_t)p * n_qblk * k_pad;
+    const int4* rr = rowres + (size_t)p * k_pad;
+    const int32_t* na_norm = norm + (size_t)a * k_pad;
+    // train j's nearest query (lowest index) and its distance; false if none
+    auto col_winner = [&](int j, int& q, int& d) {
+        unsigned long long best = 0;
+        for (int k = 0; k < n_qblk; ++k) best = max(best, cp[(size_t)k * k_pad + j]);
+        if (best == 0) return false;
+        d = -(int)((unsigned)(best >> 32) ^ 0x80000000u);
+        q = (int)(0xFFFFFFFFu - (unsigned)best);
+        return q >= 0 && q < na;
+    };
+    // query i's nearest train (lowest index) and its distance; false if none
+    auto row_winner = [&](int i, int& j, int& d) {
+        const int4 r = rr[i];
+        j = r.y;
+        d = na_norm[i] - r.x;
+        return j >= 0 && j < nb && r.x > VALID_MIN;
+    };
+    auto dist_ok = [&](int d) { return max_dist < 0 || (long long)d < max_dist; };
+    for (int dir = 0; dir < 2; ++dir) {
+        const int nq = dir == 0 ? na : nb;   // queries of this direction
+        const int nt = dir == 0 ? nb : na;   // its trains
+        const size_t slot = (size_t)(dir == 0 ? p : n_pairs + p);
+        int32_t* om = out_match + slot * k_max * 2;
+        int32_t* od = out_dist + slot * k_max;
+        if (xc == SFM_XC_OPENCV) {
+            for (int i = tid; i < nq; i += 256) lds_best[i] = ~0ull;
+            __syncthreads();
+            for (int t = tid; t < nt; t += 256) {  // train t proposes to its nearest query
+                int q, d;
+                const bool ok = dir == 0 ? col_winner(t, q, d) : row_winner(t, q, d);
+                if (ok) atomicMin(&lds_best[q], ((unsigned long long)(unsigned)d << 32) | (unsigned)t);
+            }
+            __syncthreads();
+        }
+        int base = 0;
+        for (int i0 = 0; i0 < nq; i0 += 256) {
+            const int i = i0 + tid;
+            bool keep = false;
+            int j = 0, d = 0;
+            if (i < nq) {
+                if (xc == SFM_XC_OPENCV) {
+                    const unsigned long long e = lds_best[i];
+                    if (e != ~0ull) {
+                        d = (int)(e >> 32);
+                        j = (int)(unsigned)e;
+                        keep = true;
+                    }
+                } else {
+                    keep = dir == 0 ? row_winner(i, j, d) : col_winner(i, j, d);
+                    if (keep && xc == SFM_XC_MUTUAL) {
+                        int back, dd;
+                        keep = (dir == 0 ? col_winner(j, back, dd) : row_winner(j, back, dd)) &&
+                               back == i;
+                    }
+                }
+                keep = keep && dist_ok(d);
+            }
+            base = sfm::compact256(keep, i, j, d, base, wsum, om, od);
+        }
+        if (tid == 0) out_count[slot] = base;
+        __syncthreads();  // lds_best is reused by the reverse direction
+    }
+}
+
 }  // namespace
 
 // MFMA matcher for both metrics (L2: D = 128; Hamming: D = 256 bit-expanded).
@@ -1105,6 +1201,65 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
                            n_kp, k_max, k_pad, norm, pairs, fin_qblk, colpart,
                            (long long)prm->max_dist, out_count, out_match, out_dist);
     }
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
+// Both directions of every (unordered) pair from one fused-key tile, TOP2 off (no ratio test).
+int sfm_match_both_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const int32_t* n_kp,
+                          int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                          const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                          int32_t* out_dist) {
+    hipStream_t st = ctx->stream;
+    if (k_max == 0) {
+        SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * 2 * (size_t)n_pairs, st));
+        return SFM_OK;
+    }
+    const bool l2 = metric == SFM_METRIC_L2;
+    const int D = l2 ? 128 : 256;
+    const int QB = l2 ? Geo<128>::QB : Geo<256>::QB;
+    const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
+    SFM_REQUIRE(k_pad <= KMAX_L2, "sfm_match_batch_both: k_max <= 4096 required");
+    const int n_qblk = (k_max + QB - 1) / QB;
+    const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
+    const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
+    const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
+    const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
+    const size_t ordb = sfm::align_up(sizeof(int32_t) * ((size_t)n_pairs + n_img), 256);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + 1024);
+    if (!ws) return SFM_ERR_NOMEM;
+    uint8_t* zero_row = (uint8_t*)ws;
+    int32_t* norm = (int32_t*)(ws + 256);
+    int32_t* crow = (int32_t*)(ws + 256 + tab);
+    int4* rowres = (int4*)(ws + 256 + 2 * tab);
+    unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
+    uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
+    int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
+    const int n_blk = n_pairs * n_qblk;
+    const int grid = 8 * ((n_blk + 7) / 8);
+    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
+                       pairs, n_pairs, n_img, pair_order, pair_order + n_pairs);
+    SFM_HIP_CHECK(hipGetLastError());
+    if (l2) {
+        hipLaunchKernelGGL(mfma_prep_kernel<SFM_METRIC_L2>, dim3(k_pad / 256, n_img), dim3(256), 0,
+                           st, desc, n_kp, k_max, k_pad, norm, crow, zero_row, (uint4*)desc_i8);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL((mfma_match_kernel<128, false>), dim3(grid), dim3(512), 0, st, desc_i8,
+                           n_kp, k_max, k_pad, norm, crow, zero_row, pairs, n_qblk, pair_order,
+                           n_blk, rowres, colpart);
+    } else {
+        hipLaunchKernelGGL(mfma_prep_kernel<SFM_METRIC_HAMMING>, dim3(k_pad / 256, n_img),
+                           dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, crow, zero_row,
+                           (uint4*)desc_i8);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL((mfma_match_kernel<256, false>), dim3(grid), dim3(512), 0, st, desc_i8,
+                           n_kp, k_max, k_pad, norm, crow, zero_row, pairs, n_qblk, pair_order,
+                           n_blk, rowres, colpart);
+    }
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(both_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st, n_kp,
+                       k_max, k_pad, norm, pairs, n_pairs, n_qblk, rowres, colpart,
+                       prm->cross_check, (long long)prm->max_dist, out_count, out_match, out_dist);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }

@@ -143,6 +143,11 @@ __device__ __forceinline__ bool fit_f8(const V4<T> s[8], T F[9]) {
 #pragma unroll
         for (int r = k + 1; r < 9; ++r) z[r] = fmaT(-f, Mt[r][k], z[r]);
     }
+#ifdef RANSAC_ABL_NORANK2  // ablation: no rank-2 step (timing only; results invalid)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) F[i] = z[i];
+    return ok;
+#endif
     // rank 2 (oracle_fit_f8): smallest eigen-direction of G = F^T F by power iteration on adj(G)
     T G[3][3];
 #pragma unroll
@@ -559,7 +564,12 @@ __global__ __launch_bounds__(256) RANSAC_FIT_ATTR void ransac_fit_kernel(
     sampson_scales(s1, s2, thr, k1, k2);
     const uint32_t h = hb * 256 + threadIdx.x;
     int idx[8];
+#ifdef RANSAC_ABL_NOSAMPLE  // ablation: no Philox / Floyd sampling (timing only; results invalid)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) idx[k] = (int)((h * 8u + (uint32_t)k) % (uint32_t)M);
+#else
     sample8(seed, pa, pb, h, M, idx);
+#endif
     V4<T> smp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -792,17 +802,22 @@ struct RansacWs {
     void* hypG;
     int32_t* prev;
     uint16_t* order;
+    uint32_t* exec_w;  // sfm_ransac_stats: per-wave scored-match counts (nullptr when off)
 };
 // Workspace of one batch (scalar size `rs`: 4 = f32 spec, 8 = fp64 mode).  ordered: hypothesis
-// table, previews, order.
+// table, previews, order, and with sfm_ransac_stats on the per-wave execution counts (inside the
+// one workspace, so enabling the counters never allocates on the launch path by itself).
 int ransac_ws(sfm_ctx* ctx, int n_pairs, int kp, int H, bool ordered, RansacWs& w, size_t rs = 4) {
     const size_t plb = sfm::align_up((size_t)n_pairs * 8 * kp * rs, 256);
     const size_t bb = sfm::align_up((size_t)n_pairs * sizeof(unsigned long long), 256);
     const size_t gb = ordered ? sfm::align_up((size_t)n_pairs * HREC * H * rs, 256) : 0;
     const size_t vb = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(int32_t), 256) : 0;
     const size_t ob = ordered ? sfm::align_up((size_t)n_pairs * H * sizeof(uint16_t), 256) : 0;
-    char* ws = (char*)sfm::workspace(ctx, plb + bb + gb + vb + ob + 1024);
+    const bool stats = ordered && ctx->ransac_stats;
+    const size_t eb = stats ? sfm::align_up((size_t)n_pairs * (H / 64) * sizeof(uint32_t), 256) : 0;
+    char* ws = (char*)sfm::workspace(ctx, plb + bb + gb + vb + ob + eb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
+    w.exec_w = stats ? (uint32_t*)(ws + plb + bb + gb + vb + ob) : nullptr;
     w.planes = (void*)ws;
     w.best = (unsigned long long*)(ws + plb);
     w.hypG = (void*)(ws + plb + bb);
@@ -848,17 +863,7 @@ static int ransac_batch(sfm_ctx* ctx, const T* kps, int32_t k_max, const int32_t
                        pairs, match_count, matches, thr, planes, out_norm);
     SFM_HIP_CHECK(hipGetLastError());
     const dim3 grid(n_pairs, H / 256);
-    uint32_t* exec_w = nullptr;  // sfm_ransac_stats (ordered schedule only)
-    if (ctx->ransac_stats && ordered) {
-        const size_t need = (size_t)n_pairs * (H / 64);
-        if (need > ctx->rs_wave_n) {
-            if (ctx->rs_wave) SFM_HIP_CHECK(hipFree(ctx->rs_wave));
-            ctx->rs_wave = nullptr;
-            SFM_HIP_CHECK(hipMalloc(&ctx->rs_wave, need * sizeof(uint32_t)));
-            ctx->rs_wave_n = need;
-        }
-        exec_w = ctx->rs_wave;
-    }
+    uint32_t* exec_w = w.exec_w;  // sfm_ransac_stats (ordered schedule only)
     if (ordered) {
         const dim3 xgrid(xcd_grid(n_pairs, H / 256));
         const int gp = ransac_group(n_pairs);

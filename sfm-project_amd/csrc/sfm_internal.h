@@ -15,11 +15,9 @@ struct sfm_ctx {
     hipEvent_t handoff = nullptr;  // orders the workspace across sfm_ctx_set_stream switches
     int32_t* pinned = nullptr;     // small pinned host buffer (device -> host flag reads)
     int n_cu = 256;
-    // RANSAC execution statistics (sfm_ransac_stats): per-wave scored-match counts of the last
-    // batch and the accumulated (executed, algorithmic, pairs) evaluation counters
+    // RANSAC execution statistics (sfm_ransac_stats): on/off and the accumulated (executed,
+    // algorithmic, pairs) evaluation counters; the per-wave counts live in the batch workspace
     int ransac_stats = 0;
-    uint32_t* rs_wave = nullptr;
-    size_t rs_wave_n = 0;
     unsigned long long* rs_acc = nullptr;
 };
 
@@ -49,6 +47,10 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 }  // namespace sfm
 
 // Kernel-launch entry points implemented in the per-stage translation units.
+int sfm_match_both_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const int32_t* n_kp,
+                          int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                          const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                          int32_t* out_dist);
 int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
                         int32_t k_max, const int32_t* pairs, int32_t n_pairs,
                         const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,

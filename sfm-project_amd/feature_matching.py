@@ -132,7 +132,9 @@ def match_all_pairs(descriptors, norm: str = "hamming", cross_check=True,
     reference's enumeration) or every i < j (ordered=False) the matches of
     match_descriptors(des_i, des_j, ...) are computed; pairs with no match are dropped, exactly
     as `if match:` at code/pipeline.py:42.  Returns a list of Pair(i, j, [DMatch]) in the
-    reference's (i, j) order."""
+    reference's (i, j) order.  Ordered lists without a ratio test compute each unordered pair's
+    distances once and read both orders from them (sfm_match_batch_both, bit-identical to
+    matching (i, j) and (j, i) separately)."""
     import torch
     n = len(descriptors)
     dim = 32 if norm == "hamming" else 128
@@ -142,10 +144,6 @@ def match_all_pairs(descriptors, norm: str = "hamming", cross_check=True,
     for i, d in enumerate(descriptors):
         if ks[i]:
             desc[i, :ks[i]] = np.asarray(d, np.uint8)
-    pairs = np.array([(i, j) for i in range(n) for j in range(n)
-                      if (i != j if ordered else i < j)], np.int32).reshape(-1, 2)
-    if len(pairs) == 0:
-        return []
     metric = sfmcore.METRIC_HAMMING if norm == "hamming" else sfmcore.METRIC_L2
     xc = {True: sfmcore.XC_OPENCV, "opencv": sfmcore.XC_OPENCV, "mutual": sfmcore.XC_MUTUAL,
           False: sfmcore.XC_NONE, None: sfmcore.XC_NONE}[cross_check]
@@ -153,10 +151,33 @@ def match_all_pairs(descriptors, norm: str = "hamming", cross_check=True,
         ratio = _ratio_fraction(float(ratio))
     md = _max_dist(metric, max_distance)
     dev = torch.device("cuda", device)
-    cnt, mt, dist = sfmcore.context(device).match_batch(
-        torch.from_numpy(desc).to(dev), torch.tensor(ks, dtype=torch.int32, device=dev),
-        torch.from_numpy(pairs).to(dev), metric=metric, cross_check=xc, ratio=ratio, max_dist=md)
-    cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+    ctx = sfmcore.context(device)
+    desc_t = torch.from_numpy(desc).to(dev)
+    ks_t = torch.tensor(ks, dtype=torch.int32, device=dev)
+    upper = np.stack(np.triu_indices(n, 1), axis=1).astype(np.int32).reshape(-1, 2)
+    if ordered and ratio is None and k_max <= 4096 and len(upper):
+        # one distance tile serves (i, j) and (j, i) (sfm_match_batch_both): the reference's
+        # ordered enumeration at the cost of the unordered one
+        cnt, mt, dist = ctx.match_batch_both(desc_t, ks_t, torch.from_numpy(upper).to(dev),
+                                             metric=metric, cross_check=xc, max_dist=md)
+        cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+        # slot of ordered (i, j): its unordered pair u = (min, max); forward if i < j
+        slot = np.zeros((n, n), np.int64)
+        u = np.arange(len(upper))
+        slot[upper[:, 0], upper[:, 1]] = u
+        slot[upper[:, 1], upper[:, 0]] = len(upper) + u
+        pairs = np.array([(i, j) for i in range(n) for j in range(n) if i != j],
+                         np.int32).reshape(-1, 2)
+        sel = slot[pairs[:, 0], pairs[:, 1]]
+        cnt, mt, dist = cnt[sel], mt[sel], dist[sel]
+    else:
+        pairs = np.array([(i, j) for i in range(n) for j in range(n)
+                          if (i != j if ordered else i < j)], np.int32).reshape(-1, 2)
+        if len(pairs) == 0:
+            return []
+        cnt, mt, dist = ctx.match_batch(desc_t, ks_t, torch.from_numpy(pairs).to(dev),
+                                        metric=metric, cross_check=xc, ratio=ratio, max_dist=md)
+        cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
     out = []
     for p, (i, j) in enumerate(pairs.tolist()):
         k = int(cnt[p])

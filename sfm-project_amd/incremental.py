@@ -67,6 +67,8 @@ class Reconstruction:
         self.points = None
         self.has_point = None
         self.history = []
+        self.ba_log = []           # per bundle adjustment: size, LM / CG iterations, PCG branch
+        self.n_verified = 0        # rows of the verified match graph
         self.gauge = None          # (reference camera, scale camera) of the initial pair
 
 
@@ -106,7 +108,7 @@ def _match_graph(gb, pairs, pairs_t, n_kp, group):
 
 def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
                 ba_iter=20, loss_s=2.0, device=0, log=None, group=None, shard_ba=False,
-                ba_cg_tol=0.1):
+                ba_cg_tol=0.1, ba_pcg="auto"):
     """desc [n_img,K,D] u8, kps [n_img,K,2] pixels, n_kp [n_img], intr [n_img,4] = (f, k1, cx, cy).
     Returns a Reconstruction (cams [n_img,8], registered mask, points per track, track arrays).
     With torch.distributed initialised (one process per GPU, `group` or the default group) the
@@ -118,7 +120,9 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     ba_cg_tol: relative residual at which each LM step's Schur-complement PCG stops (Ceres'
     ITERATIVE_SCHUR forcing default, eta = 0.1): an inexact Newton step.  At 500 x 4096 the
     final BA takes 333 CG iterations instead of 3640 (1e-10) for the same optimum to 1e-7 of
-    the cost and the same reconstruction."""
+    the cost and the same reconstruction.
+    ba_pcg: the sharded bundle adjustments' PCG branch (reconstruction.bundle_adjust `pcg`:
+    auto | sharded | replicated); rec.ba_log records the branch each one took."""
     import time
     import torch
     dev = torch.device("cuda", device)
@@ -152,6 +156,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
 
     rec = Reconstruction(n_img)
     rec.timings = tim
+    rec.n_verified = int(rows.shape[0])
     tk = lap("tracks", tk)
     rec.points = np.zeros((n_tr, 3))
     rec.has_point = np.zeros(n_tr, bool)
@@ -184,9 +189,12 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             good = int(np.sum((st[:, 3] == 0) & (st[:, 0] < max_err)))
             if best is None or good > best[0]:
                 best = (good, cams, pts, st)
-        if best[0] >= 30:
-            good, rec.cams, pts, st = best
-            ok = (st[:, 3] == 0) & (st[:, 0] < max_err) & (st[:, 1] > 1.0)
+        good, cams_b, pts, st = best
+        ok = (st[:, 3] == 0) & (st[:, 0] < max_err) & (st[:, 1] > 1.0)
+        # at least 30 points with a triangulation angle above 1 degree: a near-zero baseline
+        # (neighbouring views of a dense sequence) cannot seed the model
+        if good >= 30 and int(ok.sum()) >= 30:
+            rec.cams = cams_b
             rec.points[common[ok]] = pts[ok]
             rec.has_point[common[ok]] = True
             rec.registered[[a, b]] = True
@@ -197,7 +205,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         raise RuntimeError("reconstruct: no initial pair with enough well-conditioned matches")
     tk = lap("initial_pair", tk)
     _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-            shard_ba, group, ba_cg_tol)
+            shard_ba, group, ba_cg_tol, ba_pcg)
     tk = lap("bundle_adjust", tk)
     tim["rounds"] = 0
 
@@ -235,7 +243,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev)
         tk = lap("triangulate", tk)
         _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-                shard_ba, group, ba_cg_tol)
+                shard_ba, group, ba_cg_tol, ba_pcg)
         tk = lap("bundle_adjust", tk)
     return rec
 
@@ -275,7 +283,7 @@ def _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev):
 
 
 def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-            shard_ba=False, group=None, cg_tol=0.1):
+            shard_ba=False, group=None, cg_tol=0.1, pcg="auto"):
     """Global LM over the registered cameras and the triangulated points (GPU), then drop points
     whose mean reprojection error stays above max_err.  Gauge: the initial pair's first camera
     keeps its pose and the second one translation coordinate (the scale); the intrinsics are
@@ -287,11 +295,16 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
     fixed = reconstruction.gauge_mask(rec.cams, ref=ref, second=second, fix_intrinsics=True)
     tr = obs_track[use]
     pts_ids, pt_idx = np.unique(tr, return_inverse=True)
+    info = {}
     cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
                                                    timg[use], pt_idx.astype(np.int32),
                                                    obs_xy[use], loss_s=loss_s, max_iter=ba_iter,
                                                    cg_tol=cg_tol, device=device, fixed=fixed,
-                                                   shard=shard_ba, group=group)
+                                                   shard=shard_ba, group=group, pcg=pcg,
+                                                   info=info)
+    rec.ba_log.append(dict(info, n_cam=int(rec.registered.sum()), n_pt=int(len(pts_ids)),
+                           n_obs=int(use.sum()), lm_steps=len(hist),
+                           cg_iters=int(sum(h[3] for h in hist))))
     reg = rec.registered
     rec.cams[reg] = cams[reg]
     rec.points[pts_ids] = pts

@@ -50,31 +50,44 @@ def _check(rc, what):
 
 class RcclComm:
     """RCCL communicator over the ranks of a torch.distributed group (collective to create:
-    every rank of the group constructs it at the same point).  `allreduce_(t)` sums the
-    contiguous fp64 device tensor t over the ranks in place, on the current stream."""
+    every rank of the group constructs it at the same point) on GPU `device` (default: the
+    current device).  Each rank passes its OWN device (one process per GPU, every GPU visible:
+    device = local rank), so the id broadcast, ncclCommInitRank and every collective run on that
+    GPU.  `allreduce_(t)` sums the contiguous fp64 device tensor t (on that GPU) over the ranks
+    in place, on the current stream of t's device."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, device=None):
         import torch
         import torch.distributed as dist
         lib = _load()
+        self._torch = torch
+        self.comm = None
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else
+                           (device.index if isinstance(device, torch.device) else int(device)))
+        self.device = dev.index
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         uid = _UniqueId()
         if self.rank == 0:
             _check(lib.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
         box = [bytes(uid) if self.rank == 0 else None]
         src = dist.get_global_rank(group, 0) if group is not None else 0
-        dist.broadcast_object_list(box, src=src, group=group)
-        uid = _UniqueId.from_buffer_copy(box[0])
-        self.device = torch.cuda.current_device()
-        self._torch = torch
-        self.comm = C.c_void_p()
-        _check(lib.ncclCommInitRank(C.byref(self.comm), self.world, uid, self.rank),
-               "ncclCommInitRank")
+        with torch.cuda.device(dev):
+            # the object broadcast stages through this rank's GPU (nccl groups), not GPU 0
+            dist.broadcast_object_list(box, src=src, group=group,
+                                       device=dev if dist.get_backend(group) == "nccl" else None)
+            uid = _UniqueId.from_buffer_copy(box[0])
+            comm = C.c_void_p()
+            _check(lib.ncclCommInitRank(C.byref(comm), self.world, uid, self.rank),
+                   "ncclCommInitRank")
+        self.comm = comm
 
     def allreduce_(self, t):
         torch = self._torch
         if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
             raise ValueError("RcclComm.allreduce_: contiguous float64 device tensor required")
+        if t.device.index != self.device:
+            raise ValueError(f"RcclComm.allreduce_: tensor on cuda:{t.device.index}, communicator "
+                             f"on cuda:{self.device}")
         if self.comm is None:
             raise RuntimeError("RcclComm.allreduce_: communicator is closed")
         s = torch.cuda.current_stream(t.device).cuda_stream

@@ -202,23 +202,27 @@ def _rotmat_np(r):
 _rccl_comms = {}
 
 
-def make_allreduce(group=None, direct: bool = True):
+def make_allreduce(group=None, direct: bool = True, device=None):
     """In-place fp64 sum over the ranks of `group`, ordered on the current stream.
 
-    `nccl` groups: by default a direct RCCL communicator (rccl.RcclComm, created once per group
-    and cached: collective, so every rank calls this at the same point) that enqueues
-    ncclAllReduce on the current stream itself, without ProcessGroupNCCL's side stream and its
-    two event waits per call; direct=False goes through torch.distributed.all_reduce.  Both are
+    `nccl` groups: by default a direct RCCL communicator (rccl.RcclComm, created once per
+    (group, device) and cached: collective, so every rank calls this at the same point) that
+    enqueues ncclAllReduce on the current stream itself, without ProcessGroupNCCL's side stream
+    and its two event waits per call; direct=False goes through torch.distributed.all_reduce.
+    `device`: this rank's GPU (default: the current device) — with every GPU visible each rank
+    passes its local rank, so the communicator lives on the GPU the tensors live on.  Both are
     marked graph_safe (ba_solve_sharded may replay its CG windows as HIP graphs).  Other
     backends (gloo: the CPU tests and the same-GPU rehearsals) sum through a host copy."""
     import torch.distributed as dist
     if dist.get_backend(group) == "nccl":
         if direct:
             import rccl
-            key = group if group is not None else dist.group.WORLD
+            import torch
+            dev = torch.cuda.current_device() if device is None else int(device)
+            key = (group if group is not None else dist.group.WORLD, dev)
             comm = _rccl_comms.get(key)
             if comm is None:
-                comm = _rccl_comms[key] = rccl.RcclComm(group)
+                comm = _rccl_comms[key] = rccl.RcclComm(group, device=dev)
 
             def allreduce(t):
                 comm.allreduce_(t)
@@ -236,19 +240,105 @@ def make_allreduce(group=None, direct: bool = True):
 
 
 def release_allreduce(group=None):
-    """Destroys the RCCL communicator that make_allreduce opened for `group` (collective; call it
-    on every rank before torch.distributed.destroy_process_group)."""
+    """Destroys the RCCL communicators that make_allreduce opened for `group` (collective; call
+    it on every rank before torch.distributed.destroy_process_group)."""
     import torch.distributed as dist
-    key = group if group is not None else dist.group.WORLD
-    comm = _rccl_comms.pop(key, None)
-    if comm is not None:
-        comm.close()
+    g = group if group is not None else dist.group.WORLD
+    for key in [k for k in _rccl_comms if k[0] is g or k[0] == g]:
+        _rccl_comms.pop(key).close()
+
+
+# ---- shard / replicate rule for the multi-GPU PCG (DESIGN.md §6) --------------------------------
+# Per-CG-iteration cost model of the Schur-complement PCG (world-size-1 measurements at cfg5,
+# 500 cameras x 100 k points x 5 observations, profiles/r03/ba_solve_cfg5_r3q.json):
+#   unsharded iteration   t(n_obs)      = PCG_FIXED_US + PCG_OBS_US * n_obs   (49.7 us at 500 k)
+#   sharded, N ranks      t(n_obs / N)  + PCG_SPLIT_US + L_ar(8 n_cam doubles)
+#     PCG_SPLIT_US: the split camera pass + finish launch measured at world size 1 (53.5 - 49.7)
+#   replicated            t(n_obs) per iteration, plus once per linearisation an all-gather of
+#                         the point-side blocks (W 192 B/obs, V 72 B + g_p 24 B per point)
+# L_ar and the all-gather bandwidth are MEASURED on the group (probe_collectives, once per
+# communicator and camera count, averaged over the ranks so every rank takes the same branch).
+PCG_FIXED_US = 12.0       # three launches' floor (2 300-obs problems: 13.6 ms / 20 steps / ~55 it)
+PCG_OBS_US = (49.7 - PCG_FIXED_US) / 500_000.0
+PCG_SPLIT_US = 3.8
+PCG_ITERS_PER_STEP = 20   # CG iterations per LM step assumed by the rule (cg_tol 0.1: 17 measured)
+_probe_cache = {}
+
+
+def probe_collectives(allreduce, n_cam: int, device, group=None, reps: int = 20,
+                      big_mb: float = 8.0):
+    """Measured (latency of one in-place all-reduce of 8·n_cam doubles in µs, all-reduce bus
+    bandwidth in B/s) on this group: `reps` back-to-back calls of each size, timed on the
+    current stream, then averaged over the ranks with the same all-reduce (every rank gets the
+    same numbers, so the branch decision is collective-safe).  Cached per (allreduce, n_cam)."""
+    import time
+    import torch
+    import torch.distributed as dist
+    key = (id(getattr(allreduce, "comm", allreduce)), n_cam)
+    if key in _probe_cache:
+        return _probe_cache[key]
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    dev = torch.device("cuda", device) if not isinstance(device, torch.device) else device
+    small = torch.zeros(8 * n_cam, dtype=torch.float64, device=dev)
+    big = torch.zeros(int(big_mb * 2 ** 20) // 8, dtype=torch.float64, device=dev)
+    out = []
+    for buf, n in ((small, reps), (big, max(2, reps // 4))):
+        allreduce(buf)                         # warm the path
+        torch.cuda.synchronize(dev)
+        if dist.is_initialized():
+            dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            allreduce(buf)
+        torch.cuda.synchronize(dev)
+        out.append((time.perf_counter() - t0) / n)
+    lat_us = out[0] * 1e6
+    # ring all-reduce bus bandwidth (2(N-1)/N of the bytes cross each link); world 1: bytes / time
+    busbw = (2.0 * (world - 1) / world if world > 1 else 1.0) * big.numel() * 8 / max(out[1], 1e-9)
+    m = torch.tensor([lat_us, busbw], dtype=torch.float64, device=dev)
+    allreduce(m)
+    lat_us, busbw = (float(v) / world for v in m.cpu().tolist())
+    _probe_cache[key] = (lat_us, busbw)
+    return lat_us, busbw
+
+
+def pcg_rule(n_obs: int, n_pt: int, n_cam: int, world: int, allreduce_us: float,
+             busbw: float, iters: int = PCG_ITERS_PER_STEP):
+    """'sharded' or 'replicated' for a world-rank PCG, and the model terms (µs per LM step).
+
+    sharded    : iters * (t(n_obs / N) + PCG_SPLIT_US + allreduce_us)
+    replicated : iters * t(n_obs) + gather (W, V, g_p of the other ranks once per linearisation:
+                 (N-1)/N of the bytes at the measured bus bandwidth)
+    with t(n) = PCG_FIXED_US + PCG_OBS_US * n.  Ties go to 'sharded'."""
+    t = lambda n: PCG_FIXED_US + PCG_OBS_US * n
+    sharded = iters * (t(n_obs / world) + PCG_SPLIT_US + allreduce_us)
+    gbytes = (world - 1) / world * (192.0 * n_obs + 96.0 * n_pt)
+    gather_us = gbytes / max(busbw, 1.0) * 1e6 + allreduce_us
+    replicated = iters * t(n_obs) + gather_us
+    mode = "sharded" if sharded <= replicated else "replicated"
+    return mode, {"sharded_us_per_step": sharded, "replicated_us_per_step": replicated,
+                  "gather_us": gather_us, "allreduce_us": allreduce_us, "busbw_GBs": busbw / 1e9,
+                  "iters_assumed": iters, "n_obs": n_obs, "n_pt": n_pt, "world": world}
+
+
+def _gather_rows(t, counts, group):
+    """All-gather of a [n_r, ...] f64 device tensor whose first dimension differs per rank
+    (counts[r]): zero-padded to max(counts), one collective, concatenated in rank order."""
+    import torch
+    import match_graph
+    world = len(counts)
+    mx = max(max(counts), 1)
+    inner = t.shape[1:]
+    pad = torch.zeros((mx,) + tuple(inner), dtype=t.dtype, device=t.device)
+    pad[:t.shape[0]] = t
+    g = match_graph._gather(pad.reshape(-1), world, group).reshape((world, mx) + tuple(inner))
+    return torch.cat([g[r, :counts[r]] for r in range(world)]).contiguous()
 
 
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
                   lam0: float = 1e-4, ftol: float = 1e-12, max_cg: int = 200,
                   cg_tol: float = 1e-10, device: int = 0, fixed=None, shard: bool = False,
-                  group=None):
+                  group=None, pcg: str = "auto", info=None):
     """Levenberg-Marquardt on paper eq. (1): every step on the GPU
     (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
     accept / reject it.
@@ -261,22 +351,32 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     sfm_ba_fix_params after every linearisation).
 
     shard (multi-GPU; needs an initialised torch.distributed group): every rank
-    takes the points of its `shard_points` range with their observations; the camera blocks
-    U / g_c are all-reduced after each linearisation, the Schur-complement PCG runs sharded
-    (sfm_ba_solve_stage: one 8·n_cam fp64 all-reduce per CG iteration), the trial cost is
-    all-reduced and the points are gathered at the end.  Every rank returns the same result,
-    equal to the unsharded one up to the fp64 summation order.
+    linearises the points of its `shard_points` range with their observations and the camera
+    blocks U / g_c are all-reduced after each linearisation (the north_star's J^TJ all-reduce);
+    the trial cost is all-reduced.  The PCG then runs in one of two branches (`pcg`):
+      'sharded'    — sfm_ba_solve_stage on the shard: one 8·n_cam fp64 all-reduce per CG
+                     iteration; the points are gathered at the end;
+      'replicated' — the point-side blocks (W, V, g_p) are all-gathered once per linearisation
+                     and every rank runs the whole PCG itself (no collective per iteration);
+      'auto'       — pcg_rule on the measured all-reduce latency / bandwidth of the group
+                     (probe_collectives); world size 1 always takes 'sharded'.
+    Every rank returns the same result, equal to the unsharded one up to the fp64 summation
+    order.  `info` (optional dict) receives the branch taken and the rule's terms.
 
     Returns (cams [n_cam,8], pts [n_pt,3], history [(cost, λ, accepted, cg_iterations)])."""
+    import os
     import torch
     n_cam, n_pt = len(cams), len(pts)
     allreduce = None
+    world = 1
     if shard:
         import torch.distributed as dist
         if dist.is_available() and dist.is_initialized():
-            allreduce = make_allreduce(group)
+            allreduce = make_allreduce(group, device=device)
             rank, world = dist.get_rank(group), dist.get_world_size(group)
+    mode = "single"
     lo, hi = 0, n_pt
+    full = None
     if allreduce is not None:
         cam_idx = np.asarray(cam_idx, np.int32)
         pt_idx = np.asarray(pt_idx, np.int32)
@@ -286,16 +386,38 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
         lo, hi = shard_points(pt_ptr, rank, world)
         o0, o1 = int(pt_ptr[lo]), int(pt_ptr[hi])
+        mode = os.environ.get("SFM_BA_PCG", pcg)
+        if mode not in ("auto", "sharded", "replicated"):
+            raise ValueError(f"bundle_adjust: pcg must be auto|sharded|replicated, got {mode!r}")
+        if mode == "auto":
+            if world == 1:
+                mode = "sharded"
+            else:
+                lat, bw = probe_collectives(allreduce, n_cam, device, group)
+                mode, terms = pcg_rule(len(pt_idx), n_pt, n_cam, world, lat, bw)
+                if info is not None:
+                    info["rule"] = terms
+        if mode == "replicated":
+            # the whole problem for the solve (every rank), the shard for the linearisation
+            full = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device)
+            counts_pt = [b - a for a, b in (shard_points(pt_ptr, r, world) for r in range(world))]
+            counts_obs = [int(pt_ptr[b] - pt_ptr[a])
+                          for a, b in (shard_points(pt_ptr, r, world) for r in range(world))]
         cam_idx, pt_idx, uv = cam_idx[o0:o1], pt_idx[o0:o1] - lo, uv[o0:o1]
+    if info is not None:
+        info.update(pcg=mode, world=world)
     prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, hi - lo, device)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(prob.dev)
-    cams_d, pts_d = T(cams), T(np.asarray(pts, np.float64)[lo:hi])
+    cams_d = T(cams)
+    # replicated: every rank keeps all points (the solve's δp is whole); the shard is a view
+    pts_d = T(pts) if full is not None else T(np.asarray(pts, np.float64)[lo:hi])
+    shard_of = (lambda p: p[lo:hi]) if full is not None else (lambda p: p)
     fixed_d = None
     if fixed is not None and np.any(fixed):
         fixed_d = torch.from_numpy(np.ascontiguousarray(fixed, np.uint8).reshape(n_cam, 8)).to(prob.dev)
 
     def linearize(c, p):
-        lin = prob.linearize(c, p, loss_s)
+        lin = prob.linearize(c, shard_of(p), loss_s)
         if allreduce is not None:   # global camera blocks before the gauge is applied
             nu_, ng = lin["U"].numel(), lin["gc"].numel()
             buf = torch.cat([lin["U"].reshape(-1), lin["gc"].reshape(-1)])
@@ -304,29 +426,36 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             lin["gc"].copy_(buf[nu_:nu_ + ng].view_as(lin["gc"]))
         if fixed_d is not None:
             prob.ctx.ba_fix_params(lin, prob.cam_idx, fixed_d)
+        if full is not None:        # the point-side blocks of every rank, once per linearisation
+            lin = dict(lin, W=_gather_rows(lin["W"], counts_obs, group),
+                       V=_gather_rows(lin["V"], counts_pt, group),
+                       gp=_gather_rows(lin["gp"], counts_pt, group))
         return lin
 
     def cost(c, p):
-        t = prob.cost(c, p, loss_s)
+        t = prob.cost(c, shard_of(p), loss_s)
         if allreduce is not None:
             allreduce(t)
         return t
 
     def solve(lin, lam):
+        if full is not None:
+            return full.solve(lin, lam, max_cg, cg_tol)
         if allreduce is None:
             return prob.solve(lin, lam, max_cg, cg_tol)
         return prob.ctx.ba_solve_sharded(lin, prob.cam_idx, prob.pt_idx, prob.pt_ptr,
                                          prob.cam_ptr, prob.cam_obs, lam, allreduce,
                                          max_iter=max_cg, tol=cg_tol)
+    upd = full if full is not None else prob
     lam, nu = lam0, 2.0
     hist = []
     old = float(cost(cams_d, pts_d).item())
     lin = linearize(cams_d, pts_d)
     for _ in range(max_iter):
-        dc, dp, info = solve(lin, lam)
-        c2, p2 = prob.update(cams_d, dc, pts_d, dp)
+        dc, dp, sinfo = solve(lin, lam)
+        c2, p2 = upd.update(cams_d, dc, pts_d, dp)
         new_t = cost(c2, p2)
-        vals = torch.cat([info, new_t]).cpu().numpy()       # the one host sync of the step
+        vals = torch.cat([sinfo, new_t]).cpu().numpy()      # the one host sync of the step
         it, gd, q, new = int(vals[0]), float(vals[2]), float(vals[3]), float(vals[5])
         pred = -(gd + 0.5 * q)
         if new < old and pred > 0:
@@ -346,9 +475,10 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             hist.append((old, lam, False, it))
             if lam > 1e16:
                 break
-    if allreduce is not None:   # gather the point shards: one all-reduce of the zero-padded set
-        full = torch.zeros((n_pt, 3), dtype=torch.float64, device=prob.dev)
-        full[lo:hi] = pts_d
-        allreduce(full.view(-1))
-        pts_d = full
+    if allreduce is not None and full is None:
+        # gather the point shards: one all-reduce of the zero-padded set
+        allp = torch.zeros((n_pt, 3), dtype=torch.float64, device=prob.dev)
+        allp[lo:hi] = pts_d
+        allreduce(allp.view(-1))
+        pts_d = allp
     return cams_d.cpu().numpy(), pts_d.cpu().numpy(), hist

@@ -26,7 +26,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
             "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
             "sfm_ransac_stats", "sfm_ransac_f_batch_f64", "sfm_graph_rows_packed",
-            "sfm_graph_expand"]
+            "sfm_graph_expand", "sfm_match_batch_both"]
 
 
 class SfmCoreError(RuntimeError):
@@ -93,6 +93,7 @@ def load_library(path: str = LIB_PATH):
         L.sfm_version.restype = i32
         L.sfm_match_batch.argtypes = [vp, vp, vp, i32, i32, i32, vp, i32, C.POINTER(MatchParams),
                                       vp, vp, vp]
+        L.sfm_match_batch_both.argtypes = L.sfm_match_batch.argtypes
         L.sfm_ransac_f_batch.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
                                          C.POINTER(RansacParams), vp, vp, vp, vp, vp]
         L.sfm_ransac_f_batch_f64.argtypes = L.sfm_ransac_f_batch.argtypes
@@ -189,6 +190,30 @@ class Context:
         _check(self.lib.sfm_match_batch(self.handle, _ptr(desc), _ptr(n_kp), n_img, k_max, dim,
                                         _ptr(pairs), P, C.byref(prm), _ptr(out[0]), _ptr(out[1]),
                                         _ptr(out[2])))
+        return out
+
+    def match_batch_both(self, desc, n_kp, pairs, metric=METRIC_HAMMING, cross_check=XC_OPENCV,
+                         max_dist=-1, out=None):
+        """Both orders of every pair from one distance tile (sfm_match_batch_both): pairs [P,2]
+        (a, b).  Returns (count [2P], match [2P,k_max,2], dist [2P,k_max]): rows p = match_batch
+        on (a, b), rows P + p = match_batch on (b, a), bit for bit.  No ratio test."""
+        torch = self.torch
+        n_img, k_max, dim = desc.shape
+        P = pairs.shape[0]
+        for t, dt in ((desc, torch.uint8), (n_kp, torch.int32), (pairs, torch.int32)):
+            if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+                raise SfmCoreError("match_batch_both: expected contiguous device tensors "
+                                   "(desc u8, n_kp i32, pairs i32)")
+        dev = desc.device
+        if out is None:
+            out = (torch.empty(2 * P, dtype=torch.int32, device=dev),
+                   torch.empty((2 * P, k_max, 2), dtype=torch.int32, device=dev),
+                   torch.empty((2 * P, k_max), dtype=torch.int32, device=dev))
+        prm = MatchParams(metric, cross_check, 0, 0, int(max_dist))
+        self._bind_stream()
+        _check(self.lib.sfm_match_batch_both(self.handle, _ptr(desc), _ptr(n_kp), n_img, k_max,
+                                             dim, _ptr(pairs), P, C.byref(prm), _ptr(out[0]),
+                                             _ptr(out[1]), _ptr(out[2])))
         return out
 
     # ---- feature extraction ----------------------------------------------------------------
@@ -404,7 +429,8 @@ class Context:
                    torch.empty((npt, 3), dtype=f64, device=dev),
                    torch.empty(5, dtype=f64, device=dev))
         dc, dp, info = out
-        prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll))
+        # C ABI: poll 0 = every SFM_BA_POLL_DEFAULT, < 0 = never; here poll <= 0 = never
+        prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll) if poll > 0 else -1)
         self._bind_stream()
         _check(self.lib.sfm_ba_solve(self.handle, nc, npt, no, _ptr(cam_idx), _ptr(pt_idx),
                                      _ptr(pt_ptr), _ptr(cam_ptr), _ptr(cam_obs), _ptr(U),

@@ -77,12 +77,47 @@ def _sift_bases(rng, n):
 def make_scene(n_img: int, n_kp: int, seed: int = 0, n_pts: int | None = None,
                inlier_frac: float = 0.7, noise_px: float = 0.5, desc_noise: float = 6.0,
                k1_range: float = 0.0, orb: bool = False, arc_deg: float = 120.0,
-               misplace_frac: float = 0.25) -> dict:
-    """Build a scene; returns a dict of numpy arrays (see module docstring)."""
+               misplace_frac: float = 0.25, window: int | None = None, grid=None,
+               track_len: float | None = None) -> dict:
+    """Build a scene; returns a dict of numpy arrays (see module docstring).
+
+    window: if set, every 3-D point has a home cell among the camera positions (uniform, drawn from
+    a separate stream so scenes without a window are unchanged) and only cameras within `window`
+    cells of it can observe it: local overlap, as in a real image collection, instead of every
+    camera seeing the whole point cloud.
+    grid: (n_az, n_el, az_deg, el_deg) puts the cameras on a sphere-cap grid (azimuth-major, the
+    first n_img of n_az x n_el positions, all looking at the origin) instead of the arc; the
+    window is then 2-D.  Neighbouring views are az_deg / n_az and el_deg / n_el apart, which gives
+    the triangulation angles an arc of 500 views (0.24 degrees apart) cannot.
+    track_len: mean observations per point with a window (default: every camera of the window);
+    n_pts then defaults to n_img * n_in / track_len and each camera observes a random n_in of its
+    candidate points."""
     rng = np.random.Generator(np.random.PCG64(seed))
     n_in = int(round(inlier_frac * n_kp))
+    wcams = None
+    if window is not None:
+        wcams = (2 * window + 1) ** (2 if grid is not None else 1)
+        track_len = float(wcams if track_len is None else track_len)
     if n_pts is None:
-        n_pts = max(int(1.5 * n_in), 16)
+        n_pts = (max(int(1.5 * n_in), 16) if window is None
+                 else max(int(np.ceil(n_img * n_in / track_len)), 16))
+    if grid is not None:
+        n_az, n_el, az_deg, el_deg = grid
+        if n_az * n_el < n_img:
+            raise ValueError("make_scene: grid has fewer positions than images")
+        cell = np.stack([np.arange(n_img) // n_el, np.arange(n_img) % n_el], 1)
+    else:
+        n_az, n_el = n_img, 1
+        cell = np.stack([np.arange(n_img), np.zeros(n_img, np.int64)], 1)
+    home_key = None
+    if window is not None:
+        hr = np.random.Generator(np.random.PCG64([seed, 0x5EC]))
+        ha = np.clip(np.rint(hr.uniform(-0.5, n_az - 0.5, size=n_pts)), 0, n_az - 1).astype(np.int64)
+        he = (np.clip(np.rint(hr.uniform(-0.5, n_el - 0.5, size=n_pts)), 0, n_el - 1).astype(np.int64)
+              if grid is not None else np.zeros(n_pts, np.int64))
+        home_key = ha * n_el + he
+        by_home = np.argsort(home_key, kind="stable")
+        hs = home_key[by_home]
     pts = rng.uniform(-2.0, 2.0, size=(n_pts, 3))
     cx, cy = WIDTH / 2.0, HEIGHT / 2.0
 
@@ -90,8 +125,13 @@ def make_scene(n_img: int, n_kp: int, seed: int = 0, n_pts: int | None = None,
     pp = np.tile(np.array([cx, cy]), (n_img, 1))
     Rs = []
     for i in range(n_img):
-        ang = np.deg2rad(-arc_deg / 2 + arc_deg * (i + 0.5) / n_img)
-        C = 8.0 * np.array([np.sin(ang), 0.15 * np.cos(3 * ang), np.cos(ang)])
+        if grid is not None:
+            az = np.deg2rad(-az_deg / 2 + az_deg * (cell[i, 0] + 0.5) / n_az)
+            el = np.deg2rad(-el_deg / 2 + el_deg * (cell[i, 1] + 0.5) / n_el)
+            C = 8.0 * np.array([np.sin(az) * np.cos(el), np.sin(el), np.cos(az) * np.cos(el)])
+        else:
+            ang = np.deg2rad(-arc_deg / 2 + arc_deg * (i + 0.5) / n_img)
+            C = 8.0 * np.array([np.sin(ang), 0.15 * np.cos(3 * ang), np.cos(ang)])
         R = _look_at(C)
         t = -R @ C
         Rs.append(R)
@@ -99,6 +139,19 @@ def make_scene(n_img: int, n_kp: int, seed: int = 0, n_pts: int | None = None,
         cams[i, 3:6] = t
         cams[i, 6] = FOCAL
         cams[i, 7] = rng.uniform(-k1_range, k1_range) if k1_range > 0 else 0.0
+
+    def candidates(i):
+        """points whose home cell is within `window` cells of camera i's (sorted indices)"""
+        out = []
+        for da in range(-window, window + 1):
+            a = cell[i, 0] + da
+            if a < 0 or a >= n_az:
+                continue
+            lo_e = max(cell[i, 1] - window, 0) if grid is not None else 0
+            hi_e = min(cell[i, 1] + window, n_el - 1) if grid is not None else 0
+            out.append(by_home[np.searchsorted(hs, a * n_el + lo_e):
+                               np.searchsorted(hs, a * n_el + hi_e, side="right")])
+        return np.sort(np.concatenate(out))
 
     if orb:
         pbase = rng.integers(0, 256, size=(n_pts, 32), dtype=np.uint8)
@@ -109,9 +162,15 @@ def make_scene(n_img: int, n_kp: int, seed: int = 0, n_pts: int | None = None,
     desc = np.zeros((n_img, n_kp, 32 if orb else 128), np.uint8)
     pid = np.full((n_img, n_kp), -1, np.int32)
     for i in range(n_img):
-        uv, z = project(Rs[i], cams[i, 3:6], cams[i, 6], cams[i, 7], cx, cy, pts)
-        vis = np.nonzero((z > 0) & (uv[:, 0] >= 0) & (uv[:, 0] < WIDTH)
-                         & (uv[:, 1] >= 0) & (uv[:, 1] < HEIGHT))[0]
+        cand = candidates(i) if home_key is not None else slice(None)
+        uv, z = project(Rs[i], cams[i, 3:6], cams[i, 6], cams[i, 7], cx, cy, pts[cand])
+        vis_m = (z > 0) & (uv[:, 0] >= 0) & (uv[:, 0] < WIDTH) & (uv[:, 1] >= 0) & (uv[:, 1] < HEIGHT)
+        vis = np.nonzero(vis_m)[0]
+        if home_key is not None:
+            vis, uv = cand[vis], uv[vis]
+            uv_full = np.empty((n_pts, 2))
+            uv_full[vis] = uv
+            uv = uv_full
         sel = rng.choice(vis, size=min(n_in, vis.size), replace=False)
         n_out = n_kp - sel.size
         xy_in = uv[sel] + rng.normal(0.0, noise_px, size=(sel.size, 2))
@@ -137,6 +196,24 @@ def make_scene(n_img: int, n_kp: int, seed: int = 0, n_pts: int | None = None,
         pid[i] = ids[perm]
     return dict(kps=kps, desc=desc, point_ids=pid, cams=cams, pp=pp, pts=pts,
                 n_kp=np.full(n_img, n_kp, np.int32))
+
+
+def camera_centres(cams: np.ndarray) -> np.ndarray:
+    """World-frame centres -R^T t of [n, 8] cameras (angle-axis, t, f, k1)."""
+    return np.array([-angle_axis_to_rotmat(c[:3]).T @ c[3:6] for c in np.asarray(cams)])
+
+
+def similarity_align(src: np.ndarray, dst: np.ndarray):
+    """Umeyama: the similarity (s, R, t) minimising |s R src + t - dst| over point sets [n, 3]
+    (a reconstruction is defined up to one; compare it with the scene's truth after this)."""
+    ms, md = src.mean(0), dst.mean(0)
+    a, b = src - ms, dst - md
+    U, S, Vt = np.linalg.svd(b.T @ a / len(src))
+    D = np.eye(3)
+    D[2, 2] = np.sign(np.linalg.det(U @ Vt))
+    Rm = U @ D @ Vt
+    s = np.trace(np.diag(S) @ D) / (a * a).sum(1).mean()
+    return s, Rm, md - s * Rm @ ms
 
 
 def unordered_pairs(n_img: int) -> np.ndarray:

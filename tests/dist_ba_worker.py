@@ -3,8 +3,9 @@ torch.distributed.run job (gloo, every rank on GPU 0 — RCCL cannot share a dev
 the point-sharded bundle adjustment (reconstruction.bundle_adjust(shard=True): camera-block
 all-reduce, sfm_ba_solve_stage with one all-reduce per CG iteration, all-reduced trial cost,
 gathered points) and one sharded solve from the initial linearisation; it writes OUT.rank<r>.npz.
-A second argument `tiny` uses a 2-point problem (with 3 ranks one shard is empty).
-Usage: python -m torch.distributed.run --nproc-per-node N ... dist_ba_worker.py OUT [tiny]"""
+A second argument `tiny` uses a 2-point problem (with 3 ranks one shard is empty); a third one
+picks bundle_adjust's PCG branch (sharded | replicated | auto; default sharded).
+Usage: python -m torch.distributed.run --nproc-per-node N ... dist_ba_worker.py OUT [tiny|std] [pcg]"""
 import os
 import sys
 
@@ -29,10 +30,13 @@ def main():
     prob = tiny_problem() if len(sys.argv) > 2 and sys.argv[2] == "tiny" else problem()
     args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
     fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
-    cams, pts, hist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed, shard=True)
+    pcg = sys.argv[3] if len(sys.argv) > 3 else "sharded"
+    binfo = {}
+    cams, pts, hist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed, shard=True,
+                                      pcg=pcg, info=binfo)
     dc, dp, info, lo, hi = shard_solve(prob, rank, world, R.make_allreduce())
     np.savez(f"{out}.rank{rank}.npz", cams=cams, pts=pts, hist=np.array(hist, np.float64),
-             dc=dc, dp=dp, info=info, lo=lo, hi=hi)
+             dc=dc, dp=dp, info=info, lo=lo, hi=hi, pcg=np.array(binfo["pcg"]))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -10,6 +10,11 @@
    build's Philox sampler), scikit-image's 8-point F and Sampson decisions per hypothesis.
 3. oracle_fixtures.npz — inputs and the CPU oracle's outputs (match lists, RANSAC winner, inlier
    mask, F bits) for small seeded cases; the GPU tests compare against these stored vectors.
+4. skimage_xc_fixtures.npz — tie-heavy L2 and Hamming descriptor sets with scikit-image's
+   nearest-neighbour tables in BOTH directions (match_descriptors(cross_check=False) on (A, B) and
+   on (B, A)) and scipy's distances of those neighbours (scipy.spatial.distance.cdist).  The tests
+   apply OpenCV's crossCheck update loop to these third-party tables, so the reference's own rule
+   (BFMatcher(crossCheck=True), code/feature_matching.py:48) is pinned with only its loop restated.
 
 Usage:  python tests/golden/make_golden.py      (system python 3.10; calls python3.9 for skimage)
 """
@@ -115,6 +120,55 @@ for i in range(int(d["n_pairs"])):
     out[f"p{i}_F"] = np.array(Fs); out[f"p{i}_res2"] = np.array(R) ** 2; out[f"p{i}_cond"] = np.array(C)
 np.savez(sys.argv[2], **out)
 """
+SKIMAGE_XC_SCRIPT = r"""
+import sys, numpy as np
+from scipy.spatial.distance import cdist
+from skimage.feature import match_descriptors
+d = np.load(sys.argv[1]); out = {}
+for kind in ("l2", "ham"):
+    A, B = d[kind + "_A"], d[kind + "_B"]
+    if kind == "l2":
+        A, B, metric = A.astype(np.float64), B.astype(np.float64), "euclidean"
+    else:
+        A, B, metric = np.unpackbits(A, axis=1).astype(bool), np.unpackbits(B, axis=1).astype(bool), "hamming"
+    for tag, X, Y in (("ab", A, B), ("ba", B, A)):
+        nn = match_descriptors(X, Y, metric=metric, cross_check=False)   # (query, its NN), every query
+        dd = cdist(X[nn[:, 0]], Y[nn[:, 1]], metric=metric).diagonal()
+        out[f"{kind}_{tag}_nn"] = nn
+        out[f"{kind}_{tag}_d"] = dd * (256 if kind == "ham" else 1)
+np.savez(sys.argv[2], **out)
+"""
+
+
+def skimage_xc_fixtures():
+    """Tie-heavy descriptor sets + scikit-image NN tables both ways (module docstring, item 4)."""
+    import synth
+    rng = np.random.Generator(np.random.PCG64(301))
+    s = synth.make_scene(2, 400, seed=302)
+    A, B = s["desc"][0][:330].copy(), s["desc"][1][:310].copy()
+    B[20:25] = B[30]          # five identical trains: ties in every query's row
+    A[50:54] = A[60]          # four identical queries: ties in the column direction
+    A[100] = B[200]           # an exact zero distance
+    pool = rng.integers(0, 256, size=(40, 32), dtype=np.uint8)     # Hamming: 40 bases, 0-2 flips
+    def draw(n):
+        x = pool[rng.integers(0, 40, size=n)].copy()
+        for r in range(n):
+            for _ in range(int(rng.integers(0, 3))):
+                bit = int(rng.integers(0, 256))
+                x[r, bit // 8] ^= np.uint8(1 << (bit % 8))
+        return x
+    inputs = dict(l2_A=A, l2_B=B, ham_A=draw(300), ham_B=draw(280))
+    with tempfile.TemporaryDirectory() as td:
+        fi, fo = os.path.join(td, "in.npz"), os.path.join(td, "out.npz")
+        np.savez(fi, **inputs)
+        subprocess.run([SKIMAGE_PY, "-c", SKIMAGE_XC_SCRIPT, fi, fo], check=True,
+                       stderr=subprocess.DEVNULL)
+        outs = dict(np.load(fo))
+    np.savez_compressed(os.path.join(HERE, "skimage_xc_fixtures.npz"), **inputs,
+                        **{"sk_" + k: v for k, v in outs.items()})
+    return {k: v.shape for k, v in outs.items()}
+
+
 RANSAC_PAIRS = [(0, 1), (5, 6), (12, 30), (40, 41)]  # cfg3 scene (50 x 2048, seed 0)
 RANSAC_H = 256
 RANSAC_BAND = 1e-5  # decisions may differ only where |res^2 / thr - 1| < RANSAC_BAND
@@ -191,3 +245,4 @@ if __name__ == "__main__":
     print("skimage:", skimage_fixtures())
     print("skimage ransac bytes:", skimage_ransac_fixtures())
     print("oracle entries:", oracle_fixtures())
+    print("skimage crossCheck tables:", skimage_xc_fixtures())

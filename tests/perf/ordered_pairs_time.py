@@ -1,0 +1,68 @@
+"""Ordered-pair matching at the reference's shape: N images x K ORB-like
+descriptors (default 500 x 500, OpenCV nfeatures), every ordered pair i != j matched with the
+reference's rule (Hamming, crossCheck=True, distance < 26; code/pipeline.py:38-41,
+code/feature_matching.py:48-58).
+
+  two_launch : sfm_match_batch on the N(N-1) ordered pairs (column-winner kernel per order)
+  both       : sfm_match_batch_both on the N(N-1)/2 unordered pairs (one fused tile, both orders)
+
+HIP events on the launch stream, best of `reps`; results compared bit for bit.
+Usage: python tests/perf/ordered_pairs_time.py [n_img [k [reps]]]   -> one JSON line.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "sfm-project_amd")]
+
+import numpy as np
+import torch
+
+import sfmcore
+import synth
+
+
+def main():
+    a = [int(x) for x in sys.argv[1:]]
+    n_img, k, reps = (a + [500, 500, 5][len(a):])[:3]
+    s = synth.make_scene(n_img, k, seed=3, orb=True)
+    ctx = sfmcore.context(0)
+    d = torch.from_numpy(s["desc"]).cuda()
+    n = torch.from_numpy(s["n_kp"]).cuda()
+    up = synth.unordered_pairs(n_img)
+    ordered = np.concatenate([up, up[:, ::-1]])
+    up_t = torch.from_numpy(up).cuda()
+    ord_t = torch.from_numpy(np.ascontiguousarray(ordered)).cuda()
+    kw = dict(metric=sfmcore.METRIC_HAMMING, cross_check=sfmcore.XC_OPENCV, max_dist=26)
+
+    def timed(fn):
+        best = None
+        out = fn()
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn(out)
+            e1.record()
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1)
+            best = t if best is None else min(best, t)
+        return best, out
+    t_two, o2 = timed(lambda out=None: ctx.match_batch(d, n, ord_t, ratio=None, out=out, **kw))
+    t_both, ob = timed(lambda out=None: ctx.match_batch_both(d, n, up_t, out=out, **kw))
+    c2, m2, _ = (x.cpu().numpy() for x in o2)
+    cb, mb, _ = (x.cpu().numpy() for x in ob)
+    same = bool((c2 == cb).all())
+    if same:
+        kk = np.arange(m2.shape[1])[None, :] < c2[:, None]
+        same = bool((m2[kk] == mb[kk]).all())
+    n_ops = 2.0 * 256 * float(np.sum(s["n_kp"][up[:, 0]] * s["n_kp"][up[:, 1]]))
+    print(json.dumps({"stage": "ordered-pair matching, Hamming + OpenCV crossCheck + < 26",
+                      "n_img": n_img, "k": k, "ordered_pairs": int(len(ordered)),
+                      "two_launch_ms": t_two, "both_ms": t_both, "ratio": t_both / t_two,
+                      "bit_identical": same, "matches": int(c2.sum()),
+                      "both_tops_i8": n_ops / (t_both * 1e-3) / 1e12}))
+
+
+if __name__ == "__main__":
+    main()

@@ -125,3 +125,60 @@ def test_ransac_hypotheses_vs_skimage():
         np.testing.assert_array_equal(idx, fx[f"p{i}_idx"])
         Fn = np.stack([O.fit_f8(n1[ix], n2[ix])[1] for ix in idx])
         check_hypotheses_vs_skimage(fx, i, Fn, masks, norm)
+
+
+# ---- the reference's own crossCheck rule against third-party NN tables -------
+def opencv_crosscheck_from_tables(train_nn, train_d, n_query, max_d=None):
+    """OpenCV's BFMatcher(crossCheck=True) update loop (code/feature_matching.py:48; batchDistance's
+    per-train pass, ascending train, strict <) applied to a train -> nearest-query table computed
+    by scikit-image (`train_nn` rows (train, query), `train_d` its distances).  Returns [m, 2]
+    (query, train) rows in ascending query order and their distances."""
+    best = np.full(n_query, np.inf)
+    part = np.full(n_query, -1, np.int64)
+    for (t, q), d in zip(np.asarray(train_nn), np.asarray(train_d)):
+        if d < best[q]:
+            best[q], part[q] = d, t
+    keep = part >= 0
+    if max_d is not None:
+        keep &= best < max_d
+    q = np.nonzero(keep)[0]
+    return np.stack([q, part[q]], 1), best[q]
+
+
+def xc_expectations():
+    """(kind, direction, max_d) -> (descriptors X, Y, expected rows, expected integer distances)
+    from tests/golden/skimage_xc_fixtures.npz: the forward (X = A) result uses the trains' table
+    `ba`, the reverse (X = B) result the table `ab`."""
+    sk = np.load(os.path.join(G, "skimage_xc_fixtures.npz"))
+    out = {}
+    for kind in ("l2", "ham"):
+        A, B = sk[kind + "_A"], sk[kind + "_B"]
+        for direc, X, Y, tab in (("fwd", A, B, "ba"), ("rev", B, A, "ab")):
+            d = sk[f"sk_{kind}_{tab}_d"]
+            dint = np.rint(d * d if kind == "l2" else d).astype(np.int64)   # d^2 resp. bits
+            for md in ((None, 26) if kind == "ham" else (None, 60000)):
+                rows, bd = opencv_crosscheck_from_tables(sk[f"sk_{kind}_{tab}_nn"], dint,
+                                                         len(X), md)
+                out[(kind, direc, md)] = (X, Y, rows, bd.astype(np.int64))
+    return out
+
+
+def test_oracle_opencv_rule_equals_loop_on_skimage_tables():
+    """The oracle's OpenCV cross-check (oracle/sfm_oracle.c cross_check 2) equals OpenCV's update
+    loop run on scikit-image's NN tables, on tie-heavy L2 and Hamming sets, both directions."""
+    for (kind, direc, md), (X, Y, rows, bd) in xc_expectations().items():
+        q, t, d = O.match(X, Y, metric=0 if kind == "l2" else 1, cross_check=O.XC_OPENCV,
+                          max_dist=-1 if md is None else md)
+        np.testing.assert_array_equal(np.stack([q, t], 1), rows, err_msg=str((kind, direc, md)))
+        np.testing.assert_array_equal(np.asarray(d, np.int64), bd)
+
+
+def test_skimage_xc_fixtures_are_tie_heavy():
+    sk = np.load(os.path.join(G, "skimage_xc_fixtures.npz"))
+    for kind in ("l2", "ham"):
+        for tab in ("ab", "ba"):
+            nn = sk[f"sk_{kind}_{tab}_nn"]
+            # many trains share a nearest query: the loop's lowest-index / strict-< order matters
+            assert len(np.unique(nn[:, 1])) < len(nn)
+    ham = np.load(os.path.join(G, "skimage_xc_fixtures.npz"))["sk_ham_ab_d"]
+    assert (np.diff(np.sort(ham)) == 0).mean() > 0.5

@@ -188,3 +188,65 @@ def test_ba_sharded_two_ranks(tmp_path):
     np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-7, atol=1e-10)
     np.testing.assert_allclose(d[0]["pts"], rpts, rtol=1e-7, atol=1e-10)
     np.testing.assert_array_equal(d[0]["cams"][fixed], prob["cams"][fixed])
+
+
+@pytest.mark.parametrize("pcg", ["sharded", "replicated"])
+def test_ba_two_ranks_both_pcg_branches_match_oracle(tmp_path, pcg):
+    """both PCG branches of the multi-GPU bundle adjustment — 'sharded' (one
+    all-reduce per CG iteration) and 'replicated' (W / V / g_p all-gathered once per
+    linearisation, every rank runs the whole PCG) — on 2 gloo ranks: the ranks agree bit for
+    bit, the branch taken is the one asked for, and the LM end state equals the oracle LM
+    (oracle/ba_lm.py) and the single-process GPU LM to fp64 reassociation."""
+    import ba_lm as L
+    prob = problem()
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
+    rcams, rpts, rhist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
+    ocams, opts, ohist = L.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
+    d = _run_ranks(tmp_path, 2, "std", pcg)
+    for key in ("cams", "pts", "hist"):
+        np.testing.assert_array_equal(d[0][key], d[1][key])
+    assert str(d[0]["pcg"]) == str(d[1]["pcg"]) == pcg
+    cost = d[0]["hist"][-1][0]
+    assert abs(cost - ohist[-1][0]) <= 1e-9 * ohist[-1][0]
+    assert abs(cost - rhist[-1][0]) <= 1e-9 * rhist[-1][0]
+    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-7, atol=1e-10)
+    np.testing.assert_allclose(d[0]["pts"], rpts, rtol=1e-7, atol=1e-10)
+    np.testing.assert_allclose(d[0]["cams"], ocams, rtol=1e-6, atol=1e-9)
+    np.testing.assert_array_equal(d[0]["cams"][fixed], prob["cams"][fixed])
+
+
+def test_ba_replicated_three_ranks_with_an_empty_shard(tmp_path):
+    """The replicated branch with a rank that owns no point: its zero-length W / V / g_p take
+    part in the all-gathers; all ranks agree bit for bit and match the single process."""
+    prob = tiny_problem()
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
+    rcams, rpts, rhist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
+    d = _run_ranks(tmp_path, 3, "tiny", "replicated")
+    for k in (1, 2):
+        for key in ("cams", "pts", "hist"):
+            np.testing.assert_array_equal(d[0][key], d[k][key])
+    assert abs(d[0]["hist"][-1][0] - rhist[-1][0]) <= 1e-6 * rhist[-1][0] + 1e-20
+    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-5, atol=1e-8)
+
+
+def test_ba_auto_rule_reports_its_branch():
+    """World size 1: 'auto' takes the sharded branch (bit-identical to sfm_ba_solve there) and
+    says so; the rule itself is covered on the CPU (tests/test_host_cpu.py)."""
+    import torch
+    import torch.distributed as dist
+    assert not dist.is_initialized()
+    prob = problem()
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        info = {}
+        R.bundle_adjust(*args, loss_s=2.0, max_iter=3, shard=True, info=info)
+        assert info["pcg"] == "sharded" and info["world"] == 1
+        lat, bw = R.probe_collectives(R.make_allreduce(), len(prob["cams"]), 0)
+        assert lat > 0 and bw > 0
+    finally:
+        R.release_allreduce()
+        dist.destroy_process_group()

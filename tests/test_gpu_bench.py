@@ -69,3 +69,83 @@ def test_bench_two_ranks_same_graph():
     assert two["n_gpus"] == 2 and two["config"]["pairs_total"] == 1225
     assert two["verified_matches_per_step"] == one["verified_matches_per_step"] == 554009
     assert two["graph_checksum"] == one["graph_checksum"]
+
+
+def _bench(args, launcher=None, timeout=600):
+    import socket
+    pre = [sys.executable]
+    if launcher:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        pre = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+               str(launcher), "--master-addr", "127.0.0.1", "--master-port", str(port)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "SFM_BENCH_LAUNCHER")}
+    env["OMP_NUM_THREADS"] = "4"
+    return subprocess.run(pre + [os.path.join(ROOT, "bench.py")] + args, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` with NO torch.distributed.run starts its two ranks
+    itself (gloo rehearsal: both on GPU 0) and reports n_gpus 2 with the N = 1 graph."""
+    out = _bench(["--config", "cfg3", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+                  "--gpus", "2", "--dist-backend", "gloo", "--device", "0"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["distributed"]["launcher"] == "self"
+    assert d["distributed"]["world"] == 2 and len(d["distributed"]["per_rank"]) == 2
+    assert [r["rank"] for r in d["distributed"]["per_rank"]] == [0, 1]
+    assert sum(r["pairs"] for r in d["distributed"]["per_rank"]) == 1225
+    assert d["verified_matches_per_step"] == 554009
+    one = _bench(["--config", "cfg3", "--steps", "1", "--warmup", "1", "--no-cpu-baseline"])
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = json.loads([l for l in one.stdout.splitlines() if l.strip()][-1])
+    assert d1["n_gpus"] == 1 and d1["distributed"]["launcher"] == "none"
+    assert d["graph_checksum"] == d1["graph_checksum"]
+
+
+def test_bench_refuses_more_gpus_than_the_box_has():
+    """`--gpus N` with fewer than N visible GPUs exits non-zero with a clear message and no JSON
+    line (the box has one MI355X)."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    out = _bench(["--config", "cfg3", "--gpus", str(n)], timeout=300)
+    assert out.returncode == 2, out.stderr[-2000:]
+    assert f"needs {n} visible GPUs" in out.stderr and out.stdout.strip() == ""
+
+
+def test_bench_cfg5_line_and_two_rank_rehearsal():
+    """`--config cfg5` (a step = one whole incremental reconstruction) on a
+    small scene: the line carries the end-to-end value, quality against the scene's truth, BA
+    sizes / iterations and the PCG branch, and the K3 / CG-iteration HBM fractions; a 2-rank gloo
+    rehearsal through the self-launcher (matching sharded, BA sharded, each PCG branch) returns
+    the single-process reconstruction."""
+    base = ["--config", "cfg5", "--n-img", "12", "--k", "1024", "--steps", "1", "--warmup", "1"]
+    one = _bench(base)
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = json.loads([l for l in one.stdout.splitlines() if l.strip()][-1])
+    c1 = d1["cfg5"]
+    assert d1["n_gpus"] == 1 and "BASELINE configs[4]" in d1["config"]["baseline_config"]
+    assert c1["registered"] == 12 and c1["median_reproj_px"] < 0.8
+    assert c1["max_centre_err_rel_radius"] < 0.02
+    assert abs(d1["value"] - c1["verified_matches"] * 1e3 / d1["ms_per_step"]) <= 1e-6 * d1["value"]
+    assert c1["pcg_branches"] == ["single"] and c1["lm_steps"] > 0 and c1["cg_iters"] > 0
+    rf = c1["ba_rooflines"]
+    assert 0 < rf["k3"]["frac"] < 1 and 0 < rf["cg_iteration"]["frac"] < 1
+    assert d1["roofline"]["bound"] == "hbm" and abs(d1["roofline"]["frac"] - rf["k3"]["frac"]) < 1e-12
+    for pcg in ("sharded", "replicated"):
+        two = _bench(base + ["--gpus", "2", "--dist-backend", "gloo", "--device", "0",
+                             "--ba-pcg", pcg])
+        assert two.returncode == 0, two.stderr[-3000:]
+        d2 = json.loads([l for l in two.stdout.splitlines() if l.strip()][-1])
+        c2 = d2["cfg5"]
+        assert d2["n_gpus"] == 2 and d2["distributed"]["launcher"] == "self"
+        assert c2["pcg_branches"] == [pcg] and c2["shard_ba"] is True
+        assert c2["verified_matches"] == c1["verified_matches"]
+        assert c2["registered"] == c1["registered"]
+        assert abs(c2["points"] - c1["points"]) <= max(2, c1["points"] // 1000)
+        assert abs(c2["median_reproj_px"] - c1["median_reproj_px"]) <= 1e-6 * c1["median_reproj_px"]

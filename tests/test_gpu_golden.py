@@ -105,3 +105,36 @@ def test_gpu_ransac_hypotheses_vs_skimage(ctx):
         ok = counts[i] >= 0  # -1: degenerate sample
         np.testing.assert_array_equal(mk[i][ok, :Ms[i]].sum(1), counts[i][ok])
         check_hypotheses_vs_skimage(fx, i, F[i], mk[i], norm[i])
+
+
+def test_gpu_opencv_rule_vs_skimage_nn_tables(ctx):
+    """the reference's BFMatcher(crossCheck=True) rule on the GPU against
+    OpenCV's update loop applied to scikit-image's nearest-neighbour tables (both directions, tie-
+    heavy L2 and Hamming, with and without the reference's `< 26` cut), through sfm_match_batch
+    and through the one-tile sfm_match_batch_both."""
+    import torch
+    from test_golden_cpu import xc_expectations
+    exp = xc_expectations()
+    for (kind, direc, md), (X, Y, rows, bd) in exp.items():
+        metric = 0 if kind == "l2" else 1
+        mdi = -1 if md is None else md
+        got = _gpu_pair(ctx, X, Y, metric=metric, cross_check=2, max_dist=mdi)
+        np.testing.assert_array_equal(got, rows.astype(np.int64), err_msg=str((kind, direc, md)))
+    # both orders from one tile: forward = (A, B), reverse = (B, A)
+    for kind in ("l2", "ham"):
+        for md in ((None, 26) if kind == "ham" else (None, 60000)):
+            A, B = exp[(kind, "fwd", md)][0], exp[(kind, "fwd", md)][1]
+            k = max(len(A), len(B))
+            desc = np.zeros((2, k, A.shape[1]), np.uint8)
+            desc[0, :len(A)], desc[1, :len(B)] = A, B
+            T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+            cnt, mt, dist = ctx.match_batch_both(
+                T(desc), T(np.array([len(A), len(B)], np.int32)), T(np.array([[0, 1]], np.int32)),
+                metric=0 if kind == "l2" else 1, cross_check=2, max_dist=-1 if md is None else md)
+            torch.cuda.synchronize()
+            cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+            for slot, direc in ((0, "fwd"), (1, "rev")):
+                _, _, rows, bd = exp[(kind, direc, md)]
+                n = int(cnt[slot])
+                np.testing.assert_array_equal(mt[slot, :n], rows, err_msg=str((kind, direc, md)))
+                np.testing.assert_array_equal(dist[slot, :n], bd)

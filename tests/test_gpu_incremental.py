@@ -13,24 +13,8 @@ import synth
 pytestmark = pytest.mark.gpu
 
 
-def _centres(cams):
-    out = []
-    for c in cams:
-        Rm = synth.angle_axis_to_rotmat(c[:3])
-        out.append(-Rm.T @ c[3:6])
-    return np.array(out)
-
-
-def _umeyama(src, dst):
-    """Similarity (s, R, t) minimising |s R src + t - dst|."""
-    ms, md = src.mean(0), dst.mean(0)
-    a, b = src - ms, dst - md
-    U, S, Vt = np.linalg.svd(b.T @ a / len(src))
-    D = np.eye(3)
-    D[2, 2] = np.sign(np.linalg.det(U @ Vt))
-    Rm = U @ D @ Vt
-    s = np.trace(np.diag(S) @ D) / (a * a).sum(1).mean()
-    return s, Rm, md - s * Rm @ ms
+_centres = synth.camera_centres
+_umeyama = synth.similarity_align
 
 
 def test_incremental_reconstruction_matches_truth():

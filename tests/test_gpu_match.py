@@ -212,3 +212,73 @@ def test_hamming_column_winner_kernel(ctx, xc):
                      ratio=(4, 5) if xc == 1 else None)
     finally:
         os.environ.pop("SFM_HAMMING_PATH", None)
+
+
+def _both(ctx, desc, n_kp, pairs, **kw):
+    import torch
+    d = torch.from_numpy(np.ascontiguousarray(desc)).cuda()
+    n = torch.from_numpy(np.ascontiguousarray(n_kp, np.int32)).cuda()
+    pr = torch.from_numpy(np.ascontiguousarray(pairs, np.int32)).cuda()
+    cnt, mt, dist = ctx.match_batch_both(d, n, pr, **kw)
+    torch.cuda.synchronize()
+    return cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+
+
+def _assert_both_equals_two_launches(ctx, desc, n_kp, metric, xc, maxd):
+    """sfm_match_batch_both on the unordered pairs == sfm_match_batch on (a, b) and on (b, a),
+    bit for bit (counts, indices, distances), and both == the oracle."""
+    n = len(desc)
+    up = synth.unordered_pairs(n)
+    cnt, mt, dist = _both(ctx, desc, n_kp, up, metric=metric, cross_check=xc, max_dist=maxd)
+    P = len(up)
+    for half, prs in ((0, up), (1, up[:, ::-1].copy())):
+        c2, m2, d2 = _gpu_match(ctx, desc, n_kp, prs, metric=metric, cross_check=xc,
+                                max_dist=maxd)
+        np.testing.assert_array_equal(cnt[half * P:(half + 1) * P], c2)
+        for p in range(P):
+            k = c2[p]
+            np.testing.assert_array_equal(mt[half * P + p, :k], m2[p, :k])
+            np.testing.assert_array_equal(dist[half * P + p, :k], d2[p, :k])
+    _check_pairs(ctx, desc, n_kp, np.concatenate([up, up[:, ::-1]]), metric=metric,
+                 cross_check=xc, max_dist=maxd)
+    return cnt
+
+
+@pytest.mark.parametrize("xc,maxd", [(2, 26), (2, -1), (1, 26), (0, -1)])
+def test_both_orders_hamming_reference_shape(ctx, xc, maxd):
+    """ORB-like descriptors at the reference's K = 500, ragged counts (an
+    empty image, a single descriptor), planted duplicates (exact ties on both sides): one tile
+    per unordered pair gives both ordered results bit-identical to two launches."""
+    s = synth.make_scene(6, 500, seed=29, orb=True)
+    desc, n_kp = s["desc"].copy(), s["n_kp"].copy()
+    n_kp[1], n_kp[3], n_kp[4] = 313, 0, 1
+    desc[2, 7] = desc[2, 9]          # two identical trains
+    desc[0, 40:44] = desc[5, 100]    # one train equidistant to four queries
+    cnt = _assert_both_equals_two_launches(ctx, desc, n_kp, 1, xc, maxd)
+    assert cnt.sum() > 0
+
+
+@pytest.mark.parametrize("xc,maxd", [(2, -1), (1, -1), (0, -1), (2, 30000)])
+def test_both_orders_l2(ctx, xc, maxd):
+    s = synth.make_scene(4, 1000, seed=31)
+    desc, n_kp = s["desc"].copy(), s["n_kp"].copy()
+    n_kp[2] = 517
+    desc[1, 3] = desc[1, 8]
+    cnt = _assert_both_equals_two_launches(ctx, desc, n_kp, 0, xc, maxd)
+    assert cnt.sum() > 0
+
+
+def test_both_orders_rejects_ratio_and_large_k(ctx):
+    import torch
+    s = synth.make_scene(2, 64, seed=1)
+    d = torch.from_numpy(s["desc"]).cuda()
+    n = torch.from_numpy(s["n_kp"]).cuda()
+    pr = torch.tensor([[0, 1]], dtype=torch.int32).cuda()
+    prm = sfmcore.MatchParams(0, 1, 4, 5, -1)
+    out = [torch.empty(2, dtype=torch.int32).cuda(), torch.empty((2, 64, 2), dtype=torch.int32).cuda(),
+           torch.empty((2, 64), dtype=torch.int32).cuda()]
+    import ctypes as C
+    rc = ctx.lib.sfm_match_batch_both(ctx.handle, d.data_ptr(), n.data_ptr(), 2, 64, 128,
+                                      pr.data_ptr(), 1, C.byref(prm), out[0].data_ptr(),
+                                      out[1].data_ptr(), out[2].data_ptr())
+    assert rc != 0 and b"ratio" in ctx.lib.sfm_last_error()
