@@ -211,6 +211,14 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
         crow[o] = (j < n_kp[img]) ? (-128 * nv + 127 - (j & 127)) : ROW_PAD;
 }
 
+// K1 prologue: with MU_PAIR_INFO the pair_order kernel also writes one 16-B record per ordered
+// slot (p, a, b, na | nb << 16), so a block of the mutual kernel finds its pair with ONE dependent
+// load instead of the chain pair_order -> pairs -> n_kp (three round trips before the first
+// address of the stage-0 DMA is known).
+#ifndef MU_PAIR_INFO
+#define MU_PAIR_INFO 1
+#endif
+
 // Pair order by train image (counting sort in LDS; one block): consecutive entries share image b.
 __global__ __launch_bounds__(1024) void pair_order_kernel(const int32_t* __restrict__ pairs,
                                                           int n_pairs, int n_img,
@@ -228,6 +236,18 @@ __global__ __launch_bounds__(1024) void pair_order_kernel(const int32_t* __restr
     }
     __syncthreads();
     for (int p = tid; p < n_pairs; p += 1024) order[atomicAdd(&hist[pairs[2 * p + 1]], 1)] = p;
+}
+
+// The per-slot pair record of MU_PAIR_INFO (after pair_order_kernel).
+__global__ __launch_bounds__(256) void pair_info_kernel(const int32_t* __restrict__ pairs,
+                                                        const int32_t* __restrict__ n_kp,
+                                                        int n_pairs, const int32_t* __restrict__ order,
+                                                        int4* __restrict__ info) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= n_pairs) return;
+    const int p = order[s];
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    info[s] = make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
 }
 
 // TOP2 = false: the row side keeps only (best, argbest) — the second-best value is what the ratio
@@ -549,7 +569,7 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
     const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
-    unsigned long long* __restrict__ colpart, int col_atomic) {
+    unsigned long long* __restrict__ colpart, int col_atomic, const int4* __restrict__ pair_info) {
     constexpr int QT = Geo<D>::QT, QB = mu_qb<D>(), CHUNK = MU_CHUNK_BYTES / D, NK = Geo<D>::NK;
     constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32, NTHR = 64 * MU_WAVES;
     constexpr int PIECES = CHUNK * D / 1024 / MU_WAVES, RPP = 1024 / D;
@@ -564,9 +584,15 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     const int per_xcd = (int)(gridDim.x >> 3);
     const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
     if (sblk >= n_blk) return;  // block-uniform, before any barrier
-    const int p = pair_order[sblk / n_qblk], qb = sblk % n_qblk;
+    const int qb = sblk % n_qblk;
+#if MU_PAIR_INFO
+    const int4 pinf = pair_info[sblk / n_qblk];
+    const int p = pinf.x, a = pinf.y, b = pinf.z, na = pinf.w & 0xFFFF, nb = pinf.w >> 16;
+#else
+    const int p = pair_order[sblk / n_qblk];
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
+#endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     for (int j = tid; j < k_pad; j += NTHR) lds_col[j] = 0ull;
 
@@ -1141,7 +1167,8 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
     const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
     const size_t ordb = sfm::align_up(sizeof(int32_t) * ((size_t)n_pairs + n_img), 256);
-    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + 1024);
+    const size_t infb = sfm::align_up(sizeof(int4) * (size_t)n_pairs, 256);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + infb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     uint8_t* zero_row = (uint8_t*)ws;
     int32_t* norm = (int32_t*)(ws + 256);
@@ -1150,6 +1177,7 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
     uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
     int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
+    int4* pair_info = (int4*)(ws + 256 + 2 * tab + rowb + colb + descb + ordb);
     const int n_blk = n_pairs * n_qblk;
     // column winners merged by atomics (default) or as per-query-block partials the finalize
     // reduces (SFM_MU_COLPART=1); DESIGN.md 4.1
@@ -1165,6 +1193,11 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
                        pairs, n_pairs, n_img, pair_order, pair_order + n_pairs);
     SFM_HIP_CHECK(hipGetLastError());
+    if (MU_PAIR_INFO) {
+        hipLaunchKernelGGL(pair_info_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, st, pairs,
+                           n_kp, n_pairs, pair_order, pair_info);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
     if (l2)
         hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_L2, true>), dim3(k_pad / 256, n_img),
                            dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row,
@@ -1178,7 +1211,7 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(64 * MU_WAVES),             \
                        (size_t)k_pad * 8, st, desc_i8, n_kp,                                      \
                        k_max, k_pad, norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk,     \
-                       rowres, colpart, col_atomic)
+                       rowres, colpart, col_atomic, pair_info)
     if (l2 && rows) SFM_MU_SCAN(128, true);
     else if (l2) SFM_MU_SCAN(128, false);
     else if (rows) SFM_MU_SCAN(256, true);

@@ -72,42 +72,49 @@ def _match_array(matches) -> np.ndarray:
 
 
 def verify_pairs(pair_matches, keypoints, n_hyp=DEFAULT_HYPOTHESES, seed=DEFAULT_SEED,
-                 thr=DEFAULT_THRESHOLD, min_inliers=DEFAULT_MIN_INLIERS, device=0):
+                 thr=DEFAULT_THRESHOLD, min_inliers=DEFAULT_MIN_INLIERS, device=0,
+                 chunk=8192):
     """Verifies the reference's pair list (code/pipeline.py:36-47: Pair objects with img_inx_1,
-    img_inx_2, matches; the ordered N(N-1) enumeration or any subset) in ONE batched call:
-    keypoints[i] = [K_i,2] pixel coordinates of image i.  Returns the verified subset (input
-    order) with `.matches` reduced to the inliers (ascending match index) and `.F` (pixel F,
-    unit norm) attached.  Results equal verify_pair on each pair (the RNG is keyed by the pair's
-    image ids, so they do not depend on the batch)."""
+    img_inx_2, matches; the ordered N(N-1) enumeration or any subset) in batched calls of at most
+    `chunk` pairs (host and device buffers are [chunk, k_max] — constant memory however long the
+    list): keypoints[i] = [K_i,2] pixel coordinates of image i.  Returns the verified
+    subset (input order) with `.matches` reduced to the inliers (ascending match index) and `.F`
+    (pixel F, unit norm) attached.  Results equal verify_pair on each pair (the RNG is keyed by the
+    pair's image ids, so they depend neither on the batch nor on the chunking)."""
     import torch
     if not pair_matches:
         return []
-    mts = [_match_array(pr.matches) for pr in pair_matches]
-    P = len(pair_matches)
     pairs = np.array([[int(pr.img_inx_1), int(pr.img_inx_2)] for pr in pair_matches], np.int32)
     n_img = int(pairs.max()) + 1
     kl = [np.asarray(keypoints[i], np.float32).reshape(-1, 2) for i in range(n_img)]
-    k_max = max([len(k) for k in kl] + [len(m) for m in mts] + [1])
+    counts = np.array([len(pr.matches) for pr in pair_matches], np.int32)
+    k_max = max([len(k) for k in kl] + [int(counts.max()), 1])
     kps = np.zeros((n_img, k_max, 2), np.float32)
     for i, k in enumerate(kl):
         kps[i, :len(k)] = k
-    counts = np.array([len(m) for m in mts], np.int32)
-    match = np.zeros((P, k_max, 2), np.int32)
-    for p, m in enumerate(mts):
-        match[p, :len(m)] = m
     dev = torch.device("cuda", device)
-    out = sfmcore.context(device).ransac_batch(
-        torch.from_numpy(kps).to(dev), torch.from_numpy(pairs).to(dev),
-        torch.from_numpy(counts).to(dev), torch.from_numpy(match).to(dev), n_hyp=n_hyp,
-        seed=seed, thr=thr, min_inliers=min_inliers)
-    cnt = out["inl_count"].cpu().numpy()
-    mask = out["mask"].cpu().numpy()
-    Fn, nrm = out["F"].cpu().numpy(), out["norm"].cpu().numpy()
+    ctx = sfmcore.context(device)
+    kps_d = torch.from_numpy(kps).to(dev)
     verified = []
-    for p, pr in enumerate(pair_matches):
-        if cnt[p] >= min_inliers:
-            keep = np.nonzero(mask[p, :counts[p]])[0]
-            pr.matches = [pr.matches[i] for i in keep]
-            pr.F = denormalize_F(Fn[p], nrm[p])
-            verified.append(pr)
+    for c0 in range(0, len(pair_matches), max(int(chunk), 1)):
+        prs = pair_matches[c0:c0 + chunk]
+        P = len(prs)
+        match = np.zeros((P, k_max, 2), np.int32)
+        for p, pr in enumerate(prs):
+            m = _match_array(pr.matches)
+            match[p, :len(m)] = m
+        cc = counts[c0:c0 + P]
+        out = ctx.ransac_batch(kps_d, torch.from_numpy(np.ascontiguousarray(pairs[c0:c0 + P])).to(dev),
+                               torch.from_numpy(np.ascontiguousarray(cc)).to(dev),
+                               torch.from_numpy(match).to(dev), n_hyp=n_hyp, seed=seed, thr=thr,
+                               min_inliers=min_inliers)
+        cnt = out["inl_count"].cpu().numpy()
+        mask = out["mask"].cpu().numpy()
+        Fn, nrm = out["F"].cpu().numpy(), out["norm"].cpu().numpy()
+        for p, pr in enumerate(prs):
+            if cnt[p] >= min_inliers:
+                keep = np.nonzero(mask[p, :cc[p]])[0]
+                pr.matches = [pr.matches[i] for i in keep]
+                pr.F = denormalize_F(Fn[p], nrm[p])
+                verified.append(pr)
     return verified

@@ -293,8 +293,10 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
         return
     ref, second = rec.gauge
     fixed = reconstruction.gauge_mask(rec.cams, ref=ref, second=second, fix_intrinsics=True)
-    tr = obs_track[use]
-    pts_ids, pt_idx = np.unique(tr, return_inverse=True)
+    tr = obs_track[use]   # non-decreasing (obs_track is track-major): unique by run starts
+    first = np.r_[True, tr[1:] != tr[:-1]] if len(tr) else np.zeros(0, bool)
+    pts_ids = tr[first]
+    pt_idx = np.cumsum(first) - 1
     info = {}
     cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
                                                    timg[use], pt_idx.astype(np.int32),

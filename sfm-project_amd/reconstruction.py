@@ -52,9 +52,19 @@ def build_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, device: i
 
 
 def reprojection_errors(cams, pp, pts, cam_idx, pt_idx, uv, device: int = 0) -> np.ndarray:
-    """Per-observation reprojection error (px) from the GPU residuals."""
-    r = build_jtj(cams, pp, pts, cam_idx, pt_idx, uv, device=device)["res"]
-    return np.sqrt(np.sum(r * r, axis=1))
+    """Per-observation reprojection error (px) from the GPU residuals, in the caller's order.
+    The norms are formed on the device; only n_obs doubles cross PCIe (not the J^TJ blocks)."""
+    import torch
+    out = build_jtj(cams, pp, pts, cam_idx, pt_idx, uv, device=device, as_numpy=False)
+    r = out["res"]
+    err = torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1]).cpu().numpy()
+    pt_idx = np.asarray(pt_idx)
+    if len(pt_idx) and np.any(np.diff(pt_idx) < 0):   # build_jtj regrouped by point
+        order = np.argsort(pt_idx, kind="stable")
+        e = np.empty_like(err)
+        e[order] = err
+        err = e
+    return err
 
 
 # ---- multi-GPU: observations sharded by point, camera blocks all-reduced (SURVEY.md §8e) --------

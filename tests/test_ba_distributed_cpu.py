@@ -47,8 +47,15 @@ def _worker(rank, world, port, out_dir):
     reconstruction.allreduce_camera_blocks(U, gc, cost)
     ar = torch.arange(6, dtype=torch.float64) * (rank + 1)   # the sharded solve's hook (gloo path)
     reconstruction.make_allreduce()(ar[1:5])
+    # the replicated PCG branch's gather of the point-side blocks (ragged shards, rank order)
+    cuts = [reconstruction.shard_points(pt_ptr, r, world) for r in range(world)]
+    c_obs = [int(pt_ptr[b] - pt_ptr[a]) for a, b in cuts]
+    Wall = reconstruction._gather_rows(torch.from_numpy(o["W"]), c_obs, None).numpy()
+    Vall = reconstruction._gather_rows(torch.from_numpy(o["V"]), [b - a for a, b in cuts],
+                                       None).numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), U=U.numpy(), gc=gc.numpy(), ar=ar.numpy(),
-             cost=cost.numpy(), V=o["V"], W=o["W"], res=o["res"], lo=lo, hi=hi, o0=o0, o1=o1)
+             cost=cost.numpy(), V=o["V"], W=o["W"], res=o["res"], lo=lo, hi=hi, o0=o0, o1=o1,
+             Wall=Wall, Vall=Vall)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -80,3 +87,6 @@ def test_ba_allreduce_gloo_world2(tmp_path):
         np.testing.assert_array_equal(r[k]["W"], full["W"][o0:o1])
         np.testing.assert_array_equal(r[k]["res"], full["res"][o0:o1])
         np.testing.assert_array_equal(r[k]["ar"], [0, 3, 6, 9, 12, 5 * (k + 1)])
+        # replicated branch: every rank holds the whole W / V after the ragged all-gather
+        np.testing.assert_array_equal(r[k]["Wall"], full["W"])
+        np.testing.assert_array_equal(r[k]["Vall"], full["V"])

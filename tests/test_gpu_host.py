@@ -253,3 +253,20 @@ def test_verify_pairs_batched_equals_per_pair_on_ordered_list():
         assert [(m.queryIdx, m.trainIdx) for m in o.matches] == \
             [(b.matches[i].queryIdx, b.matches[i].trainIdx) for i in r["inliers"]]
         np.testing.assert_array_equal(o.F, r["F"])
+
+
+def test_verify_pairs_chunked_equals_one_batch():
+    """verify_pairs works in fixed-size chunks (constant memory for the ordered
+    N(N-1) list); the RNG is keyed by image ids, so chunking changes nothing."""
+    import copy
+    s = synth.make_scene(5, 1024, seed=17)
+    prs = fm.match_all_pairs([s["desc"][i] for i in range(5)], norm="l2", cross_check="mutual",
+                             max_distance=None, ratio=(4, 5), ordered=True, sort=False)
+    one = gv.verify_pairs(copy.deepcopy(prs), s["kps"], n_hyp=1024)
+    chunked = gv.verify_pairs(copy.deepcopy(prs), s["kps"], n_hyp=1024, chunk=3)
+    assert len(one) == len(chunked) > 0
+    for a, b in zip(one, chunked):
+        assert (a.img_inx_1, a.img_inx_2) == (b.img_inx_1, b.img_inx_2)
+        assert [(m.queryIdx, m.trainIdx) for m in a.matches] == \
+            [(m.queryIdx, m.trainIdx) for m in b.matches]
+        np.testing.assert_array_equal(a.F, b.F)
