@@ -211,12 +211,14 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
         crow[o] = (j < n_kp[img]) ? (-128 * nv + 127 - (j & 127)) : ROW_PAD;
 }
 
-// K1 prologue: with MU_PAIR_INFO the pair_order kernel also writes one 16-B record per ordered
-// slot (p, a, b, na | nb << 16), so a block of the mutual kernel finds its pair with ONE dependent
-// load instead of the chain pair_order -> pairs -> n_kp (three round trips before the first
-// address of the stage-0 DMA is known).
+// K1 prologue (round 4): with MU_PAIR_INFO=1 a small kernel after pair_order
+// writes one 16-B record per ordered slot (p, a, b, na | nb << 16), so a block of the mutual
+// kernel finds its pair with ONE dependent load instead of the chain pair_order -> pairs -> n_kp.
+// Measured equal at cfg3 (0.974 / 0.983 / 0.976 ms vs 0.972 / 0.978 / 0.981 ms per launch,
+// interleaved, profiles/r04/k1_prologue_ab.txt): the chain is hidden behind the other blocks'
+// streams, so the knob stays off (A/B only).
 #ifndef MU_PAIR_INFO
-#define MU_PAIR_INFO 1
+#define MU_PAIR_INFO 0
 #endif
 
 // Pair order by train image (counting sort in LDS; one block): consecutive entries share image b.

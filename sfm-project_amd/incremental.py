@@ -108,7 +108,7 @@ def _match_graph(gb, pairs, pairs_t, n_kp, group):
 
 def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
                 ba_iter=20, loss_s=2.0, device=0, log=None, group=None, shard_ba=False,
-                ba_cg_tol=0.1, ba_pcg="auto"):
+                ba_cg_tol=0.1, ba_pcg="auto", ba_ftol=1e-6):
     """desc [n_img,K,D] u8, kps [n_img,K,2] pixels, n_kp [n_img], intr [n_img,4] = (f, k1, cx, cy).
     Returns a Reconstruction (cams [n_img,8], registered mask, points per track, track arrays).
     With torch.distributed initialised (one process per GPU, `group` or the default group) the
@@ -122,7 +122,10 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     final BA takes 333 CG iterations instead of 3640 (1e-10) for the same optimum to 1e-7 of
     the cost and the same reconstruction.
     ba_pcg: the sharded bundle adjustments' PCG branch (reconstruction.bundle_adjust `pcg`:
-    auto | sharded | replicated); rec.ba_log records the branch each one took."""
+    auto | sharded | replicated); rec.ba_log records the branch each one took.
+    ba_ftol: an LM run stops once an accepted step lowers the cost by <= ba_ftol * cost (Ceres'
+    and COLMAP's function tolerance, 1e-6); at 1e-12 every bundle adjustment of the 500-image
+    cfg5 scene ran its 20 steps."""
     import time
     import torch
     dev = torch.device("cuda", device)
@@ -205,7 +208,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         raise RuntimeError("reconstruct: no initial pair with enough well-conditioned matches")
     tk = lap("initial_pair", tk)
     _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-            shard_ba, group, ba_cg_tol, ba_pcg)
+            shard_ba, group, ba_cg_tol, ba_pcg, ba_ftol)
     tk = lap("bundle_adjust", tk)
     tim["rounds"] = 0
 
@@ -243,7 +246,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev)
         tk = lap("triangulate", tk)
         _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-                shard_ba, group, ba_cg_tol, ba_pcg)
+                shard_ba, group, ba_cg_tol, ba_pcg, ba_ftol)
         tk = lap("bundle_adjust", tk)
     return rec
 
@@ -283,7 +286,7 @@ def _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev):
 
 
 def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-            shard_ba=False, group=None, cg_tol=0.1, pcg="auto"):
+            shard_ba=False, group=None, cg_tol=0.1, pcg="auto", ftol=1e-6):
     """Global LM over the registered cameras and the triangulated points (GPU), then drop points
     whose mean reprojection error stays above max_err.  Gauge: the initial pair's first camera
     keeps its pose and the second one translation coordinate (the scale); the intrinsics are
@@ -297,13 +300,15 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
     first = np.r_[True, tr[1:] != tr[:-1]] if len(tr) else np.zeros(0, bool)
     pts_ids = tr[first]
     pt_idx = np.cumsum(first) - 1
+    import time
+    t0 = time.perf_counter()
     info = {}
     cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
                                                    timg[use], pt_idx.astype(np.int32),
                                                    obs_xy[use], loss_s=loss_s, max_iter=ba_iter,
-                                                   cg_tol=cg_tol, device=device, fixed=fixed,
-                                                   shard=shard_ba, group=group, pcg=pcg,
-                                                   info=info)
+                                                   cg_tol=cg_tol, ftol=ftol, device=device,
+                                                   fixed=fixed, shard=shard_ba, group=group,
+                                                   pcg=pcg, info=info)
     rec.ba_log.append(dict(info, n_cam=int(rec.registered.sum()), n_pt=int(len(pts_ids)),
                            n_obs=int(use.sum()), lm_steps=len(hist),
                            cg_iters=int(sum(h[3] for h in hist))))
@@ -315,5 +320,6 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
     mean = np.bincount(pt_idx, err, minlength=len(pts_ids)) / np.maximum(
         np.bincount(pt_idx, minlength=len(pts_ids)), 1)
     rec.has_point[pts_ids[mean > max_err]] = False
+    rec.ba_log[-1]["s"] = time.perf_counter() - t0   # setup + LM + reprojection filter
     rec.history.append((int(reg.sum()), int(rec.has_point.sum()),
                         float(hist[-1][0]) if hist else float("nan")))

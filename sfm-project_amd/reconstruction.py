@@ -32,13 +32,14 @@ def build_jtj(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, device: i
     if len(pt_idx) and np.any(np.diff(pt_idx) < 0):
         order = np.argsort(pt_idx, kind="stable")
         cam_idx, pt_idx, uv = cam_idx[order], pt_idx[order], uv[order]
-    pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
-    cam_ptr, cam_obs = sfmcore.csr_by(cam_idx, n_cam)
     dev = torch.device("cuda", device)
     T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)
+    cam_d, pt_d = T(cam_idx), T(pt_idx)
+    pt_ptr, _ = sfmcore.csr_by_device(pt_d, n_pt)
+    cam_ptr, cam_obs = sfmcore.csr_by_device(cam_d, n_cam)
     out = sfmcore.context(device).ba_jtj(T(cams, np.float64), T(pp, np.float64),
-                                         T(pts, np.float64), T(cam_idx), T(pt_idx), T(uv),
-                                         T(pt_ptr), T(cam_ptr), T(cam_obs), loss_s=loss_s)
+                                         T(pts, np.float64), cam_d, pt_d, T(uv),
+                                         pt_ptr, cam_ptr, cam_obs, loss_s=loss_s)
     if not as_numpy:
         return out
     res = {k: v.cpu().numpy() for k, v in out.items()}
@@ -141,13 +142,12 @@ class BAProblem:
         if len(pt_idx) and np.any(np.diff(pt_idx) < 0):
             self.order = np.argsort(pt_idx, kind="stable")
             cam_idx, pt_idx, uv = cam_idx[self.order], pt_idx[self.order], uv[self.order]
-        pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
-        cam_ptr, cam_obs = sfmcore.csr_by(cam_idx, n_cam)
         self.dev = torch.device("cuda", device)
         T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dt)).to(self.dev)
         self.pp = T(pp, np.float64)
         self.cam_idx, self.pt_idx, self.uv = T(cam_idx), T(pt_idx), T(uv)
-        self.pt_ptr, self.cam_ptr, self.cam_obs = T(pt_ptr), T(cam_ptr), T(cam_obs)
+        self.pt_ptr, _ = sfmcore.csr_by_device(self.pt_idx, n_pt)
+        self.cam_ptr, self.cam_obs = sfmcore.csr_by_device(self.cam_idx, n_cam)
         self.n_cam, self.n_pt = n_cam, n_pt
         self.ctx = sfmcore.context(device)
 
@@ -457,6 +457,10 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                                          prob.cam_ptr, prob.cam_obs, lam, allreduce,
                                          max_iter=max_cg, tol=cg_tol)
     upd = full if full is not None else prob
+    if info is not None:
+        import time
+        torch.cuda.synchronize(prob.dev)
+        t_lm = time.perf_counter()
     lam, nu = lam0, 2.0
     hist = []
     old = float(cost(cams_d, pts_d).item())
@@ -485,6 +489,8 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             hist.append((old, lam, False, it))
             if lam > 1e16:
                 break
+    if info is not None:
+        info["lm_s"] = time.perf_counter() - t_lm   # the loop ends in a host sync (the last step)
     if allreduce is not None and full is None:
         # gather the point shards: one all-reduce of the zero-padded set
         allp = torch.zeros((n_pt, 3), dtype=torch.float64, device=prob.dev)

@@ -160,3 +160,16 @@ def test_draw_matches_numpy():
     assert (img[10, 50 + 23] == col).all()                # ring of kp2[1] (shifted by w1 = 50)
     assert (img[15, 41] == col).all()                     # on the line (10,20) -> (70,10)
     assert (img[5, 43] == 10).all() and (img[50, 58] == 200).all()  # unmatched points not drawn
+
+
+def test_csr_by_device_equals_host_csr():
+    """BAProblem builds its CSR indices with torch's stable sort (sfmcore.csr_by_device); the
+    result is the host csr_by's, bit for bit (run here on CPU tensors)."""
+    import torch
+    rng = np.random.default_rng(4)
+    for n, m in ((7, 0), (1, 5), (500, 20000), (3, 1000)):
+        idx = rng.integers(0, n, m).astype(np.int32)
+        ptr, order = sfmcore.csr_by(idx, n)
+        dptr, dorder = sfmcore.csr_by_device(torch.from_numpy(idx), n)
+        np.testing.assert_array_equal(dptr.numpy(), ptr)
+        np.testing.assert_array_equal(dorder.numpy(), order)
