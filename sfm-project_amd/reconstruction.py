@@ -348,7 +348,7 @@ def _gather_rows(t, counts, group):
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
                   lam0: float = 1e-4, ftol: float = 1e-12, max_cg: int = 200,
                   cg_tol: float = 1e-10, device: int = 0, fixed=None, shard: bool = False,
-                  group=None, pcg: str = "auto", info=None):
+                  group=None, pcg: str = "auto", info=None, reproj_err: bool = False):
     """Levenberg-Marquardt on paper eq. (1): every step on the GPU
     (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
     accept / reject it.
@@ -371,7 +371,11 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
       'auto'       — pcg_rule on the measured all-reduce latency / bandwidth of the group
                      (probe_collectives); world size 1 always takes 'sharded'.
     Every rank returns the same result, equal to the unsharded one up to the fp64 summation
-    order.  `info` (optional dict) receives the branch taken and the rule's terms.
+    order.  `info` (optional dict) receives the branch taken and the rule's terms; with
+    reproj_err it also receives `err`: every observation's reprojection error (px) at the returned
+    parameters, in the caller's order — from the device-resident problem (one more K3 launch;
+    sharded: each rank's shard summed into a zero-padded vector), instead of a second host ->
+    device copy of the whole problem through reprojection_errors.
 
     Returns (cams [n_cam,8], pts [n_pt,3], history [(cost, λ, accepted, cg_iterations)])."""
     import os
@@ -395,6 +399,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         cam_idx, pt_idx, uv = cam_idx[order], pt_idx[order], uv[order]
         pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
         lo, hi = shard_points(pt_ptr, rank, world)
+        n_obs_all = len(pt_idx)
         o0, o1 = int(pt_ptr[lo]), int(pt_ptr[hi])
         mode = os.environ.get("SFM_BA_PCG", pcg)
         if mode not in ("auto", "sharded", "replicated"):
@@ -491,6 +496,22 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                 break
     if info is not None:
         info["lm_s"] = time.perf_counter() - t_lm   # the loop ends in a host sync (the last step)
+    if reproj_err and info is not None:
+        r = prob.linearize(cams_d, shard_of(pts_d), loss_s)["res"]
+        e = torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1])
+        if allreduce is None:
+            err = e.cpu().numpy()
+            if prob.order is not None:   # BAProblem regrouped the observations by point
+                back = np.empty_like(err)
+                back[prob.order] = err
+                err = back
+        else:
+            ev = torch.zeros(n_obs_all, dtype=torch.float64, device=prob.dev)
+            ev[o0:o1] = e
+            allreduce(ev)
+            err = np.empty(n_obs_all)
+            err[order] = ev.cpu().numpy()
+        info["err"] = err
     if allreduce is not None and full is None:
         # gather the point shards: one all-reduce of the zero-padded set
         allp = torch.zeros((n_pt, 3), dtype=torch.float64, device=prob.dev)
