@@ -98,6 +98,14 @@ __device__ __forceinline__ int vmed3(int a, int b, int c) {
     return r;
 }
 
+// v_max3_i32 issued after `d0` and `d1` are computed (extra asm operands): lets an asm max3 read
+// MFMA results once a compiler-emitted instruction has taken the padded first read.
+__device__ __forceinline__ int vmax3_after(int a, int b, int c, int d0, int d1) {
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c), "v"(d0), "v"(d1));
+    return r;
+}
+
 // No-return 64-bit LDS atomic max.  Inline asm: the compiler's LDS-DMA alias tracking treats a
 // builtin atomic to the column-state object as possibly aliasing the in-flight staging DMA and
 // inserts vmcnt(0); this one is ordered only by the lgkmcnt(0) of the barrier that precedes
@@ -151,7 +159,9 @@ __device__ __forceinline__ int transpose_max16(const int (&c)[16], int lane) {
 
 // Per descriptor: the i8 feature row (L2: x ^ 0x80; Hamming: bits -> 0/1 bytes), its norm
 // (|x'|^2 resp. popcount) and the row-key constant, padded to k_pad (multiple of 256).
-template <int METRIC, bool CINIT = false>
+// BITV: the byte value of a set bit (Hamming): 1 for the fused / column-winner kernels, 16 for the
+// key-in-the-accumulator Hamming kernel (16 x 16 = 256: the MFMA then yields 256 dot).
+template <int METRIC, bool CINIT = false, int BITV = 1>
 __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
                                  int k_max, int k_pad, int32_t* __restrict__ norm,
                                  int32_t* __restrict__ crow, uint8_t* __restrict__ zero_row,
@@ -194,7 +204,8 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {  // 4 bits of word e -> one u32 of 0/1 bytes
                         const unsigned nib = (w[e] >> (4 * t)) & 0xFu;
-                        o[t] = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+                        o[t] = ((nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21)) *
+                               (unsigned)BITV;
                     }
                     o8[8 * q + 2 * e] = make_uint4(o[0], o[1], o[2], o[3]);
                     o8[8 * q + 2 * e + 1] = make_uint4(o[4], o[5], o[6], o[7]);
@@ -767,6 +778,204 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
 #endif
 }
 
+// ---- Hamming with the key built by the MFMA itself (sfm_match_batch_both's Hamming path) ----------
+//
+// The reference's own matcher is Hamming (ORB, code/feature_matching.py:48).  With the bits as
+// 0/16 bytes the i8 MFMA yields 256 dot exactly, the accumulator init is the train constant
+// crow_j = -128 n_j + (127 - j mod 128) (from LDS, as the mutual kernel's init), and ONE extra
+// 32-deep MFMA k-step adds the query constant -128 n_q + (127 - q mod 64): its A fragment is a
+// constant (eight 64s and a 1 in the lane-half-0 bytes), its B fragment per query holds eight
+// digits d_t in [-128, 0] with sum -2 n_q and the byte 127 - q mod 64.  So every element's
+// accumulator is already
+//     K = -128 d + (127 - j mod 128) + (127 - q mod 64),        d = n_j + n_q - 2 dot,
+// the key of BOTH directions: for a fixed query (lane) the q term is a constant (row top-1 by
+// max3, the nearest train and its lowest index decode from K - (127 - q mod 64)); for a fixed
+// train the j term is (column max over the query tiles + the wave transpose, as the fused kernel).
+// No VALU op builds a key: per element 0.5 (row max3) + 0.5 (column max) + the transpose, against
+// the fused key kernel's mad24 + max3 + add + max3 + transpose.  Padded queries get eight -128
+// digits (K <= -65536 + 254, below every real key >= -32768); padded trains the prep's ROW_PAD.
+// Outputs the fused kernel's formats: rowres (n_q - d1, J1) per query, column winners merged by
+// 64-bit atomicMax into one row per pair (colpart zeroed before the launch); both_finalize_kernel
+// then writes (a, b) and (b, a).
+template <bool ROWS>
+__global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void ham_key_kernel(
+    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+    const int32_t* __restrict__ norm, const int32_t* __restrict__ crow_tab,
+    const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
+    const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
+    unsigned long long* __restrict__ colpart) {
+    constexpr int D = 256, QT = Geo<D>::QT, QB = mu_qb<D>(), CHUNK = MU_CHUNK_BYTES / D;
+    constexpr int NK = Geo<D>::NK, SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32, NTHR = 64 * MU_WAVES;
+    constexpr int PIECES = CHUNK * D / 1024 / MU_WAVES, RPP = 1024 / D;
+    static_assert(QT == 2 && QT * 32 <= 128, "query index field: 127 - q mod 64");
+    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
+    extern __shared__ unsigned long long lds_col[];  // [k_pad], dynamic
+
+    const int per_xcd = (int)(gridDim.x >> 3);
+    const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+    if (sblk >= n_blk) return;  // block-uniform, before any barrier
+    const int p = pair_order[sblk / n_qblk], qb = sblk % n_qblk;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    const int na = n_kp[a], nb = n_kp[b];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+    for (int j = tid; j < k_pad; j += NTHR) lds_col[j] = 0ull;
+
+    const uint8_t* db = desc + (size_t)b * k_max * D;
+    const int32_t* crb = crow_tab + (size_t)b * k_pad;
+    const int n_chunk = (nb + CHUNK - 1) / CHUNK;
+    auto stage = [&](int ch, unsigned char* dst) {
+#pragma unroll
+        for (int i = 0; i < PIECES; ++i) {
+            const int piece = wave * PIECES + i;
+            const int row = piece * RPP + lane / SLOTS;
+            const int slot = (lane % SLOTS) ^ swz<D>(row);
+            const int j = ch * CHUNK + row;
+            const uint8_t* src = (j < nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
+        }
+        if (wave == 0 && lane < CHUNK / 4) {
+            const int32_t* src = crb + ch * CHUNK + lane * 4;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D), 16, 0, 0);
+        }
+    };
+
+    const int qbase = qb * QB + wave * QT * 32;
+    const bool active = qbase < na;  // wave-uniform
+    v4i bq[QT][NK], bx[QT];
+    int nq[QT], tb[QT], B1[QT], J1[QT];
+    const uint8_t* da = desc + (size_t)a * k_max * D;
+    // the extra k-step: A = 64 in bytes 0..7 and 1 in byte 8 of the lane-half-0 fragment
+    const v4i ax = h ? v4i{0, 0, 0, 0} : v4i{0x40404040, 0x40404040, 1, 0};
+#pragma unroll
+    for (int c = 0; c < QT; ++c) {
+        const int q = qbase + c * 32 + r32;
+        const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * D + (D / 2) * h : zero_row + (D / 2) * h);
+#pragma unroll
+        for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
+        nq[c] = (q < na) ? norm[(size_t)a * k_pad + q] : 0;
+        // digits of -2 n_q (each in [-128, 0]) in bytes 0..7, 127 - q mod 64 in byte 8
+        const int m = (q < na) ? 2 * nq[c] : 1024;
+        unsigned w0 = 0, w1 = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int dgt = -min(max(m - 128 * t, 0), 128);
+            const unsigned byte = (unsigned)(dgt & 0xFF);
+            if (t < 4) w0 |= byte << (8 * t); else w1 |= byte << (8 * (t - 4));
+        }
+        bx[c] = h ? v4i{0, 0, 0, 0} : v4i{(int)w0, (int)w1, 127 - (c * 32 + r32), 0};
+        tb[c] = INT_MIN; B1[c] = INT_MIN; J1[c] = -1;
+    }
+    const int rr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 + ((lane >> 3) & 1) * 2 +
+                   ((lane >> 4) & 1);
+    const int rowoff = (rr & 3) + 8 * (rr >> 2) + 4 * h;
+    // merge the 128-train group's running row maximum into (best, argbest)
+    auto row_merge = [&](int gbase) {
+#pragma unroll
+        for (int c = 0; c < QT; ++c) {
+            const int v = tb[c] - (127 - (c * 32 + r32));  // -128 d + (127 - j mod 128)
+            const int v1 = v >> 7;
+            const int j1 = gbase + 127 - (v & 127);
+            const bool up = v1 > B1[c];
+            J1[c] = up ? j1 : J1[c];
+            B1[c] = up ? v1 : B1[c];
+            tb[c] = INT_MIN;
+        }
+    };
+
+    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
+        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
+        const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
+        if (active) {
+            const unsigned char* A = cur;
+            const int* Ci = (const int*)(cur + CHUNK * D);
+            for (int tt = 0; tt < nt; ++tt) {
+                const int row = tt * 32 + r32;
+                const int sw = swz<D>(row);
+                v4i af[NK];
+#pragma unroll
+                for (int s = 0; s < NK; ++s)
+                    af[s] = *(const v4i*)(A + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
+                v16i init;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
+                    init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
+                    init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
+                }
+                v16i acc0 = init, acc1 = init;
+#pragma unroll
+                for (int s = 0; s < NK; ++s) {
+                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[0][s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[1][s], acc1, 0, 0, 0);
+                }
+#ifdef HAMKEY_VALU_QCONST  // debug build: the query constant added on the VALU instead
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    acc0[r] += -128 * nq[0] + 127 - r32;
+                    acc1[r] += -128 * nq[1] + 127 - (32 + r32);
+                }
+#else
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ax, bx[0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ax, bx[1], acc1, 0, 0, 0);
+#endif
+                int colacc[16];
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    // the column max first: compiler-emitted, so the MFMA -> VALU read hazard
+                    // is padded (hipcc pads nothing into an asm statement); the row max3 is asm
+                    // ordered after it through the extra operands (one v_max3 per 2 elements)
+                    colacc[r] = max(acc0[r], acc1[r]);
+                    colacc[r + 1] = max(acc0[r + 1], acc1[r + 1]);
+                    if constexpr (ROWS) {
+                        tb[0] = vmax3_after(tb[0], acc0[r], acc0[r + 1], colacc[r], colacc[r + 1]);
+                        tb[1] = vmax3_after(tb[1], acc1[r], acc1[r + 1], colacc[r], colacc[r + 1]);
+                    }
+                }
+                const int key = transpose_max16(colacc, lane);
+                const int j = ch * CHUNK + tt * 32 + rowoff;
+                const int e = key - (127 - (j & 127));   // -128 d + (127 - q_in_wave)
+                const int nd = e >> 7;                    // -d; padded queries: < -256
+                if (!(lane & 1) && j < nb && nd >= -256) {
+                    const unsigned gq = (unsigned)(qbase + 127 - (e & 127));
+                    lds_max_u64(&lds_col[j], ((unsigned long long)((unsigned)nd ^ 0x80000000u) << 32) |
+                                                 (unsigned long long)(0xFFFFFFFFu - gq));
+                }
+                if (ROWS) {
+                    const int g = ch * NT + tt;          // global tile: groups of 4 = 128 trains
+                    if ((g & 3) == 3 || ch * CHUNK + tt * 32 + 32 >= nb) row_merge((g & ~3) * 32);
+                }
+            }
+        }
+    };
+    if (n_chunk > 0) stage(0, lds0);
+    __syncthreads();
+    for (int ch = 0; ch < n_chunk; ch += 2) {
+        process(ch, lds0, lds1);
+        __syncthreads();
+        if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
+        __syncthreads();
+    }
+    if (ROWS && active) {
+#pragma unroll
+        for (int c = 0; c < QT; ++c) {
+            const int P1 = __shfl_xor(B1[c], 32), PJ = __shfl_xor(J1[c], 32);
+            const bool take = (P1 > B1[c]) || (P1 == B1[c] && PJ >= 0 && PJ < J1[c]);
+            if (take) { B1[c] = P1; J1[c] = PJ; }
+            const int q = qbase + c * 32 + r32;
+            // the fused kernel's row record: x = n_q - d1 (= vr), y = J1
+            if (h == 0 && q < na)
+                rowres[(size_t)p * k_pad + q] =
+                    make_int4(B1[c] == INT_MIN ? INT_MIN : nq[c] + B1[c], J1[c], INT_MIN, 0);
+        }
+    }
+    unsigned long long* dst = colpart + (size_t)p * k_pad;
+    for (int j = tid; j < k_pad; j += NTHR) {
+        const unsigned long long v = lds_col[j];
+        if (v != 0ull) atomicMax(dst + j, v);
+    }
+}
+
 // Exact dot product of two D-byte i8 rows (v_dot4_i32_i8).
 template <int D>
 __device__ __forceinline__ int mu_dot(const uint4* x, const uint4* y) {
@@ -984,20 +1193,24 @@ __global__ __launch_bounds__(256) void opencv_finalize_kernel(
 //   mutual:       forward keeps i iff colwin(J1[i]) = i;  reverse keeps j iff J1[colwin(j)] = j.
 //   none:         forward (J1[i], d1[i]);  reverse (colwin(j), its d).
 // No ratio test (it needs the reverse problem's second-best; the caller matches both orders).
-// Outputs: pair p's forward result in slot p, its reverse in slot n_pairs + p.
+// Outputs: pair p's forward result in slot p, its reverse (n_dirs = 2) in slot n_pairs + p.
+// n_dirs = 1 is the single-order Hamming path (ham_key_kernel, sfm_match_batch).
 __global__ __launch_bounds__(256) void both_finalize_kernel(
     const int32_t* __restrict__ n_kp, int k_max, int k_pad, const int32_t* __restrict__ norm,
     const int32_t* __restrict__ pairs, int n_pairs, int n_qblk, const int4* __restrict__ rowres,
     const unsigned long long* __restrict__ colpart, int xc, long long max_dist,
     int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
-    int32_t* __restrict__ out_dist) {
+    int32_t* __restrict__ out_dist, int n_dirs) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
     __shared__ int wsum[4];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
     if (na <= 0 || nb <= 0) {
-        if (tid == 0) { out_count[p] = 0; out_count[n_pairs + p] = 0; }
+        if (tid == 0) {
+            out_count[p] = 0;
+            if (n_dirs == 2) out_count[n_pairs + p] = 0;
+        }
         return;
     }
     const unsigned long long* cp = colpart + (size_t)p * n_qblk * k_pad;
@@ -1020,7 +1233,7 @@ __global__ __launch_bounds__(256) void both_finalize_kernel(
         return j >= 0 && j < nb && r.x > VALID_MIN;
     };
     auto dist_ok = [&](int d) { return max_dist < 0 || (long long)d < max_dist; };
-    for (int dir = 0; dir < 2; ++dir) {
+    for (int dir = 0; dir < n_dirs; ++dir) {
         const int nq = dir == 0 ? na : nb;   // queries of this direction
         const int nt = dir == 0 ? nb : na;   // its trains
         const size_t slot = (size_t)(dir == 0 ? p : n_pairs + p);
@@ -1240,19 +1453,34 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     return SFM_OK;
 }
 
-// Both directions of every (unordered) pair from one fused-key tile, TOP2 off (no ratio test).
-int sfm_match_both_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const int32_t* n_kp,
-                          int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
-                          const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
-                          int32_t* out_dist) {
+// Both directions of every (unordered) pair from one tile (n_dirs = 2; no ratio test): Hamming on
+// the key-in-the-accumulator kernel, L2 on the fused key kernel with TOP2 off.  n_dirs = 1 (Hamming
+// only): the single-order call of sfm_match_batch on the same kernel (rows only when the rule
+// needs them: not for the OpenCV rule).
+static int match_tile_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const int32_t* n_kp,
+                             int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                             const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                             int32_t* out_dist, int n_dirs) {
     hipStream_t st = ctx->stream;
     if (k_max == 0) {
-        SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * 2 * (size_t)n_pairs, st));
+        SFM_HIP_CHECK(hipMemsetAsync(out_count, 0, sizeof(int32_t) * n_dirs * (size_t)n_pairs, st));
         return SFM_OK;
     }
+    const bool rows = n_dirs == 2 || prm->cross_check != SFM_XC_OPENCV;
     const bool l2 = metric == SFM_METRIC_L2;
+    // Hamming: the key-in-the-accumulator kernel (ham_key_kernel); SFM_HAM_BOTH=fused keeps the
+    // fused key kernel (A/B only)
+    static const bool ham_fused = [] {
+        const char* e = getenv("SFM_HAM_BOTH");
+        return e && strcmp(e, "fused") == 0;
+    }();
+    if (l2 && n_dirs != 2) {
+        sfm::set_error("match_tile_launch: the single-order tile path is Hamming only");
+        return SFM_ERR_INVALID;
+    }
+    const bool hkey = !l2 && (n_dirs == 1 || !ham_fused);
     const int D = l2 ? 128 : 256;
-    const int QB = l2 ? Geo<128>::QB : Geo<256>::QB;
+    const int QB = l2 ? Geo<128>::QB : (hkey ? mu_qb<256>() : Geo<256>::QB);
     const int k_pad = (int)sfm::align_up((size_t)k_max, KALIGN);
     SFM_REQUIRE(k_pad <= KMAX_L2, "sfm_match_batch_both: k_max <= 4096 required");
     const int n_qblk = (k_max + QB - 1) / QB;
@@ -1275,6 +1503,30 @@ int sfm_match_both_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const i
     hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
                        pairs, n_pairs, n_img, pair_order, pair_order + n_pairs);
     SFM_HIP_CHECK(hipGetLastError());
+    if (hkey) {
+        SFM_HIP_CHECK(hipMemsetAsync(colpart, 0, sizeof(unsigned long long) * (size_t)n_pairs * k_pad, st));
+        hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_HAMMING, false, 16>), dim3(k_pad / 256, n_img),
+                           dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, crow, zero_row,
+                           (uint4*)desc_i8);
+        SFM_HIP_CHECK(hipGetLastError());
+        // whole pairs per XCD (the column merge of a pair stays in one L2), as the mutual kernel
+        const int hgrid = 8 * ((n_pairs + 7) / 8) * n_qblk;
+        if (rows)
+            hipLaunchKernelGGL(ham_key_kernel<true>, dim3(hgrid), dim3(64 * MU_WAVES),
+                               (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, crow,
+                               zero_row, pairs, n_qblk, pair_order, n_blk, rowres, colpart);
+        else
+            hipLaunchKernelGGL(ham_key_kernel<false>, dim3(hgrid), dim3(64 * MU_WAVES),
+                               (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, crow,
+                               zero_row, pairs, n_qblk, pair_order, n_blk, rowres, colpart);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(both_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st,
+                           n_kp, k_max, k_pad, norm, pairs, n_pairs, 1, rowres, colpart,
+                           prm->cross_check, (long long)prm->max_dist, out_count, out_match,
+                           out_dist, n_dirs);
+        SFM_HIP_CHECK(hipGetLastError());
+        return SFM_OK;
+    }
     if (l2) {
         hipLaunchKernelGGL(mfma_prep_kernel<SFM_METRIC_L2>, dim3(k_pad / 256, n_img), dim3(256), 0,
                            st, desc, n_kp, k_max, k_pad, norm, crow, zero_row, (uint4*)desc_i8);
@@ -1294,9 +1546,18 @@ int sfm_match_both_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const i
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(both_finalize_kernel, dim3(n_pairs), dim3(256), (size_t)k_pad * 8, st, n_kp,
                        k_max, k_pad, norm, pairs, n_pairs, n_qblk, rowres, colpart,
-                       prm->cross_check, (long long)prm->max_dist, out_count, out_match, out_dist);
+                       prm->cross_check, (long long)prm->max_dist, out_count, out_match, out_dist,
+                       2);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
+}
+
+int sfm_match_both_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, const int32_t* n_kp,
+                          int32_t n_img, int32_t k_max, const int32_t* pairs, int32_t n_pairs,
+                          const sfm_match_params* prm, int32_t* out_count, int32_t* out_match,
+                          int32_t* out_dist) {
+    return match_tile_launch(ctx, metric, desc, n_kp, n_img, k_max, pairs, n_pairs, prm, out_count,
+                             out_match, out_dist, 2);
 }
 
 int sfm_match_l2_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp, int32_t n_img,
@@ -1335,6 +1596,12 @@ int sfm_match_hamming_mfma_launch(sfm_ctx* ctx, const uint8_t* desc, const int32
     // value-only row side an exact row scan (0.68 vs 0.16 ms).  SFM_HAMMING_PATH=fused|mutual
     // overrides.
     const char* pe = getenv("SFM_HAMMING_PATH");
+    // Round 4: without a ratio test every rule runs on the key-in-the-accumulator kernel
+    // (ham_key_kernel: no VALU key build; rows only for the mutual / no rule).
+    // SFM_HAMMING_PATH=mutual|fused selects the round-3 kernels (A/B only).
+    if (prm->ratio_den == 0 && !(pe && (strcmp(pe, "mutual") == 0 || strcmp(pe, "fused") == 0)))
+        return match_tile_launch(ctx, SFM_METRIC_HAMMING, desc, n_kp, n_img, k_max, pairs, n_pairs,
+                                 prm, out_count, out_match, out_dist, 1);
     const bool col = pe && strcmp(pe, "mutual") == 0 ? prm->cross_check != SFM_XC_NONE
                                                     : prm->cross_check == SFM_XC_OPENCV;
     if (col && !(pe && strcmp(pe, "fused") == 0))

@@ -309,13 +309,13 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
                                                    cg_tol=cg_tol, ftol=ftol, device=device,
                                                    fixed=fixed, shard=shard_ba, group=group,
                                                    pcg=pcg, info=info, reproj_err=True)
+    err = info.pop("err")   # at the returned parameters (bundle_adjust reproj_err)
     rec.ba_log.append(dict(info, n_cam=int(rec.registered.sum()), n_pt=int(len(pts_ids)),
                            n_obs=int(use.sum()), lm_steps=len(hist),
                            cg_iters=int(sum(h[3] for h in hist))))
     reg = rec.registered
     rec.cams[reg] = cams[reg]
     rec.points[pts_ids] = pts
-    err = info.pop("err")   # at the returned parameters (bundle_adjust reproj_err)
     mean = np.bincount(pt_idx, err, minlength=len(pts_ids)) / np.maximum(
         np.bincount(pt_idx, minlength=len(pts_ids)), 1)
     rec.has_point[pts_ids[mean > max_err]] = False

@@ -26,13 +26,14 @@ def main():
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
     res = {}
+    # key = the key-in-the-accumulator kernel (round 4 default without a ratio test),
     # mfma = the column-winner kernel (OpenCV rule: column side only; mutual: + value-only rows),
     # fused = the packed-key MFMA kernel, valu = the popcount kernel
-    runs = [(f"{path}_{name}", path, xc, md) for path in ("mfma", "fused", "valu")
+    runs = [(f"{path}_{name}", path, xc, md) for path in ("key", "mfma", "fused", "valu")
             for name, xc, md in (("opencv_lt26", 2, 26), ("mutual", 1, -1))]
     for name, path, xc, md in runs:
         os.environ["SFM_HAMMING_VALU"] = "1" if path == "valu" else "0"
-        os.environ["SFM_HAMMING_PATH"] = "fused" if path == "fused" else "mutual"
+        os.environ["SFM_HAMMING_PATH"] = {"fused": "fused", "mfma": "mutual"}.get(path, "")
         kw = dict(metric=sfmcore.METRIC_HAMMING, cross_check=xc, max_dist=md)
         out = ctx.match_batch(desc, n_kp, pr, **kw)
         torch.cuda.synchronize()

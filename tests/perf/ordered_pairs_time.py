@@ -3,8 +3,9 @@ descriptors (default 500 x 500, OpenCV nfeatures), every ordered pair i != j mat
 reference's rule (Hamming, crossCheck=True, distance < 26; code/pipeline.py:38-41,
 code/feature_matching.py:48-58).
 
-  two_launch : sfm_match_batch on the N(N-1) ordered pairs (column-winner kernel per order)
-  both       : sfm_match_batch_both on the N(N-1)/2 unordered pairs (one fused tile, both orders)
+  two_launch    : sfm_match_batch on the N(N-1) ordered pairs (default single-order kernel)
+  two_launch_r3 : the same with round 3's column-winner kernel (SFM_HAMMING_PATH=mutual)
+  both          : sfm_match_batch_both on the N(N-1)/2 unordered pairs (one tile, both orders)
 
 HIP events on the launch stream, best of `reps`; results compared bit for bit.
 Usage: python tests/perf/ordered_pairs_time.py [n_img [k [reps]]]   -> one JSON line.
@@ -49,17 +50,22 @@ def main():
             best = t if best is None else min(best, t)
         return best, out
     t_two, o2 = timed(lambda out=None: ctx.match_batch(d, n, ord_t, ratio=None, out=out, **kw))
+    os.environ["SFM_HAMMING_PATH"] = "mutual"     # round 3's single-order kernel (column winners)
+    t_two_r3, o3 = timed(lambda out=None: ctx.match_batch(d, n, ord_t, ratio=None, out=out, **kw))
+    del os.environ["SFM_HAMMING_PATH"]
     t_both, ob = timed(lambda out=None: ctx.match_batch_both(d, n, up_t, out=out, **kw))
     c2, m2, _ = (x.cpu().numpy() for x in o2)
     cb, mb, _ = (x.cpu().numpy() for x in ob)
-    same = bool((c2 == cb).all())
+    c3, m3, _ = (x.cpu().numpy() for x in o3)
+    same = bool((c2 == cb).all() and (c3 == cb).all())
     if same:
         kk = np.arange(m2.shape[1])[None, :] < c2[:, None]
-        same = bool((m2[kk] == mb[kk]).all())
+        same = bool((m2[kk] == mb[kk]).all() and (m3[kk] == mb[kk]).all())
     n_ops = 2.0 * 256 * float(np.sum(s["n_kp"][up[:, 0]] * s["n_kp"][up[:, 1]]))
     print(json.dumps({"stage": "ordered-pair matching, Hamming + OpenCV crossCheck + < 26",
                       "n_img": n_img, "k": k, "ordered_pairs": int(len(ordered)),
-                      "two_launch_ms": t_two, "both_ms": t_both, "ratio": t_both / t_two,
+                      "two_launch_ms": t_two, "two_launch_r3_kernel_ms": t_two_r3,
+                      "both_ms": t_both, "ratio": t_both / t_two, "ratio_vs_r3": t_both / t_two_r3,
                       "bit_identical": same, "matches": int(c2.sum()),
                       "both_tops_i8": n_ops / (t_both * 1e-3) / 1e12}))
 
