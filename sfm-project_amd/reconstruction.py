@@ -134,18 +134,31 @@ class BAProblem:
     """Device-resident observations + CSR indices for repeated linearisation / solves."""
 
     def __init__(self, pp, cam_idx, pt_idx, uv, n_cam: int, n_pt: int, device: int = 0):
+        """cam_idx / pt_idx / uv: numpy arrays, or device tensors (int32, int32, f64 [n,2]) that
+        are used in place (no host round trip; the incremental driver selects its observations
+        on the device).  `order` (numpy, or a device tensor for tensor inputs) is the stable
+        regrouping by point when pt_idx was not already point-major, else None."""
         import torch
-        cam_idx = np.asarray(cam_idx, np.int32)
-        pt_idx = np.asarray(pt_idx, np.int32)
-        uv = np.asarray(uv, np.float64)
-        self.order = None
-        if len(pt_idx) and np.any(np.diff(pt_idx) < 0):
-            self.order = np.argsort(pt_idx, kind="stable")
-            cam_idx, pt_idx, uv = cam_idx[self.order], pt_idx[self.order], uv[self.order]
         self.dev = torch.device("cuda", device)
-        T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dt)).to(self.dev)
-        self.pp = T(pp, np.float64)
-        self.cam_idx, self.pt_idx, self.uv = T(cam_idx), T(pt_idx), T(uv)
+        self.order = None
+        if isinstance(pt_idx, torch.Tensor):
+            cam_d = cam_idx.to(self.dev, torch.int32).contiguous()
+            pt_d = pt_idx.to(self.dev, torch.int32).contiguous()
+            uv_d = uv.to(self.dev, torch.float64).contiguous()
+            if pt_d.numel() > 1 and bool((pt_d[1:] < pt_d[:-1]).any()):
+                self.order = torch.argsort(pt_d.long(), stable=True)
+                cam_d, pt_d, uv_d = cam_d[self.order], pt_d[self.order], uv_d[self.order]
+            self.cam_idx, self.pt_idx, self.uv = cam_d, pt_d, uv_d
+        else:
+            cam_idx = np.asarray(cam_idx, np.int32)
+            pt_idx = np.asarray(pt_idx, np.int32)
+            uv = np.asarray(uv, np.float64)
+            if len(pt_idx) and np.any(np.diff(pt_idx) < 0):
+                self.order = np.argsort(pt_idx, kind="stable")
+                cam_idx, pt_idx, uv = cam_idx[self.order], pt_idx[self.order], uv[self.order]
+            T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dt)).to(self.dev)
+            self.cam_idx, self.pt_idx, self.uv = T(cam_idx), T(pt_idx), T(uv)
+        self.pp = torch.from_numpy(np.ascontiguousarray(pp, np.float64)).to(self.dev)
         self.pt_ptr, _ = sfmcore.csr_by_device(self.pt_idx, n_pt)
         self.cam_ptr, self.cam_obs = sfmcore.csr_by_device(self.cam_idx, n_cam)
         self.n_cam, self.n_pt = n_cam, n_pt
@@ -351,7 +364,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                   group=None, pcg: str = "auto", info=None, reproj_err: bool = False):
     """Levenberg-Marquardt on paper eq. (1): every step on the GPU
     (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
-    accept / reject it.
+    accept / reject it.  cam_idx / pt_idx / uv may be device tensors (used in place).
 
     Step rule (oracle/ba_lm.py, Nielsen): predicted decrease = -(gᵀδ + ½ δᵀJᵀJδ); accept iff
     the cost decreases, then λ *= max(1/3, 1 - (2ρ-1)³); otherwise λ *= ν, ν *= 2.  Stops after
@@ -391,7 +404,10 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     mode = "single"
     lo, hi = 0, n_pt
     full = None
+    tensors = isinstance(pt_idx, torch.Tensor)
     if allreduce is not None:
+        if tensors:   # the sharded path slices on the host
+            cam_idx, pt_idx, uv = (t.cpu().numpy() for t in (cam_idx, pt_idx, uv))
         cam_idx = np.asarray(cam_idx, np.int32)
         pt_idx = np.asarray(pt_idx, np.int32)
         uv = np.asarray(uv, np.float64)
@@ -500,11 +516,11 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         r = prob.linearize(cams_d, shard_of(pts_d), loss_s)["res"]
         e = torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1])
         if allreduce is None:
-            err = e.cpu().numpy()
             if prob.order is not None:   # BAProblem regrouped the observations by point
-                back = np.empty_like(err)
-                back[prob.order] = err
-                err = back
+                back = torch.empty_like(e)
+                back[torch.as_tensor(prob.order, device=e.device)] = e
+                e = back
+            err = e.cpu().numpy()
         else:
             ev = torch.zeros(n_obs_all, dtype=torch.float64, device=prob.dev)
             ev[o0:o1] = e
