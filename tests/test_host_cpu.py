@@ -173,3 +173,37 @@ def test_csr_by_device_equals_host_csr():
         dptr, dorder = sfmcore.csr_by_device(torch.from_numpy(idx), n)
         np.testing.assert_array_equal(dptr.numpy(), ptr)
         np.testing.assert_array_equal(dorder.numpy(), order)
+
+
+@pytest.mark.parametrize("kw,digest", [
+    (dict(n_img=5, n_kp=300, seed=3), "0fa28c8d2d4c31a4"),
+    (dict(n_img=4, n_kp=256, seed=13, orb=True), "3651d5334fb017ee"),
+    (dict(n_img=6, n_kp=200, seed=21, k1_range=0.02), "1c3760a59af7cc39"),
+])
+def test_default_scenes_unchanged(kw, digest):
+    """Round 4 added local visibility to synth.make_scene (window / grid / track_len) from a
+    separate random stream: scenes without a window keep every descriptor and point id (the
+    fixtures and the committed bench checksums depend on them)."""
+    import hashlib
+    s = synth.make_scene(**kw)
+    h = hashlib.sha256(np.ascontiguousarray(s["desc"]).tobytes()
+                       + np.ascontiguousarray(s["point_ids"]).tobytes()).hexdigest()[:16]
+    assert h == digest
+
+
+def test_grid_scene_local_visibility():
+    """cfg5's scene shape: views on a sphere-cap grid, each point observed by ~track_len of the
+    3 x 3 views around its home cell, and only those."""
+    n_az, n_el = 8, 4
+    s = synth.make_scene(32, 400, seed=5, window=1, grid=(n_az, n_el, 60.0, 20.0), track_len=5)
+    pid = s["point_ids"]
+    cnt = np.bincount(pid[pid >= 0].ravel(), minlength=len(s["pts"]))
+    assert abs(cnt[cnt > 0].mean() - 5.0) < 0.6
+    cell = np.stack([np.arange(32) // n_el, np.arange(32) % n_el], 1)
+    for p in np.nonzero(cnt >= 2)[0][:200]:
+        views = np.nonzero((pid == p).any(1))[0]
+        span = cell[views].max(0) - cell[views].min(0)
+        assert (span <= 2).all()          # all observers within one 3 x 3 window
+    c = synth.camera_centres(s["cams"])
+    d01 = np.linalg.norm(c[1] - c[0])     # elevation neighbours: 20/4 = 5 degrees at radius 8
+    assert abs(d01 - 2 * 8 * np.sin(np.deg2rad(2.5))) < 1e-9
