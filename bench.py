@@ -224,31 +224,42 @@ def launch_ranks(args, argv):
         port = s_.getsockname()[1]
     out0 = tempfile.TemporaryFile(mode="w+")
     procs = []
+
+    def die_with_parent():  # in the child, before exec: SIGTERM when the launcher dies
+        import ctypes
+        try:
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    def forward(signum, _frame):  # a signal to the launcher stops the ranks too
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        sys.exit(128 + signum)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), SFM_BENCH_LAUNCHER="self")
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv,
-                                      env=env, stdout=out0 if r == 0 else sys.stderr))
+                                      env=env, stdout=out0 if r == 0 else sys.stderr,
+                                      preexec_fn=die_with_parent))
     rc = 0
     live = list(range(n))
-    try:
-        while live:
-            for r in list(live):
-                c = procs[r].poll()
-                if c is None:
-                    continue
-                live.remove(r)
-                if c != 0 and rc == 0:
-                    rc = c if c > 0 else 128 - c
-                    log(f"bench.py: rank {r} exited with {c}; stopping the other ranks")
-                    for q in live:
-                        procs[q].send_signal(signal.SIGTERM)
-            time.sleep(0.05)
-    except KeyboardInterrupt:
-        for p in procs:
-            p.kill()
-        raise
+    while live:
+        for r in list(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.remove(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                log(f"bench.py: rank {r} exited with {c}; stopping the other ranks")
+                for q in live:
+                    procs[q].send_signal(signal.SIGTERM)
+        time.sleep(0.05)
     for p in procs:
         p.wait()
     out0.seek(0)

@@ -73,3 +73,4 @@ def test_pcg_rule_branches():
     tn = lambda n: R.PCG_FIXED_US + R.PCG_OBS_US * n
     assert abs(t["sharded_us_per_step"] - it * (tn(500_000 / 8) + R.PCG_SPLIT_US + 20.0)) < 1e-6
     assert abs(t["replicated_us_per_step"] - (it * tn(500_000) + t["gather_us"])) < 1e-6
+
