@@ -489,8 +489,11 @@ __global__ __launch_bounds__(256) void ransac_hyp_kernel(
 //   ransac_score_kernel  rank r of pair p scores hypothesis order[p][r] from match PV on, starting
 //                        from its preview count, with the same exact pruning; grid x = pair so the
 //                        best-previewed block of every pair runs first and publishes a strong bound.
+// PV = 128: interleaved A/B at cfg4 (profiles/r04/ransac_preview_ab_r6i.txt, _r6j.txt): 32 206.5,
+// 64 202.2, 96 200.7, 128 199.7 ms; second box 64 207.0-207.6 vs 128-224 a plateau at 204.3-205.2;
+// cfg3 within noise, outputs identical.  (hist[PV + 2] in 256 threads: PV <= 240, multiple of 16.)
 #ifndef RANSAC_PV
-#define RANSAC_PV 64
+#define RANSAC_PV 128
 #endif
 constexpr int PV = RANSAC_PV;  // preview matches (multiple of CH and of 8)
 constexpr int HREC = 12;  // hypothesis record: G[9], preview count (int bits), 2 pad floats

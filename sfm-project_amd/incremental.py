@@ -107,6 +107,37 @@ def _match_graph(gb, pairs, pairs_t, n_kp, group):
     return graph, inl.cpu().numpy()
 
 
+def track_obs(otr, timg, n_tr, tracks, in_img):
+    """Observations of `tracks` (ascending track ids) whose image is flagged in `in_img`, as the
+    triangulation kernel's CSR: (o, ptr) with o the observation indices in track order, ascending
+    within a track (the observation arrays are track-major), ptr [len(tracks) + 1] int32.  Torch
+    tensors of one device (the GPU in the driver; the CPU in tests/test_host_cpu.py)."""
+    import torch
+    want = torch.zeros(n_tr, dtype=torch.bool, device=otr.device)
+    want[tracks] = True
+    o = torch.nonzero(want[otr] & in_img[timg]).squeeze(1)
+    ptr = torch.zeros(len(tracks) + 1, dtype=torch.int32, device=otr.device)
+    ptr[1:] = torch.cumsum(torch.bincount(otr[o], minlength=n_tr)[tracks], 0)
+    return o, ptr
+
+
+def registration_obs(otr, timg, has_point, registered, min_corr=30):
+    """2-D/3-D correspondences of every unregistered image with >= min_corr of them: observations
+    of triangulated tracks in unregistered images, grouped by image (ascending) and ascending
+    observation index within an image.  Returns (sel, ids, cptr): the selected observations, the
+    candidate images and their CSR offsets (ids and cptr are small and come back to the host)."""
+    import torch
+    cand = torch.nonzero(has_point[otr] & ~registered[timg]).squeeze(1)
+    img_sorted, by_img = torch.sort(timg[cand], stable=True)
+    img_u, img_n = torch.unique_consecutive(img_sorted, return_counts=True)
+    keep = img_n >= min_corr
+    sel = cand[by_img][torch.repeat_interleave(keep, img_n)]
+    n_keep = img_n[keep]
+    cptr = torch.zeros(len(n_keep) + 1, dtype=torch.int64, device=otr.device)
+    cptr[1:] = torch.cumsum(n_keep, 0)
+    return sel, img_u[keep].cpu().numpy().astype(np.int32), cptr.cpu().numpy().astype(np.int32)
+
+
 def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
                 ba_iter=20, loss_s=2.0, device=0, log=None, group=None, shard_ba=False,
                 ba_cg_tol=0.1, ba_pcg="auto", ba_ftol=1e-6):
@@ -194,7 +225,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             cams[a, :6] = 0.0
             cams[b, :3] = _angle_axis(R)
             cams[b, 3:6] = t
-            pts, st = _triangulate(ctx, cams, intr, [a, b], common, tptr, timg, obs_xy, dev)
+            pts, st = _triangulate(ctx, cams, intr, [a, b], common, rec.obs_d, n_tr)
             good = int(np.sum((st[:, 3] == 0) & (st[:, 0] < max_err)))
             if best is None or good > best[0]:
                 best = (good, cams, pts, st)
@@ -222,19 +253,16 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     while not rec.registered.all():
         # 2-D/3-D correspondences of every unregistered image with >= 30 of them, grouped by
         # image (ascending) and ascending observation index within an image: one pass
-        obs_sel = np.nonzero(rec.has_point[obs_track] & ~rec.registered[timg])[0]
-        by_img = np.argsort(timg[obs_sel], kind="stable")
-        obs_sel = obs_sel[by_img]
-        img_u, img_n = np.unique(timg[obs_sel], return_counts=True)
-        keep = img_n >= 30
-        if not keep.any():
+        # (selected on the device from rec.obs_d: ~1.5 M observations at cfg5)
+        otr_d, timg_d, oxy_d = obs_d
+        sel, ids, cptr = registration_obs(otr_d, timg_d, torch.from_numpy(rec.has_point).to(dev),
+                                          torch.from_numpy(rec.registered).to(dev))
+        if len(ids) == 0:
             break
-        ids = img_u[keep].astype(np.int32)
-        cptr = np.r_[0, np.cumsum(img_n[keep])].astype(np.int32)
-        sel = obs_sel[np.repeat(keep, img_n)]
         T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
-        cams_r, cnt, _, _ = ctx.register_batch(T(cptr, np.int32), T(obs_xy[sel], np.float64),
-                                               T(rec.points[obs_track[sel]], np.float64),
+        pts_d = T(rec.points, np.float64)
+        cams_r, cnt, _, _ = ctx.register_batch(T(cptr, np.int32), oxy_d[sel].contiguous(),
+                                               pts_d[otr_d[sel]].contiguous(),
                                                T(intr[ids], np.float64), T(ids, np.int32),
                                                n_hyp=n_hyp, thr=reg_thr)
         cams_r, cnt = cams_r.cpu().numpy(), cnt.cpu().numpy()
@@ -249,7 +277,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         say(f"registered {added} of {len(ids)} candidates, total {int(rec.registered.sum())}")
         if not added:
             break
-        _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev)
+        _triangulate_new(rec, ctx, intr, max_err)
         tk = lap("triangulate", tk)
         _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
                 shard_ba, group, ba_cg_tol, ba_pcg, ba_ftol)
@@ -257,35 +285,36 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     return rec
 
 
-def _triangulate(ctx, cams, intr, imgs, tracks, tptr, timg, obs_xy, dev):
-    """Triangulate `tracks` from their observations in the images `imgs` (GPU kernel)."""
+def _triangulate(ctx, cams, intr, imgs, tracks, obs_d, n_tr):
+    """Triangulate `tracks` (ascending ids) from their observations in the images `imgs` (GPU
+    kernel; the observations are selected on the device from obs_d = (obs_track, timg, obs_xy))."""
     import torch
-    tracks = np.asarray(tracks, np.int64)
-    in_img = np.zeros(len(cams), bool)
-    in_img[np.asarray(imgs, np.int64)] = True
-    # every observation of the tracks (track order, ascending within a track), kept if its image
-    # is in `imgs`: vectorised CSR gather
-    lens = (tptr[tracks + 1] - tptr[tracks]).astype(np.int64)
-    start = np.r_[0, np.cumsum(lens)[:-1]]
-    o = np.arange(int(lens.sum()), dtype=np.int64) + np.repeat(tptr[tracks] - start, lens)
-    keep = in_img[timg[o]]
-    o = o[keep]
-    per = np.bincount(np.repeat(np.arange(len(tracks)), lens)[keep], minlength=len(tracks))
-    ptr = np.r_[0, np.cumsum(per)].astype(np.int32)
+    otr_d, timg_d, oxy_d = obs_d
+    dev = otr_d.device
+    in_img = torch.zeros(len(cams), dtype=torch.bool, device=dev)
+    in_img[torch.as_tensor(np.asarray(imgs, np.int64), device=dev)] = True
+    o, ptr = track_obs(otr_d, timg_d, n_tr, torch.as_tensor(np.asarray(tracks, np.int64),
+                                                             device=dev), in_img)
     T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
-    pts, st = ctx.triangulate(T(cams, np.float64), T(intr[:, 2:4], np.float64), T(ptr, np.int32),
-                              T(timg[o], np.int32), T(obs_xy[o], np.float64))
+    pts, st = ctx.triangulate(T(cams, np.float64), T(intr[:, 2:4], np.float64), ptr,
+                              timg_d[o].to(torch.int32), oxy_d[o].contiguous())
     return pts.cpu().numpy(), st.cpu().numpy()
 
 
-def _triangulate_new(rec, ctx, intr, tptr, timg, obs_xy, max_err, dev):
-    reg_obs = rec.registered[timg]
-    n_reg = np.add.reduceat(reg_obs.astype(np.int64), tptr[:-1]) if len(timg) else np.zeros(0)
-    todo = np.nonzero(~rec.has_point & (n_reg >= 2))[0]
+def _triangulate_new(rec, ctx, intr, max_err):
+    """Triangulate every track without a point that has >= 2 observations in registered images."""
+    import torch
+    otr_d, timg_d, _ = rec.obs_d
+    dev = otr_d.device
+    n_tr = len(rec.has_point)
+    reg_d = torch.from_numpy(rec.registered).to(dev)
+    n_reg = torch.bincount(otr_d[reg_d[timg_d]], minlength=n_tr)
+    todo_d = torch.nonzero(~torch.from_numpy(rec.has_point).to(dev) & (n_reg >= 2)).squeeze(1)
+    todo = todo_d.cpu().numpy()
     if len(todo) == 0:
         return
-    pts, st = _triangulate(ctx, rec.cams, intr, np.nonzero(rec.registered)[0], todo, tptr, timg,
-                           obs_xy, dev)
+    pts, st = _triangulate(ctx, rec.cams, intr, np.nonzero(rec.registered)[0], todo, rec.obs_d,
+                           n_tr)
     ok = (st[:, 3] == 0) & (st[:, 0] < max_err) & (st[:, 1] > 1.0)
     rec.points[todo[ok]] = pts[ok]
     rec.has_point[todo[ok]] = True

@@ -134,6 +134,18 @@ def _ptr(t) -> int:
     return t.data_ptr()
 
 
+def _expect(fn: str, *specs):
+    """Raise SfmCoreError unless every (name, tensor, dtype, trailing shape) is a contiguous device
+    tensor of that dtype whose trailing dimensions match (the kernels index raw pointers)."""
+    for name, t, dt, tail in specs:
+        ok = t.dtype == dt and t.is_cuda and t.is_contiguous()
+        ok = ok and tuple(t.shape[t.dim() - len(tail):]) == tuple(tail) and t.dim() == len(tail) + 1
+        if not ok:
+            raise SfmCoreError(f"{fn}: {name} must be a contiguous device {dt} tensor of shape "
+                               f"[n, {', '.join(map(str, tail))}]" if tail else
+                               f"{fn}: {name} must be a contiguous device {dt} vector")
+
+
 class Context:
     """One per device (not thread-safe).  Calls run on torch's current stream of that device."""
 
@@ -390,6 +402,11 @@ class Context:
         dev = xy.device
         n_img = corr_ptr.shape[0] - 1
         n = xy.shape[0]
+        _expect("register_batch", ("corr_ptr", corr_ptr, torch.int32, ()),
+                ("xy", xy, torch.float64, (2,)), ("X", X, torch.float64, (3,)),
+                ("intr", intr, torch.float64, (4,)), ("img_id", img_id, torch.int32, ()))
+        if X.shape[0] != n or intr.shape[0] != n_img or img_id.shape[0] != n_img:
+            raise SfmCoreError("register_batch: xy / X and intr / img_id / corr_ptr sizes differ")
         cams = torch.empty((max(n_img, 0), 8), dtype=torch.float64, device=dev)
         count = torch.empty(max(n_img, 0), dtype=torch.int32, device=dev)
         key = torch.empty(max(n_img, 0), dtype=torch.int32, device=dev)
@@ -405,6 +422,11 @@ class Context:
         """(pts [n_pt,3], stats [n_pt,4]) f64 device tensors; see include/sfmcore.h."""
         torch = self.torch
         n_pt = pt_ptr.shape[0] - 1
+        _expect("triangulate", ("cams", cams, torch.float64, (8,)), ("pp", pp, torch.float64, (2,)),
+                ("pt_ptr", pt_ptr, torch.int32, ()), ("cam_idx", cam_idx, torch.int32, ()),
+                ("uv", uv, torch.float64, (2,)))
+        if pp.shape[0] != cams.shape[0] or uv.shape[0] != cam_idx.shape[0]:
+            raise SfmCoreError("triangulate: cams / pp or cam_idx / uv sizes differ")
         pts = torch.empty((max(n_pt, 0), 3), dtype=torch.float64, device=cams.device)
         stats = torch.empty((max(n_pt, 0), 4), dtype=torch.float64, device=cams.device)
         self._bind_stream()

@@ -104,10 +104,10 @@ def _ransac_direct(ctx, kps, count, match, pairs, H):
     return {k: v.cpu().numpy() for k, v in out.items()}
 
 
-@pytest.mark.parametrize("M", [8, 9, 20, 63, 64, 65, 79, 80, 127, 130])
+@pytest.mark.parametrize("M", [8, 9, 20, 63, 64, 65, 79, 80, 127, 128, 129, 130, 143, 144, 145])
 def test_ransac_preview_boundaries(ctx, M):
-    """Match counts around the 64-match preview and the 16-match scoring chunks of the ordered
-    schedule (fit + preview / ordered scoring), on a real two-view geometry with outliers."""
+    """Match counts around the PV-match preview (128; 64 through round 3) and the 16-match scoring
+    chunks of the ordered schedule (fit + preview / ordered scoring), on a real two-view geometry with outliers."""
     s = synth.make_scene(2, 512, seed=30 + M)
     q, t, _ = O.match(s["desc"][0], s["desc"][1], 0, 1, (4, 5))
     assert len(q) >= M
@@ -199,8 +199,9 @@ def test_ransac_counts_every_hypothesis(ctx, thr):
 
 
 def test_ransac_counts_k4096_and_tails(ctx):
-    """cfg4-sized pairs (K = 4096, ~1000+ tentative matches) and match counts around the 64-match
-    preview and the 16-match scoring chunks: every hypothesis count equals the oracle's."""
+    """cfg4-sized pairs (K = 4096, ~1000+ tentative matches) and match counts around the
+    PV-match preview (128) and the 16-match scoring chunks: every hypothesis count equals the
+    oracle's."""
     import torch
     s = synth.make_scene(3, 4096, seed=5)
     pairs = synth.unordered_pairs(3)
@@ -208,8 +209,8 @@ def test_ransac_counts_k4096_and_tails(ctx):
     pr = T(pairs)
     cnt, mt, _ = ctx.match_batch(T(s["desc"]), T(s["n_kp"]), pr, ratio=(4, 5))
     cnt_h, mt_h = cnt.cpu().numpy(), mt.cpu().numpy()
-    # truncated copies of pair 0 around the preview (64) and the scoring chunks (16)
-    Ms = [9, 64, 65, 79, 80, 95, 96, 97, 129, 161, 200]
+    # truncated copies of pair 0 around the preview (64 / 128) and the scoring chunks (16)
+    Ms = [9, 64, 65, 79, 80, 95, 96, 97, 127, 128, 129, 144, 145, 161, 200]
     P = len(pairs) + len(Ms)
     pairs2 = np.concatenate([pairs, np.repeat(pairs[:1], len(Ms), 0)]).astype(np.int32)
     cnt2 = np.concatenate([cnt_h, np.minimum(Ms, cnt_h[0])]).astype(np.int32)
@@ -229,7 +230,7 @@ def test_ransac_f64_small_pairs_bit_exact(ctx):
     import torch
     s = synth.make_scene(4, 700, seed=31)
     pairs = np.array([[0, 1], [1, 2], [2, 3], [0, 3]], np.int32)
-    n_keep = [700, 8, 5, 65]
+    n_keep = [700, 8, 5, 129]
     cnt, mt = [], []
     k_max = 700
     match = np.zeros((len(pairs), k_max, 2), np.int32)

@@ -207,3 +207,63 @@ def test_grid_scene_local_visibility():
     c = synth.camera_centres(s["cams"])
     d01 = np.linalg.norm(c[1] - c[0])     # elevation neighbours: 20/4 = 5 degrees at radius 8
     assert abs(d01 - 2 * 8 * np.sin(np.deg2rad(2.5))) < 1e-9
+
+
+def _track_arrays(rng, n_tr=400, n_img=20):
+    lens = rng.integers(1, 7, n_tr)
+    tptr = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    obs_track = np.repeat(np.arange(n_tr), lens)
+    timg = rng.integers(0, n_img, len(obs_track)).astype(np.int64)
+    return tptr, obs_track, timg
+
+
+def test_track_obs_equals_host_gather():
+    """incremental.track_obs (the device-side observation selection of the triangulation step)
+    equals the host CSR gather it replaced, on CPU tensors."""
+    import torch
+    import incremental
+    rng = np.random.default_rng(3)
+    tptr, obs_track, timg = _track_arrays(rng)
+    n_tr = len(tptr) - 1
+    for trial in range(4):
+        tracks = np.sort(rng.choice(n_tr, size=int(rng.integers(1, n_tr)), replace=False))
+        imgs = rng.choice(20, size=int(rng.integers(1, 20)), replace=False)
+        in_img = np.zeros(20, bool)
+        in_img[imgs] = True
+        lens = tptr[tracks + 1] - tptr[tracks]
+        start = np.r_[0, np.cumsum(lens)[:-1]]
+        o_ref = np.arange(int(lens.sum())) + np.repeat(tptr[tracks] - start, lens)
+        keep = in_img[timg[o_ref]]
+        o_ref = o_ref[keep]
+        per = np.bincount(np.repeat(np.arange(len(tracks)), lens)[keep], minlength=len(tracks))
+        ptr_ref = np.r_[0, np.cumsum(per)].astype(np.int32)
+        o, ptr = incremental.track_obs(torch.from_numpy(obs_track), torch.from_numpy(timg), n_tr,
+                                       torch.from_numpy(tracks), torch.from_numpy(in_img))
+        np.testing.assert_array_equal(o.numpy(), o_ref)
+        np.testing.assert_array_equal(ptr.numpy(), ptr_ref)
+        assert ptr.dtype == torch.int32
+
+
+def test_registration_obs_equals_host_selection():
+    """incremental.registration_obs equals the host selection it replaced (observations of
+    triangulated tracks in unregistered images, grouped by image, images with >= min_corr)."""
+    import torch
+    import incremental
+    rng = np.random.default_rng(4)
+    tptr, obs_track, timg = _track_arrays(rng, n_tr=3000)
+    for trial in range(4):
+        has_point = rng.random(len(tptr) - 1) < 0.6
+        registered = rng.random(20) < 0.4
+        obs_sel = np.nonzero(has_point[obs_track] & ~registered[timg])[0]
+        obs_sel = obs_sel[np.argsort(timg[obs_sel], kind="stable")]
+        img_u, img_n = np.unique(timg[obs_sel], return_counts=True)
+        thr = int(np.median(img_n)) + 1            # some candidate images kept, some not
+        keep = img_n >= thr
+        assert keep.any() and not keep.all()
+        sel, ids, cptr = incremental.registration_obs(
+            torch.from_numpy(obs_track), torch.from_numpy(timg), torch.from_numpy(has_point),
+            torch.from_numpy(registered), min_corr=thr)
+        np.testing.assert_array_equal(ids, img_u[keep])
+        np.testing.assert_array_equal(cptr, np.r_[0, np.cumsum(img_n[keep])])
+        np.testing.assert_array_equal(sel.numpy(), obs_sel[np.repeat(keep, img_n)])
+        assert ids.dtype == np.int32 and cptr.dtype == np.int32
