@@ -113,7 +113,7 @@ def workload_string(cfg, n_img, k, n_hyp, chunk):
 class Runner:
     """One image set resident on this GPU and this rank's pair shard, cut into launch chunks."""
 
-    def __init__(self, scene, pairs, lo, hi, chunk, n_hyp, local, pieces=1):
+    def __init__(self, scene, pairs, lo, hi, chunk, n_hyp, local):
         import numpy as np
         import torch
         import match_graph
@@ -123,7 +123,6 @@ class Runner:
                                            thr=1.0, min_inliers=15)
         self.ctx = self.gb.ctx
         self.lo, self.hi = lo, hi
-        self.pieces = pieces   # > 1: K1 of piece i + 1 beside K2 of piece i (run_overlapped)
         shard = pairs[lo:hi]
         self.chunks = []
         for c0 in range(0, len(shard), chunk):
@@ -138,18 +137,14 @@ class Runner:
         torch = self.torch
         rows_l, cnt_l, pk_l = [], [], []
         for ci, (base, pt) in enumerate(self.chunks):
-            if self.pieces > 1:
-                count, match, _, rs = self.gb.run_overlapped(pt, self.pieces,
-                                                             None if ev is None else ev[ci])
-            else:
-                if ev is not None:
-                    ev[ci][0].record()
-                count, match, _ = self.gb.match(pt)
-                if ev is not None:
-                    ev[ci][1].record()
-                rs = self.gb.verify(pt, count, match)
-                if ev is not None:
-                    ev[ci][2].record()
+            if ev is not None:
+                ev[ci][0].record()
+            count, match, _ = self.gb.match(pt)
+            if ev is not None:
+                ev[ci][1].record()
+            rs = self.gb.verify(pt, count, match)
+            if ev is not None:
+                ev[ci][2].record()
             if ranges is None:
                 rows_l.append(self.gb.graph_rows(base, count, match, rs))
             else:
@@ -164,21 +159,13 @@ class Runner:
 
     def events(self):
         torch = self.torch
-        n = 4 if self.pieces > 1 else 3
-        return [[torch.cuda.Event(enable_timing=True) for _ in range(n)] for _ in self.chunks]
+        return [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in self.chunks]
 
     @staticmethod
     def stage_ms(ev):
-        """(K1 ms, K2 ms, K1 start -> K2 end ms) summed over the chunks.  Overlapped (4 events
-        per chunk): K1 = its stream's span, K2 = the second stream's span; they overlap, so the
-        span is less than their sum."""
-        if len(ev[0]) == 4:
-            m = sum(e[0].elapsed_time(e[1]) for e in ev)
-            r = sum(e[2].elapsed_time(e[3]) for e in ev)
-            return m, r, sum(e[0].elapsed_time(e[3]) for e in ev)
         m = sum(e[0].elapsed_time(e[1]) for e in ev)
         r = sum(e[1].elapsed_time(e[2]) for e in ev)
-        return m, r, m + r
+        return m, r
 
 
 def parse_args(argv=None):
@@ -192,9 +179,6 @@ def parse_args(argv=None):
     ap.add_argument("--n-pts", type=int, default=0,
                     help="cfg5: override the scene's 3-D point count (default n_img*n_in/5)")
     ap.add_argument("--n-hyp", type=int, default=4096)
-    ap.add_argument("--pieces", type=int, default=1,
-                    help="cut every launch chunk into this many pieces and run K1 of piece i + 1 "
-                         "beside K2 of piece i on a second stream (GraphBuilder.run_overlapped)")
     ap.add_argument("--chunk", type=int, default=131072,
                     help="pairs per K1/K2 launch (default: a cfg4 shard in one launch, ~90 GB of "
                          "buffers at N = 1; same graph checksum as 16384-pair chunks, 1.7-2.2 %% "
@@ -360,7 +344,7 @@ def pairs_main(args, world, rank, local, dist_info):
     pairs = synth.unordered_pairs(n_img)
     ranges = [match_graph.shard_range(pairs, r, world, scene["n_kp"]) for r in range(world)]
     lo, hi = ranges[rank]
-    run = Runner(scene, pairs, lo, hi, args.chunk, args.n_hyp, local, args.pieces)
+    run = Runner(scene, pairs, lo, hi, args.chunk, args.n_hyp, local)
     log(f"[rank {rank}] {args.config}: {n_img} imgs x {k} kps, {len(pairs)} pairs, shard "
         f"[{lo},{hi}) in {len(run.chunks)} launches (gen {time.time() - t0:.1f}s)")
     xr = ranges if world > 1 else None
@@ -373,7 +357,7 @@ def pairs_main(args, world, rank, local, dist_info):
     for _ in range(args.warmup):
         run.step(xr)
     torch.cuda.synchronize()
-    run.gb.ransac_ctx.ransac_stats(enable=True, read=True)
+    run.ctx.ransac_stats(enable=True, read=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -394,12 +378,11 @@ def pairs_main(args, world, rank, local, dist_info):
 
     verified_per_step = int(graph.shape[0])
     checksum = graph_checksum(torch, graph)  # after the timed region
-    r_alg, r_exec, r_evals = ransac_flops(run.gb.ransac_ctx.ransac_stats(enable=False, read=True),
+    r_alg, r_exec, r_evals = ransac_flops(run.ctx.ransac_stats(enable=False, read=True),
                                           args.n_hyp, args.steps)
     st = [Runner.stage_ms(e) for e in evs]
     match_ms = float(np.mean([s[0] for s in st]))
     ransac_ms = float(np.mean([s[1] for s in st]))
-    span_ms = float(np.mean([s[2] for s in st]))
     per_rank = gather_ranks(world, {
         "rank": rank, "device": local, "pairs": int(hi - lo),
         "shard_ms_per_step": t_own / args.steps * 1e3, "match_ms": match_ms,
@@ -441,8 +424,7 @@ def pairs_main(args, world, rank, local, dist_info):
                      "practical_peak_note": "i8 MFMA-only loop on random operands holds ~1.75 GHz "
                                             "(profiles/r02/mfma_peak_i8.json, tools/mfma_peak.hip)"},
         "stages": {"match_ms": match_ms, "ransac_ms": ransac_ms,
-                   "k1_k2_span_ms": span_ms, "pieces": args.pieces,
-                   "graph_ms": elapsed / args.steps * 1e3 - span_ms,
+                   "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,
                    "ransac_roofline": {
                        "bound": "f32 VALU", "peak": PEAK_F32_VALU_TFLOPS, "unit": "TFLOP/s",
                        "achieved": r_alg * r_exec / (ransac_ms * 1e-3) / 1e12,
@@ -481,7 +463,7 @@ def pairs_main(args, world, rank, local, dist_info):
         if args.config != "cfg3" and not args.no_cfg3:
             del run, graph
             torch.cuda.empty_cache()
-            result["cfg3"] = cfg3_side(args.n_hyp, args.chunk, args.pieces)
+            result["cfg3"] = cfg3_side(args.n_hyp, args.chunk)
         if args.config == "cfg4" and not args.no_cfg5:
             torch.cuda.empty_cache()
             try:   # a side leg: its failure is recorded, the cfg4 line stands
@@ -873,7 +855,7 @@ def cfg1_timing():
     return out
 
 
-def cfg3_side(n_hyp, chunk, pieces=1):
+def cfg3_side(n_hyp, chunk):
     """cfg3 (50 x 2048, 1225 pairs) on this GPU: the north_star's 2048 x 128 K1 kernel and the
     cfg3 step, 10 timed steps after 3 warmups."""
     import numpy as np
@@ -881,7 +863,7 @@ def cfg3_side(n_hyp, chunk, pieces=1):
     import synth
     scene = synth.make_scene(50, 2048, seed=0)
     pairs = synth.unordered_pairs(50)
-    run = Runner(scene, pairs, 0, len(pairs), chunk, n_hyp, torch.cuda.current_device(), pieces)
+    run = Runner(scene, pairs, 0, len(pairs), chunk, n_hyp, torch.cuda.current_device())
     for _ in range(3):
         run.step()
     torch.cuda.synchronize()

@@ -63,7 +63,6 @@ class GraphBuilder:
         self.ransac_kw = dict(n_hyp=n_hyp, seed=seed, thr=thr, min_inliers=min_inliers)
         self.min_inliers = min_inliers
         self._bufs = {}
-        self._ctx2 = self._s2 = None   # K2's context + stream of run_overlapped (created lazily)
 
     def _buffers(self, P):
         """Output buffers for a batch of P pairs, reused by every later call with the same P.
@@ -97,67 +96,11 @@ class GraphBuilder:
         return self.ctx.ransac_batch(self.kps, pairs_t, count, match, out=b["ransac"],
                                      **self.ransac_kw)
 
-    def run(self, pairs_t, pieces: int = 1, events=None):
-        """K1 + K2 on one pair batch; returns (count, match, dist, ransac dict) device tensors.
-
-        pieces > 1: run_overlapped (K1 of piece i + 1 beside K2 of piece i), the same outputs."""
-        if pieces > 1:
-            return self.run_overlapped(pairs_t, pieces, events)
+    def run(self, pairs_t):
+        """K1 + K2 on one pair batch; returns (count, match, dist, ransac dict) device tensors."""
         count, match, dist = self.match(pairs_t)
         rs = self.verify(pairs_t, count, match)
         return count, match, dist, rs
-
-    @property
-    def ransac_ctx(self):
-        """The context K2 runs on (run_overlapped's second context once it exists)."""
-        return self._ctx2 if self._ctx2 is not None else self.ctx
-
-    def run_overlapped(self, pairs_t, pieces: int, events=None):
-        """K1 + K2 over one pair batch cut into `pieces` contiguous pieces: K1 of every piece on
-        the current stream, K2 of piece i on a second stream once K1 of piece i is done, so K2 of
-        piece i runs beside K1 of piece i + 1.  K2 has its own sfm context (its own workspace:
-        one context's workspace is shared by every call on it).  K1 fills 2 waves per SIMD
-        (LDS-bound, 66.5 KB per block) and leaves VALU issue slots idle (~28 % of its waves'
-        cycles wait on memory); the K2 kernels (24-40 VGPRs, no LDS) fit beside it.  Per-pair work
-        is independent and K2's RNG is keyed by the pair's images, so the outputs equal run()'s
-        bit for bit.  The current stream waits for the last K2 piece before returning.
-        events: optional [K1 start, K1 end, K2 start, K2 end] timing events (recorded here)."""
-        torch = self.torch
-        P = pairs_t.shape[0]
-        b = self._buffers(P)
-        if self._ctx2 is None:
-            self._ctx2 = sfmcore.Context(self.dev.index)
-            self._s2 = torch.cuda.Stream(self.dev)
-        if self._ctx2.ransac_stats_enabled != self.ctx.ransac_stats_enabled:
-            self._ctx2.ransac_stats(enable=self.ctx.ransac_stats_enabled)
-        cur = torch.cuda.current_stream(self.dev)
-        cnt, mt, dist = b["match"]
-        rs = b["ransac"]
-        bounds = np.linspace(0, P, max(1, min(pieces, P)) + 1).astype(np.int64)
-        parts = [(int(a), int(c)) for a, c in zip(bounds[:-1], bounds[1:]) if c > a]
-        if events is not None:
-            events[0].record(cur)
-        done_k1 = []
-        for b0, b1 in parts:
-            self.ctx.match_batch(self.desc, self.n_kp, pairs_t[b0:b1],
-                                 out=(cnt[b0:b1], mt[b0:b1], dist[b0:b1]), **self.match_kw)
-            e = torch.cuda.Event()
-            e.record(cur)
-            done_k1.append(e)
-        if events is not None:
-            events[1].record(cur)
-        with torch.cuda.stream(self._s2):
-            for i, ((b0, b1), e) in enumerate(zip(parts, done_k1)):
-                self._s2.wait_event(e)
-                if i == 0 and events is not None:
-                    events[2].record(self._s2)
-                self._ctx2.ransac_batch(self.kps, pairs_t[b0:b1], cnt[b0:b1], mt[b0:b1],
-                                        out={k: v[b0:b1] for k, v in rs.items()},
-                                        **self.ransac_kw)
-            fin = events[3] if events is not None else torch.cuda.Event()
-            fin.record(self._s2)
-        cur.wait_event(fin)
-        return cnt, mt, dist, rs
 
     def graph_rows(self, pair_base: int, count, match, rs, return_offsets=False, packed=False):
         """Verified inlier rows [n,3] int32 (global pair index, queryIdx, trainIdx), on device

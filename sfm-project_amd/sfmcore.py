@@ -156,7 +156,6 @@ class Context:
             raise SfmCoreError("no HIP device visible: the sfm core has no CPU fallback")
         self.lib = load_library()
         self.device = device
-        self.ransac_stats_enabled = False
         h = C.c_void_p()
         _check(self.lib.sfm_ctx_create(device, C.byref(h)))
         self.handle = h
@@ -310,7 +309,6 @@ class Context:
         out = (C.c_uint64 * 3)()
         self._bind_stream()
         _check(self.lib.sfm_ransac_stats(self.handle, 1 if enable else 0, out if read else None))
-        self.ransac_stats_enabled = bool(enable)
         return (int(out[0]), int(out[1]), int(out[2])) if read else None
 
     # ---- verified match graph --------------------------------------------------------------

@@ -111,41 +111,6 @@ def test_graph_builder_matches_oracle():
     np.testing.assert_array_equal(rows, np.array(want, np.int32).reshape(-1, 3))
 
 
-@pytest.mark.parametrize("pieces", [2, 5, 64])
-def test_graph_builder_overlapped_equals_one_stream(pieces):
-    """GraphBuilder.run_overlapped (K1 of piece i + 1 on the current stream beside K2 of piece i on
-    a second stream and context) returns run()'s outputs bit for bit, with more pieces than pairs
-    too; the ransac_stats flag follows the first context."""
-    import torch
-    s = synth.make_scene(9, 1024, seed=17)
-    pairs = synth.unordered_pairs(9)               # 36 pairs
-    pt = torch.from_numpy(pairs).cuda()
-    gb = match_graph.GraphBuilder(s["desc"], s["kps"], s["n_kp"], ratio=(4, 5), n_hyp=512)
-    ref = [t.clone() for t in gb.run(pt)[:3]]
-    ref_rs = {k: v.clone() for k, v in gb.run(pt)[3].items()}
-    ref_rows = gb.graph_rows(0, ref[0], ref[1], ref_rs).cpu().numpy()
-    for t in gb._buffers(len(pairs))["match"]:     # poison the shared buffers
-        t.fill_(-7)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    count, match, dist, rs = gb.run(pt, pieces=pieces, events=evs)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(count.cpu().numpy(), ref[0].cpu().numpy())
-    c = count.cpu().numpy()
-    m, mr = match.cpu().numpy(), ref[1].cpu().numpy()
-    for p in range(len(pairs)):
-        np.testing.assert_array_equal(m[p, :c[p]], mr[p, :c[p]])
-    for k in ("inl_count", "best_h", "F", "norm"):
-        np.testing.assert_array_equal(rs[k].cpu().numpy(), ref_rs[k].cpu().numpy())
-    np.testing.assert_array_equal(gb.graph_rows(0, count, match, rs).cpu().numpy(), ref_rows)
-    assert evs[0].elapsed_time(evs[3]) > 0
-    gb.ctx.ransac_stats(enable=True)
-    gb.run(pt, pieces=pieces)
-    assert gb.ransac_ctx is not gb.ctx and gb.ransac_ctx.ransac_stats_enabled
-    ex, alg, npairs = gb.ransac_ctx.ransac_stats(enable=False, read=True)
-    assert npairs == int((c >= 8).sum()) and 0 < ex <= alg
-    gb.ctx.ransac_stats(enable=False)
-
-
 def test_build_jtj_and_sharded_single_rank():
     pr = synth.make_ba_problem(9, 300, obs_per_pt=4, seed=17)
     o = O.ba_jtj(pr["cams"], pr["pp"], pr["pts"], pr["cam_idx"], pr["pt_idx"], pr["uv"],

@@ -3,8 +3,12 @@ set -o pipefail
 # standalone A/B (tests/perf/overlap_ab.py), then bench.py --pieces 1 / 2 / 4 interleaved.
 OUT=gpurun_out/r6l; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_host.py -k overlapped -v -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_overlap.log 2>&1 || { tail -40 $OUT/pytest_overlap.log; exit 1; }
-tail -2 $OUT/pytest_overlap.log
+timeout -k 10 120 python -u tests/perf/overlap_stats_probe.py > $OUT/stats_probe.txt 2>&1 || { tail -30 $OUT/stats_probe.txt; exit 1; }
+cat $OUT/stats_probe.txt
+timeout -k 10 300 python -u -m pytest tests/test_gpu_host.py -k overlapped -v -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_overlap.log 2>&1
+rc=$?
+grep -E "^E  |FAILED|passed|failed" $OUT/pytest_overlap.log | head -20
+[ $rc -le 1 ] || exit $rc
 timeout -k 10 600 python -u tests/perf/overlap_ab.py 500 4096 2 > $OUT/overlap.jsonl 2> $OUT/overlap.err || { tail -30 $OUT/overlap.err; exit 1; }
 cat $OUT/overlap.jsonl
 for r in 1 2; do
