@@ -138,6 +138,22 @@ def registration_obs(otr, timg, has_point, registered, min_corr=30):
     return sel, img_u[keep].cpu().numpy().astype(np.int32), cptr.cpu().numpy().astype(np.int32)
 
 
+def point_mean(err, first):
+    """Mean of `err` over each run of observations (runs start where `first` is set; every point's
+    observations are contiguous), summed left to right within a run — the additions of
+    numpy.bincount(pt_idx, err) / max(count, 1), so the same doubles — on the device: one
+    masked gather-add per observation rank (tracks are short) instead of a host round trip."""
+    import torch
+    n_obs = err.shape[0]
+    starts = torch.nonzero(first).squeeze(1)
+    lens = torch.diff(starts, append=torch.tensor([n_obs], device=err.device))
+    acc = torch.zeros(starts.shape[0], dtype=err.dtype, device=err.device)
+    for k in range(int(lens.max()) if n_obs else 0):
+        take = err[torch.clamp(starts + k, max=n_obs - 1)]
+        acc = torch.where(lens > k, acc + take, acc)
+    return acc / torch.clamp(lens, min=1).to(err.dtype)
+
+
 def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max_err=4.0,
                 ba_iter=20, loss_s=2.0, device=0, log=None, group=None, shard_ba=False,
                 ba_cg_tol=0.1, ba_pcg="auto", ba_ftol=1e-6):
@@ -334,35 +350,35 @@ def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device
     dev = otr_d.device
     reg_d = torch.from_numpy(rec.registered).to(dev)
     has_d = torch.from_numpy(rec.has_point).to(dev)
-    use_d = reg_d[timg_d] & has_d[otr_d]
-    n_use = int(use_d.sum().item())
+    use = torch.nonzero(reg_d[timg_d] & has_d[otr_d]).squeeze(1)   # the one sizing sync
+    n_use = int(use.shape[0])
     if n_use == 0:
         return
     ref, second = rec.gauge
     fixed = reconstruction.gauge_mask(rec.cams, ref=ref, second=second, fix_intrinsics=True)
-    tr = otr_d[use_d]   # non-decreasing (track-major): unique tracks by run starts
+    tr = otr_d[use]   # non-decreasing (track-major): unique tracks by run starts
     first = torch.ones(n_use, dtype=torch.bool, device=dev)
     first[1:] = tr[1:] != tr[:-1]
     pts_ids = tr[first].cpu().numpy()
     pt_idx_d = torch.cumsum(first, 0, dtype=torch.int32) - 1
     info = {}
+    t_sel = time.perf_counter() - t0    # observation selection (ends in host syncs)
     cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
-                                                   timg_d[use_d].to(torch.int32), pt_idx_d,
-                                                   oxy_d[use_d], loss_s=loss_s, max_iter=ba_iter,
+                                                   timg_d[use].to(torch.int32), pt_idx_d,
+                                                   oxy_d[use], loss_s=loss_s, max_iter=ba_iter,
                                                    cg_tol=cg_tol, ftol=ftol, device=device,
                                                    fixed=fixed, shard=shard_ba, group=group,
-                                                   pcg=pcg, info=info, reproj_err=True)
-    err = info.pop("err")   # at the returned parameters (bundle_adjust reproj_err)
-    pt_idx = pt_idx_d.cpu().numpy()
+                                                   pcg=pcg, info=info, reproj_err="device")
+    err_d = info.pop("err")   # device, at the returned parameters (bundle_adjust reproj_err)
     rec.ba_log.append(dict(info, n_cam=int(rec.registered.sum()), n_pt=int(len(pts_ids)),
                            n_obs=n_use, lm_steps=len(hist),
                            cg_iters=int(sum(h[3] for h in hist))))
     reg = rec.registered
     rec.cams[reg] = cams[reg]
     rec.points[pts_ids] = pts
-    mean = np.bincount(pt_idx, err, minlength=len(pts_ids)) / np.maximum(
-        np.bincount(pt_idx, minlength=len(pts_ids)), 1)
-    rec.has_point[pts_ids[mean > max_err]] = False
+    mean = point_mean(err_d, first)
+    rec.has_point[pts_ids[(mean > max_err).cpu().numpy()]] = False
     rec.ba_log[-1]["s"] = time.perf_counter() - t0   # setup + LM + reprojection filter
+    rec.ba_log[-1]["select_s"] = t_sel
     rec.history.append((int(reg.sum()), int(rec.has_point.sum()),
                         float(hist[-1][0]) if hist else float("nan")))

@@ -361,7 +361,7 @@ def _gather_rows(t, counts, group):
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
                   lam0: float = 1e-4, ftol: float = 1e-12, max_cg: int = 200,
                   cg_tol: float = 1e-10, device: int = 0, fixed=None, shard: bool = False,
-                  group=None, pcg: str = "auto", info=None, reproj_err: bool = False):
+                  group=None, pcg: str = "auto", info=None, reproj_err=False):
     """Levenberg-Marquardt on paper eq. (1): every step on the GPU
     (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
     accept / reject it.  cam_idx / pt_idx / uv may be device tensors (used in place).
@@ -388,11 +388,14 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     reproj_err it also receives `err`: every observation's reprojection error (px) at the returned
     parameters, in the caller's order — from the device-resident problem (one more K3 launch;
     sharded: each rank's shard summed into a zero-padded vector), instead of a second host ->
-    device copy of the whole problem through reprojection_errors.
+    device copy of the whole problem through reprojection_errors.  reproj_err="device" leaves
+    `err` as an f64 device tensor (same order) instead of a host array.
 
     Returns (cams [n_cam,8], pts [n_pt,3], history [(cost, λ, accepted, cg_iterations)])."""
     import os
+    import time
     import torch
+    t_entry = time.perf_counter()
     n_cam, n_pt = len(cams), len(pts)
     allreduce = None
     world = 1
@@ -479,9 +482,9 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                                          max_iter=max_cg, tol=cg_tol)
     upd = full if full is not None else prob
     if info is not None:
-        import time
         torch.cuda.synchronize(prob.dev)
         t_lm = time.perf_counter()
+        info["setup_s"] = t_lm - t_entry    # problem upload / CSR build before the first LM step
     lam, nu = lam0, 2.0
     hist = []
     old = float(cost(cams_d, pts_d).item())
@@ -520,13 +523,15 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                 back = torch.empty_like(e)
                 back[torch.as_tensor(prob.order, device=e.device)] = e
                 e = back
-            err = e.cpu().numpy()
+            err = e if reproj_err == "device" else e.cpu().numpy()
         else:
             ev = torch.zeros(n_obs_all, dtype=torch.float64, device=prob.dev)
             ev[o0:o1] = e
             allreduce(ev)
             err = np.empty(n_obs_all)
             err[order] = ev.cpu().numpy()
+            if reproj_err == "device":
+                err = torch.from_numpy(err).to(prob.dev)
         info["err"] = err
     if allreduce is not None and full is None:
         # gather the point shards: one all-reduce of the zero-padded set
@@ -534,4 +539,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         allp[lo:hi] = pts_d
         allreduce(allp.view(-1))
         pts_d = allp
-    return cams_d.cpu().numpy(), pts_d.cpu().numpy(), hist
+    out = cams_d.cpu().numpy(), pts_d.cpu().numpy(), hist
+    if info is not None:
+        info["post_s"] = time.perf_counter() - t_lm - info["lm_s"]   # errors + results to host
+    return out

@@ -267,3 +267,20 @@ def test_registration_obs_equals_host_selection():
         np.testing.assert_array_equal(cptr, np.r_[0, np.cumsum(img_n[keep])])
         np.testing.assert_array_equal(sel.numpy(), obs_sel[np.repeat(keep, img_n)])
         assert ids.dtype == np.int32 and cptr.dtype == np.int32
+
+
+def test_point_mean_equals_host_bincount():
+    """incremental.point_mean (device-side reprojection filter of the bundle adjustments) gives
+    numpy.bincount(pt_idx, err) / max(count, 1) bit for bit on runs of observations."""
+    import torch
+    import incremental
+    rng = np.random.default_rng(5)
+    lens = rng.integers(1, 12, 3000)
+    pt_idx = np.repeat(np.arange(len(lens)), lens)
+    err = rng.gamma(1.0, 1.5, len(pt_idx)) * np.exp(rng.normal(0, 3, len(pt_idx)))
+    ref = np.bincount(pt_idx, err, minlength=len(lens)) / np.maximum(
+        np.bincount(pt_idx, minlength=len(lens)), 1)
+    first = np.ones(len(pt_idx), bool)
+    first[1:] = pt_idx[1:] != pt_idx[:-1]
+    got = incremental.point_mean(torch.from_numpy(err), torch.from_numpy(first)).numpy()
+    np.testing.assert_array_equal(got.view(np.uint64), ref.view(np.uint64))
