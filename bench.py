@@ -312,6 +312,7 @@ def main(argv=None):
         print(json.dumps(result), flush=True)
     if world > 1:
         import reconstruction
+        dist.barrier()   # rank 0's side legs (fp64 K2) end before any rank tears the group down
         reconstruction.release_allreduce()
         dist.destroy_process_group()
     return 0
