@@ -222,16 +222,6 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
         crow[o] = (j < n_kp[img]) ? (-128 * nv + 127 - (j & 127)) : ROW_PAD;
 }
 
-// K1 prologue (round 4): with MU_PAIR_INFO=1 a small kernel after pair_order
-// writes one 16-B record per ordered slot (p, a, b, na | nb << 16), so a block of the mutual
-// kernel finds its pair with ONE dependent load instead of the chain pair_order -> pairs -> n_kp.
-// Measured equal at cfg3 (0.974 / 0.983 / 0.976 ms vs 0.972 / 0.978 / 0.981 ms per launch,
-// interleaved, profiles/r04/k1_prologue_ab.txt): the chain is hidden behind the other blocks'
-// streams, so the knob stays off (A/B only).
-#ifndef MU_PAIR_INFO
-#define MU_PAIR_INFO 0
-#endif
-
 // Pair order by train image (counting sort in LDS; one block): consecutive entries share image b.
 __global__ __launch_bounds__(1024) void pair_order_kernel(const int32_t* __restrict__ pairs,
                                                           int n_pairs, int n_img,
@@ -249,18 +239,6 @@ __global__ __launch_bounds__(1024) void pair_order_kernel(const int32_t* __restr
     }
     __syncthreads();
     for (int p = tid; p < n_pairs; p += 1024) order[atomicAdd(&hist[pairs[2 * p + 1]], 1)] = p;
-}
-
-// The per-slot pair record of MU_PAIR_INFO (after pair_order_kernel).
-__global__ __launch_bounds__(256) void pair_info_kernel(const int32_t* __restrict__ pairs,
-                                                        const int32_t* __restrict__ n_kp,
-                                                        int n_pairs, const int32_t* __restrict__ order,
-                                                        int4* __restrict__ info) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
-    if (s >= n_pairs) return;
-    const int p = order[s];
-    const int a = pairs[2 * p], b = pairs[2 * p + 1];
-    info[s] = make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
 }
 
 // TOP2 = false: the row side keeps only (best, argbest) — the second-best value is what the ratio
@@ -573,16 +551,13 @@ constexpr int MU_CLOCK_W = 8;  // per block: loop memtime/realtime start+end, en
 __device__ unsigned long long g_mu_clock[MU_CLOCK_W * MU_CLOCK_SLOTS];
 #endif
 
-#ifndef MU_ROW_I4
-#define MU_ROW_I4 0  // 1: the round-1 16-B row records (A/B only)
-#endif
 template <int D, bool ROWS>
 __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
     const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
     const int32_t* __restrict__ pair_order, int n_blk, int4* __restrict__ rowres,
-    unsigned long long* __restrict__ colpart, int col_atomic, const int4* __restrict__ pair_info) {
+    unsigned long long* __restrict__ colpart, int col_atomic) {
     constexpr int QT = Geo<D>::QT, QB = mu_qb<D>(), CHUNK = MU_CHUNK_BYTES / D, NK = Geo<D>::NK;
     constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32, NTHR = 64 * MU_WAVES;
     constexpr int PIECES = CHUNK * D / 1024 / MU_WAVES, RPP = 1024 / D;
@@ -598,14 +573,9 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
     if (sblk >= n_blk) return;  // block-uniform, before any barrier
     const int qb = sblk % n_qblk;
-#if MU_PAIR_INFO
-    const int4 pinf = pair_info[sblk / n_qblk];
-    const int p = pinf.x, a = pinf.y, b = pinf.z, na = pinf.w & 0xFFFF, nb = pinf.w >> 16;
-#else
     const int p = pair_order[sblk / n_qblk];
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
-#endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     for (int j = tid; j < k_pad; j += NTHR) lds_col[j] = 0ull;
 
@@ -669,13 +639,8 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
             };
             v4i af[NK];
             v16i init;
-#ifdef MU_PF
-            load_tile(0, af, init);
-#endif
             for (int tt = 0; tt < nt; ++tt) {
-#ifndef MU_PF
                 load_tile(tt, af, init);
-#endif
                 int colacc[16];
 #pragma unroll
                 for (int c = 0; c < QT; c += 2) {
@@ -685,10 +650,6 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
                         acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
                         acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
                     }
-#ifdef MU_PF
-                    // the next tile's fragments load behind this tile's last epilogue
-                    if (c + 2 == QT && tt + 1 < nt) load_tile(tt + 1, af, init);
-#endif
 #pragma unroll
                     for (int r = 0; r < 16; r += 2) {
                         if constexpr (ROWS) {
@@ -748,11 +709,8 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
             const int e1 = max(tb[c], P1);
             const int e2 = max(min(tb[c], P1), max(ts[c], P2));
             const int q = qbase + c * 32 + r32;
-#if MU_ROW_I4
-            if (h == 0 && q < na) rowres[(size_t)p * k_pad + q] = make_int4(e1, e2, 0, 0);
-#else  // 8-B row records (e1, e2): half the row bytes of the 16-B layout
+            // 8-B row records (e1, e2): half the row bytes of round 1's 16-B layout
             if (h == 0 && q < na) ((int2*)rowres)[(size_t)p * k_pad + q] = make_int2(e1, e2);
-#endif
         }
     }
 #ifdef MU_DIAG_NOMERGE  // timing-only bound (wrong results): no column-table merge at block end
@@ -909,16 +867,8 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void ham_key_kernel(
                     acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[0][s], acc0, 0, 0, 0);
                     acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[1][s], acc1, 0, 0, 0);
                 }
-#ifdef HAMKEY_VALU_QCONST  // debug build: the query constant added on the VALU instead
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    acc0[r] += -128 * nq[0] + 127 - r32;
-                    acc1[r] += -128 * nq[1] + 127 - (32 + r32);
-                }
-#else
                 acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ax, bx[0], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(ax, bx[1], acc1, 0, 0, 0);
-#endif
                 int colacc[16];
 #pragma unroll
                 for (int r = 0; r < 16; r += 2) {
@@ -1053,11 +1003,7 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
         long long d1 = 0;
         if (tid == 0) nslow = 0;
         if (i < na) {
-#if MU_ROW_I4
-            const int4 r = rowres[(size_t)p * k_pad + i];
-#else
             const int2 r = ((const int2*)rowres)[(size_t)p * k_pad + i];
-#endif
             const long long A = na_norm[i];
             const unsigned long long e = lds_best[i];
             const long long Dp = e != ~0ull ? (long long)(e >> 32) : sfm::DIST_INF;  // best proposal
@@ -1378,12 +1324,11 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     }
     const int n_qblk = (k_max + QB - 1) / QB;
     const size_t tab = (size_t)n_img * k_pad * sizeof(int32_t);
-    const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int4);
+    const size_t rowb = (size_t)n_pairs * k_pad * sizeof(int2);   // (e1, e2) per query
     const size_t colb = (size_t)n_pairs * n_qblk * k_pad * sizeof(unsigned long long);
     const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
     const size_t ordb = sfm::align_up(sizeof(int32_t) * ((size_t)n_pairs + n_img), 256);
-    const size_t infb = sfm::align_up(sizeof(int4) * (size_t)n_pairs, 256);
-    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + infb + 1024);
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + rowb + colb + descb + ordb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     uint8_t* zero_row = (uint8_t*)ws;
     int32_t* norm = (int32_t*)(ws + 256);
@@ -1392,7 +1337,6 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     unsigned long long* colpart = (unsigned long long*)(ws + 256 + 2 * tab + rowb);
     uint8_t* desc_i8 = (uint8_t*)(ws + 256 + 2 * tab + rowb + colb);
     int32_t* pair_order = (int32_t*)(ws + 256 + 2 * tab + rowb + colb + descb);
-    int4* pair_info = (int4*)(ws + 256 + 2 * tab + rowb + colb + descb + ordb);
     const int n_blk = n_pairs * n_qblk;
     // column winners merged by atomics (default) or as per-query-block partials the finalize
     // reduces (SFM_MU_COLPART=1); DESIGN.md 4.1
@@ -1408,11 +1352,6 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
                        pairs, n_pairs, n_img, pair_order, pair_order + n_pairs);
     SFM_HIP_CHECK(hipGetLastError());
-    if (MU_PAIR_INFO) {
-        hipLaunchKernelGGL(pair_info_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, st, pairs,
-                           n_kp, n_pairs, pair_order, pair_info);
-        SFM_HIP_CHECK(hipGetLastError());
-    }
     if (l2)
         hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_L2, true>), dim3(k_pad / 256, n_img),
                            dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row,
@@ -1426,7 +1365,7 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     hipLaunchKernelGGL((mfma_mutual_kernel<DD, RR>), dim3(grid), dim3(64 * MU_WAVES),             \
                        (size_t)k_pad * 8, st, desc_i8, n_kp,                                      \
                        k_max, k_pad, norm, cinit, zero_row, pairs, n_qblk, pair_order, n_blk,     \
-                       rowres, colpart, col_atomic, pair_info)
+                       rowres, colpart, col_atomic)
     if (l2 && rows) SFM_MU_SCAN(128, true);
     else if (l2) SFM_MU_SCAN(128, false);
     else if (rows) SFM_MU_SCAN(256, true);
