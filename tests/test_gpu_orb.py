@@ -109,6 +109,27 @@ def test_extract_and_match_on_gpu_without_cv2():
     assert ok > 0.85 * len(ms)   # the rest: repeated texture and the replicated right margin
 
 
+def test_extract_and_match_cache_is_transparent(monkeypatch):
+    """The content-keyed ORB cache of extract_and_match returns what fresh extractions give: the
+    same matches cached and uncached, and an image changed in place is re-extracted."""
+    import feature_matching as fm
+    img = synth.make_image(480, 640, seed=6)
+    sh = np.zeros_like(img)
+    sh[:, :-11] = img[:, 11:]
+    monkeypatch.setattr(fm, "_orb_cache", None)
+    first = fm.extract_and_match(img, sh)
+    again = fm.extract_and_match(img, sh)            # both images from the cache
+    back = fm.extract_and_match(sh, img)
+    monkeypatch.setattr(fm, "ORB_CACHE_SIZE", 0)
+    assert first == again == fm.extract_and_match(img, sh) and len(first) > 100
+    assert back == fm.extract_and_match(sh, img)
+    monkeypatch.setattr(fm, "ORB_CACHE_SIZE", 1024)
+    sh[100:200, 100:300] = 255 - sh[100:200, 100:300]  # in place: a new cache key
+    cached = fm.extract_and_match(img, sh)
+    monkeypatch.setattr(fm, "ORB_CACHE_SIZE", 0)
+    assert cached == fm.extract_and_match(img, sh) and cached != first
+
+
 def test_extract_and_match_draw_without_cv2(monkeypatch):
     """The reference's debug entry (code/feature_matching.py:15-37) on the GPU with the numpy
     drawMatches: the same matches as extract_and_match, and the drawing shown (headless)."""

@@ -284,3 +284,37 @@ def test_point_mean_equals_host_bincount():
     first[1:] = pt_idx[1:] != pt_idx[:-1]
     got = incremental.point_mean(torch.from_numpy(err), torch.from_numpy(first)).numpy()
     np.testing.assert_array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+def test_orb_cache_extracts_each_distinct_image_once(monkeypatch):
+    """extract_and_match's content-keyed ORB cache (the reference loop calls it 2 (N-1) times per
+    image): one extraction per distinct image content, duplicates inside a call extracted once,
+    an in-place change is a new key, LRU-bounded, read-only cached arrays."""
+    calls = []
+
+    def fake_orb(images, device=0, **kw):
+        calls.append(len(images))
+        return [(np.full((3, 6), float(im.sum()), np.float32),
+                 np.full((3, 32), int(im.sum()) % 251, np.uint8)) for im in images]
+
+    monkeypatch.setattr(fm, "_orb_gpu", fake_orb)
+    monkeypatch.setattr(fm, "_orb_cache", None)
+    monkeypatch.setattr(fm, "ORB_CACHE_SIZE", 3)
+    rng = np.random.default_rng(0)
+    a, b, c, d = (rng.integers(0, 255, (40, 60), dtype=np.uint8) for _ in range(4))
+    r1 = fm._orb_cached([a, b])
+    assert calls == [2]
+    r2 = fm._orb_cached([b, a, a])
+    assert calls == [2] and r2[1][1] is r1[0][1] and r2[0][1] is r1[1][1]
+    assert not r1[0][1].flags.writeable
+    a2 = a.copy()
+    a2[0, 0] ^= 1                                   # same shape, different content
+    fm._orb_cached([a2, a2])
+    assert calls == [2, 1]
+    fm._orb_cached([c, d])                          # 5 distinct keys > 3: the oldest go
+    assert calls == [2, 1, 2] and len(fm._orb_cache) == 3
+    fm._orb_cached([b])                             # evicted (least recently used)
+    assert calls == [2, 1, 2, 1]
+    monkeypatch.setattr(fm, "ORB_CACHE_SIZE", 0)
+    fm._orb_cached([c])
+    assert calls == [2, 1, 2, 1, 1]
