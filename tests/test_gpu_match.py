@@ -258,6 +258,20 @@ def test_both_orders_hamming_reference_shape(ctx, xc, maxd):
     assert cnt.sum() > 0
 
 
+@pytest.mark.parametrize("xc,maxd", [(2, 26), (1, -1)])
+def test_both_orders_hamming_k4096(ctx, xc, maxd):
+    """Both orders from one tile at the largest k_max (4096: 16 query blocks of the key kernel per
+    pair, the row merges every 4 tiles, train indices past 127 / 2047 in the key's low bits),
+    ragged counts and planted duplicates: bit-identical to two launches and to the oracle."""
+    s = synth.make_scene(3, 4096, seed=41, orb=True)
+    desc, n_kp = s["desc"].copy(), s["n_kp"].copy()
+    n_kp[1] = 3001
+    desc[0, 4000] = desc[0, 129]        # a duplicated train far apart in index
+    desc[2, 2048:2052] = desc[1, 7]     # one row equidistant to four neighbours
+    cnt = _assert_both_equals_two_launches(ctx, desc, n_kp, 1, xc, maxd)
+    assert cnt.sum() > 0
+
+
 @pytest.mark.parametrize("xc,maxd", [(2, -1), (1, -1), (0, -1), (2, 30000)])
 def test_both_orders_l2(ctx, xc, maxd):
     s = synth.make_scene(4, 1000, seed=31)
