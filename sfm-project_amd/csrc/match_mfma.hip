@@ -1529,15 +1529,13 @@ int sfm_match_hamming_mfma_launch(sfm_ctx* ctx, const uint8_t* desc, const int32
                                   int32_t n_img, int32_t k_max, const int32_t* pairs,
                                   int32_t n_pairs, const sfm_match_params* prm,
                                   int32_t* out_count, int32_t* out_match, int32_t* out_dist) {
-    // The reference's OpenCV cross-check rule: the column side alone (0.126 vs 0.156 ms at 50 x 500,
-    // 1.30 vs 1.73 ms at 50 x 2048).  Mutual and no cross check: the fused key kernel — with
-    // Hamming distances (0..256) ties in e are the rule, not the exception, and every tie costs the
-    // value-only row side an exact row scan (0.68 vs 0.16 ms).  SFM_HAMMING_PATH=fused|mutual
-    // overrides.
-    const char* pe = getenv("SFM_HAMMING_PATH");
-    // Round 4: without a ratio test every rule runs on the key-in-the-accumulator kernel
-    // (ham_key_kernel: no VALU key build; rows only for the mutual / no rule).
+    // Without a ratio test (the reference's rules) every cross-check rule runs on the
+    // key-in-the-accumulator kernel (ham_key_kernel: no VALU key build; the row side only for the
+    // mutual / no rule).  With a ratio test: the OpenCV rule on the column-winner
+    // kernel, the others on the fused key kernel — with Hamming distances (0..256) ties in e are
+    // the rule, and every tie would cost the value-only row side an exact row scan.
     // SFM_HAMMING_PATH=mutual|fused selects the round-3 kernels (A/B only).
+    const char* pe = getenv("SFM_HAMMING_PATH");
     if (prm->ratio_den == 0 && !(pe && (strcmp(pe, "mutual") == 0 || strcmp(pe, "fused") == 0)))
         return match_tile_launch(ctx, SFM_METRIC_HAMMING, desc, n_kp, n_img, k_max, pairs, n_pairs,
                                  prm, out_count, out_match, out_dist, 1);
