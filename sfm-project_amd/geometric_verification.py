@@ -53,16 +53,23 @@ def verify_pair(kp1, kp2, matches, pair=(0, 1), n_hyp=DEFAULT_HYPOTHESES, seed=D
     kps_full = np.zeros((n_img, k_max, 2), np.float32)
     kps_full[a] = kps[0]
     kps_full[b] = kps[1]
-    out = ctx.ransac_batch(torch.from_numpy(kps_full).to(dev),
-                           torch.tensor([[a, b]], dtype=torch.int32, device=dev),
-                           torch.tensor([len(mt)], dtype=torch.int32, device=dev),
-                           torch.from_numpy(match).to(dev), n_hyp=n_hyp, seed=seed, thr=thr,
+    # one int32 upload (pair, match count, 61 pad, matches) and one byte download of the results
+    head = np.zeros(64, np.int32)
+    head[:3] = (a, b, len(mt))
+    up = torch.from_numpy(np.concatenate([head, match.reshape(-1)])).to(dev)
+    out = ctx.ransac_batch(torch.from_numpy(kps_full).to(dev), up[:2].view(1, 2), up[2:3],
+                           up[64:].view(1, k_max, 2), n_hyp=n_hyp, seed=seed, thr=thr,
                            min_inliers=min_inliers)
-    cnt = int(out["inl_count"].cpu()[0])
-    mask = out["mask"][0, :len(mt)].cpu().numpy().astype(bool)
-    F = denormalize_F(out["F"][0].cpu().numpy(), out["norm"][0].cpu().numpy())
+    M = len(mt)
+    u8 = lambda t: t.reshape(-1).view(torch.uint8)
+    back = torch.cat([u8(out["inl_count"][:1]), u8(out["best_h"][:1]), u8(out["F"][0]),
+                      u8(out["norm"][0]), out["mask"][0, :M]]).cpu().numpy()
+    cnt = int(back[0:4].view(np.int32)[0])
+    best_h = int(back[4:8].view(np.int32)[0])
+    F = denormalize_F(back[8:44].view(np.float32).copy(), back[44:68].view(np.float32).copy())
+    mask = back[68:68 + M].astype(bool)
     return dict(F=F, inliers=np.nonzero(mask)[0], count=max(cnt, 0),
-                verified=cnt >= min_inliers, best_h=int(out["best_h"].cpu()[0]))
+                verified=cnt >= min_inliers, best_h=best_h)
 
 
 def _match_array(matches) -> np.ndarray:
