@@ -34,9 +34,12 @@ cfg4 line carries a `cfg5` object measured in the same run.
 
 Launch: `--gpus N` with no external launcher (WORLD_SIZE unset) starts N fresh rank processes
 itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT, rank r on GPU
-r) before anything touches the GPU, relays rank 0's JSON line and exits non-zero if any rank fails;
-it refuses (rc 2) when fewer than N GPUs are visible.  Under torch.distributed.run, `--gpus` must
-equal WORLD_SIZE (rc 2 otherwise).
+r), relays rank 0's JSON line and exits non-zero if any rank fails; it refuses (rc 2) when fewer
+than N GPUs are visible.  The launcher never imports torch: it counts GPUs from the KFD topology
+(visible_gpus) and prints a `launcher-selfcheck` line on stderr showing that no HIP runtime was
+mapped into it.  `--ranks-per-gpu R --dist-backend gloo` rehearses the same count-then-spawn path
+with R ranks per GPU on a smaller box.  Under torch.distributed.run, `--gpus` must equal
+WORLD_SIZE (rc 2 otherwise).
 """
 import argparse
 import json
@@ -189,48 +192,124 @@ def parse_args(argv=None):
     ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 side measurement")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 side measurement")
     ap.add_argument("--no-fp64", action="store_true", help="skip the fp64-K2 side measurement")
+    ap.add_argument("--no-local", action="store_true",
+                    help="skip the cfg4_local side measurement (local-visibility scene)")
     ap.add_argument("--ba-pcg", default="auto", choices=("auto", "sharded", "replicated"),
                     help="cfg5: the sharded BA's PCG branch (reconstruction.pcg_rule)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: 'gloo' lets N ranks share one GPU (RCCL cannot)")
     ap.add_argument("--device", type=int, default=-1, help="rehearsal only: force this GPU")
+    ap.add_argument("--ranks-per-gpu", type=int, default=1,
+                    help="rehearsal only (with --dist-backend gloo): the self-launcher puts rank r "
+                         "on GPU r // R, going through the same count-then-spawn path as N GPUs")
     return ap.parse_args(argv)
 
 
+# SFM_BENCH_KFD_NODES: tests point the launcher at a fake topology
+KFD_NODES = os.environ.get("SFM_BENCH_KFD_NODES", "/sys/class/kfd/kfd/topology/nodes")
+
+
+def visible_gpus(kfd_nodes=None, environ=None):
+    """(number of GPUs this process could open, how it was counted) WITHOUT loading the HIP
+    runtime: the KFD topology's GPU nodes (simd_count > 0; CPU nodes have none), cut down by
+    ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (each an ordinal list
+    into what the previous one left, read up to the first bad entry, as the runtimes do; ROCR
+    also takes GPU-<uuid> entries).  Without a readable topology the count comes from a
+    throwaway child process (it may initialise HIP; this process does not).  An empty variable
+    is the runtimes' default (all devices), as HIP's and ROCr's flag parsing treat it."""
+    import glob
+    import re
+    env = os.environ if environ is None else environ
+    kfd_nodes = kfd_nodes or KFD_NODES
+    n = None
+    props = glob.glob(os.path.join(kfd_nodes, "*", "properties"))
+    if props:
+        n = 0
+        for p in props:
+            try:
+                m = re.search(r"^simd_count\s+(\d+)", open(p).read(), re.M)
+            except OSError:
+                continue
+            n += bool(m and int(m.group(1)) > 0)
+        source = "kfd-topology"
+    if n is None:
+        import subprocess
+        r = subprocess.run([sys.executable, "-c",
+                            "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=300, env=dict(env))
+        try:
+            return int(r.stdout.strip().splitlines()[-1]), "child-process"
+        except (ValueError, IndexError):
+            return 0, "child-process (failed)"
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if not env.get(var, "").strip():   # unset or empty: the runtimes' default, all devices
+            continue
+        keep, seen = 0, set()
+        for tok in (t.strip() for t in env[var].split(",")):
+            ok = (tok.isdigit() and int(tok) < n and tok not in seen) or \
+                 (var == "ROCR_VISIBLE_DEVICES" and tok.upper().startswith("GPU-"))
+            if not ok:
+                break
+            seen.add(tok)
+            keep += 1
+        n = min(n, keep)
+    return n, source
+
+
+def launcher_selfcheck():
+    """Proof that the launcher stayed GPU-free: torch never imported, no HIP / HSA runtime
+    library mapped into this process."""
+    try:
+        maps = open("/proc/self/maps").read()
+    except OSError:
+        maps = ""
+    return {"torch_imported": "torch" in sys.modules,
+            "hip_runtime_mapped": "libamdhip64" in maps or "libhsa-runtime64" in maps}
+
+
+def die_with_launcher():
+    """In a self-launched rank, first thing: SIGTERM when the launcher dies (PR_SET_PDEATHSIG set
+    by the child itself, so the launcher needs no preexec_fn / plain fork)."""
+    import ctypes
+    import signal
+    try:
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)
+    except OSError:
+        return
+    ppid = os.environ.get("SFM_BENCH_PARENT_PID")
+    if ppid and os.getppid() != int(ppid):   # the launcher died before the prctl
+        sys.exit(1)
+
+
 def launch_ranks(args, argv):
-    """`--gpus N` without an external launcher: N fresh child processes, one per GPU, started
-    before this process touches the GPU (it only counts devices, which does not initialise one).
+    """`--gpus N` without an external launcher: N fresh child processes, one per GPU (rank r on
+    GPU r // --ranks-per-gpu), started by a launcher that never imports torch nor maps the HIP
+    runtime (GPUs counted by visible_gpus; checked by launcher_selfcheck, printed on stderr).
     Rank 0's stdout (the JSON line) is relayed; the other ranks' stdout goes to stderr.  Any
     failing rank stops the others; returns the exit code."""
     import signal
     import socket
     import subprocess
     import tempfile
-    n = args.gpus
-    if args.device >= 0:
-        if args.dist_backend == "nccl":
-            log(f"bench.py: --gpus {n} --device {args.device} puts every rank on one GPU, which "
-                f"RCCL cannot do; use --dist-backend gloo for a same-GPU rehearsal")
-            return 2
-    else:
-        import torch
-        have = torch.cuda.device_count()
-        if have < n:
-            log(f"bench.py: --gpus {n} needs {n} visible GPUs, {have} visible "
-                f"(one rank per GPU; --device D --dist-backend gloo rehearses on one GPU)")
-            return 2
+    n, rpg = args.gpus, args.ranks_per_gpu
+    if rpg < 1:
+        log("bench.py: --ranks-per-gpu must be >= 1")
+        return 2
+    if (args.device >= 0 or rpg > 1) and args.dist_backend == "nccl":
+        log(f"bench.py: --gpus {n} with --device / --ranks-per-gpu > 1 puts several ranks on one "
+            f"GPU, which RCCL cannot do; use --dist-backend gloo for a same-GPU rehearsal")
+        return 2
+    have, source = visible_gpus()
+    need = 1 if args.device >= 0 else -(-n // rpg)
+    if have < need:
+        log(f"bench.py: --gpus {n} needs {need} visible GPUs, {have} visible ({source}; one rank "
+            f"per GPU; --ranks-per-gpu R --dist-backend gloo rehearses R ranks per GPU)")
+        return 2
     with socket.socket() as s_:
         s_.bind(("127.0.0.1", 0))
         port = s_.getsockname()[1]
     out0 = tempfile.TemporaryFile(mode="w+")
     procs = []
-
-    def die_with_parent():  # in the child, before exec: SIGTERM when the launcher dies
-        import ctypes
-        try:
-            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
-        except OSError:
-            pass
 
     def forward(signum, _frame):  # a signal to the launcher stops the ranks too
         for p in procs:
@@ -242,10 +321,14 @@ def launch_ranks(args, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), SFM_BENCH_LAUNCHER="self")
+                   MASTER_PORT=str(port), SFM_BENCH_LAUNCHER="self",
+                   SFM_BENCH_PARENT_PID=str(os.getpid()),
+                   SFM_BENCH_DEVICE=str(args.device if args.device >= 0 else r // rpg))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv,
-                                      env=env, stdout=out0 if r == 0 else sys.stderr,
-                                      preexec_fn=die_with_parent))
+                                      env=env, stdout=out0 if r == 0 else sys.stderr))
+    log("bench.py launcher-selfcheck " + json.dumps(dict(
+        launcher_selfcheck(), stage="spawned", visible_gpus=have, count_source=source,
+        ranks=n, ranks_per_gpu=rpg)))
     rc = 0
     live = list(range(n))
     while live:
@@ -262,6 +345,7 @@ def launch_ranks(args, argv):
         time.sleep(0.05)
     for p in procs:
         p.wait()
+    log("bench.py launcher-selfcheck " + json.dumps(dict(launcher_selfcheck(), stage="exit")))
     out0.seek(0)
     for line in out0.read().splitlines():  # the JSON line to stdout; library chatter to stderr
         (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line + "\n")
@@ -283,6 +367,8 @@ def main(argv=None):
     else:
         world = int(env_world)
         launcher = os.environ.get("SFM_BENCH_LAUNCHER", "external")
+        if launcher == "self":
+            die_with_launcher()
         if world != args.gpus:
             log(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
             return 2
@@ -292,6 +378,8 @@ def main(argv=None):
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if launcher == "self":
+        local = int(os.environ.get("SFM_BENCH_DEVICE", local))
     if args.device >= 0:
         local = args.device
     torch.cuda.set_device(local)
@@ -434,11 +522,16 @@ def pairs_main(args, world, rank, local, dist_info):
                        "algorithmic_flops_per_step": r_alg,
                        "executed_frac": r_exec,
                        "evaluations_per_step": r_evals,
+                       "executed_counts_masked_lanes": True,
                        "note": "achieved / frac count the EXECUTED work (the exact pruning skips "
                                "the rest): Sampson evaluations counted by the score waves in the "
                                "timed steps (sfm_ransac_stats) x 33 flop + 1400 flop per fitted "
                                "hypothesis; algorithmic = every hypothesis on every match "
-                               "(pairs with >= 8 matches); executed_frac = executed / algorithmic",
+                               "(pairs with >= 8 matches); executed_frac = executed / algorithmic. "
+                               "executed = ISSUED lane-slots (a score wave runs until its last "
+                               "live lane stops: lanes already pruned count as masked slots; plus "
+                               "the final kernel's M per pair), so frac is an issue-slot figure, "
+                               "an upper bound on useful-work utilisation",
                        "practical_peak": PRACTICAL_F32_VALU_TFLOPS,
                        "frac_of_practical":
                            r_alg * r_exec / (ransac_ms * 1e-3) / 1e12 / PRACTICAL_F32_VALU_TFLOPS}},
@@ -461,10 +554,16 @@ def pairs_main(args, world, rank, local, dist_info):
             result["cpu_baseline"] = cpu_baseline(scene, pairs, lo, hi, graph, run.gb,
                                                   args.cpu_seconds, args.n_hyp)
             result["cfg1_cpu"] = cfg1_timing()
+        del run, graph   # the side legs below build their own buffers
+        torch.cuda.empty_cache()
         if args.config != "cfg3" and not args.no_cfg3:
-            del run, graph
-            torch.cuda.empty_cache()
             result["cfg3"] = cfg3_side(args.n_hyp, args.chunk)
+        if args.config == "cfg4" and not args.no_local:
+            torch.cuda.empty_cache()
+            try:   # a side leg: its failure is recorded, the cfg4 line stands
+                result["cfg4_local"] = cfg4_local_side(n_img, k, args.n_hyp, args.chunk)
+            except Exception as e:  # noqa: BLE001
+                result["cfg4_local"] = {"error": f"{type(e).__name__}: {e}"}
         if args.config == "cfg4" and not args.no_cfg5:
             torch.cuda.empty_cache()
             try:   # a side leg: its failure is recorded, the cfg4 line stands
@@ -473,6 +572,59 @@ def pairs_main(args, world, rank, local, dist_info):
             except Exception as e:  # noqa: BLE001
                 result["cfg5"] = {"error": f"{type(e).__name__}: {e}"}
     return result
+
+
+def local_scene(n_img, k, n_pts=None):
+    """The cfg5 scene (seeded CFG5_SEED, k1 in +-0.02, local visibility on a sphere-cap view
+    grid, ~CFG5_TRACK observations per point); returns (scene, grid)."""
+    import synth
+    n_el = max(1, int(round((n_img / 2) ** 0.5)))
+    grid = (-(-n_img // n_el), n_el, CFG5_GRID[2], CFG5_GRID[3])
+    return synth.make_scene(n_img, k, seed=CFG5_SEED, k1_range=0.02, n_pts=n_pts,
+                            window=CFG5_WINDOW, grid=grid, track_len=CFG5_TRACK), grid
+
+
+def cfg4_local_side(n_img, k, n_hyp, chunk, steps=3, warmup=1):
+    """the cfg4 step (all pairs of n_img x k 128-D, L2 mutual + ratio 4/5,
+    RANSAC n_hyp, seed 42) on the local-visibility scene of cfg5, where most pairs share no
+    points and fail verification (code/pipeline.py:42 drops them) — the realistic-overlap
+    counterpart of the headline's arc scene, on which every pair verifies."""
+    import numpy as np
+    import torch
+    import synth
+    scene, _ = local_scene(n_img, k)
+    pairs = synth.unordered_pairs(n_img)
+    run = Runner(scene, pairs, 0, len(pairs), chunk, n_hyp, torch.cuda.current_device())
+    run.ctx.ransac_stats(enable=True)
+    for _ in range(warmup):
+        run.step()
+    torch.cuda.synchronize()
+    run.ctx.ransac_stats(enable=True, read=True)
+    evs = [run.events() for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s_ in range(steps):
+        graph = run.step(None, evs[s_])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    r_alg, r_exec, r_evals = ransac_flops(run.ctx.ransac_stats(enable=False, read=True), n_hyp,
+                                          steps)
+    st = [Runner.stage_ms(e) for e in evs]
+    m = float(np.mean([x[0] for x in st]))
+    r = float(np.mean([x[1] for x in st]))
+    # verified pairs of the last step: pairs with at least one graph row
+    n_ver = int(torch.unique(graph[:, 0]).numel()) if graph.shape[0] else 0
+    tops = run.k1_ops / (m * 1e-3) / 1e12
+    return {"workload": (f"cfg4_local: all {len(pairs)} unordered pairs of the cfg5 local-"
+                         f"visibility scene ({n_img} x {k} 128-D, seed {CFG5_SEED}, ~{CFG5_TRACK} "
+                         f"views per point); same K1 / K2 settings as the headline"),
+            "value": graph.shape[0] * steps / el, "unit": "verified matches/s",
+            "ms_per_step": el / steps * 1e3, "steps": steps,
+            "verified_matches_per_step": int(graph.shape[0]),
+            "verified_pairs": n_ver, "pairs": int(len(pairs)),
+            "match_ms": m, "ransac_ms": r,
+            "k1_frac": tops / PEAK_I8_TOPS,
+            "k2_executed_frac": r_exec, "k2_evaluations_per_step": r_evals,
+            "graph_checksum": graph_checksum(torch, graph)}
 
 
 def cfg5_run(n_img, k, n_pts, steps, warmup, world, rank, local, pcg):
@@ -490,10 +642,7 @@ def cfg5_run(n_img, k, n_pts, steps, warmup, world, rank, local, pcg):
     import reconstruction as R
     import synth
     t0 = time.time()
-    n_el = max(1, int(round((n_img / 2) ** 0.5)))
-    grid = (-(-n_img // n_el), n_el, CFG5_GRID[2], CFG5_GRID[3])
-    scene = synth.make_scene(n_img, k, seed=CFG5_SEED, k1_range=0.02, n_pts=n_pts,
-                             window=CFG5_WINDOW, grid=grid, track_len=CFG5_TRACK)
+    scene, grid = local_scene(n_img, k, n_pts)
     n_pts = len(scene["pts"])
     intr = np.c_[scene["cams"][:, 6:8], scene["pp"]]
     log(f"[rank {rank}] cfg5 scene {n_img} x {k}, {n_pts} points (gen {time.time() - t0:.1f}s)")

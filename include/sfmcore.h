@@ -144,6 +144,12 @@ int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, int32_t k_m
  * the exact pruning did not skip.
  */
 int sfm_ransac_stats(sfm_ctx* ctx, int32_t enable, uint64_t* out);
+/* Diagnostic companion of sfm_ransac_stats: the last counted sfm_ransac_f_batch{,_f64} batch's
+ * per-wave counts (host out [n_pairs][n_hyp / 64] u32: matches the score wave scored past the
+ * preview; entries of pairs with < 8 matches are undefined).  n_pairs / n_hyp must equal that
+ * batch's; no other sfm_* call on ctx in between (the counts live in its workspace).
+ * Synchronises the stream.  executed = Σ_{M>=8} n_hyp·min(128, M) + 64·Σ_w out[p][w] + M. */
+int sfm_ransac_wave_stops(sfm_ctx* ctx, int32_t n_pairs, int32_t n_hyp, uint32_t* out);
 
 /* ---- verified match graph -------------------------------------------------------------------
  * Replaces the pair_matches list of code/pipeline.py:42-47 (Pair(img_inx_1, img_inx_2, matches)

@@ -1018,8 +1018,13 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
     SFM_HIP_CHECK(hipGetLastError());
     // 0 (the zero-initialised struct) = every 8 iterations, the library default; < 0 = never
-    // (no host synchronisation: fully asynchronous, capturable in a hip graph)
-    const int poll = prm->poll == 0 ? SFM_BA_POLL_DEFAULT : prm->poll;
+    // (no host synchronisation: fully asynchronous, capturable in a hip graph).  A stream under
+    // capture never polls, whatever prm->poll says: a sfm_version-1 caller that captures with a
+    // zero-initialised struct (then "never") keeps working, with the same results.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    SFM_HIP_CHECK(hipStreamIsCapturing(st, &cap));
+    const int poll = cap != hipStreamCaptureStatusNone ? -1
+                   : prm->poll == 0 ? SFM_BA_POLL_DEFAULT : prm->poll;
     for (int k = 0; k < prm->max_iter; ++k) {
         // state->done is set by bas_pcg_point of the first iteration after convergence: once it
         // reads 1, every later iteration would exit at once, so stop enqueueing them

@@ -741,8 +741,11 @@ __global__ __launch_bounds__(256) void ransac_hyp_mask_kernel(
 }
 
 // sfm_ransac_stats: (executed, algorithmic) Sampson evaluations of a batch and its pairs with >= 8
-// matches.  executed = every hypothesis's preview (min(PV, M)) + 64 x the matches each score wave
-// scored past the preview + the final kernel's M; algorithmic = H x M.
+// matches.  executed = issued lane-slots: every hypothesis's preview (min(PV, M)) + 64 x the matches
+// each score wave scored past the preview (a wave runs until its last live lane stops, so lanes
+// already pruned count as masked slots) + the final kernel's M; algorithmic = H x M.  Identity
+// (tests/test_gpu_ransac.py, sfm_ransac_wave_stops): executed = sum over pairs with M >= 8 of
+// H min(PV, M) + 64 sum_w stop_w + M, and H min(PV, M) + M <= executed <= H M + M.
 __global__ __launch_bounds__(256) void ransac_stats_kernel(int n_pairs, int n_hyp,
                                                            const int32_t* __restrict__ match_count,
                                                            const uint32_t* __restrict__ exec_w,
@@ -884,6 +887,9 @@ static int ransac_batch(sfm_ctx* ctx, const T* kps, int32_t k_max, const int32_t
             SFM_HIP_CHECK(hipGetLastError());
             hipLaunchKernelGGL(ransac_stats_kernel, dim3(std::min((n_pairs + 3) / 4, 512)),
                                dim3(256), 0, st, n_pairs, H, match_count, exec_w, ctx->rs_acc);
+            ctx->rs_last_w = exec_w;
+            ctx->rs_last_pairs = n_pairs;
+            ctx->rs_last_hyp = H;
         }
     } else if constexpr (sizeof(T) == 4) {
         if (mode == 1)
@@ -967,6 +973,19 @@ extern "C" int sfm_ransac_counts(sfm_ctx* ctx, const float* kps, int32_t n_img, 
                            match_count, planes, H, hypG, out_hyp_mask);
         SFM_HIP_CHECK(hipGetLastError());
     }
+    return SFM_OK;
+}
+
+extern "C" int sfm_ransac_wave_stops(sfm_ctx* ctx, int32_t n_pairs, int32_t n_hyp,
+                                     uint32_t* out) {
+    SFM_REQUIRE(ctx && out, "sfm_ransac_wave_stops: ctx/out is NULL");
+    SFM_REQUIRE(ctx->rs_last_w && n_pairs == ctx->rs_last_pairs && n_hyp == ctx->rs_last_hyp,
+                "sfm_ransac_wave_stops: no counted batch of this shape (enable sfm_ransac_stats "
+                "and run sfm_ransac_f_batch first; no other call on ctx in between)");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    SFM_HIP_CHECK(hipMemcpyAsync(out, ctx->rs_last_w, (size_t)n_pairs * (n_hyp / 64) * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    SFM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return SFM_OK;
 }
 

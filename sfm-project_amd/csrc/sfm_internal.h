@@ -19,6 +19,9 @@ struct sfm_ctx {
     // algorithmic, pairs) evaluation counters; the per-wave counts live in the batch workspace
     int ransac_stats = 0;
     unsigned long long* rs_acc = nullptr;
+    // the last counted batch's per-wave counts (sfm_ransac_wave_stops): where, and its shape
+    const uint32_t* rs_last_w = nullptr;
+    int rs_last_pairs = 0, rs_last_hyp = 0;
 };
 
 namespace sfm {

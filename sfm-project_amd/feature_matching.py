@@ -250,8 +250,14 @@ _orb_cache = None
 
 
 def _image_key(im):
-    import xxhash
+    """(shape, 128-bit digest of the bytes): xxh3-128 when xxhash is importable, else hashlib's
+    blake2b-128 (slower, same role; xxhash is an optional dependency of the drop-in)."""
     a = np.ascontiguousarray(np.asarray(im, np.uint8))
+    try:
+        import xxhash
+    except ImportError:
+        import hashlib
+        return a.shape, "b2:" + hashlib.blake2b(a.data, digest_size=16).hexdigest()
     return a.shape, xxhash.xxh3_128_hexdigest(a.data)
 
 

@@ -89,6 +89,9 @@ def verify_pairs(pair_matches, keypoints, n_hyp=DEFAULT_HYPOTHESES, seed=DEFAULT
     (pixel F, unit norm) attached.  Results equal verify_pair on each pair (the RNG is keyed by the
     pair's image ids, so they depend neither on the batch nor on the chunking)."""
     import torch
+    chunk = int(chunk)
+    if chunk < 1:   # ADVICE r4: a non-positive chunk used to return no verified pair, silently
+        raise ValueError(f"verify_pairs: chunk must be >= 1, got {chunk}")
     if not pair_matches:
         return []
     pairs = np.array([[int(pr.img_inx_1), int(pr.img_inx_2)] for pr in pair_matches], np.int32)
@@ -103,7 +106,7 @@ def verify_pairs(pair_matches, keypoints, n_hyp=DEFAULT_HYPOTHESES, seed=DEFAULT
     ctx = sfmcore.context(device)
     kps_d = torch.from_numpy(kps).to(dev)
     verified = []
-    for c0 in range(0, len(pair_matches), max(int(chunk), 1)):
+    for c0 in range(0, len(pair_matches), chunk):
         prs = pair_matches[c0:c0 + chunk]
         P = len(prs)
         match = np.zeros((P, k_max, 2), np.int32)

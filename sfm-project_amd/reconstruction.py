@@ -269,6 +269,8 @@ def release_allreduce(group=None):
     g = group if group is not None else dist.group.WORLD
     for key in [k for k in _rccl_comms if k[0] is g or k[0] == g]:
         _rccl_comms.pop(key).close()
+    for key in [k for k in _probe_cache if k[1] is g or k[1] == g]:   # probes of a dead comm
+        del _probe_cache[key]
 
 
 # ---- shard / replicate rule for the multi-GPU PCG --------------------------------
@@ -293,15 +295,17 @@ def probe_collectives(allreduce, n_cam: int, device, group=None, reps: int = 20,
     """Measured (latency of one in-place all-reduce of 8·n_cam doubles in µs, all-reduce bus
     bandwidth in B/s) on this group: `reps` back-to-back calls of each size, timed on the
     current stream, then averaged over the ranks with the same all-reduce (every rank gets the
-    same numbers, so the branch decision is collective-safe).  Cached per (allreduce, n_cam)."""
+    same numbers, so the branch decision is collective-safe).  Cached per (backend, group, device,
+    collective path, n_cam): a key every rank computes identically (not an object id, which a
+    rank may or may not see reused), so all ranks hit or miss the cache together."""
     import time
     import torch
     import torch.distributed as dist
-    key = (id(getattr(allreduce, "comm", allreduce)), n_cam)
+    dev = torch.device("cuda", device) if not isinstance(device, torch.device) else device
+    key = _probe_key(allreduce, n_cam, dev, group)
     if key in _probe_cache:
         return _probe_cache[key]
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    dev = torch.device("cuda", device) if not isinstance(device, torch.device) else device
     small = torch.zeros(8 * n_cam, dtype=torch.float64, device=dev)
     big = torch.zeros(int(big_mb * 2 ** 20) // 8, dtype=torch.float64, device=dev)
     out = []
@@ -323,6 +327,14 @@ def probe_collectives(allreduce, n_cam: int, device, group=None, reps: int = 20,
     lat_us, busbw = (float(v) / world for v in m.cpu().tolist())
     _probe_cache[key] = (lat_us, busbw)
     return lat_us, busbw
+
+
+def _probe_key(allreduce, n_cam, dev, group=None):
+    import torch.distributed as dist
+    init = dist.is_available() and dist.is_initialized()
+    g = group if group is not None else (dist.group.WORLD if init else None)
+    return (dist.get_backend(group) if init else None, g, str(dev),
+            "rccl-direct" if hasattr(allreduce, "comm") else "torch", int(n_cam))
 
 
 def pcg_rule(n_obs: int, n_pt: int, n_cam: int, world: int, allreduce_us: float,

@@ -26,7 +26,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
             "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
             "sfm_ransac_stats", "sfm_ransac_f_batch_f64", "sfm_graph_rows_packed",
-            "sfm_graph_expand", "sfm_match_batch_both"]
+            "sfm_graph_expand", "sfm_match_batch_both", "sfm_ransac_wave_stops"]
 
 
 class SfmCoreError(RuntimeError):
@@ -100,6 +100,7 @@ def load_library(path: str = LIB_PATH):
         L.sfm_ransac_counts.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp,
                                         C.POINTER(RansacParams), vp, vp, vp, vp]
         L.sfm_ransac_stats.argtypes = [vp, i32, vp]
+        L.sfm_ransac_wave_stops.argtypes = [vp, i32, i32, vp]
         L.sfm_ba_jtj.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp,
                                  vp, vp, vp, vp, vp, vp]
         L.sfm_ba_solve.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -310,6 +311,15 @@ class Context:
         self._bind_stream()
         _check(self.lib.sfm_ransac_stats(self.handle, 1 if enable else 0, out if read else None))
         return (int(out[0]), int(out[1]), int(out[2])) if read else None
+
+    def ransac_wave_stops(self, n_pairs, n_hyp):
+        """sfm_ransac_wave_stops: [n_pairs, n_hyp / 64] u32 numpy array, the last counted batch's
+        matches scored past the preview per score wave (synchronises the stream)."""
+        out = np.zeros((n_pairs, n_hyp // 64), np.uint32)
+        self._bind_stream()
+        _check(self.lib.sfm_ransac_wave_stops(self.handle, int(n_pairs), int(n_hyp),
+                                              out.ctypes.data_as(C.c_void_p)))
+        return out
 
     # ---- verified match graph --------------------------------------------------------------
     def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15,

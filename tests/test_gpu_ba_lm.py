@@ -13,6 +13,7 @@ import pytest
 import ba_lm as L
 import oracle as O
 import reconstruction as R
+import sfmcore
 import synth
 
 pytestmark = pytest.mark.gpu
@@ -237,3 +238,45 @@ def test_solve_async_default_under_graph_capture():
     torch.cuda.synchronize()
     for a, b, c in zip(out, eager, polled):
         assert torch.equal(a, b) and torch.equal(b, c)
+
+
+def test_c_abi_capture_with_zero_initialised_poll():
+    """a C caller that captures sfm_ba_solve in a HIP graph with a zero-initialised
+    sfm_ba_solve_params (sfm_version 1: poll 0 = never; version 2: poll 0 = every 8) must not hit
+    a host synchronisation inside the capture: the library never polls on a capturing stream.
+    Called through the raw ctypes binding (poll 0 and poll -1 structs); the replays equal the
+    eager polled solve bit for bit."""
+    import ctypes as C
+    import torch
+    prob = synth.make_ba_problem(10, 300, obs_per_pt=4, seed=22, perturb=2e-3)
+    P, _, _, lin = _problem(prob)
+    ref = [t.clone() for t in P.solve(lin, 1e-3, max_iter=60, tol=1e-10, poll=8)]
+    ctx = P.ctx
+    p = lambda t: C.c_void_p(t.data_ptr())
+    s = torch.cuda.Stream()
+    for poll in (0, -1):
+        out = [torch.empty_like(t) for t in ref]
+        prm = sfmcore.BaSolveParams(1e-3, 1e-10, 60, poll)
+
+        def call():
+            ctx._bind_stream()
+            rc = ctx.lib.sfm_ba_solve(ctx.handle, ref[0].shape[0], ref[1].shape[0],
+                                      P.cam_idx.shape[0], p(P.cam_idx), p(P.pt_idx), p(P.pt_ptr),
+                                      p(P.cam_ptr), p(P.cam_obs), p(lin["U"]), p(lin["V"]),
+                                      p(lin["W"]), p(lin["gc"]), p(lin["gp"]), C.byref(prm),
+                                      p(out[0]), p(out[1]), p(out[2]))
+            assert rc == 0, ctx.lib.sfm_last_error()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            call()                      # eager on the capture stream (polls: poll 0 = every 8)
+        torch.cuda.synchronize()
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b)
+            a.zero_()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            call()
+        g.replay()
+        torch.cuda.synchronize()
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b), poll

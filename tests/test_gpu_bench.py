@@ -88,17 +88,27 @@ def _bench(args, launcher=None, timeout=600):
 
 
 def test_bench_self_launch_two_ranks():
-    """`bench.py --gpus 2` with NO torch.distributed.run starts its two ranks
-    itself (gloo rehearsal: both on GPU 0) and reports n_gpus 2 with the N = 1 graph."""
+    """`bench.py --gpus 2` with NO torch.distributed.run starts
+    its two ranks itself through the real count-then-spawn path (GPUs counted from the KFD
+    topology; --ranks-per-gpu 2 puts both gloo ranks on GPU 0 of this 1-GPU box), the launcher
+    never imports torch nor maps the HIP runtime, and the line has n_gpus 2 with the N = 1
+    graph."""
     out = _bench(["--config", "cfg3", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
-                  "--gpus", "2", "--dist-backend", "gloo", "--device", "0"])
+                  "--gpus", "2", "--dist-backend", "gloo", "--ranks-per-gpu", "2"])
     assert out.returncode == 0, out.stderr[-3000:]
+    checks = [json.loads(l.split("launcher-selfcheck", 1)[1]) for l in out.stderr.splitlines()
+              if "launcher-selfcheck" in l]
+    assert [c["stage"] for c in checks] == ["spawned", "exit"], out.stderr[-3000:]
+    for c in checks:
+        assert c["torch_imported"] is False and c["hip_runtime_mapped"] is False, c
+    assert checks[0]["count_source"] == "kfd-topology" and checks[0]["visible_gpus"] >= 1
     lines = [l for l in out.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, out.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["distributed"]["launcher"] == "self"
     assert d["distributed"]["world"] == 2 and len(d["distributed"]["per_rank"]) == 2
     assert [r["rank"] for r in d["distributed"]["per_rank"]] == [0, 1]
+    assert [r["device"] for r in d["distributed"]["per_rank"]] == [0, 0]
     assert sum(r["pairs"] for r in d["distributed"]["per_rank"]) == 1225
     assert d["verified_matches_per_step"] == 554009
     one = _bench(["--config", "cfg3", "--steps", "1", "--warmup", "1", "--no-cpu-baseline"])
@@ -149,3 +159,19 @@ def test_bench_cfg5_line_and_two_rank_rehearsal():
         assert c2["registered"] == c1["registered"]
         assert abs(c2["points"] - c1["points"]) <= max(2, c1["points"] // 1000)
         assert abs(c2["median_reproj_px"] - c1["median_reproj_px"]) <= 1e-6 * c1["median_reproj_px"]
+
+
+def test_bench_cfg4_local_leg():
+    """the N = 1 cfg4 line carries `cfg4_local`, the same step on the cfg5
+    local-visibility scene (most pairs fail verification, as in a real capture); small shape."""
+    out = _bench(["--config", "cfg4", "--n-img", "24", "--k", "1024", "--steps", "1",
+                  "--warmup", "1", "--no-cpu-baseline", "--no-cfg3", "--no-cfg5", "--no-fp64"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.strip()][-1])
+    loc = d["cfg4_local"]
+    assert "error" not in loc, loc
+    assert loc["pairs"] == 276 and 0 < loc["verified_pairs"] < loc["pairs"]
+    assert loc["verified_matches_per_step"] < d["verified_matches_per_step"]
+    assert abs(loc["value"] - loc["verified_matches_per_step"] * 1e3 / loc["ms_per_step"]) \
+        <= 1e-6 * loc["value"]
+    assert 0 < loc["k2_executed_frac"] <= 1.0 and loc["match_ms"] > 0

@@ -254,3 +254,37 @@ def test_ransac_f64_small_pairs_bit_exact(ctx):
             np.testing.assert_array_equal(rs["mask"][p, :m], o["mask"])
             assert rs["F"][p].view(np.uint64).tolist() == o["F"].view(np.uint64).tolist()
             assert rs["norm"][p].view(np.uint64).tolist() == o["norm"].view(np.uint64).tolist()
+
+
+def test_ransac_stats_identity(ctx):
+    """K2's `executed` counter is issued lane-slots, and it satisfies an exact
+    identity with the per-wave counts read back separately (sfm_ransac_wave_stops):
+    executed = sum over pairs with M >= 8 of H min(PV, M) + 64 sum_w stop_w + M;
+    algorithmic = H sum M; H min(PV, M) + M <= executed <= H M + M per batch.  Pairs with M < 8
+    and M <= PV (no wave scores past the preview) are in the batch."""
+    import torch
+    PV, H = 128, 1024
+    s = synth.make_scene(7, 2048, seed=5)
+    pairs = synth.unordered_pairs(7)
+    desc = torch.from_numpy(s["desc"]).cuda()
+    kps = torch.from_numpy(s["kps"]).cuda()
+    pr = torch.from_numpy(np.ascontiguousarray(pairs, np.int32)).cuda()
+    cnt, mt, _ = ctx.match_batch(desc, torch.from_numpy(s["n_kp"]).cuda(), pr, ratio=(4, 5))
+    cnt[0], cnt[1], cnt[2] = 5, 100, 128          # M < 8, M < PV, M == PV
+    ctx.ransac_stats(enable=True, read=True)      # reset
+    out = ctx.ransac_batch(kps, pr, cnt, mt, n_hyp=H, seed=42, thr=1.0)
+    stops = ctx.ransac_wave_stops(len(pairs), H).astype(np.int64)
+    ex, al, npairs = ctx.ransac_stats(enable=False, read=True)
+    M = cnt.cpu().numpy().astype(np.int64)
+    sel = M >= 8
+    assert sel.sum() == npairs == len(pairs) - 1
+    assert al == H * M[sel].sum()
+    assert (stops[sel] <= np.maximum(M[sel] - PV, 0)[:, None]).all()
+    assert (stops[1:3] == 0).all()
+    exp = (H * np.minimum(PV, M[sel]) + 64 * stops[sel].sum(1) + M[sel]).sum()
+    assert ex == exp
+    assert (H * np.minimum(PV, M[sel]) + M[sel]).sum() <= ex <= (H * M[sel] + M[sel]).sum()
+    # the counters do not change the results
+    ref = ctx.ransac_batch(kps, pr, cnt, mt, n_hyp=H, seed=42, thr=1.0)
+    for k in ("inl_count", "best_h", "mask"):
+        assert torch.equal(out[k], ref[k])

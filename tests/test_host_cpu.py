@@ -318,3 +318,30 @@ def test_orb_cache_extracts_each_distinct_image_once(monkeypatch):
     monkeypatch.setattr(fm, "ORB_CACHE_SIZE", 0)
     fm._orb_cached([c])
     assert calls == [2, 1, 2, 1, 1]
+
+
+def test_verify_pairs_rejects_non_positive_chunk():
+    """chunk <= 0 raises (it used to give empty slices: no verified pair, silently)."""
+    import geometric_verification as gv
+    for c in (0, -3):
+        with pytest.raises(ValueError, match="chunk must be >= 1"):
+            gv.verify_pairs([object()], [np.zeros((1, 2))], chunk=c)
+
+
+def test_image_key_without_xxhash(monkeypatch):
+    """the ORB cache key falls back to blake2b-128 when xxhash is not importable; equal
+    images give equal keys, a changed pixel a different key."""
+    import builtins
+    import feature_matching as fm
+    real = builtins.__import__
+
+    def no_xxhash(name, *a, **k):
+        if name == "xxhash":
+            raise ImportError("no xxhash")
+        return real(name, *a, **k)
+    monkeypatch.setattr(builtins, "__import__", no_xxhash)
+    im = np.arange(64, dtype=np.uint8).reshape(8, 8)
+    k1, k2 = fm._image_key(im), fm._image_key(im.copy())
+    im2 = im.copy()
+    im2[3, 3] ^= 1
+    assert k1 == k2 and k1[1].startswith("b2:") and fm._image_key(im2) != k1
