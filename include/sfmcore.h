@@ -277,6 +277,39 @@ int sfm_ba_cost(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* p
 int sfm_ba_update(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* dc, int32_t n_pt,
                   const double* pts, const double* dp, double* cams_out, double* pts_out);
 
+/* Sharding-invariant sums (chunk mode, sfm_version 3).  The points of the WHOLE problem are cut
+ * into n_total fixed chunks (contiguous point ranges; a rank's shard is a run of whole chunks), and
+ * every sum that runs over points or observations into a camera-space or scalar value — U / g_c
+ * and the cost of sfm_ba_jtj, sfm_ba_cost, the Schur diagonal blocks and b of the solve set-up,
+ * the CG product Σ_o u_o, the LM model terms — is computed per chunk (an order that depends only
+ * on the chunk's own observations) and the chunk partials are combined by ONE canonical pairwise
+ * tree over all n_total chunks: while n > 1, a[i] = a[2i] + a[2i+1] (i < n/2), an odd last
+ * element is carried, n = ceil(n/2).  Results are then bit-identical for every split of the
+ * chunks over ranks, the single process included.
+ *   sfm_ba_set_chunks(ctx, n_chunk, chunk_pt, chunk_obs, n_total, cam_bounds): the next BA calls
+ *   on ctx work on a problem holding n_chunk of the chunks; chunk_pt / chunk_obs (host, n_chunk +
+ *   1) are their LOCAL point offsets and the matching observation offsets (pt_ptr[chunk_pt[k]];
+ *   chunk_pt[0] = 0, chunk_pt[n_chunk] = n_pt, non-decreasing; empty chunks allowed); cam_bounds
+ *   (device, [n_cam][n_chunk + 1] i32, caller-owned) are the positions in cam_obs where each
+ *   camera's observation list crosses those offsets (the list is ascending, so each chunk's part
+ *   is contiguous): cam_bounds[c][0] = cam_ptr[c], cam_bounds[c][n_chunk] = cam_ptr[c + 1].
+ *   n_total = 0: the problem is the whole one (n_chunk = n_total chunks), every result is final.
+ *   n_total > 0: a shard (export form): sfm_ba_jtj writes U as [n_chunk][n_cam][8][8], gc as
+ *   [n_chunk][n_cam][8] and cost as [n_chunk] (chunk partials, combined by the caller after
+ *   gathering every rank's chunks in chunk order: sfm_ba_chunk_tree), sfm_ba_cost writes cost
+ *   [n_chunk]; the sharded solve's stages write chunk partials to comm and the stages after the
+ *   exchange read ALL n_total chunks' partials in chunk order: SETUP -> comm [n_chunk][n_cam][44],
+ *   gathered [n_total][n_cam][44] -> SETUP_FINISH; ITER -> [n_chunk][n_cam][8], gathered ->
+ *   ITER_FINISH; BACKSUB -> [n_chunk][2], gathered -> MODEL (an all-GATHER instead of the
+ *   all-reduce; comm >= n_total * 44 * n_cam doubles).
+ *   n_chunk = 0 switches chunk mode off (the default: the round-4 sums).  1 <= n_chunk <= 16.
+ *   sfm_ba_chunk_tree(ctx, n_total, n, parts, out): out[i] = canonical tree over k of
+ *   parts[k * n + i] (device arrays), i < n — the combine the library applies itself. */
+#define SFM_BA_MAX_CHUNKS 16
+int sfm_ba_set_chunks(sfm_ctx* ctx, int32_t n_chunk, const int32_t* chunk_pt,
+                      const int32_t* chunk_obs, int32_t n_total, const int32_t* cam_bounds);
+int sfm_ba_chunk_tree(sfm_ctx* ctx, int32_t n_total, int64_t n, const double* parts, double* out);
+
 /* ---- feature tracks ----------------------------------------------------------------------------
  * the verified match graph (sfm_graph_rows) -> tracks, the input of
  * triangulation and bundle adjustment.  Nodes are (image, keypoint), node = img_base[image] +

@@ -129,12 +129,23 @@ __device__ __forceinline__ void obs_block(
     const double* __restrict__ uv, double loss_s, double* __restrict__ W,
     double* __restrict__ res, double* __restrict__ V, double* __restrict__ gp,
     double* __restrict__ seg, int32_t* __restrict__ seg_pt, double* __restrict__ cost_blk,
-    double* __restrict__ lds) {
+    double* __restrict__ lds, int nck, const sfm::ChunkOff& cobs, const sfm::ChunkOff& vst) {
     __shared__ double cred[4];
-    const int o = ob * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const int wv = o >> 6;  // global wave index (blocks are whole waves)
-    const bool valid = o < n_obs;
+    // Chunk mode (nck > 0): waves tile a virtual index space in which every chunk starts at a
+    // multiple of 64 (vst: the chunks' virtual starts), so where a point's observations are cut
+    // into waves — and with it the association of its V_p / g_p sums — depends only on its chunk.
+    const int vo = ob * 256 + threadIdx.x;
+    const int wv = vo >> 6;  // wave index (blocks are whole waves)
+    int o = vo, wfirst = wv << 6, wend = n_obs;
+    if (nck > 0) {
+        int k = 0;
+        while (k + 1 < nck && vo >= vst.v[k + 1]) ++k;
+        o = cobs.v[k] + (vo - vst.v[k]);
+        wfirst = cobs.v[k] + ((wv << 6) - vst.v[k]);
+        wend = vo < vst.v[nck] ? cobs.v[k + 1] : 0;
+    }
+    const bool valid = o < wend;
     double* wimg = lds + (threadIdx.x >> 6) * OBS_LDS;
     int p = -1;
     double t[NV];
@@ -162,9 +173,9 @@ __device__ __forceinline__ void obs_block(
         for (int i = 0; i < 3; ++i) t[6 + i] = L.w * (L.Jp[i] * L.r[0] + L.Jp[3 + i] * L.r[1]);
         t[9] = 0.5 * L.rho;
     }
-    {   // the wave's W block: 64 rows x 24 doubles, contiguous in W from observation wv*64
-        const int nrow = min(64, n_obs - (wv << 6));
-        double2* Wo = (double2*)(W + 24 * ((size_t)wv << 6));
+    {   // the wave's W block: 64 rows x 24 doubles, contiguous in W from observation wfirst
+        const int nrow = min(64, wend - wfirst);
+        double2* Wo = (double2*)(W + 24 * (size_t)max(wfirst, 0));
         double* wr = wimg + lane * WROW;
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
@@ -211,10 +222,9 @@ __device__ __forceinline__ void obs_block(
     }
     const int pn = __shfl_down(p, 1, 64);
     const bool seg_end = valid && (lane == 63 || pn != p);
-    const int wbase = wv << 6;
     int o_first = 0, o_last = 0;
     if (seg_end) { o_first = pt_ptr[p]; o_last = pt_ptr[p + 1] - 1; }
-    const bool starts_here = o_first >= wbase, ends_here = o_last == o;
+    const bool starts_here = o_first >= wfirst, ends_here = o_last == o;
     // the wave's tail record id (read by the fix-up) is always written: no memset needed
     if (lane == 63) seg_pt[wv * 2 + 1] = (seg_end && starts_here && !ends_here) ? p : -1;
     if (!seg_end) return;
@@ -279,7 +289,7 @@ __device__ __forceinline__ void camera_wave(
     const double* __restrict__ pts, const int32_t* __restrict__ pt_idx,
     const double* __restrict__ uv, const int32_t* __restrict__ cam_ptr,
     const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
-    double* __restrict__ U, double* __restrict__ gc) {
+    double* __restrict__ U, double* __restrict__ gc, const int32_t* __restrict__ cb) {
     const int lane = threadIdx.x & 63;
     const int hw = cw % CH;  // which NUH of the 44 sums this wave accumulates (wave-uniform)
     cw /= CH;
@@ -294,9 +304,16 @@ __device__ __forceinline__ void camera_wave(
 #else
     rotmat(cam[0], cam[1], cam[2], R);
 #endif
-    const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
-    const int len = (c1 - c0 + splits - 1) / splits;
-    const int e0 = c0 + s * len, e1 = min(c1, e0 + len);
+    int e0, e1;
+    if (cb) {   // chunk mode: split s = the camera's observations in chunk s (sfm_ba_set_chunks)
+        e0 = cb[(size_t)c * (splits + 1) + s];
+        e1 = cb[(size_t)c * (splits + 1) + s + 1];
+    } else {
+        const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
+        const int len = (c1 - c0 + splits - 1) / splits;
+        e0 = c0 + s * len;
+        e1 = min(c1, e0 + len);
+    }
     // CAM_MLP observations per step: the dependent gathers (cam_obs -> pt_idx -> point, uv) of
     // all of them are issued before any is used (memory-level parallelism; latency-bound waves)
     for (int e = e0 + lane; e < e1; e += CAM_MLP * 64) {
@@ -353,7 +370,7 @@ __device__ __forceinline__ void camera_wave(
 #endif
     if (lane != 0) return;
     const int t0 = CH == 1 ? 0 : hw * NUH;  // sum index of acc[0]
-    if (splits > 1) {
+    if (splits > 1 || cb) {
         double* o = part + ((size_t)c * splits + s) * NU + t0;
 #pragma unroll
         for (int i = 0; i < NR; ++i) o[i] = acc[i];
@@ -383,17 +400,18 @@ __global__ __launch_bounds__(256) BA_JTJ_ATTR void ba_jtj_kernel(
     int splits, double* __restrict__ part, double* __restrict__ U, double* __restrict__ gc,
     double* __restrict__ W, double* __restrict__ res, double* __restrict__ V,
     double* __restrict__ gp, double* __restrict__ seg, int32_t* __restrict__ seg_pt,
-    double* __restrict__ cost_blk) {
+    double* __restrict__ cost_blk, const int32_t* __restrict__ cb, int nck, sfm::ChunkOff cobs,
+    sfm::ChunkOff vst) {
     __shared__ double lds[4 * OBS_LDS];
     const int b = blockIdx.x;
     if (b < n_camb) {
         const int cw = b * 4 + (threadIdx.x >> 6);
         if (cw < n_camw)
             camera_wave(cw, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U,
-                        gc);
+                        gc, cb);
     } else {
         obs_block(b - n_camb, n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res,
-                  V, gp, seg, seg_pt, cost_blk, lds);
+                  V, gp, seg, seg_pt, cost_blk, lds, nck, cobs, vst);
     }
 }
 
@@ -406,7 +424,8 @@ __global__ __launch_bounds__(256) void ba_cam_kernel(
     double* __restrict__ U, double* __restrict__ gc) {
     const int cw = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cw < n_camw)
-        camera_wave(cw, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U, gc);
+        camera_wave(cw, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U, gc,
+                    nullptr);
 }
 __global__ __launch_bounds__(256) void ba_obs_kernel(
     int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
@@ -416,8 +435,9 @@ __global__ __launch_bounds__(256) void ba_obs_kernel(
     double* __restrict__ V, double* __restrict__ gp, double* __restrict__ seg,
     int32_t* __restrict__ seg_pt, double* __restrict__ cost_blk) {
     __shared__ double lds[4 * OBS_LDS];
+    sfm::ChunkOff none{};
     obs_block(blockIdx.x, n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res, V, gp,
-              seg, seg_pt, cost_blk, lds);
+              seg, seg_pt, cost_blk, lds, 0, none, none);
 }
 #endif
 
@@ -425,13 +445,16 @@ __device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
                              const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
                              const int32_t* __restrict__ seg_pt, double* __restrict__ V,
                              double* __restrict__ gp, const double* __restrict__ cost_blk,
-                             double* __restrict__ cost);
+                             double* __restrict__ cost, int nck, const sfm::ChunkOff& cobs,
+                             const sfm::ChunkOff& vst);
 
 __global__ __launch_bounds__(256) void ba_finish_kernel(
     int n_wave, int n_blk, int n_pt, const int32_t* __restrict__ pt_ptr,
     const double* __restrict__ seg, const int32_t* __restrict__ seg_pt, double* __restrict__ V,
-    double* __restrict__ gp, const double* __restrict__ cost_blk, double* __restrict__ cost) {
-    finish_block(blockIdx.x, n_wave, n_blk, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost);
+    double* __restrict__ gp, const double* __restrict__ cost_blk, double* __restrict__ cost,
+    int nck, sfm::ChunkOff cobs, sfm::ChunkOff vst) {
+    finish_block(blockIdx.x, n_wave, n_blk, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost, nck,
+                 cobs, vst);
 }
 
 // Finish work (256-thread block fb): points spanning waves (the point whose tail record wave g
@@ -442,7 +465,8 @@ __device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
                              const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
                              const int32_t* __restrict__ seg_pt, double* __restrict__ V,
                              double* __restrict__ gp, const double* __restrict__ cost_blk,
-                             double* __restrict__ cost) {
+                             double* __restrict__ cost, int nck, const sfm::ChunkOff& cobs,
+                             const sfm::ChunkOff& vst) {
     const int tid = threadIdx.x;
     const int g = fb * 256 + tid;
     if (fb == 0) {
@@ -469,7 +493,13 @@ __device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
 #pragma unroll
             for (int k = 0; k < NV - 1; ++k) a[k] = seg[((size_t)g * 2 + 1) * NV + k];
             a[NV - 1] = 0.0;
-            const int w_last = (pt_ptr[p + 1] - 1) >> 6;
+            int vl = pt_ptr[p + 1] - 1;   // the point's last observation, as a virtual index
+            if (nck > 0) {
+                int k = 0;
+                while (k + 1 < nck && vl >= cobs.v[k + 1]) ++k;
+                vl = vst.v[k] + (vl - cobs.v[k]);
+            }
+            const int w_last = vl >> 6;
             for (int w = g + 1; w <= w_last; ++w) {
 #pragma unroll
                 for (int k = 0; k < NV - 1; ++k) a[k] += seg[((size_t)w * 2) * NV + k];
@@ -498,6 +528,40 @@ __global__ __launch_bounds__(256) void ba_final_kernel(int n_cam, int splits,
         U[64 * (size_t)c + 8 * i + j] = v;
         U[64 * (size_t)c + 8 * j + i] = v;
     }
+}
+
+// Chunk mode: thread per (camera, sum t).  exp = 0: U_c / g_c = the canonical tree over the chunk
+// partials; exp = 1 (a shard): the chunk partials themselves, U [nck][n_cam][64], gc [nck][n_cam][8].
+__global__ __launch_bounds__(256) void ba_chunk_final_kernel(int n_cam, int nck, int exp,
+                                                             const double* __restrict__ part,
+                                                             double* __restrict__ U,
+                                                             double* __restrict__ gc) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_cam * NU) return;
+    const int c = g / NU, k = g - c * NU;
+    int i = 0, j = 0;
+    if (k < 36) {
+        int t = k;
+        while (t >= 8 - i) { t -= 8 - i; ++i; }
+        j = i + t;
+    }
+    auto put = [&](int slot, double v) {
+        if (k >= 36) {
+            gc[8 * ((size_t)slot * n_cam + c) + k - 36] = v;
+        } else {
+            double* u = U + 64 * ((size_t)slot * n_cam + c);
+            u[8 * i + j] = v;
+            u[8 * j + i] = v;
+        }
+    };
+    if (exp) {
+        for (int ch = 0; ch < nck; ++ch) put(ch, part[((size_t)c * nck + ch) * NU + k]);
+        return;
+    }
+    double a[16];
+#pragma unroll
+    for (int ch = 0; ch < 16; ++ch) a[ch] = ch < nck ? part[((size_t)c * nck + ch) * NU + k] : 0.0;
+    put(0, sfm::chunk_tree16(a));
 }
 
 // ---- LM support: cost at trial parameters, parameter update -----------------
@@ -540,6 +604,90 @@ __global__ __launch_bounds__(256) void ba_cost_kernel(
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = h;
     __syncthreads();
     if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// Chunk mode: CKB blocks per chunk; block b of chunk k sums 0.5 rho over the chunk's observations
+// at chunk-relative positions (b + i CKB) 256 + tid (an order that depends only on the chunk), a
+// per-thread sum, then the wave trees and the 4 waves in order -> part[k CKB + b].
+constexpr int CKB = 64;
+__device__ __forceinline__ double half_rho(const double* __restrict__ cams, const double* __restrict__ pp,
+                                           const double* __restrict__ pts, int c, int p, double u,
+                                           double v, double loss_s) {
+    const double* cam = cams + 8 * (size_t)c;
+    double R[9];
+    rotmat(cam[0], cam[1], cam[2], R);
+    const double X0 = pts[3 * (size_t)p], X1 = pts[3 * (size_t)p + 1], X2 = pts[3 * (size_t)p + 2];
+    double P[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) P[i] = (R[3 * i] * X0 + R[3 * i + 1] * X1 + R[3 * i + 2] * X2) + cam[3 + i];
+    const double iz = 1.0 / P[2];
+    const double p0 = P[0] * iz, p1 = P[1] * iz;
+    const double f = cam[6], k1 = cam[7];
+    const double d = 1.0 + k1 * (p0 * p0 + p1 * p1);
+    const double e0 = f * d * p0 + pp[2 * (size_t)c] - u;
+    const double e1 = f * d * p1 + pp[2 * (size_t)c + 1] - v;
+    const double e = e0 * e0 + e1 * e1;
+    double rho = e;
+    if (loss_s > 0.0) {
+        const double s2 = loss_s * loss_s;
+        rho = s2 * log1p(e / s2);
+    }
+    return 0.5 * rho;
+}
+
+__global__ __launch_bounds__(256) void ba_cost_chunk_kernel(
+    sfm::ChunkOff co, const double* __restrict__ cams, const double* __restrict__ pp,
+    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
+    const int32_t* __restrict__ pt_idx, const double* __restrict__ uv, double loss_s,
+    double* __restrict__ part) {
+    __shared__ double red[4];
+    const int k = blockIdx.x / CKB, b = blockIdx.x - k * CKB;
+    const int o0 = co.v[k], o1 = co.v[k + 1];
+    double h = 0.0;
+    for (int o = o0 + b * 256 + (int)threadIdx.x; o < o1; o += CKB * 256)
+        h += half_rho(cams, pp, pts, cam_idx[o], pt_idx[o], uv[2 * (size_t)o], uv[2 * (size_t)o + 1],
+                      loss_s);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) h += __shfl_down(h, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// One wave: chunk k's cost = its CKB block partials in order (lane-strided + shuffle tree);
+// exp = 0: cost[0] = the canonical tree over the chunks; exp = 1: cost[k] per chunk.
+__global__ __launch_bounds__(64) void ba_cost_chunk_final(int nck, int exp, const double* __restrict__ part,
+                                                          double* __restrict__ cost) {
+    const int lane = threadIdx.x;
+    double a[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        double v = 0.0;
+        if (k < nck) {
+            v = part[(size_t)k * CKB + lane];   // CKB == 64: one partial per lane
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+        }
+        a[k] = v;
+    }
+    if (lane != 0) return;
+    if (exp) {
+        for (int k = 0; k < nck; ++k) cost[k] = a[k];
+        return;
+    }
+    cost[0] = sfm::chunk_tree16(a);
+}
+static_assert(CKB == 64, "ba_cost_chunk_final: one block partial per lane");
+
+__global__ __launch_bounds__(256) void ba_chunk_tree_kernel(int nck, long long n,
+                                                            const double* __restrict__ parts,
+                                                            double* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double a[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] = k < nck ? parts[(size_t)k * n + i] : 0.0;
+    out[i] = sfm::chunk_tree16(a);
 }
 
 __global__ __launch_bounds__(1024) void ba_cost_final(int n_blk, const double* __restrict__ part,
@@ -629,11 +777,16 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     SFM_REQUIRE(cost != nullptr, "sfm_ba_jtj: cost is NULL");
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
+    // chunk mode, export form: U / gc / cost hold one slot per local chunk
+    const size_t nslot = (ctx->ba_nchunk > 0 && ctx->ba_ntotal > 0) ? ctx->ba_nchunk : 1;
+    if (ctx->ba_nchunk > 0)
+        SFM_REQUIRE(ctx->ba_chunk_pt[ctx->ba_nchunk] == n_pt && ctx->ba_chunk_obs[ctx->ba_nchunk] == n_obs,
+                    "sfm_ba_jtj: chunk offsets do not match n_pt / n_obs");
     if (n_pt == 0 || n_cam == 0) {
-        SFM_HIP_CHECK(hipMemsetAsync(cost, 0, sizeof(double), st));
+        SFM_HIP_CHECK(hipMemsetAsync(cost, 0, sizeof(double) * nslot, st));
         if (n_cam > 0) {
-            SFM_HIP_CHECK(hipMemsetAsync(U, 0, sizeof(double) * 64 * n_cam, st));
-            SFM_HIP_CHECK(hipMemsetAsync(gc, 0, sizeof(double) * 8 * n_cam, st));
+            SFM_HIP_CHECK(hipMemsetAsync(U, 0, sizeof(double) * 64 * n_cam * nslot, st));
+            SFM_HIP_CHECK(hipMemsetAsync(gc, 0, sizeof(double) * 8 * n_cam * nslot, st));
         }
         if (n_pt > 0) {
             SFM_HIP_CHECK(hipMemsetAsync(V, 0, sizeof(double) * 9 * n_pt, st));
@@ -644,16 +797,35 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     SFM_REQUIRE(cams && pp && pts && cam_idx && pt_idx && uv && pt_ptr && cam_ptr && cam_obs && U &&
                     V && W && gc && gp && res,
                 "sfm_ba_jtj: NULL array");
+    // chunk mode: the observation waves tile a virtual index space in which every chunk starts at
+    // a multiple of 64 (obs_block); cobs / vst = the chunks' real / virtual starts
+    sfm::ChunkOff cobs{}, vst{};
+    int n_vobs = n_obs;
+    if (ctx->ba_nchunk > 0) {
+        const int nck = ctx->ba_nchunk;
+        vst.v[0] = 0;
+        for (int k = 0; k < nck; ++k) {
+            cobs.v[k] = ctx->ba_chunk_obs[k];
+            vst.v[k + 1] = vst.v[k] + ((ctx->ba_chunk_obs[k + 1] - ctx->ba_chunk_obs[k] + 63) & ~63);
+        }
+        cobs.v[nck] = ctx->ba_chunk_obs[nck];
+        n_vobs = vst.v[nck];
+    }
     // workspace: segment records (2 per wave) | their point ids | cost per block | camera partials
-    const int n_wave = (n_obs + 63) / 64;
-    const int n_obsb = (n_obs + 255) / 256;
-    // few cameras: split each camera's observations so the camera waves still fill the chip
-    const int splits = std::max(1, std::min(16, (SPLIT_TARGET + n_cam - 1) / n_cam));
+    const int n_wave = (n_vobs + 63) / 64;
+    const int n_obsb = (n_vobs + 255) / 256;
+    // few cameras: split each camera's observations so the camera waves still fill the chip;
+    // chunk mode: one split per chunk (sfm_ba_set_chunks)
+    const bool ck = ctx->ba_nchunk > 0;
+    const int splits = ck ? ctx->ba_nchunk
+                          : std::max(1, std::min(16, (SPLIT_TARGET + n_cam - 1) / n_cam));
+    SFM_REQUIRE(!ck || ctx->ba_cam_bounds, "sfm_ba_jtj: chunk mode without cam_bounds");
     const size_t sb = sfm::align_up(sizeof(double) * NV * 2 * (size_t)std::max(n_wave, 1), 256);
     const size_t ib = sfm::align_up(sizeof(int32_t) * 2 * (size_t)std::max(n_wave, 1), 256);
     const size_t cb = sfm::align_up(sizeof(double) * (size_t)std::max(n_obsb, 1), 256);
-    const size_t pb = sizeof(double) * NU * (size_t)n_cam * splits;
-    char* ws = (char*)sfm::workspace(ctx, sb + ib + cb + pb + 1024);
+    const size_t pb = sfm::align_up(sizeof(double) * NU * (size_t)n_cam * splits, 256);
+    const size_t kb = ck ? sizeof(double) * CKB * ctx->ba_nchunk : 0;   // chunk cost partials
+    char* ws = (char*)sfm::workspace(ctx, sb + ib + cb + pb + kb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     double* seg = (double*)ws;
     int32_t* seg_pt = (int32_t*)(ws + sb);
@@ -677,14 +849,30 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
 #else
     hipLaunchKernelGGL(ba_jtj_kernel, dim3(n_camb + n_ob_launch), dim3(256), 0, st, n_camb, n_camw,
                        n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, cam_ptr, cam_obs, loss_s,
-                       splits, part, U, gc, W, res, V, gp, seg, seg_pt, cost_blk);
+                       splits, part, U, gc, W, res, V, gp, seg, seg_pt, cost_blk,
+                       ck ? ctx->ba_cam_bounds : nullptr, ctx->ba_nchunk, cobs, vst);
 #endif
     SFM_HIP_CHECK(hipGetLastError());
     const int nw = n_obs > 0 ? n_wave : 0;
     const int n_fin = std::max(std::max((nw + 255) / 256, (n_pt + 255) / 256), 1);
     hipLaunchKernelGGL(ba_finish_kernel, dim3(n_fin), dim3(256), 0, st, nw, n_obs > 0 ? n_obsb : 0,
-                       n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost);
+                       n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost, ctx->ba_nchunk, cobs, vst);
     SFM_HIP_CHECK(hipGetLastError());
+    if (ck) {   // U / g_c and the cost from the chunk partials (tree, or exported for the caller)
+        const int exp = ctx->ba_ntotal > 0 ? 1 : 0;
+        hipLaunchKernelGGL(ba_chunk_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, st,
+                           n_cam, splits, exp, part, U, gc);
+        SFM_HIP_CHECK(hipGetLastError());
+        double* kpart = (double*)(ws + sb + ib + cb + pb);
+        sfm::ChunkOff co;
+        for (int k = 0; k <= splits; ++k) co.v[k] = ctx->ba_chunk_obs[k];
+        hipLaunchKernelGGL(ba_cost_chunk_kernel, dim3(splits * CKB), dim3(256), 0, st, co, cams,
+                           pp, pts, cam_idx, pt_idx, uv, loss_s, kpart);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(ba_cost_chunk_final, dim3(1), dim3(64), 0, st, splits, exp, kpart, cost);
+        SFM_HIP_CHECK(hipGetLastError());
+        return SFM_OK;
+    }
     if (splits > 1) {
         hipLaunchKernelGGL(ba_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, st,
                            n_cam, splits, part, U, gc);
@@ -701,10 +889,26 @@ extern "C" int sfm_ba_cost(sfm_ctx* ctx, int32_t n_cam, const double* cams, cons
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     if (n_obs == 0) {
-        SFM_HIP_CHECK(hipMemsetAsync(cost, 0, sizeof(double), st));
+        const size_t nslot = (ctx->ba_nchunk > 0 && ctx->ba_ntotal > 0) ? ctx->ba_nchunk : 1;
+        SFM_HIP_CHECK(hipMemsetAsync(cost, 0, sizeof(double) * nslot, st));
         return SFM_OK;
     }
     SFM_REQUIRE(cams && pp && pts && cam_idx && pt_idx && uv, "sfm_ba_cost: NULL array");
+    if (ctx->ba_nchunk > 0) {   // chunk mode (sfm_ba_set_chunks): chunk partials, tree or export
+        const int nck = ctx->ba_nchunk;
+        SFM_REQUIRE(ctx->ba_chunk_obs[nck] == n_obs, "sfm_ba_cost: chunk offsets do not match n_obs");
+        double* kpart = (double*)sfm::workspace(ctx, sizeof(double) * CKB * nck + 256);
+        if (!kpart) return SFM_ERR_NOMEM;
+        sfm::ChunkOff co;
+        for (int k = 0; k <= nck; ++k) co.v[k] = ctx->ba_chunk_obs[k];
+        hipLaunchKernelGGL(ba_cost_chunk_kernel, dim3(nck * CKB), dim3(256), 0, st, co, cams, pp,
+                           pts, cam_idx, pt_idx, uv, loss_s, kpart);
+        SFM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(ba_cost_chunk_final, dim3(1), dim3(64), 0, st, nck,
+                           ctx->ba_ntotal > 0 ? 1 : 0, kpart, cost);
+        SFM_HIP_CHECK(hipGetLastError());
+        return SFM_OK;
+    }
     const int nb = (n_obs + 255) / 256;
     double* part = (double*)sfm::workspace(ctx, sizeof(double) * (size_t)nb + 256);
     if (!part) return SFM_ERR_NOMEM;
@@ -728,6 +932,48 @@ extern "C" int sfm_ba_update(sfm_ctx* ctx, int32_t n_cam, const double* cams, co
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipLaunchKernelGGL(ba_update_kernel, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, n_cam,
                        cams, dc, n_pt, pts, dp, cams_out, pts_out);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
+extern "C" int sfm_ba_set_chunks(sfm_ctx* ctx, int32_t n_chunk, const int32_t* chunk_pt,
+                                 const int32_t* chunk_obs, int32_t n_total,
+                                 const int32_t* cam_bounds) {
+    SFM_REQUIRE(ctx != nullptr, "sfm_ba_set_chunks: ctx is NULL");
+    SFM_REQUIRE(n_chunk >= 0 && n_chunk <= SFM_BA_MAX_CHUNKS,
+                "sfm_ba_set_chunks: n_chunk must be in [0, 16]");
+    if (n_chunk == 0) {
+        ctx->ba_nchunk = ctx->ba_ntotal = 0;
+        ctx->ba_cam_bounds = nullptr;
+        return SFM_OK;
+    }
+    SFM_REQUIRE(chunk_pt && chunk_obs && cam_bounds, "sfm_ba_set_chunks: NULL array");
+    SFM_REQUIRE(n_total == 0 || (n_total >= n_chunk && n_total <= SFM_BA_MAX_CHUNKS),
+                "sfm_ba_set_chunks: n_total must be 0 or in [n_chunk, 16]");
+    SFM_REQUIRE(chunk_pt[0] == 0 && chunk_obs[0] == 0, "sfm_ba_set_chunks: offsets must start at 0");
+    for (int k = 0; k < n_chunk; ++k)
+        SFM_REQUIRE(chunk_pt[k + 1] >= chunk_pt[k] && chunk_obs[k + 1] >= chunk_obs[k],
+                    "sfm_ba_set_chunks: offsets must be non-decreasing");
+    ctx->ba_nchunk = n_chunk;
+    ctx->ba_ntotal = n_total;
+    for (int k = 0; k <= n_chunk; ++k) {
+        ctx->ba_chunk_pt[k] = chunk_pt[k];
+        ctx->ba_chunk_obs[k] = chunk_obs[k];
+    }
+    ctx->ba_cam_bounds = cam_bounds;
+    return SFM_OK;
+}
+
+extern "C" int sfm_ba_chunk_tree(sfm_ctx* ctx, int32_t n_total, int64_t n, const double* parts,
+                                 double* out) {
+    SFM_REQUIRE(ctx != nullptr, "sfm_ba_chunk_tree: ctx is NULL");
+    SFM_REQUIRE(n_total >= 1 && n_total <= SFM_BA_MAX_CHUNKS && n >= 0,
+                "sfm_ba_chunk_tree: bad size");
+    if (n == 0) return SFM_OK;
+    SFM_REQUIRE(parts && out, "sfm_ba_chunk_tree: NULL array");
+    SFM_HIP_CHECK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(ba_chunk_tree_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, n_total, (long long)n, parts, out);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }

@@ -175,19 +175,14 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
     double* __restrict__ Ud, double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ pv,
     double* __restrict__ rz_c, double* __restrict__ bb_c, int32_t* __restrict__ bad, int phase,
-    double* __restrict__ comm) {
+    double* __restrict__ comm, const int32_t* __restrict__ cb, int nck, int ntot) {
     constexpr int N = 44;
     __shared__ double red[4][N];
     __shared__ double tot[N];
+    __shared__ double cpart[SFM_BA_MAX_CHUNKS][N];
     const int c = blockIdx.x, tid = threadIdx.x;
-    if (phase == 2) {
-        if (tid < N) tot[tid] = comm[N * (size_t)c + tid];
-        __syncthreads();
-    } else {
-    double acc[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) acc[i] = 0.0;
-    for (int e = cam_ptr[c] + tid; e < cam_ptr[c + 1]; e += CT) {
+    // the 44 sums of one observation e (camera-major position) into acc
+    auto accum = [&](int e, double (&acc)[N]) {
         const int p = ptc[e];
         const double* Vi = Vinv + 9 * (size_t)p;
         const double* g = vg + 3 * (size_t)p;
@@ -215,7 +210,59 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
                 acc[t++] += wv[3 * i] * w[3 * j] + wv[3 * i + 1] * w[3 * j + 1] + wv[3 * i + 2] * w[3 * j + 2];
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[36 + i] += w[3 * i] * g[0] + w[3 * i + 1] * g[1] + w[3 * i + 2] * g[2];
-    }
+    };
+    if (cb) {   // chunk mode (sfm_ba_set_chunks): wave w sums chunks w, w + 4, ... of the camera
+        if (phase == 2) {   // the gathered partials of all ntot chunks: the canonical tree
+            if (tid < N) {
+                double a[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    a[k] = k < ntot ? comm[((size_t)k * n_cam + c) * N + tid] : 0.0;
+                tot[tid] = sfm::chunk_tree16(a);
+            }
+            __syncthreads();
+        } else {
+            const int wv = tid >> 6, lane = tid & 63;
+            for (int k = wv; k < nck; k += CT / 64) {
+                double acc[N];
+#pragma unroll
+                for (int i = 0; i < N; ++i) acc[i] = 0.0;
+                const int e1 = cb[(size_t)c * (nck + 1) + k + 1];
+                for (int e = cb[(size_t)c * (nck + 1) + k] + lane; e < e1; e += 64) accum(e, acc);
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    double v = acc[i];
+#pragma unroll
+                    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+                    acc[i] = v;
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < N; ++i) cpart[k][i] = acc[i];
+                }
+            }
+            __syncthreads();
+            if (phase == 1) {   // export: this rank's chunk partials, [chunk][camera][44]
+                for (int t = tid; t < nck * N; t += CT)
+                    comm[((size_t)(t / N) * n_cam + c) * N + t % N] = cpart[t / N][t % N];
+                return;
+            }
+            if (tid < N) {
+                double a[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) a[k] = k < nck ? cpart[k][tid] : 0.0;
+                tot[tid] = sfm::chunk_tree16(a);
+            }
+            __syncthreads();
+        }
+    } else if (phase == 2) {
+        if (tid < N) tot[tid] = comm[N * (size_t)c + tid];
+        __syncthreads();
+    } else {
+    double acc[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc[i] = 0.0;
+    for (int e = cam_ptr[c] + tid; e < cam_ptr[c + 1]; e += CT) accum(e, acc);
     if (phase == 1) {
         block_sum<N>(acc, red, comm + N * (size_t)c);
         return;
@@ -530,9 +577,10 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
     int k, int n_cam, const int32_t* __restrict__ cam_ptr, const int32_t* __restrict__ cam_obs,
     const double* __restrict__ u, const double* __restrict__ Ud, const double* __restrict__ z, double* __restrict__ pv,
     const PcgState* __restrict__ st, double* __restrict__ q, double* __restrict__ pq, int phase,
-    double* __restrict__ comm) {
+    double* __restrict__ comm, const int32_t* __restrict__ cb, int nck, int ntot) {
     __shared__ double red[CC / 64][8];
     __shared__ double pc_s[8];
+    __shared__ double cpart[SFM_BA_MAX_CHUNKS][8];
     if (st->done) return;
     const double beta = st->beta;
     const int c = blockIdx.x, tid = threadIdx.x;
@@ -545,8 +593,7 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
     double acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.0;
-    const int e_end = phase == 2 ? 0 : cam_ptr[c + 1];
-    for (int e = (phase == 2 ? 0 : cam_ptr[c]) + tid; e < e_end; e += CC) {
+    auto add_obs = [&](int e) {
         const double2* uo = (const double2*)(u + 8 * (size_t)cam_obs[e]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -554,7 +601,31 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
             acc[2 * i] += v.x;
             acc[2 * i + 1] += v.y;
         }
-    }
+    };
+    if (cb) {   // chunk mode: wave w sums chunks w, w + 4, ... (lane-strided, xor tree)
+        if (phase != 2) {
+            const int wv = tid >> 6, lane = tid & 63;
+            for (int k = wv; k < nck; k += CC / 64) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) acc[i] = 0.0;
+                const int e1 = cb[(size_t)c * (nck + 1) + k + 1];
+                for (int e = cb[(size_t)c * (nck + 1) + k] + lane; e < e1; e += 64) add_obs(e);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    double v = acc[i];
+#pragma unroll
+                    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+                    acc[i] = v;
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) cpart[k][i] = acc[i];
+                }
+            }
+        }
+    } else {
+    const int e_end = phase == 2 ? 0 : cam_ptr[c + 1];
+    for (int e = (phase == 2 ? 0 : cam_ptr[c]) + tid; e < e_end; e += CC) add_obs(e);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         double v = acc[i];
@@ -566,6 +637,7 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
 #pragma unroll
         for (int i = 0; i < 8; ++i) red[tid >> 6][i] = acc[i];
     }
+    }
     if (tid < 8) {
         const size_t kk = 8 * (size_t)c + tid;
         const double pk = z[kk] + beta * pv[kk];  // p_k, the same expression as bas_pcg_point
@@ -575,11 +647,23 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
     if (tid < 8) {
         const size_t kk = 8 * (size_t)c + tid;
         double wt = 0.0;
+        if (cb) {
+            if (phase == 1 || phase == 3)   // export: [chunk][camera][8]
+                for (int k = 0; k < nck; ++k) comm[((size_t)k * n_cam + c) * 8 + tid] = cpart[k][tid];
+            if (phase == 1) return;
+            double a[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                a[k] = phase == 2 ? (k < ntot ? comm[((size_t)k * n_cam + c) * 8 + tid] : 0.0)
+                                  : (k < nck ? cpart[k][tid] : 0.0);
+            wt = sfm::chunk_tree16(a);
+        } else {
 #pragma unroll
         for (int w = 0; w < CC / 64; ++w) wt += red[w][tid];
         if (phase == 1 || phase == 3) comm[kk] = wt;
         if (phase == 1) return;
         if (phase == 2) wt = comm[kk];
+        }
         double sU = 0.0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) sU += ur[j] * pc_s[j];
@@ -666,7 +750,7 @@ __global__ __launch_bounds__(FV) void bas_pcg_finish_vec(
     int k, int n_cam, const double* __restrict__ su, const double* __restrict__ comm,
     const double* __restrict__ pv, const double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ rzc,
-    double* __restrict__ rrc, PcgState* __restrict__ st) {
+    double* __restrict__ rrc, PcgState* __restrict__ st, int ntot) {
     __shared__ double pq_s[FINISH_VEC_MAX_CAM];
     __shared__ double red4[4];
     const int tid = threadIdx.x;
@@ -685,7 +769,14 @@ __global__ __launch_bounds__(FV) void bas_pcg_finish_vec(
             const size_t b = 8 * (size_t)cc + i;
             pj[m] = pv[b];
             sj[m] = su[b];
-            cm[m] = comm[b];
+            if (ntot > 0) {   // chunk mode: the gathered chunk partials [chunk][camera][8], tree
+                double a[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) a[k] = k < ntot ? comm[(size_t)k * 8 * n_cam + b] : 0.0;
+                cm[m] = sfm::chunk_tree16(a);
+            } else {
+                cm[m] = comm[b];
+            }
         }
     };
     load_round(0);
@@ -851,6 +942,124 @@ __global__ __launch_bounds__(256) void bas_backsub(int n_pt, int n_obs,
     }
 }
 
+// Chunk mode: bas_backsub over chunk-aligned point groups.  Block (k, b) of the nck x BPB grid
+// takes chunk k's point groups b, b + BPB, ... (32 points each, PG lanes per point, bas_backsub's
+// per-point code) and accumulates each lane's model terms in that order; then the wave trees and
+// the 4 waves in order -> mpart[(k BPB + b)][2].  The order depends only on the chunk.
+constexpr int BPB = 64;
+__global__ __launch_bounds__(256) void bas_backsub_ck(sfm::ChunkOff cpt, int n_obs,
+                                                      const int32_t* __restrict__ pt_ptr,
+                                                      const int32_t* __restrict__ cam_idx,
+                                                      const double* __restrict__ Wp,
+                                                      const double* __restrict__ V,
+                                                      const double* __restrict__ Vinv,
+                                                      const double* __restrict__ vg,
+                                                      const double* __restrict__ gp,
+                                                      const double* __restrict__ dc,
+                                                      double* __restrict__ dp,
+                                                      double* __restrict__ mpart) {
+    __shared__ double red[2][4];
+    const int k = blockIdx.x / BPB, b = blockIdx.x - k * BPB;
+    const int p0 = cpt.v[k], p1 = cpt.v[k + 1];
+    const int j = threadIdx.x % PG;
+    const size_t n = (size_t)n_obs;
+    double m0 = 0.0, m1 = 0.0;
+    for (int gb = p0 + b * (256 / PG); gb < p1; gb += BPB * (256 / PG)) {
+        const int g = gb + threadIdx.x / PG;
+        const bool valid = g < p1;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        const int o1 = valid ? pt_ptr[g + 1] : 0;
+        for (int o = (valid ? pt_ptr[g] : 0) + j; o < o1; o += PG) {
+            const double* Wo = Wp + o;
+            const double* x = dc + 8 * (size_t)cam_idx[o];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const double xi = x[i];
+                s0 += Wo[(3 * i) * n] * xi;
+                s1 += Wo[(3 * i + 1) * n] * xi;
+                s2 += Wo[(3 * i + 2) * n] * xi;
+            }
+        }
+#pragma unroll
+        for (int off = PG / 2; off >= 1; off >>= 1) {
+            s0 += __shfl_down(s0, off, PG);
+            s1 += __shfl_down(s1, off, PG);
+            s2 += __shfl_down(s2, off, PG);
+        }
+        if (valid && j == 0) {
+            const double* Vi = Vinv + 9 * (size_t)g;
+            const double* gv = vg + 3 * (size_t)g;
+            const double d0 = -gv[0] - (Vi[0] * s0 + Vi[1] * s1 + Vi[2] * s2);
+            const double d1 = -gv[1] - (Vi[3] * s0 + Vi[4] * s1 + Vi[5] * s2);
+            const double d2 = -gv[2] - (Vi[6] * s0 + Vi[7] * s1 + Vi[8] * s2);
+            dp[3 * (size_t)g] = d0;
+            dp[3 * (size_t)g + 1] = d1;
+            dp[3 * (size_t)g + 2] = d2;
+            const double* gg = gp + 3 * (size_t)g;
+            const double* Vp = V + 9 * (size_t)g;
+            m0 += gg[0] * d0 + gg[1] * d1 + gg[2] * d2;
+            const double v0 = Vp[0] * d0 + Vp[1] * d1 + Vp[2] * d2;
+            const double v1 = Vp[3] * d0 + Vp[4] * d1 + Vp[5] * d2;
+            const double v2 = Vp[6] * d0 + Vp[7] * d1 + Vp[8] * d2;
+            m1 += d0 * v0 + d1 * v1 + d2 * v2 + 2.0 * (s0 * d0 + s1 * d1 + s2 * d2);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        m0 += __shfl_down(m0, off, 64);
+        m1 += __shfl_down(m1, off, 64);
+    }
+    const int tid = threadIdx.x;
+    if ((tid & 63) == 0) { red[0][tid >> 6] = m0; red[1][tid >> 6] = m1; }
+    __syncthreads();
+    if (tid == 0) {
+        mpart[2 * (size_t)blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        mpart[2 * (size_t)blockIdx.x + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    }
+}
+
+// Chunk mode, one wave: chunk k's model terms = its BPB block partials (one per lane, xor tree);
+// exp: this rank's chunks to out[k][2] (the exchange form); else the canonical tree -> out[0..2).
+// gathered (ntot > 0, in = the gathered [ntot][2]): out[0..2) = the tree of in.
+__global__ __launch_bounds__(64) void bas_mchunk(int nck, int exp, int ntot,
+                                                 const double* __restrict__ mpart,
+                                                 const double* __restrict__ in,
+                                                 double* __restrict__ out) {
+    const int lane = threadIdx.x;
+    double a[16], b[16];
+    if (ntot > 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            a[k] = k < ntot ? in[2 * k] : 0.0;
+            b[k] = k < ntot ? in[2 * k + 1] : 0.0;
+        }
+    } else {
+        static_assert(BPB == 64, "one block partial per lane");
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            double u = 0.0, v = 0.0;
+            if (k < nck) {
+                u = mpart[2 * ((size_t)k * BPB + lane)];
+                v = mpart[2 * ((size_t)k * BPB + lane) + 1];
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    u += __shfl_xor(u, off, 64);
+                    v += __shfl_xor(v, off, 64);
+                }
+            }
+            a[k] = u;
+            b[k] = v;
+        }
+    }
+    if (lane != 0) return;
+    if (exp) {
+        for (int k = 0; k < nck; ++k) { out[2 * k] = a[k]; out[2 * k + 1] = b[k]; }
+        return;
+    }
+    out[0] = sfm::chunk_tree16(a);
+    out[1] = sfm::chunk_tree16(b);
+}
+
 // Sharded solve, one block: this rank's point-block partials of bas_backsub summed into
 // comm[0..2) (fixed order), the operand of the all-reduce that precedes bas_model.
 __global__ __launch_bounds__(1024) void bas_mpart_total(int n_pblk, const double* __restrict__ mpart,
@@ -906,8 +1115,25 @@ __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const d
 
 // Device workspace of a solve (one carve for the unsharded solve and every stage of the sharded
 // one: the same sizes give the same pointers, so state persists across the stage calls).
+// Chunk mode of a call (sfm_ba_set_chunks), read from the context.
+struct ChunkArgs {
+    const int32_t* cb = nullptr;   // [n_cam][nck + 1] positions in cam_obs (nullptr: off)
+    int nck = 0, ntot = 0;
+    sfm::ChunkOff cpt;             // local chunk point offsets
+};
+static ChunkArgs chunk_args(const sfm_ctx* ctx) {
+    ChunkArgs a;
+    if (ctx->ba_nchunk > 0) {
+        a.cb = ctx->ba_cam_bounds;
+        a.nck = ctx->ba_nchunk;
+        a.ntot = ctx->ba_ntotal;
+        for (int k = 0; k <= a.nck; ++k) a.cpt.v[k] = ctx->ba_chunk_pt[k];
+    }
+    return a;
+}
+
 struct SolveWs {
-    double *Vinv, *vg, *Ud, *Mc, *r, *z, *pv, *q, *rzc, *rrc, *pq, *mpart, *Wp, *u;
+    double *Vinv, *vg, *Ud, *Mc, *r, *z, *pv, *q, *rzc, *rrc, *pq, *mpart, *mtot, *Wp, *u;
     PcgState* state;
     int32_t* bad;
     int32_t* long_cnt;   // long-track points (bas_point_setup)
@@ -926,7 +1152,9 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     const size_t b_pt = sfm::align_up(sizeof(double) * 12 * np + sizeof(int32_t) * np, 256);
     const size_t b_cam = sfm::align_up(sizeof(double) * (128 + 32 + 5) * nc, 256);
     w.gblk = std::max(1, (n_pt + 256 / PG - 1) / (256 / PG));  // PG lanes per point
-    const size_t b_part = sfm::align_up(sizeof(double) * 2 * (size_t)w.gblk, 256);
+    // backsub partials: per point block, or (chunk mode) BPB per chunk + the combined 2 terms
+    const size_t n_part = std::max((size_t)2 * w.gblk, (size_t)2 * SFM_BA_MAX_CHUNKS * BPB + 2);
+    const size_t b_part = sfm::align_up(sizeof(double) * n_part, 256);
     const size_t no = (size_t)std::max(n_obs, 1);
     const size_t b_soa = sfm::align_up(sizeof(double) * 32 * no + sizeof(int32_t) * no, 256);
     char* ws = (char*)sfm::workspace(ctx, b_pt + b_cam + b_part + 512 + b_soa);
@@ -944,6 +1172,7 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     w.rrc = w.rzc + 2 * nc;  // [2][n_cam]
     w.pq = w.rrc + 2 * nc;
     w.mpart = (double*)(ws + b_pt + b_cam);
+    w.mtot = w.mpart + n_part - 2;   // chunk mode: the combined model terms
     w.state = (PcgState*)(ws + b_pt + b_cam + b_part);
     w.bad = (int32_t*)(ws + b_pt + b_cam + b_part + 256);
     w.long_cnt = w.bad + 1;
@@ -956,7 +1185,8 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
 }
 
 // Point setup, SoA W and the camera setup (phase 0: whole; 1: partial sums -> comm).
-static int solve_setup(hipStream_t st, const SolveWs& w, int32_t n_cam, int32_t n_pt, int32_t n_obs,
+static int solve_setup(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, int32_t n_cam,
+                       int32_t n_pt, int32_t n_obs,
                        const int32_t* pt_idx, const int32_t* pt_ptr, const int32_t* cam_ptr,
                        const int32_t* cam_obs, const double* U, const double* V, const double* W,
                        const double* gc, const double* gp, double lam, double* dc, int phase,
@@ -974,7 +1204,28 @@ static int solve_setup(hipStream_t st, const SolveWs& w, int32_t n_cam, int32_t 
     }
     hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
                        w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
-                       w.rzc, w.rrc, w.bad, phase, comm);
+                       w.rzc, w.rrc, w.bad, phase, comm, ck.cb, ck.nck, ck.ntot);
+    SFM_HIP_CHECK(hipGetLastError());
+    return SFM_OK;
+}
+
+// Back-substitution + the model terms (chunk mode: chunk-aligned blocks, combined by the tree into
+// mtot, or exported to comm[k][2] when exp).  Returns the (n_pblk, mpart) pair bas_model reads.
+static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, int32_t n_pt,
+                         int32_t n_obs, const int32_t* pt_ptr, const int32_t* cam_idx,
+                         const double* V, const double* gp, const double* dc, double* dp, bool exp,
+                         double* comm) {
+    if (!ck.cb) {
+        hipLaunchKernelGGL(bas_backsub, dim3(w.gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr,
+                           cam_idx, w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
+        SFM_HIP_CHECK(hipGetLastError());
+        return SFM_OK;
+    }
+    hipLaunchKernelGGL(bas_backsub_ck, dim3(ck.nck * BPB), dim3(256), 0, st, ck.cpt, n_obs, pt_ptr,
+                       cam_idx, w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bas_mchunk, dim3(1), dim3(64), 0, st, ck.nck, exp ? 1 : 0, 0, w.mpart,
+                       (const double*)nullptr, exp ? comm : w.mtot);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
@@ -1012,8 +1263,12 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     SolveWs w;
     if (solve_ws(ctx, n_cam, n_pt, n_obs, w) != SFM_OK) return SFM_ERR_NOMEM;
     const double lam = prm->lambda, tol = prm->tol;
-    const int rc = solve_setup(st, w, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
-                               W, gc, gp, lam, dc, 0, nullptr);
+    const ChunkArgs ck = chunk_args(ctx);
+    SFM_REQUIRE(ck.ntot == 0, "sfm_ba_solve: chunk mode of a shard (n_total > 0) needs the stages");
+    if (ck.cb)
+        SFM_REQUIRE(ck.cpt.v[ck.nck] == n_pt, "sfm_ba_solve: chunk offsets do not match n_pt");
+    const int rc = solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U,
+                               V, W, gc, gp, lam, dc, 0, nullptr);
     if (rc != SFM_OK) return rc;
     hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
     SFM_HIP_CHECK(hipGetLastError());
@@ -1038,16 +1293,16 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
                            n_obs, pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol,
                            w.state, w.u, w.lblk, w.long_list, w.long_cnt);
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
-                           cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 0, nullptr);
+                           cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 0, nullptr, ck.cb,
+                           ck.nck, 0);
         hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
                            w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);
     }
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bas_backsub, dim3(w.gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr, cam_idx,
-                       w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
-    SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, w.gblk, U, gc, dc, w.mpart,
-                       w.rrc, w.state, w.bad, info);
+    if (solve_backsub(st, w, ck, n_pt, n_obs, pt_ptr, cam_idx, V, gp, dc, dp, false, nullptr) != SFM_OK)
+        return SFM_ERR_HIP;
+    hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, ck.cb ? 1 : w.gblk, U, gc, dc,
+                       ck.cb ? w.mtot : w.mpart, w.rrc, w.state, w.bad, info);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
@@ -1076,14 +1331,19 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
     const double lam = prm->lambda, tol = prm->tol;
     // up to FINISH_VEC_MAX_CAM cameras an iteration ends in one launch after the all-reduce
     const bool fused = n_cam <= FINISH_VEC_MAX_CAM;
+    // chunk mode: the exchange is an all-gather of chunk partials (sfm_ba_set_chunks, n_total > 0)
+    const ChunkArgs ck = chunk_args(ctx);
+    SFM_REQUIRE(!ck.cb || ck.ntot > 0, "sfm_ba_solve_stage: chunk mode needs n_total > 0");
+    if (ck.cb)
+        SFM_REQUIRE(ck.cpt.v[ck.nck] == n_pt, "sfm_ba_solve_stage: chunk offsets do not match n_pt");
     switch (stage) {
-    case SFM_BA_STAGE_SETUP:  // -> comm[0, 44 n_cam)
-        return solve_setup(st, w, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V, W,
-                           gc, gp, lam, dc, 1, comm);
+    case SFM_BA_STAGE_SETUP:  // -> comm[0, 44 n_cam) (chunk mode: [n_chunk][n_cam][44])
+        return solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
+                           W, gc, gp, lam, dc, 1, comm);
     case SFM_BA_STAGE_SETUP_FINISH:
         hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
                            w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z,
-                           w.pv, w.rzc, w.rrc, w.bad, 2, comm);
+                           w.pv, w.rzc, w.rrc, w.bad, 2, comm, ck.cb, ck.nck, ck.ntot);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
         break;
@@ -1094,30 +1354,41 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
                            cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, fused ? 3 : 1,
-                           comm);
+                           comm, ck.cb, ck.nck, ck.ntot);
         break;
     case SFM_BA_STAGE_ITER_FINISH:
         if (fused) {
             hipLaunchKernelGGL(bas_pcg_finish_vec, dim3((8 * n_cam + FV - 1) / FV), dim3(FV), 0, st,
                                k, n_cam, w.q, comm, w.pv, w.Mc, dc, w.r, w.z, w.rzc, w.rrc,
-                               w.state);
+                               w.state, ck.cb ? ck.ntot : 0);
             break;
         }
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
-                           cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 2, comm);
+                           cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 2, comm, ck.cb,
+                           ck.nck, ck.ntot);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
                            w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);
         break;
-    case SFM_BA_STAGE_BACKSUB:  // -> comm[0, 2)
+    case SFM_BA_STAGE_BACKSUB:  // -> comm[0, 2) (chunk mode: [n_chunk][2])
+        if (ck.cb) {
+            if (solve_backsub(st, w, ck, n_pt, n_obs, pt_ptr, cam_idx, V, gp, dc, dp, true, comm) != SFM_OK)
+                return SFM_ERR_HIP;
+            break;
+        }
         hipLaunchKernelGGL(bas_backsub, dim3(w.gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr,
                            cam_idx, w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_mpart_total, dim3(1), dim3(1024), 0, st, w.gblk, w.mpart, comm);
         break;
     case SFM_BA_STAGE_MODEL:
-        hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, 1, U, gc, dc, comm,
-                           w.rrc, w.state, w.bad, info);
+        if (ck.cb) {   // the gathered [n_total][2] model partials: the canonical tree
+            hipLaunchKernelGGL(bas_mchunk, dim3(1), dim3(64), 0, st, ck.nck, 0, ck.ntot,
+                               (const double*)nullptr, comm, w.mtot);
+            SFM_HIP_CHECK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, 1, U, gc, dc,
+                           ck.cb ? w.mtot : comm, w.rrc, w.state, w.bad, info);
         break;
     case SFM_BA_STAGE_POLL:
         return solve_poll(ctx, st, w, done);

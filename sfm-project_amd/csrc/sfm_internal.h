@@ -22,9 +22,27 @@ struct sfm_ctx {
     // the last counted batch's per-wave counts (sfm_ransac_wave_stops): where, and its shape
     const uint32_t* rs_last_w = nullptr;
     int rs_last_pairs = 0, rs_last_hyp = 0;
+    // BA chunk mode (sfm_ba_set_chunks): local chunk point offsets; n_total 0 = whole problem
+    int ba_nchunk = 0, ba_ntotal = 0;
+    int32_t ba_chunk_pt[17] = {0}, ba_chunk_obs[17] = {0};
+    const int32_t* ba_cam_bounds = nullptr;
 };
 
 namespace sfm {
+
+// BA chunk mode (sfm_ba_set_chunks): chunk offsets passed to kernels by value.
+struct ChunkOff {
+    int32_t v[17];
+};
+// The canonical pairwise tree over the chunk partials a[0..n) (n <= 16): a fixed 16-leaf tree with
+// the missing leaves 0 — the same as "a[i] = a[2i] + a[2i+1], an odd last one carried".
+__device__ __forceinline__ double chunk_tree16(double (&a)[16]) {
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; ++i) a[i] = a[2 * i] + a[2 * i + 1];
+    return a[0];
+}
 
 void set_error(const std::string& msg);
 

@@ -86,6 +86,27 @@ def shard_points(pt_ptr, rank: int, world: int):
     return int(cuts[rank]), int(cuts[rank + 1])
 
 
+def shard_cuts_device(pt_idx, n_pt: int, world: int):
+    """shard_points for every rank from a point-major device tensor pt_idx: the same cuts (float64
+    searchsorted of the balanced observation targets in the point CSR, made monotone), computed
+    on the GPU; returns host lists (point cuts [world + 1], observation cuts [world + 1]) — the
+    only device -> host read of the sharded set-up (2 (world + 1) integers)."""
+    import torch
+    dev = pt_idx.device
+    n_obs = int(pt_idx.numel())
+    ptr = torch.zeros(n_pt + 1, dtype=torch.int64, device=dev)
+    if n_obs:
+        ptr[1:] = torch.cumsum(torch.bincount(pt_idx.long(), minlength=n_pt), 0)
+    if world <= 1:
+        return [0, n_pt], [0, n_obs]
+    tgt = n_obs * torch.arange(world + 1, dtype=torch.float64, device=dev) / world
+    cuts = torch.searchsorted(ptr.double(), tgt, right=False)
+    cuts[0], cuts[-1] = 0, n_pt
+    cuts = torch.clamp(torch.cummax(cuts, 0).values, max=n_pt)
+    both = torch.stack([cuts, ptr[cuts]]).cpu().tolist()
+    return [int(v) for v in both[0]], [int(v) for v in both[1]]
+
+
 def allreduce_camera_blocks(U, gc, cost, group=None):
     """Sum the per-rank camera blocks with ONE all-reduce: U [n_cam,8,8], g_c [n_cam,8] and the
     cost packed into a single fp64 buffer (~290 KB at n_cam = 500: latency-bound, so one
@@ -130,14 +151,57 @@ def build_jtj_sharded(cams, pp, pts, cam_idx, pt_idx, uv, rank: int, world: int,
 
 # ---- Levenberg-Marquardt bundle adjustment ---------------
 
+# Sharding-invariant sums (include/sfmcore.h sfm_ba_set_chunks): the points of a bundle adjustment
+# are cut into BA_CHUNKS fixed chunks (balanced by observations); every sum over points /
+# observations into a camera-space or scalar value is formed per chunk and the chunk partials are
+# combined by one canonical tree, so 1 to BA_CHUNKS ranks (a rank = a run of whole chunks) give the
+# same bits.  SFM_BA_CHUNKS=0 selects the round-4 sums (A/B only; not sharding-invariant).
+BA_CHUNKS = 8
+
+
+def ba_chunk_count():
+    import os
+    v = os.environ.get("SFM_BA_CHUNKS")
+    return BA_CHUNKS if v is None else int(v)
+
+
+class BAChunks:
+    """A problem's chunk table (sfm_ba_set_chunks): chunk_pt / chunk_obs host lists of LOCAL point
+    / observation offsets (n_chunk + 1), cam_bounds a device [n_cam, n_chunk + 1] i32 table,
+    n_total 0 for the whole problem or the global chunk count for a shard (export form), k0 the
+    global index of the first local chunk."""
+
+    def __init__(self, chunk_pt, chunk_obs, cam_bounds, n_total=0, k0=0):
+        self.chunk_pt, self.chunk_obs = list(chunk_pt), list(chunk_obs)
+        self.cam_bounds, self.n_total, self.k0 = cam_bounds, int(n_total), int(k0)
+        self.n_chunk = len(self.chunk_pt) - 1
+
+
+def cam_bounds_device(cam_idx, cam_obs, n_cam: int, chunk_obs):
+    """[n_cam, n_chunk + 1] i32 device: the positions in cam_obs (the camera-major CSR order, each
+    camera's observations ascending) where camera c's list reaches observation chunk_obs[k] —
+    one torch.searchsorted over keys c * (n_obs + 1) + observation."""
+    import torch
+    dev = cam_obs.device
+    n_obs = int(cam_obs.numel())
+    key = cam_idx.long()[cam_obs.long()] * (n_obs + 1) + cam_obs.long()
+    q = (torch.arange(n_cam, dtype=torch.int64, device=dev)[:, None] * (n_obs + 1)
+         + torch.as_tensor(chunk_obs, dtype=torch.int64, device=dev)[None, :])
+    return torch.searchsorted(key, q.reshape(-1)).to(torch.int32).reshape(n_cam, -1).contiguous()
+
+
 class BAProblem:
     """Device-resident observations + CSR indices for repeated linearisation / solves."""
 
-    def __init__(self, pp, cam_idx, pt_idx, uv, n_cam: int, n_pt: int, device: int = 0):
+    def __init__(self, pp, cam_idx, pt_idx, uv, n_cam: int, n_pt: int, device: int = 0,
+                 chunks=None, n_total: int = 0, k0: int = 0):
         """cam_idx / pt_idx / uv: numpy arrays, or device tensors (int32, int32, f64 [n,2]) that
         are used in place (no host round trip; the incremental driver selects its observations
         on the device).  `order` (numpy, or a device tensor for tensor inputs) is the stable
-        regrouping by point when pt_idx was not already point-major, else None."""
+        regrouping by point when pt_idx was not already point-major, else None.
+        chunks: None (the round-4 sums), an int C (the whole problem cut into C chunks balanced
+        by observations) or a list of local chunk point offsets (a shard: n_total chunks in all,
+        the first local one global chunk k0) — see BAChunks."""
         import torch
         self.dev = torch.device("cuda", device)
         self.order = None
@@ -163,17 +227,50 @@ class BAProblem:
         self.cam_ptr, self.cam_obs = sfmcore.csr_by_device(self.cam_idx, n_cam)
         self.n_cam, self.n_pt = n_cam, n_pt
         self.ctx = sfmcore.context(device)
+        self.chunks = None
+        if chunks is not None and chunks != 0:
+            if isinstance(chunks, int):
+                cpt, cob = shard_cuts_device(self.pt_idx, n_pt, chunks)
+                n_total, k0 = 0, 0
+            else:
+                cpt = [int(v) for v in chunks]
+                ptr = self.pt_ptr[torch.as_tensor(cpt, dtype=torch.int64, device=self.dev)]
+                cob = [int(v) for v in ptr.cpu().tolist()]
+            cb = cam_bounds_device(self.cam_idx, self.cam_obs, n_cam, cob)
+            self.chunks = BAChunks(cpt, cob, cb, n_total, k0)
+
+    def _call(self, fn, *a, **kw):
+        """fn under this problem's chunk mode (set on the shared context, then cleared)."""
+        if self.chunks is None:
+            return fn(*a, **kw)
+        self.ctx.ba_set_chunks(self.chunks)
+        try:
+            return fn(*a, **kw)
+        finally:
+            self.ctx.ba_set_chunks(None)
+
+    def _slots(self):
+        ck = self.chunks
+        return ck.n_chunk if ck is not None and ck.n_total > 0 else None
 
     def linearize(self, cams, pts, loss_s=0.0):
-        return self.ctx.ba_jtj(cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv,
-                               self.pt_ptr, self.cam_ptr, self.cam_obs, loss_s=loss_s)
+        """sfm_ba_jtj; for a chunked shard U / gc / cost are the local chunks' partials."""
+        return self._call(self.ctx.ba_jtj, cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv,
+                          self.pt_ptr, self.cam_ptr, self.cam_obs, loss_s=loss_s,
+                          n_slot=self._slots())
 
     def solve(self, lin, lam, max_iter=100, tol=1e-10, poll=8):
-        return self.ctx.ba_solve(lin, self.cam_idx, self.pt_idx, self.pt_ptr, self.cam_ptr,
-                                 self.cam_obs, lam, max_iter=max_iter, tol=tol, poll=poll)
+        return self._call(self.ctx.ba_solve, lin, self.cam_idx, self.pt_idx, self.pt_ptr,
+                          self.cam_ptr, self.cam_obs, lam, max_iter=max_iter, tol=tol, poll=poll)
+
+    def solve_sharded(self, lin, lam, allreduce, max_iter=100, tol=1e-10, **kw):
+        return self._call(self.ctx.ba_solve_sharded, lin, self.cam_idx, self.pt_idx, self.pt_ptr,
+                          self.cam_ptr, self.cam_obs, lam, allreduce, max_iter=max_iter, tol=tol,
+                          chunks=self.chunks, **kw)
 
     def cost(self, cams, pts, loss_s=0.0):
-        return self.ctx.ba_cost(cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv, loss_s)
+        return self._call(self.ctx.ba_cost, cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv,
+                          loss_s, n_slot=self._slots())
 
     def update(self, cams, dc, pts, dp):
         return self.ctx.ba_update(cams, dc, pts, dp)
@@ -395,8 +492,12 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                      and every rank runs the whole PCG itself (no collective per iteration);
       'auto'       — pcg_rule on the measured all-reduce latency / bandwidth of the group
                      (probe_collectives); world size 1 always takes 'sharded'.
-    Every rank returns the same result, equal to the unsharded one up to the fp64 summation
-    order.  `info` (optional dict) receives the branch taken and the rule's terms; with
+    Every rank returns the same result, and (BA_CHUNKS) it is the
+    single-process result BIT FOR BIT, for both branches and any world size up to BA_CHUNKS: the
+    points are cut into BA_CHUNKS fixed chunks, a rank holds a run of whole chunks, every sum into
+    a camera-space or scalar value is formed per chunk and combined by one canonical tree
+    (include/sfmcore.h sfm_ba_set_chunks), and the exchanges are exact gathers of chunk partials
+    (an all-reduce of zero-padded slots) instead of sums.  `info` (optional dict) receives the branch taken and the rule's terms; with
     reproj_err it also receives `err`: every observation's reprojection error (px) at the returned
     parameters, in the caller's order — from the device-resident problem (one more K3 launch;
     sharded: each rank's shard summed into a zero-padded vector), instead of a second host ->
@@ -420,18 +521,38 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     lo, hi = 0, n_pt
     full = None
     tensors = isinstance(pt_idx, torch.Tensor)
+    nchunk = ba_chunk_count()     # sharding-invariant sums (BAChunks); 0 = the round-4 sums
+    k0, local_chunks = 0, None
     if allreduce is not None:
-        if tensors:   # the sharded path slices on the host
-            cam_idx, pt_idx, uv = (t.cpu().numpy() for t in (cam_idx, pt_idx, uv))
-        cam_idx = np.asarray(cam_idx, np.int32)
-        pt_idx = np.asarray(pt_idx, np.int32)
-        uv = np.asarray(uv, np.float64)
-        order = np.argsort(pt_idx, kind="stable")
-        cam_idx, pt_idx, uv = cam_idx[order], pt_idx[order], uv[order]
-        pt_ptr, _ = sfmcore.csr_by(pt_idx, n_pt)
-        lo, hi = shard_points(pt_ptr, rank, world)
-        n_obs_all = len(pt_idx)
-        o0, o1 = int(pt_ptr[lo]), int(pt_ptr[hi])
+        # device-resident: point-major order, CSR and the shard cuts on the
+        # GPU; the host reads world + 1 cut pairs, the observations never leave the device
+        dev = torch.device("cuda", device)
+        if not tensors:
+            cam_idx, pt_idx, uv = (torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)
+                                   for a, dt in ((cam_idx, np.int32), (pt_idx, np.int32),
+                                                 (uv, np.float64)))
+        cam_idx = cam_idx.to(dev, torch.int32).contiguous()
+        pt_idx = pt_idx.to(dev, torch.int32).contiguous()
+        uv = uv.to(dev, torch.float64).contiguous()
+        order = None
+        if pt_idx.numel() > 1 and bool((pt_idx[1:] < pt_idx[:-1]).any()):
+            order = torch.argsort(pt_idx.long(), stable=True)
+            cam_idx, pt_idx, uv = cam_idx[order], pt_idx[order], uv[order]
+        n_obs_all = int(pt_idx.numel())
+        if nchunk > 0:
+            # the whole problem's chunks (balanced by observations); rank r takes chunks
+            # [r C / N, (r + 1) C / N): every rank a run of whole chunks, so the sums match N = 1
+            if world > nchunk:
+                raise ValueError(f"bundle_adjust: {world} ranks > {nchunk} BA chunks")
+            gcuts, gocuts = shard_cuts_device(pt_idx, n_pt, nchunk)
+            kr = [r * nchunk // world for r in range(world + 1)]
+            cuts, ocuts = [gcuts[k] for k in kr], [gocuts[k] for k in kr]
+            k0 = kr[rank]
+            local_chunks = [gcuts[k] - gcuts[k0] for k in range(k0, kr[rank + 1] + 1)]
+        else:
+            cuts, ocuts = shard_cuts_device(pt_idx, n_pt, world)
+        lo, hi = cuts[rank], cuts[rank + 1]
+        o0, o1 = ocuts[rank], ocuts[rank + 1]
         mode = os.environ.get("SFM_BA_PCG", pcg)
         if mode not in ("auto", "sharded", "replicated"):
             raise ValueError(f"bundle_adjust: pcg must be auto|sharded|replicated, got {mode!r}")
@@ -445,14 +566,27 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                     info["rule"] = terms
         if mode == "replicated":
             # the whole problem for the solve (every rank), the shard for the linearisation
-            full = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device)
-            counts_pt = [b - a for a, b in (shard_points(pt_ptr, r, world) for r in range(world))]
-            counts_obs = [int(pt_ptr[b] - pt_ptr[a])
-                          for a, b in (shard_points(pt_ptr, r, world) for r in range(world))]
+            full = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device, chunks=nchunk or None)
+            counts_pt = [cuts[r + 1] - cuts[r] for r in range(world)]
+            counts_obs = [ocuts[r + 1] - ocuts[r] for r in range(world)]
         cam_idx, pt_idx, uv = cam_idx[o0:o1], pt_idx[o0:o1] - lo, uv[o0:o1]
     if info is not None:
         info.update(pcg=mode, world=world)
-    prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, hi - lo, device)
+    if local_chunks is not None:    # a shard: its chunks' partials are exchanged (export form)
+        prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, hi - lo, device, chunks=local_chunks,
+                         n_total=nchunk, k0=k0)
+    else:
+        prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, hi - lo, device, chunks=nchunk or None)
+    f64 = torch.float64
+
+    def gather_chunks(part, width):
+        """This shard's chunk partials [n_local, width] -> the canonical tree over all chunks
+        [width]: an all-reduce of a zero-filled [C, width] slot buffer (an exact all-gather)."""
+        nl = prob.chunks.n_chunk
+        slot = torch.zeros((nchunk, width), dtype=f64, device=prob.dev)
+        slot[k0:k0 + nl] = part.reshape(nl, width)
+        allreduce(slot.view(-1))
+        return prob.ctx.ba_chunk_tree(slot)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(prob.dev)
     cams_d = T(cams)
     # replicated: every rank keeps all points (the solve's δp is whole); the shard is a view
@@ -464,7 +598,13 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
 
     def linearize(c, p):
         lin = prob.linearize(c, shard_of(p), loss_s)
-        if allreduce is not None:   # global camera blocks before the gauge is applied
+        if allreduce is not None and local_chunks is not None:   # chunk partials -> the tree
+            nl = prob.chunks.n_chunk
+            tot = gather_chunks(torch.cat([lin["U"].reshape(nl, -1), lin["gc"].reshape(nl, -1)],
+                                          1), n_cam * 72)
+            lin["U"] = tot[:n_cam * 64].view(n_cam, 8, 8)
+            lin["gc"] = tot[n_cam * 64:].view(n_cam, 8)
+        elif allreduce is not None:   # global camera blocks before the gauge is applied
             nu_, ng = lin["U"].numel(), lin["gc"].numel()
             buf = torch.cat([lin["U"].reshape(-1), lin["gc"].reshape(-1)])
             allreduce(buf)
@@ -480,7 +620,9 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
 
     def cost(c, p):
         t = prob.cost(c, shard_of(p), loss_s)
-        if allreduce is not None:
+        if allreduce is not None and local_chunks is not None:
+            t = gather_chunks(t[:prob.chunks.n_chunk], 1)
+        elif allreduce is not None:
             allreduce(t)
         return t
 
@@ -489,9 +631,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             return full.solve(lin, lam, max_cg, cg_tol)
         if allreduce is None:
             return prob.solve(lin, lam, max_cg, cg_tol)
-        return prob.ctx.ba_solve_sharded(lin, prob.cam_idx, prob.pt_idx, prob.pt_ptr,
-                                         prob.cam_ptr, prob.cam_obs, lam, allreduce,
-                                         max_iter=max_cg, tol=cg_tol)
+        return prob.solve_sharded(lin, lam, allreduce, max_iter=max_cg, tol=cg_tol)
     upd = full if full is not None else prob
     if info is not None:
         torch.cuda.synchronize(prob.dev)
@@ -540,10 +680,11 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             ev = torch.zeros(n_obs_all, dtype=torch.float64, device=prob.dev)
             ev[o0:o1] = e
             allreduce(ev)
-            err = np.empty(n_obs_all)
-            err[order] = ev.cpu().numpy()
-            if reproj_err == "device":
-                err = torch.from_numpy(err).to(prob.dev)
+            if order is not None:       # back to the caller's observation order
+                back = torch.empty_like(ev)
+                back[order] = ev
+                ev = back
+            err = ev if reproj_err == "device" else ev.cpu().numpy()
         info["err"] = err
     if allreduce is not None and full is None:
         # gather the point shards: one all-reduce of the zero-padded set

@@ -26,7 +26,8 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_ba_update", "sfm_tracks", "sfm_triangulate", "sfm_register_batch",
             "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
             "sfm_ransac_stats", "sfm_ransac_f_batch_f64", "sfm_graph_rows_packed",
-            "sfm_graph_expand", "sfm_match_batch_both", "sfm_ransac_wave_stops"]
+            "sfm_graph_expand", "sfm_match_batch_both", "sfm_ransac_wave_stops",
+            "sfm_ba_set_chunks", "sfm_ba_chunk_tree"]
 
 
 class SfmCoreError(RuntimeError):
@@ -110,6 +111,8 @@ def load_library(path: str = LIB_PATH):
         L.sfm_ba_cost.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, f64, vp]
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
         L.sfm_ba_fix_params.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp]
+        L.sfm_ba_set_chunks.argtypes = [vp, i32, vp, vp, i32, vp]
+        L.sfm_ba_chunk_tree.argtypes = [vp, i32, i64, vp, vp]
         L.sfm_orb_batch.argtypes = [vp, vp, i32, i32, i32, C.POINTER(OrbParams), vp, vp, vp]
         L.sfm_register_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(RegisterParams),
                                          vp, vp, vp, vp]
@@ -363,18 +366,46 @@ class Context:
         return rows
 
     # ---- bundle adjustment -----------------------------------------------------------------
-    def ba_jtj(self, cams, pp, pts, cam_idx, pt_idx, uv, pt_ptr, cam_ptr, cam_obs, loss_s=0.0):
+    # ---- BA chunk mode (sfm_ba_set_chunks): sharding-invariant sums -----------------------------
+    def ba_set_chunks(self, spec=None):
+        """spec = BAChunks (reconstruction.py) or None (off).  Applies to the next BA calls."""
+        if spec is None:
+            _check(self.lib.sfm_ba_set_chunks(self.handle, 0, None, None, 0, None))
+            return
+        n = len(spec.chunk_pt) - 1
+        cpt = (C.c_int32 * (n + 1))(*[int(v) for v in spec.chunk_pt])
+        cob = (C.c_int32 * (n + 1))(*[int(v) for v in spec.chunk_obs])
+        _check(self.lib.sfm_ba_set_chunks(self.handle, n, cpt, cob, int(spec.n_total),
+                                          _ptr(spec.cam_bounds)))
+
+    def ba_chunk_tree(self, parts, out=None):
+        """sfm_ba_chunk_tree: parts [n_total, ...] f64 device -> out [...] (the canonical tree)."""
+        torch = self.torch
+        parts = parts.contiguous()
+        nt = parts.shape[0]
+        if out is None:
+            out = torch.empty(parts.shape[1:], dtype=torch.float64, device=parts.device)
+        self._bind_stream()
+        _check(self.lib.sfm_ba_chunk_tree(self.handle, nt, int(out.numel()), _ptr(parts),
+                                          _ptr(out)))
+        return out
+
+    def ba_jtj(self, cams, pp, pts, cam_idx, pt_idx, uv, pt_ptr, cam_ptr, cam_obs, loss_s=0.0,
+               n_slot=None):
+        """n_slot: chunk mode of a shard (export form) — U [n_slot, n_cam, 8, 8], gc [n_slot, n_cam, 8],
+        cost [n_slot] chunk partials (sfm_ba_set_chunks)."""
         torch = self.torch
         dev = cams.device
         nc, npt, no = cams.shape[0], pts.shape[0], cam_idx.shape[0]
         f64 = torch.float64
-        U = torch.empty((nc, 8, 8), dtype=f64, device=dev)
+        lead = () if n_slot is None else (n_slot,)
+        U = torch.empty(lead + (nc, 8, 8), dtype=f64, device=dev)
         V = torch.empty((npt, 3, 3), dtype=f64, device=dev)
         W = torch.empty((no, 8, 3), dtype=f64, device=dev)
-        gc = torch.empty((nc, 8), dtype=f64, device=dev)
+        gc = torch.empty(lead + (nc, 8), dtype=f64, device=dev)
         gp = torch.empty((npt, 3), dtype=f64, device=dev)
         res = torch.empty((no, 2), dtype=f64, device=dev)
-        cost = torch.empty(1, dtype=f64, device=dev)
+        cost = torch.empty(max(n_slot or 1, 1), dtype=f64, device=dev)
         self._bind_stream()
         _check(self.lib.sfm_ba_jtj(self.handle, nc, _ptr(cams), _ptr(pp), npt, _ptr(pts), no,
                                    _ptr(cam_idx), _ptr(pt_idx), _ptr(uv), _ptr(pt_ptr),
@@ -472,7 +503,7 @@ class Context:
         return dc, dp, info
 
     def ba_solve_sharded(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, allreduce,
-                         max_iter=100, tol=1e-10, out=None, poll=8, graph=False):
+                         max_iter=100, tol=1e-10, out=None, poll=8, graph=False, chunks=None):
         """ba_solve on this rank's point shard (lin: ba_jtj of the shard with U / gc already
         all-reduced), driving sfm_ba_solve_stage: allreduce(t) sums the f64 device tensor t over
         all ranks in place, ordered on the current stream (reconstruction.make_allreduce).
@@ -490,19 +521,35 @@ class Context:
                    torch.empty((npt, 3), dtype=f64, device=dev),
                    torch.empty(5, dtype=f64, device=dev))
         dc, dp, info = out
-        comm = torch.empty(44 * nc, dtype=torch.float64, device=dev)
+        # chunk mode (chunks = reconstruction.BAChunks of a shard, set on this context): every
+        # exchange is an all-reduce of a zero-filled [n_total] slot buffer in which this rank
+        # fills only its own chunks' slots — an exact all-gather (x + 0 = x), so the stages after
+        # it see every chunk's partial bit for bit, in chunk order
+        nt = chunks.n_total if chunks is not None else 1
+        k0 = chunks.k0 if chunks is not None else 0
+        comm = torch.zeros(nt * 44 * nc, dtype=torch.float64, device=dev)
         prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll))
         done = C.c_int32(0)
-        args = (nc, npt, no, _ptr(cam_idx), _ptr(pt_idx), _ptr(pt_ptr), _ptr(cam_ptr),
-                _ptr(cam_obs), _ptr(U), _ptr(lin["V"]), _ptr(lin["W"]), _ptr(lin["gc"]),
-                _ptr(lin["gp"]), C.byref(prm), _ptr(comm), _ptr(dc), _ptr(dp), _ptr(info),
-                C.byref(done))
+        cptr = comm.data_ptr()
+
+        def args(off=0):
+            return (nc, npt, no, _ptr(cam_idx), _ptr(pt_idx), _ptr(pt_ptr), _ptr(cam_ptr),
+                    _ptr(cam_obs), _ptr(U), _ptr(lin["V"]), _ptr(lin["W"]), _ptr(lin["gc"]),
+                    _ptr(lin["gp"]), C.byref(prm), C.c_void_p(cptr + 8 * off), _ptr(dc), _ptr(dp),
+                    _ptr(info), C.byref(done))
+        a_base = args()
+        a_setup, a_iter, a_back = args(k0 * 44 * nc), args(k0 * 8 * nc), args(k0 * 2)
         self._bind_stream()
 
-        def stage(s, k=0):
-            _check(self.lib.sfm_ba_solve_stage(self.handle, s, k, *args))
-        stage(BA_STAGE_SETUP)
-        allreduce(comm[:44 * nc])
+        def stage(s, k=0, a=a_base):
+            _check(self.lib.sfm_ba_solve_stage(self.handle, s, k, *a))
+
+        def produce(s, n, a, k=0):   # a producing stage, then the exchange of its n doubles
+            if chunks is not None:
+                comm[:n].zero_()
+            stage(s, k, a)
+            allreduce(comm[:n])
+        produce(BA_STAGE_SETUP, nt * 44 * nc, a_setup)
         stage(BA_STAGE_SETUP_FINISH)
         every = poll
         # windows of `poll` iterations between host polls.  With a capturable collective (RCCL)
@@ -531,8 +578,7 @@ class Context:
                         g.capture_begin()
                         try:
                             for j in range(n):
-                                stage(BA_STAGE_ITER, k + j)
-                                allreduce(comm[:8 * nc])
+                                produce(BA_STAGE_ITER, nt * 8 * nc, a_iter, k + j)
                                 stage(BA_STAGE_ITER_FINISH, k + j)
                         finally:
                             g.capture_end()
@@ -541,12 +587,10 @@ class Context:
                 g.replay()
             else:
                 for j in range(k, k + n):
-                    stage(BA_STAGE_ITER, j)
-                    allreduce(comm[:8 * nc])
+                    produce(BA_STAGE_ITER, nt * 8 * nc, a_iter, j)
                     stage(BA_STAGE_ITER_FINISH, j)
             k += n
-        stage(BA_STAGE_BACKSUB)
-        allreduce(comm[:2])
+        produce(BA_STAGE_BACKSUB, nt * 2, a_back)
         stage(BA_STAGE_MODEL)
         return dc, dp, info
 
@@ -560,9 +604,10 @@ class Context:
                                           _ptr(U), _ptr(lin["W"]), _ptr(lin["gc"])))
         return lin
 
-    def ba_cost(self, cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0, out=None):
+    def ba_cost(self, cams, pp, pts, cam_idx, pt_idx, uv, loss_s=0.0, out=None, n_slot=None):
         torch = self.torch
-        cost = out if out is not None else torch.empty(1, dtype=torch.float64, device=cams.device)
+        cost = out if out is not None else torch.empty(max(n_slot or 1, 1), dtype=torch.float64,
+                                                       device=cams.device)
         self._bind_stream()
         _check(self.lib.sfm_ba_cost(self.handle, cams.shape[0], _ptr(cams), _ptr(pp),
                                     pts.shape[0], _ptr(pts), cam_idx.shape[0], _ptr(cam_idx),

@@ -4,8 +4,9 @@ the point-sharded bundle adjustment (reconstruction.bundle_adjust(shard=True): c
 all-reduce, sfm_ba_solve_stage with one all-reduce per CG iteration, all-reduced trial cost,
 gathered points) and one sharded solve from the initial linearisation; it writes OUT.rank<r>.npz.
 A second argument `tiny` uses a 2-point problem (with 3 ranks one shard is empty); a third one
-picks bundle_adjust's PCG branch (sharded | replicated | auto; default sharded).
-Usage: python -m torch.distributed.run --nproc-per-node N ... dist_ba_worker.py OUT [tiny|std] [pcg]"""
+picks bundle_adjust's PCG branch (sharded | replicated | auto; default sharded); a fourth one
+repeats the bundle adjustment that many times (sequential auto-mode calls).
+Usage: python -m torch.distributed.run --nproc-per-node N ... dist_ba_worker.py OUT [tiny|std] [pcg] [repeat]"""
 import os
 import sys
 
@@ -31,12 +32,17 @@ def main():
     args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
     fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
     pcg = sys.argv[3] if len(sys.argv) > 3 else "sharded"
-    binfo = {}
-    cams, pts, hist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed, shard=True,
-                                      pcg=pcg, info=binfo)
+    repeat = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    branches = []
+    for _ in range(repeat):   # sequential auto-mode calls probe / cache consistently
+        binfo = {}
+        cams, pts, hist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed,
+                                          shard=True, pcg=pcg, info=binfo)
+        branches.append(binfo["pcg"])
     dc, dp, info, lo, hi = shard_solve(prob, rank, world, R.make_allreduce())
     np.savez(f"{out}.rank{rank}.npz", cams=cams, pts=pts, hist=np.array(hist, np.float64),
-             dc=dc, dp=dp, info=info, lo=lo, hi=hi, pcg=np.array(binfo["pcg"]))
+             dc=dc, dp=dp, info=info, lo=lo, hi=hi, pcg=np.array(binfo["pcg"]),
+             branches=np.array(branches))
     dist.barrier()
     dist.destroy_process_group()
 

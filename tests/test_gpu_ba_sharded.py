@@ -160,9 +160,10 @@ def test_ba_sharded_three_ranks_with_an_empty_shard(tmp_path):
     np.testing.assert_allclose(d[0]["dc"], rdc, rtol=0, atol=1e-6 * np.abs(rdc).max())
     np.testing.assert_allclose(np.concatenate([d[k]["dp"] for k in range(3)]), rdp, rtol=0,
                                atol=1e-6 * np.abs(rdp).max())
-    assert abs(d[0]["hist"][-1][0] - rhist[-1][0]) <= 1e-6 * rhist[-1][0] + 1e-20
-    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-5, atol=1e-8)
-    np.testing.assert_allclose(d[0]["pts"], rpts, rtol=1e-5, atol=1e-8)
+    # the LM itself is sharding-invariant (BA chunks): the single process's result, bit for bit
+    np.testing.assert_array_equal(d[0]["hist"], np.array(rhist, np.float64))
+    np.testing.assert_array_equal(d[0]["cams"], rcams)
+    np.testing.assert_array_equal(d[0]["pts"], rpts)
     assert len(d[2]["dp"]) == 0
 
 
@@ -183,10 +184,10 @@ def test_ba_sharded_two_ranks(tmp_path):
     np.testing.assert_allclose(dp, rdp, rtol=0, atol=1e-8 * np.abs(rdp).max())
     assert d[0]["info"][0] > 0 and d[0]["info"][1] <= 1e-12 and d[0]["info"][4] == 0
     np.testing.assert_allclose(d[0]["info"][2:4], rinfo[2:4], rtol=1e-8)
-    hist = d[0]["hist"]
-    assert abs(hist[-1][0] - rhist[-1][0]) <= 1e-9 * rhist[-1][0]
-    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-7, atol=1e-10)
-    np.testing.assert_allclose(d[0]["pts"], rpts, rtol=1e-7, atol=1e-10)
+    # the LM (chunked sums) equals the single process bit for bit
+    np.testing.assert_array_equal(d[0]["hist"], np.array(rhist, np.float64))
+    np.testing.assert_array_equal(d[0]["cams"], rcams)
+    np.testing.assert_array_equal(d[0]["pts"], rpts)
     np.testing.assert_array_equal(d[0]["cams"][fixed], prob["cams"][fixed])
 
 
@@ -209,9 +210,9 @@ def test_ba_two_ranks_both_pcg_branches_match_oracle(tmp_path, pcg):
     assert str(d[0]["pcg"]) == str(d[1]["pcg"]) == pcg
     cost = d[0]["hist"][-1][0]
     assert abs(cost - ohist[-1][0]) <= 1e-9 * ohist[-1][0]
-    assert abs(cost - rhist[-1][0]) <= 1e-9 * rhist[-1][0]
-    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-7, atol=1e-10)
-    np.testing.assert_allclose(d[0]["pts"], rpts, rtol=1e-7, atol=1e-10)
+    np.testing.assert_array_equal(d[0]["hist"], np.array(rhist, np.float64))
+    np.testing.assert_array_equal(d[0]["cams"], rcams)
+    np.testing.assert_array_equal(d[0]["pts"], rpts)
     np.testing.assert_allclose(d[0]["cams"], ocams, rtol=1e-6, atol=1e-9)
     np.testing.assert_array_equal(d[0]["cams"][fixed], prob["cams"][fixed])
 
@@ -227,8 +228,9 @@ def test_ba_replicated_three_ranks_with_an_empty_shard(tmp_path):
     for k in (1, 2):
         for key in ("cams", "pts", "hist"):
             np.testing.assert_array_equal(d[0][key], d[k][key])
-    assert abs(d[0]["hist"][-1][0] - rhist[-1][0]) <= 1e-6 * rhist[-1][0] + 1e-20
-    np.testing.assert_allclose(d[0]["cams"], rcams, rtol=1e-5, atol=1e-8)
+    np.testing.assert_array_equal(d[0]["hist"], np.array(rhist, np.float64))
+    np.testing.assert_array_equal(d[0]["cams"], rcams)
+    np.testing.assert_array_equal(d[0]["pts"], rpts)
 
 
 def test_ba_auto_rule_reports_its_branch():
@@ -250,3 +252,15 @@ def test_ba_auto_rule_reports_its_branch():
     finally:
         R.release_allreduce()
         dist.destroy_process_group()
+
+
+def test_ba_auto_mode_repeated_on_three_ranks(tmp_path):
+    """several sequential auto-mode bundle adjustments on 3 gloo ranks — the
+    collective probe's cache key is the same on every rank (backend, group, device, path, n_cam),
+    so every rank hits or misses it together and takes the same branch; the ranks agree bit for
+    bit and every call gives the same result."""
+    d = _run_ranks(tmp_path, 3, "std", "auto", "3")
+    for k in (1, 2):
+        for key in ("cams", "pts", "hist", "branches"):
+            np.testing.assert_array_equal(d[0][key], d[k][key])
+    assert len(set(d[0]["branches"].tolist())) == 1

@@ -296,3 +296,48 @@ def test_both_orders_rejects_ratio_and_large_k(ctx):
                                       pr.data_ptr(), 1, C.byref(prm), out[0].data_ptr(),
                                       out[1].data_ptr(), out[2].data_ptr())
     assert rc != 0 and b"ratio" in ctx.lib.sfm_last_error()
+
+
+@pytest.mark.parametrize("ratio", [(4, 5), (1, 1), None])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_group_kernel_equals_top2_kernel_and_oracle(ctx, ratio, metric):
+    """Round 5's K1 (mfma_mutual_grp_kernel: group-max rows, exact recheck of the best group in
+    the finalize, LDS column reduction) against round 4's top-2 kernel (SFM_K1_GRP=0) and the
+    oracle: identical outputs, including the cases the recheck exists for — a tie of the nearest
+    value inside one 16-train group (trains 0/1, 8/9: same lane half, same tile), a tie across
+    tiles (trains 2 and 34), the runner-up inside the best group, ragged sizes, tie-heavy sets."""
+    import os
+    rng = np.random.default_rng(321 + metric)
+    k, dim = 700, (128 if metric == 0 else 32)
+    desc = rng.integers(0, 256, size=(5, k, dim), dtype=np.uint8)
+    if metric == 0:
+        desc[3] = _tie_heavy(rng, 1, k, 2)[0]
+    else:
+        desc[3] = rng.integers(0, 2, size=(k, dim), dtype=np.uint8) * 255
+    desc[1, 1] = desc[1, 0]          # nearest tie inside one group
+    desc[1, 9] = desc[1, 8]
+    desc[1, 34] = desc[1, 2]         # nearest tie across tiles
+    desc[0, :40] = desc[1, :40]      # exact nearest neighbours for those queries
+    desc[1, 3] = desc[1, 0] ^ 1      # runner-up one bit / unit away, in the same group as 0
+    desc[2, 100:110] = desc[0, 5]
+    n_kp = np.array([k, k - 3, 65, k, 33], np.int32)
+    pairs = np.array([[a, b] for a in range(5) for b in range(5) if a != b], np.int32)
+    outs = []
+    if metric == 1:     # Hamming runs the mutual-rule kernels only on request (DESIGN.md 4.4)
+        os.environ["SFM_HAMMING_PATH"] = "mutual"
+    try:
+        for v in ("0", "1"):
+            os.environ["SFM_K1_GRP"] = v
+            try:
+                outs.append(_gpu_match(ctx, desc, n_kp, pairs, metric=metric, cross_check=1,
+                                       ratio=ratio))
+            finally:
+                os.environ.pop("SFM_K1_GRP", None)
+    finally:
+        os.environ.pop("SFM_HAMMING_PATH", None)
+    (c0, m0, d0), (c1, m1, d1) = outs
+    np.testing.assert_array_equal(c0, c1)
+    for p in range(len(pairs)):
+        np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
+        np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
+    _check_pairs(ctx, desc, n_kp, pairs, metric=metric, cross_check=1, ratio=ratio)

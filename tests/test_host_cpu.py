@@ -345,3 +345,21 @@ def test_image_key_without_xxhash(monkeypatch):
     im2 = im.copy()
     im2[3, 3] ^= 1
     assert k1 == k2 and k1[1].startswith("b2:") and fm._image_key(im2) != k1
+
+
+def test_shard_cuts_device_equals_shard_points():
+    """the sharded BA's cuts come from the device (torch ops; run here on CPU
+    tensors) and equal reconstruction.shard_points of the host CSR for every rank, including
+    empty points, one heavy point and more ranks than points."""
+    import torch
+    rng = np.random.default_rng(5)
+    for n_pt, n_obs in ((1000, 5000), (7, 40), (3, 2), (50, 0)):
+        pt = np.sort(rng.integers(0, n_pt, n_obs)).astype(np.int32)
+        if n_obs > 10:
+            pt[n_obs // 3: n_obs // 2] = pt[n_obs // 3]       # a heavy point
+        ptr, _ = sfmcore.csr_by(pt, n_pt)
+        for world in (1, 2, 3, 4, 8):
+            cuts, ocuts = reconstruction.shard_cuts_device(torch.from_numpy(pt), n_pt, world)
+            exp = [reconstruction.shard_points(ptr, r, world) for r in range(world)]
+            assert [(cuts[r], cuts[r + 1]) for r in range(world)] == exp
+            assert ocuts == [int(ptr[c]) for c in cuts]
