@@ -32,12 +32,14 @@ constexpr double DIAG_MIN = 1e-6, DIAG_MAX = 1e32;
 constexpr int CT = 256;  // threads per camera block
 
 struct PcgState {
-    double beta;    // β_k of the current iteration (published by bas_pcg_point)
+    double beta;    // β_k of the current iteration (published by the previous iteration's vector
+                    // kernel, or bas_pcg_init for k = 0)
     double rz;      // r·z of the current iterate
     double bb;      // |b|^2
     double rr;      // |r|^2 after the last step
     int32_t iter;   // iterations done
     int32_t done;   // converged (or max_iter reached)
+    uint32_t cnt;   // blocks of the current vector kernel that finished (last-block publish)
 };
 
 __device__ __forceinline__ double dclamp(double d) { return fmin(fmax(d, DIAG_MIN), DIAG_MAX); }
@@ -396,6 +398,38 @@ __device__ Scalars pcg_scalars(int k, int n_cam, const double* __restrict__ rzc,
     return sc;
 }
 
+// The CG scalars of iteration k + 1, computed ONCE by the last block of iteration k's vector kernel
+// (after every block wrote its per-camera partials of slot (k+1)&1: store, fence, counter) and
+// published in st for the next iteration's kernels — instead of every block of the point pass
+// re-reducing the three n_cam-long partial arrays (round 4: 12 KB of L2 reads and two block
+// barriers per point-pass block).  The same canon_sum association: the same bits.
+__device__ void publish_next(int k, int n_cam, const double* __restrict__ rzc,
+                             const double* __restrict__ rrc, double tol, PcgState* __restrict__ st,
+                             unsigned nblk, double* red4x3) {
+    __shared__ bool last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&st->cnt, 1u) == nblk - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const Scalars sc = pcg_scalars(k + 1, n_cam, rzc, rrc, st->bb, tol, red4x3);
+    if (threadIdx.x == 0) {
+        st->beta = sc.beta;
+        st->rz = sc.rz;
+        st->done = sc.done ? 1 : 0;
+        st->cnt = 0u;
+    }
+}
+
+__device__ __forceinline__ Scalars read_scalars(const PcgState* __restrict__ st) {
+    Scalars sc;
+    sc.beta = st->beta;
+    sc.rz = st->rz;
+    sc.done = st->done != 0;
+    return sc;
+}
+
 #ifndef SFM_BA_PG
 #define SFM_BA_PG 8
 #endif
@@ -474,19 +508,9 @@ __global__ __launch_bounds__(256) void bas_pcg_point(
     const double* __restrict__ rzc, const double* __restrict__ rrc, double tol,
     PcgState* __restrict__ st, double* __restrict__ u, int n_long_blk,
     const int32_t* __restrict__ long_list, const int32_t* __restrict__ long_cnt) {
-    __shared__ double red4[12];
-    // every block computes the same CG scalars; block 0 publishes them for the camera and vector
-    // kernels of this iteration (the kernel boundary orders the store before their reads)
-    auto publish = [&](const Scalars& sc) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            st->beta = sc.beta;
-            st->rz = sc.rz;
-            st->done = sc.done ? 1 : 0;
-        }
-    };
+    // the CG scalars of iteration k were published by the previous vector kernel (publish_next)
     if ((int)blockIdx.x < n_long_blk) {  // block-uniform: the long-track blocks, dispatched first
-        const Scalars sc = pcg_scalars(k, n_cam, rzc, rrc, st->bb, tol, red4);
-        publish(sc);
+        const Scalars sc = read_scalars(st);
         if (!sc.done)
             pcg_point_long(blockIdx.x, n_long_blk, n_obs, pt_ptr, cam_idx, Wp, Vinv, z, pold,
                            sc.beta, long_list, long_cnt, u);
@@ -513,8 +537,7 @@ __global__ __launch_bounds__(256) void bas_pcg_point(
             pc[i] = pold[8 * (size_t)c + i];
         }
     }
-    const Scalars sc = pcg_scalars(k, n_cam, rzc, rrc, st->bb, tol, red4);
-    publish(sc);
+    const Scalars sc = read_scalars(st);
     if (sc.done) return;
     if (valid && o1 - (o0 - j) > LONG_OBS) return;  // group-uniform: a long-track block's point
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
@@ -688,8 +711,8 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
     int k, int n_cam, const double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, const double* __restrict__ pv,
     const double* __restrict__ q, const double* __restrict__ pq, double* __restrict__ rzc,
-    double* __restrict__ rrc, PcgState* __restrict__ st) {
-    __shared__ double red4[4];
+    double* __restrict__ rrc, PcgState* __restrict__ st, double tol) {
+    __shared__ double red4[12];
     const bool done = st->done != 0;
     const double rz_k = st->rz;
     const int gi = blockIdx.x * blockDim.x + threadIdx.x;
@@ -730,6 +753,7 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
         }
     }
     if (gi == 0) st->iter = k + 1;
+    publish_next(k, n_cam, rzc, rrc, tol, st, gridDim.x, red4);
 }
 
 // Largest camera count for which the sharded solve finishes an iteration in one launch
@@ -750,9 +774,9 @@ __global__ __launch_bounds__(FV) void bas_pcg_finish_vec(
     int k, int n_cam, const double* __restrict__ su, const double* __restrict__ comm,
     const double* __restrict__ pv, const double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ rzc,
-    double* __restrict__ rrc, PcgState* __restrict__ st, int ntot) {
+    double* __restrict__ rrc, PcgState* __restrict__ st, int ntot, double tol) {
     __shared__ double pq_s[FINISH_VEC_MAX_CAM];
-    __shared__ double red4[4];
+    __shared__ double red4[12];
     const int tid = threadIdx.x;
     const int c = blockIdx.x * (FV / 8) + (tid >> 3), i = tid & 7;
     const bool valid = c < n_cam;
@@ -839,19 +863,26 @@ __global__ __launch_bounds__(FV) void bas_pcg_finish_vec(
         }
     }
     if (blockIdx.x == 0 && tid == 0) st->iter += 1;  // k-free: a captured window replays at any k
+    publish_next(k, n_cam, rzc, rrc, tol, st, gridDim.x, red4);
 }
 
 // One block: |b|^2 (canonical sum of the setup's per-camera shares) and the iteration count.
-__global__ __launch_bounds__(256) void bas_pcg_init(int n_cam, const double* __restrict__ bb_c,
+// ... and the CG scalars of iteration 0 (β = 0, rz_0, the convergence test), published as every
+// later iteration's are by publish_next.
+__global__ __launch_bounds__(256) void bas_pcg_init(int n_cam, const double* __restrict__ rzc,
+                                                    const double* __restrict__ bb_c, double tol,
                                                     PcgState* __restrict__ st) {
-    __shared__ double red4[4];
+    __shared__ double red4[12];
     const double bb = canon_sum(bb_c, n_cam, red4);
+    const Scalars sc = pcg_scalars(0, n_cam, rzc, bb_c, bb, tol, red4);
     if (threadIdx.x == 0) {
         st->bb = bb;
-        st->rz = 0.0;
+        st->rz = sc.rz;
+        st->beta = sc.beta;
         st->rr = bb;
         st->iter = 0;
-        st->done = 0;
+        st->done = sc.done ? 1 : 0;
+        st->cnt = 0u;
     }
 }
 
@@ -1270,7 +1301,7 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     const int rc = solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U,
                                V, W, gc, gp, lam, dc, 0, nullptr);
     if (rc != SFM_OK) return rc;
-    hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
+    hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
     SFM_HIP_CHECK(hipGetLastError());
     // 0 (the zero-initialised struct) = every 8 iterations, the library default; < 0 = never
     // (no host synchronisation: fully asynchronous, capturable in a hip graph).  A stream under
@@ -1296,7 +1327,7 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
                            cam_obs, w.u, w.Ud, w.z, w.pv, w.state, w.q, w.pq, 0, nullptr, ck.cb,
                            ck.nck, 0);
         hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
-                           w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);
+                           w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state, tol);
     }
     SFM_HIP_CHECK(hipGetLastError());
     if (solve_backsub(st, w, ck, n_pt, n_obs, pt_ptr, cam_idx, V, gp, dc, dp, false, nullptr) != SFM_OK)
@@ -1345,7 +1376,7 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
                            w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z,
                            w.pv, w.rzc, w.rrc, w.bad, 2, comm, ck.cb, ck.nck, ck.ntot);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rrc, w.state);
+        hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
         break;
     case SFM_BA_STAGE_ITER:  // -> comm[0, 8 n_cam)
         hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk + w.lblk), dim3(256), 0, st, k, n_pt, n_cam,
@@ -1360,7 +1391,7 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
         if (fused) {
             hipLaunchKernelGGL(bas_pcg_finish_vec, dim3((8 * n_cam + FV - 1) / FV), dim3(FV), 0, st,
                                k, n_cam, w.q, comm, w.pv, w.Mc, dc, w.r, w.z, w.rzc, w.rrc,
-                               w.state, ck.cb ? ck.ntot : 0);
+                               w.state, ck.cb ? ck.ntot : 0, tol);
             break;
         }
         hipLaunchKernelGGL(bas_pcg_camera, dim3(n_cam), dim3(CC), 0, st, k, n_cam, cam_ptr,
@@ -1368,7 +1399,7 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
                            ck.nck, ck.ntot);
         SFM_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r,
-                           w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state);
+                           w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state, tol);
         break;
     case SFM_BA_STAGE_BACKSUB:  // -> comm[0, 2) (chunk mode: [n_chunk][2])
         if (ck.cb) {
