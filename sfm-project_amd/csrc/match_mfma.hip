@@ -898,6 +898,18 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_grp_kernel
                     ts[c + 1] = vmed3(ts[c + 1], tb[c + 1], m1);
                     tb[c + 1] = max(tb[c + 1], m1);
                 }
+#ifdef MU_GRP_XPOSE  // A/B build only: round 4's permlane16_swap / DPP transpose for the column side
+                {
+                    const int key = transpose_max16(colacc, lane);
+                    const int xr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 +
+                                   ((lane >> 3) & 1) * 2 + ((lane >> 4) & 1);
+                    const int j = ch * CHUNK + tt * 32 + (xr & 3) + 8 * (xr >> 2) + 4 * h;
+                    if (!(lane & 1) && j < nb)
+                        lds_max_u32(colw_base + 4u * (unsigned)j,
+                                    ((unsigned)((key >> 7) + 0x7FFFFF) << 9) +
+                                        (unsigned)(kbase + (key & 127)));
+                }
+#else
                 // column maximum over the wave's 128 queries of each train row, through LDS
                 // (asm: the compiler neither sees these as aliasing the in-flight stage DMA nor
                 // reorders them — volatile asm keeps program order; the wait carries the data)
@@ -926,6 +938,7 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_grp_kernel
                                         (unsigned)(kbase + (k & 127));
                     lds_max_u32(colw_base + 4u * (unsigned)j, kw);
                 }
+#endif
             }
         }
     };
@@ -1309,10 +1322,14 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
 // query, one train each): a second e1 in the group means the nearest neighbour is not unique (->
 // exact row scan); else d2 = min(group runner-up d, outside bound [A - 2 e2 - 1, A - 2 e2]) and
 // the ratio test is decided exactly or, when the outside parity straddles it, by the row scan.
+// Grid: 8 * ceil(P / 8) blocks; XCD x (block b -> XCD b mod 8) takes the x-th contiguous run of
+// the pairs ordered by train image (pair_order), so the pairs one XCD finalises together share the
+// train descriptors the group rechecks read: they stay in that XCD's L2.
 template <int D>
 __global__ __launch_bounds__(MU_FT) void mutual_grp_finalize_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs,
+    const int32_t* __restrict__ pair_order, int n_pairs,
     const int2* __restrict__ rowres, const unsigned long long* __restrict__ colpart, int rnum,
     int rden, long long max_dist, int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
     int32_t* __restrict__ out_dist) {
@@ -1322,7 +1339,10 @@ __global__ __launch_bounds__(MU_FT) void mutual_grp_finalize_kernel(
     __shared__ int rj1[MU_FT];
     __shared__ unsigned char keepx[MU_FT];
     __shared__ int jx[MU_FT], dx[MU_FT];
-    const int p = blockIdx.x, tid = threadIdx.x;
+    const int per_xcd = (int)(gridDim.x >> 3);
+    const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+    if (sblk >= n_pairs) return;  // block-uniform, before any barrier
+    const int p = pair_order[sblk], tid = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
     if (na <= 0 || nb <= 0) {
@@ -1766,18 +1786,20 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
                                (size_t)k_pad * 4, st, desc_i8, n_kp, k_max, k_pad, norm, cinit,
                                zero_row, pairs, n_qblk, pair_order, n_blk, rw2, colpart);
             SFM_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(mutual_grp_finalize_kernel<128>, dim3(n_pairs), dim3(MU_FT),
-                               (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
-                               rw2, colpart, prm->ratio_num, prm->ratio_den,
+            hipLaunchKernelGGL(mutual_grp_finalize_kernel<128>, dim3(8 * ((n_pairs + 7) / 8)),
+                               dim3(MU_FT), (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad,
+                               norm, pairs, pair_order, n_pairs, rw2, colpart, prm->ratio_num,
+                               prm->ratio_den,
                                (long long)prm->max_dist, out_count, out_match, out_dist);
         } else {
             hipLaunchKernelGGL(mfma_mutual_grp_kernel<256>, dim3(grid), dim3(64 * MU_WAVES),
                                (size_t)k_pad * 4, st, desc_i8, n_kp, k_max, k_pad, norm, cinit,
                                zero_row, pairs, n_qblk, pair_order, n_blk, rw2, colpart);
             SFM_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(mutual_grp_finalize_kernel<256>, dim3(n_pairs), dim3(MU_FT),
-                               (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad, norm, pairs,
-                               rw2, colpart, prm->ratio_num, prm->ratio_den,
+            hipLaunchKernelGGL(mutual_grp_finalize_kernel<256>, dim3(8 * ((n_pairs + 7) / 8)),
+                               dim3(MU_FT), (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad,
+                               norm, pairs, pair_order, n_pairs, rw2, colpart, prm->ratio_num,
+                               prm->ratio_den,
                                (long long)prm->max_dist, out_count, out_match, out_dist);
         }
         SFM_HIP_CHECK(hipGetLastError());
