@@ -837,6 +837,28 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_grp_kernel
     const int kbase = 511 - 127 - wave * QT * 32;            // 511 - q_wg = kbase + (key & 127)
     const unsigned colw_base = lds_addr(lds_colw);
 
+    // the 16 partial keys of the reader's train row (4 ds_read_b128 in flight) -> its maximum over
+    // the wave's 128 queries -> the u32 column state
+    auto consume = [&](v4i (&g)[4], int j) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]));
+        int k = vmax3(g[0].x, g[0].y, g[0].z);
+        k = vmax3(k, g[0].w, g[1].x);
+        k = vmax3(k, g[1].y, g[1].z);
+        k = vmax3(k, g[1].w, g[2].x);
+        k = vmax3(k, g[2].y, g[2].z);
+        k = vmax3(k, g[2].w, g[3].x);
+        k = vmax3(k, g[3].y, g[3].z);
+        k = max(k, g[3].w);
+        k = max(k, __builtin_amdgcn_ds_swizzle(k, 0x401F));  // lane ^ 16: the other segment
+        if (sg == 0 && j < nb) {
+            // u32 state: (0x7FFFFF - d^2 - p_j) << 9 | (511 - query in workgroup)
+            const unsigned kw = ((unsigned)((k >> 7) + 0x7FFFFF) << 9) + (unsigned)(kbase + (k & 127));
+            lds_max_u32(colw_base + 4u * (unsigned)j, kw);
+        }
+    };
+    v4i gq[4];
+    int jq = 0;
+
     auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
         if (ch + 1 < n_chunk) stage(ch + 1, nxt);
         const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
@@ -910,6 +932,9 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_grp_kernel
                                         (unsigned)(kbase + (key & 127)));
                 }
 #else
+#ifdef MU_GRP_PIPE   // A/B build only: the previous tile's column reads consumed one tile later
+                if (tt > 0) consume(gq, jq);
+#endif
                 // column maximum over the wave's 128 queries of each train row, through LDS
                 // (asm: the compiler neither sees these as aliasing the in-flight stage DMA nor
                 // reorders them — volatile asm keeps program order; the wait carries the data)
@@ -917,29 +942,18 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_grp_kernel
                 for (int r = 0; r < 16; ++r)
                     asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(red_w), "v"(colacc[r]),
                                  "i"(r * 128));
-                v4i g[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    asm volatile("ds_read_b128 %0, %1" : "=v"(g[i]) : "v"(red_ra[i]));
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]));
-                int k = vmax3(g[0].x, g[0].y, g[0].z);
-                k = vmax3(k, g[0].w, g[1].x);
-                k = vmax3(k, g[1].y, g[1].z);
-                k = vmax3(k, g[1].w, g[2].x);
-                k = vmax3(k, g[2].y, g[2].z);
-                k = vmax3(k, g[2].w, g[3].x);
-                k = vmax3(k, g[3].y, g[3].z);
-                k = max(k, g[3].w);
-                k = max(k, __builtin_amdgcn_ds_swizzle(k, 0x401F));  // lane ^ 16: the other segment
-                const int j = ch * CHUNK + tt * 32 + jrow;
-                if (sg == 0 && j < nb) {
-                    // u32 state: (0x7FFFFF - d^2 - p_j) << 9 | (511 - query in workgroup)
-                    const unsigned kw = ((unsigned)((k >> 7) + 0x7FFFFF) << 9) +
-                                        (unsigned)(kbase + (k & 127));
-                    lds_max_u32(colw_base + 4u * (unsigned)j, kw);
-                }
+                    asm volatile("ds_read_b128 %0, %1" : "=v"(gq[i]) : "v"(red_ra[i]));
+                jq = ch * CHUNK + tt * 32 + jrow;
+#ifndef MU_GRP_PIPE
+                consume(gq, jq);
+#endif
 #endif
             }
+#if defined(MU_GRP_PIPE) && !defined(MU_GRP_XPOSE)
+            if (nt > 0) consume(gq, jq);
+#endif
         }
     };
     if (n_chunk > 0) stage(0, lds0);
