@@ -1777,9 +1777,10 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     }();
     // whole pairs per XCD (blocks of one pair never straddle two XCDs' ranges)
     const int grid = 8 * ((n_pairs + 7) / 8) * n_qblk;
-    // mutual rule: the group-max kernel (default) or the round-4 top-2 kernel (SFM_K1_GRP=0)
+    // mutual rule: the round-4 top-2 kernel (default) or the round-5 group-max kernel
+    // (SFM_K1_GRP=1: bit-identical, measured slower — DESIGN.md §4.1 "Round 5")
     const char* grp_env = getenv("SFM_K1_GRP");
-    const bool grp = rows && !(grp_env && grp_env[0] == '0');
+    const bool grp = rows && grp_env && grp_env[0] == '1';
     if (grp) {
         SFM_HIP_CHECK(hipMemsetAsync(colpart, 0, sizeof(unsigned long long) * (size_t)n_pairs * k_pad, st));
         hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
