@@ -69,6 +69,15 @@ def main():
     _, _, info = P.solve(lin, lam, max_iter=200, tol=1e-10)
     it10 = int(info[0].item())
     t_jtj = timed(lambda: P.linearize(cams, pts), 10)
+    # the sharding-invariant form bundle_adjust runs (BA_CHUNKS chunks, reconstruction.BAChunks)
+    Pc = R.BAProblem(prob["pp"], prob["cam_idx"], prob["pt_idx"], prob["uv"], n_cam, n_pt,
+                     chunks=R.BA_CHUNKS)
+    linc = Pc.linearize(cams, pts)
+    c0 = timed(lambda: Pc.solve(linc, lam, max_iter=0, tol=0.0), 20)
+    cn = timed(lambda: Pc.solve(linc, lam, max_iter=cg, tol=0.0), 10)
+    t_jtj_c = timed(lambda: Pc.linearize(cams, pts), 10)
+    t_cost = timed(lambda: P.cost(cams, pts), 20)
+    t_cost_c = timed(lambda: Pc.cost(cams, pts), 20)
     out = {
         "stage": "K4 BA step (Schur-complement PCG)", "n_cam": n_cam, "n_pt": n_pt, "n_obs": n_obs,
         "cg_iter_ms": per_it, "setup_backsub_ms": t0,
@@ -76,6 +85,8 @@ def main():
                      "achieved_GBs": bytes_it / (per_it * 1e-3) / 1e9, "peak_GBs": PEAK_HBM / 1e9,
                      "frac": bytes_it / (per_it * 1e-3) / PEAK_HBM},
         "cg_iters_to_1e-6": it6, "lm_step_ms": t_step, "jtj_ms": t_jtj,
+        "chunked": {"chunks": R.BA_CHUNKS, "cg_iter_ms": (cn - c0) / cg, "setup_backsub_ms": c0,
+                    "jtj_ms": t_jtj_c, "cost_ms": t_cost_c, "cost_ms_unchunked": t_cost},
         "default_lm_step": {"max_cg": 200, "cg_tol": 1e-10, "cg_iters": it10,
                             "ms_poll_every_8": t_def, "ms_no_poll_all_launches": t_def_async},
     }
