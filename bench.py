@@ -701,7 +701,7 @@ def cfg5_run(n_img, k, n_pts, steps, warmup, world, rank, local, pcg):
                     for kk, v in rec.timings.items()},
         "bundle_adjustments": rec.ba_log,
         "ba_phase_s": {k: round(float(sum(b.get(k, 0.0) for b in rec.ba_log)), 4)
-                       for k in ("select_s", "setup_s", "lm_s", "post_s", "s")},
+                       for k in ("select_s", "entry_wait_s", "setup_s", "problem_s", "lm_s", "post_s", "s")},
         "lm_steps": int(sum(b["lm_steps"] for b in rec.ba_log)),
         "cg_iters": int(sum(b["cg_iters"] for b in rec.ba_log)),
         "pcg_branches": sorted({b["pcg"] for b in rec.ba_log}),

@@ -6,17 +6,20 @@
 //   ba_jtj_kernel      camera waves first (wave per (camera, split), four per block: J_c
 //                      recomputed from the camera's rotation — computed once per wave — over a
 //                      contiguous share of the camera's observations (cam_ptr/cam_obs CSR), fixed
-//                      lane-strided order + shuffle tree -> U_c, g_c), then observation blocks
+//                      lane-strided order + recursive-halving wave sum -> U_c, g_c), then
+//                      observation blocks
 //                      (thread per observation, enough waves to stream HBM: residual, J_c (2x8),
 //                      J_p (2x3) -> res, W = w J_c^T J_p staged through LDS for coalesced stores;
 //                      V_p, g_p by a segmented scan of the point terms across the wave (points are
 //                      point-major contiguous), boundary-cut segments to head/tail records.  The
 //                      two halves are independent, so the latency-bound camera reduction runs
 //                      underneath the observation stream.
-//   ba_finish_kernel   points spanning waves, empty points, the cost;
+//   ba_finish_kernel   points spanning waves, empty points, the cost; chunk mode
+//                      (sfm_ba_set_chunks): also U_c / g_c and the cost from the chunk partials;
 //   ba_final_kernel    camera split sums (only with fewer than 256 cameras).
 // Algorithmic HBM traffic ~300 B/observation; this is an HBM-bound stage.
 #include <algorithm>
+#include <cstdlib>
 
 #include "camera_model.h"
 #include "sfm_internal.h"
@@ -132,18 +135,21 @@ __device__ __forceinline__ void obs_block(
     double* __restrict__ lds, int nck, const sfm::ChunkOff& cobs, const sfm::ChunkOff& vst) {
     __shared__ double cred[4];
     const int lane = threadIdx.x & 63;
-    // Chunk mode (nck > 0): waves tile a virtual index space in which every chunk starts at a
-    // multiple of 64 (vst: the chunks' virtual starts), so where a point's observations are cut
-    // into waves — and with it the association of its V_p / g_p sums — depends only on its chunk.
+    // Chunk mode (nck > 0): blocks tile a virtual index space in which every chunk starts at a
+    // multiple of 256 (vst: the chunks' virtual starts, chunk_layout), so where a point's
+    // observations are cut into waves — and with it the association of its V_p / g_p sums — and
+    // the blocks' cost shares depend only on the chunk.
     const int vo = ob * 256 + threadIdx.x;
     const int wv = vo >> 6;  // wave index (blocks are whole waves)
     int o = vo, wfirst = wv << 6, wend = n_obs;
     if (nck > 0) {
-        int k = 0;
-        while (k + 1 < nck && vo >= vst.v[k + 1]) ++k;
-        o = cobs.v[k] + (vo - vst.v[k]);
-        wfirst = cobs.v[k] + ((wv << 6) - vst.v[k]);
-        wend = vo < vst.v[nck] ? cobs.v[k + 1] : 0;
+        // chunks start at block boundaries: the block start decides (a uniform, scalar lookup)
+        int c0, c1, v0, v1;
+        sfm::chunk_of(ob << 8, nck, vst, cobs, c0, c1);
+        sfm::chunk_of(ob << 8, nck, vst, vst, v0, v1);
+        o = c0 + (vo - v0);
+        wfirst = c0 + ((wv << 6) - v0);
+        wend = vo < vst.v[nck] ? c1 : 0;
     }
     const bool valid = o < wend;
     double* wimg = lds + (threadIdx.x >> 6) * OBS_LDS;
@@ -264,39 +270,35 @@ __device__ __forceinline__ void cam_accum_half(double (&acc)[NU], const ObsLin& 
     }
 }
 
-// U_c (both triangles) and g_c entries t in [T0, T0 + N) from acc[t - T0].
-template <int T0, int N>
-__device__ __forceinline__ void cam_store(const double (&acc)[NU], double* __restrict__ Uc,
-                                          double* __restrict__ g) {
-    int t = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = i; j < 8; ++j) {
-            if (t >= T0 && t < T0 + N) {
-                Uc[8 * i + j] = acc[t - T0];
-                Uc[8 * j + i] = acc[t - T0];
-            }
-            ++t;
-        }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        if (36 + i >= T0 && 36 + i < T0 + N) g[i] = acc[36 + i - T0];
+// Sum t of the 44 (upper-triangle U_c entry in row-major order, then g_c) into U_c (both
+// triangles) or g_c.
+__device__ __forceinline__ void cam_store_one(int t, double v, double* __restrict__ Uc,
+                                              double* __restrict__ g) {
+    if (t >= 36) {
+        g[t - 36] = v;
+        return;
+    }
+    int i = 0;
+    while (t >= 8 - i) { t -= 8 - i; ++i; }
+    const int j = i + t;
+    Uc[8 * i + j] = v;
+    Uc[8 * j + i] = v;
 }
 
+// Chunk mode (cb != nullptr): `splits` = G waves per camera; wave g of camera c takes chunks
+// g, g + G, ... of the camera's observations (cb: the camera's list cut at the chunk starts), one
+// fixed-order partial per chunk into part[c][chunk], rotation computed once per wave.
 __device__ __forceinline__ void camera_wave(
     int cw, const double* __restrict__ cams, const double* __restrict__ pp,
     const double* __restrict__ pts, const int32_t* __restrict__ pt_idx,
     const double* __restrict__ uv, const int32_t* __restrict__ cam_ptr,
     const int32_t* __restrict__ cam_obs, double loss_s, int splits, double* __restrict__ part,
-    double* __restrict__ U, double* __restrict__ gc, const int32_t* __restrict__ cb) {
+    double* __restrict__ U, double* __restrict__ gc, const int32_t* __restrict__ cb, int nck) {
     const int lane = threadIdx.x & 63;
     const int hw = cw % CH;  // which NUH of the 44 sums this wave accumulates (wave-uniform)
     cw /= CH;
     const int c = cw / splits, s = cw - c * splits;
     double acc[NU];  // entries outside [hw*NUH, hw*NUH + NUH) are dead when CH > 1
-#pragma unroll
-    for (int i = 0; i < NU; ++i) acc[i] = 0.0;
     const double* cam = cams + 8 * (size_t)c;
     double R[9];
 #ifdef BA_ABL_NOROT  // ablation (timing only)
@@ -304,80 +306,73 @@ __device__ __forceinline__ void camera_wave(
 #else
     rotmat(cam[0], cam[1], cam[2], R);
 #endif
-    int e0, e1;
-    if (cb) {   // chunk mode: split s = the camera's observations in chunk s (sfm_ba_set_chunks)
-        e0 = cb[(size_t)c * (splits + 1) + s];
-        e1 = cb[(size_t)c * (splits + 1) + s + 1];
-    } else {
-        const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
-        const int len = (c1 - c0 + splits - 1) / splits;
-        e0 = c0 + s * len;
-        e1 = min(c1, e0 + len);
-    }
     // CAM_MLP observations per step: the dependent gathers (cam_obs -> pt_idx -> point, uv) of
     // all of them are issued before any is used (memory-level parallelism; latency-bound waves)
-    for (int e = e0 + lane; e < e1; e += CAM_MLP * 64) {
-        int o[CAM_MLP], pi[CAM_MLP];
-        double X[CAM_MLP][3], u[CAM_MLP], v[CAM_MLP];
+    auto accumulate = [&](int e0, int e1) {
 #pragma unroll
-        for (int q = 0; q < CAM_MLP; ++q) o[q] = (e + q * 64 < e1) ? cam_obs[e + q * 64] : -1;
-#ifdef BA_ABL_NOGATHER  // ablation (timing only): observation data from the camera-major position
+        for (int i = 0; i < NU; ++i) acc[i] = 0.0;
+        for (int e = e0 + lane; e < e1; e += CAM_MLP * 64) {
+            int o[CAM_MLP], pi[CAM_MLP];
+            double X[CAM_MLP][3], u[CAM_MLP], v[CAM_MLP];
 #pragma unroll
-        for (int q = 0; q < CAM_MLP; ++q) { pi[q] = (e + q * 64) % 100000; o[q] = o[q] >= 0 ? e + q * 64 : -1; }
-#else
+            for (int q = 0; q < CAM_MLP; ++q) o[q] = (e + q * 64 < e1) ? cam_obs[e + q * 64] : -1;
 #pragma unroll
-        for (int q = 0; q < CAM_MLP; ++q) pi[q] = o[q] >= 0 ? pt_idx[o[q]] : 0;
-#endif
+            for (int q = 0; q < CAM_MLP; ++q) pi[q] = o[q] >= 0 ? pt_idx[o[q]] : 0;
 #pragma unroll
-        for (int q = 0; q < CAM_MLP; ++q) {
-            const int oo = o[q] >= 0 ? o[q] : 0;
-            X[q][0] = pts[3 * (size_t)pi[q]];
-            X[q][1] = pts[3 * (size_t)pi[q] + 1];
-            X[q][2] = pts[3 * (size_t)pi[q] + 2];
-            u[q] = uv[2 * (size_t)oo];
-            v[q] = uv[2 * (size_t)oo + 1];
-        }
+            for (int q = 0; q < CAM_MLP; ++q) {
+                const int oo = o[q] >= 0 ? o[q] : 0;
+                X[q][0] = pts[3 * (size_t)pi[q]];
+                X[q][1] = pts[3 * (size_t)pi[q] + 1];
+                X[q][2] = pts[3 * (size_t)pi[q] + 2];
+                u[q] = uv[2 * (size_t)oo];
+                v[q] = uv[2 * (size_t)oo + 1];
+            }
 #pragma unroll
-        for (int q = 0; q < CAM_MLP; ++q) {
-            if (o[q] < 0) break;
-            ObsLin L;
-            linearize(R, cam, pp + 2 * (size_t)c, X[q], u[q], v[q], loss_s, false, L);
-            if (CH == 1) {
-                int t = 0;
+            for (int q = 0; q < CAM_MLP; ++q) {
+                if (o[q] < 0) break;
+                ObsLin L;
+                linearize(R, cam, pp + 2 * (size_t)c, X[q], u[q], v[q], loss_s, false, L);
+                if (CH == 1) {
+                    int t = 0;
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
+                    for (int i = 0; i < 8; ++i)
 #pragma unroll
-                    for (int j = i; j < 8; ++j)
-                        acc[t++] += L.w * (L.Jc[i] * L.Jc[j] + L.Jc[8 + i] * L.Jc[8 + j]);
+                        for (int j = i; j < 8; ++j)
+                            acc[t++] += L.w * (L.Jc[i] * L.Jc[j] + L.Jc[8 + i] * L.Jc[8 + j]);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) acc[36 + i] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
-            } else {
-                // the same expressions, sum t of this wave's half into acc[t - hw*NUH]
-                if (hw == 0) cam_accum_half<0>(acc, L);
-                else cam_accum_half<1>(acc, L);
+                    for (int i = 0; i < 8; ++i) acc[36 + i] += L.w * (L.Jc[i] * L.r[0] + L.Jc[8 + i] * L.r[1]);
+                } else {
+                    // the same expressions, sum t of this wave's half into acc[t - hw*NUH]
+                    if (hw == 0) cam_accum_half<0>(acc, L);
+                    else cam_accum_half<1>(acc, L);
+                }
             }
         }
-    }
+    };
+    // the wave's NR sums by recursive halving (~NR exchanges, not 6 NR): lane l ends holding sum
+    // t0 + idx and stores it, so the partial / U_c row is written by one store per lane
     constexpr int NR = CH == 1 ? NU : NUH;  // live sums of this wave
-#ifndef BA_ABL_NORED  // ablation (timing only): no cross-lane reduction
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        double v = acc[i];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
-        acc[i] = v;
-    }
-#endif
-    if (lane != 0) return;
-    const int t0 = CH == 1 ? 0 : hw * NUH;  // sum index of acc[0]
-    if (splits > 1 || cb) {
-        double* o = part + ((size_t)c * splits + s) * NU + t0;
-#pragma unroll
-        for (int i = 0; i < NR; ++i) o[i] = acc[i];
+    const int t0 = CH == 1 ? 0 : hw * NUH;
+    if (cb) {   // chunk mode: chunks s, s + G, ... (sfm_ba_set_chunks)
+        for (int k = s; k < nck; k += splits) {
+            accumulate(cb[(size_t)c * (nck + 1) + k], cb[(size_t)c * (nck + 1) + k + 1]);
+            int idx;
+            if (sfm::wave_halving_sum<NR>(acc, lane, idx))
+                part[((size_t)c * nck + k) * NU + t0 + idx] = acc[0];
+        }
         return;
     }
-    if (CH == 1 || hw == 0) cam_store<0, NR>(acc, U + 64 * (size_t)c, gc + 8 * (size_t)c);
-    else cam_store<NUH, NR>(acc, U + 64 * (size_t)c, gc + 8 * (size_t)c);
+    const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
+    const int len = (c1 - c0 + splits - 1) / splits;
+    const int e0 = c0 + s * len;
+    accumulate(e0, min(c1, e0 + len));
+    int idx;
+    if (!sfm::wave_halving_sum<NR>(acc, lane, idx)) return;
+    if (splits > 1) {
+        part[((size_t)c * splits + s) * NU + t0 + idx] = acc[0];
+        return;
+    }
+    cam_store_one(t0 + idx, acc[0], U + 64 * (size_t)c, gc + 8 * (size_t)c);
 }
 
 // One launch for both independent halves of the linearisation: blocks [0, n_camb) are the
@@ -408,7 +403,7 @@ __global__ __launch_bounds__(256) BA_JTJ_ATTR void ba_jtj_kernel(
         const int cw = b * 4 + (threadIdx.x >> 6);
         if (cw < n_camw)
             camera_wave(cw, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U,
-                        gc, cb);
+                        gc, cb, nck);
     } else {
         obs_block(b - n_camb, n_obs, cams, pp, pts, cam_idx, pt_idx, pt_ptr, uv, loss_s, W, res,
                   V, gp, seg, seg_pt, cost_blk, lds, nck, cobs, vst);
@@ -425,7 +420,7 @@ __global__ __launch_bounds__(256) void ba_cam_kernel(
     const int cw = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (cw < n_camw)
         camera_wave(cw, cams, pp, pts, pt_idx, uv, cam_ptr, cam_obs, loss_s, splits, part, U, gc,
-                    nullptr);
+                    nullptr, 0);
 }
 __global__ __launch_bounds__(256) void ba_obs_kernel(
     int n_obs, const double* __restrict__ cams, const double* __restrict__ pp,
@@ -441,35 +436,59 @@ __global__ __launch_bounds__(256) void ba_obs_kernel(
 }
 #endif
 
-__device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
-                             const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
-                             const int32_t* __restrict__ seg_pt, double* __restrict__ V,
-                             double* __restrict__ gp, const double* __restrict__ cost_blk,
-                             double* __restrict__ cost, int nck, const sfm::ChunkOff& cobs,
-                             const sfm::ChunkOff& vst);
+__device__ __forceinline__ void chunk_final_one(int g, int n_cam, int nck, int exp,
+                                                const double* __restrict__ part,
+                                                double* __restrict__ U, double* __restrict__ gc);
 
-__global__ __launch_bounds__(256) void ba_finish_kernel(
-    int n_wave, int n_blk, int n_pt, const int32_t* __restrict__ pt_ptr,
-    const double* __restrict__ seg, const int32_t* __restrict__ seg_pt, double* __restrict__ V,
-    double* __restrict__ gp, const double* __restrict__ cost_blk, double* __restrict__ cost,
-    int nck, sfm::ChunkOff cobs, sfm::ChunkOff vst) {
-    finish_block(blockIdx.x, n_wave, n_blk, n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost, nck,
-                 cobs, vst);
+// Chunk mode: chunk k's cost = the fixed-order sum of its 256-observation blocks' shares
+// blk[vst_k / 256, vst_{k+1} / 256) (chunks start at block boundaries of the virtual index space,
+// so the blocks and this order depend only on the chunk): lane-strided, then an xor tree; one wave
+// per chunk (waves w, w + nwave, ... of the calling block).  exp = 0: cost[0] = the canonical tree
+// over the chunks; exp = 1: cost[k] per chunk.  Called by every thread of the block.
+__device__ __forceinline__ void chunk_cost_finish(int nck, int exp, const sfm::ChunkOff& vst,
+                                                  const double* __restrict__ blk,
+                                                  double* __restrict__ cost, int nwave) {
+    __shared__ double kc[SFM_BA_MAX_CHUNKS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int k = tid >> 6; k < nck; k += nwave) {
+        const int b0 = vst.v[k] >> 8, b1 = vst.v[k + 1] >> 8;
+        double s = 0.0;
+#pragma unroll 4
+        for (int b = b0 + lane; b < b1; b += 64) s += blk[b];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0) kc[k] = s;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    if (exp) {
+        for (int k = 0; k < nck; ++k) cost[k] = kc[k];
+        return;
+    }
+    double a[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] = k < nck ? kc[k] : 0.0;
+    cost[0] = sfm::chunk_tree16(a);
 }
 
 // Finish work (256-thread block fb): points spanning waves (the point whose tail record wave g
 // wrote owns tail + the head records of the following waves up to its last observation, fixed
 // order), zero V_p / g_p for points without observations, and (block 0) the cost as a
-// fixed-order sum of the per-block shares.
-__device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
-                             const int32_t* __restrict__ pt_ptr, const double* __restrict__ seg,
-                             const int32_t* __restrict__ seg_pt, double* __restrict__ V,
-                             double* __restrict__ gp, const double* __restrict__ cost_blk,
-                             double* __restrict__ cost, int nck, const sfm::ChunkOff& cobs,
-                             const sfm::ChunkOff& vst) {
+// fixed-order sum of the per-block shares.  Chunk mode: block 0 forms the chunk costs
+// (chunk_cost_finish) and thread g < n_cam * 44 the camera sum g from the chunk partials.
+__global__ __launch_bounds__(256) void ba_finish_kernel(
+    int n_wave, int n_blk, int n_pt, const int32_t* __restrict__ pt_ptr,
+    const double* __restrict__ seg, const int32_t* __restrict__ seg_pt, double* __restrict__ V,
+    double* __restrict__ gp, const double* __restrict__ cost_blk, double* __restrict__ cost,
+    int nck, sfm::ChunkOff cobs, sfm::ChunkOff vst, int n_cam, int exp,
+    const double* __restrict__ part, double* __restrict__ U, double* __restrict__ gc) {
+    const int fb = blockIdx.x;
     const int tid = threadIdx.x;
     const int g = fb * 256 + tid;
-    if (fb == 0) {
+    if (nck > 0) {
+        if (fb == 0) chunk_cost_finish(nck, exp, vst, cost_blk, cost, 4);
+        if (g < n_cam * NU) chunk_final_one(g, n_cam, nck, exp, part, U, gc);
+    } else if (fb == 0) {
         __shared__ double red[4];
         double s = 0.0;  // fixed order (w = tid, tid + 256, ...); unrolled so the loads overlap
 #pragma unroll 8
@@ -495,9 +514,10 @@ __device__ void finish_block(int fb, int n_wave, int n_blk, int n_pt,
             a[NV - 1] = 0.0;
             int vl = pt_ptr[p + 1] - 1;   // the point's last observation, as a virtual index
             if (nck > 0) {
-                int k = 0;
-                while (k + 1 < nck && vl >= cobs.v[k + 1]) ++k;
-                vl = vst.v[k] + (vl - cobs.v[k]);
+                int c0, c1, v0, v1;
+                sfm::chunk_of(vl, nck, cobs, cobs, c0, c1);
+                sfm::chunk_of(vl, nck, cobs, vst, v0, v1);
+                vl = v0 + (vl - c0);
             }
             const int w_last = vl >> 6;
             for (int w = g + 1; w <= w_last; ++w) {
@@ -530,14 +550,12 @@ __global__ __launch_bounds__(256) void ba_final_kernel(int n_cam, int splits,
     }
 }
 
-// Chunk mode: thread per (camera, sum t).  exp = 0: U_c / g_c = the canonical tree over the chunk
-// partials; exp = 1 (a shard): the chunk partials themselves, U [nck][n_cam][64], gc [nck][n_cam][8].
-__global__ __launch_bounds__(256) void ba_chunk_final_kernel(int n_cam, int nck, int exp,
-                                                             const double* __restrict__ part,
-                                                             double* __restrict__ U,
-                                                             double* __restrict__ gc) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_cam * NU) return;
+// Chunk mode, thread g = (camera, sum t) (run by ba_finish_kernel).  exp = 0: U_c / g_c = the
+// canonical tree over the chunk partials; exp = 1 (a shard): the chunk partials themselves,
+// U [nck][n_cam][64], gc [nck][n_cam][8].
+__device__ __forceinline__ void chunk_final_one(int g, int n_cam, int nck, int exp,
+                                                const double* __restrict__ part,
+                                                double* __restrict__ U, double* __restrict__ gc) {
     const int c = g / NU, k = g - c * NU;
     int i = 0, j = 0;
     if (k < 36) {
@@ -606,10 +624,10 @@ __global__ __launch_bounds__(256) void ba_cost_kernel(
     if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// Chunk mode: CKB blocks per chunk; block b of chunk k sums 0.5 rho over the chunk's observations
-// at chunk-relative positions (b + i CKB) 256 + tid (an order that depends only on the chunk), a
-// per-thread sum, then the wave trees and the 4 waves in order -> part[k CKB + b].
-constexpr int CKB = 64;
+// Chunk mode: 0.5 rho at trial parameters over the virtual index space of sfm_ba_jtj (every chunk
+// starts at a 256-observation block boundary, chunk_layout): block b -> the fixed-order share of
+// its (at most 256) observations of one chunk, part[b]; ba_cost_chunk_final then forms the chunk
+// costs exactly as ba_finish_kernel forms the linearisation's (chunk_cost_finish).
 __device__ __forceinline__ double half_rho(const double* __restrict__ cams, const double* __restrict__ pp,
                                            const double* __restrict__ pts, int c, int p, double u,
                                            double v, double loss_s) {
@@ -636,17 +654,20 @@ __device__ __forceinline__ double half_rho(const double* __restrict__ cams, cons
 }
 
 __global__ __launch_bounds__(256) void ba_cost_chunk_kernel(
-    sfm::ChunkOff co, const double* __restrict__ cams, const double* __restrict__ pp,
-    const double* __restrict__ pts, const int32_t* __restrict__ cam_idx,
-    const int32_t* __restrict__ pt_idx, const double* __restrict__ uv, double loss_s,
-    double* __restrict__ part) {
+    int nck, sfm::ChunkOff cobs, sfm::ChunkOff vst, const double* __restrict__ cams,
+    const double* __restrict__ pp, const double* __restrict__ pts,
+    const int32_t* __restrict__ cam_idx, const int32_t* __restrict__ pt_idx,
+    const double* __restrict__ uv, double loss_s, double* __restrict__ part) {
     __shared__ double red[4];
-    const int k = blockIdx.x / CKB, b = blockIdx.x - k * CKB;
-    const int o0 = co.v[k], o1 = co.v[k + 1];
+    const int vo = blockIdx.x * 256 + threadIdx.x;
+    int c0, c1, v0, v1;   // chunks start at block boundaries: the block decides (scalar lookup)
+    sfm::chunk_of((int)blockIdx.x << 8, nck, vst, cobs, c0, c1);
+    sfm::chunk_of((int)blockIdx.x << 8, nck, vst, vst, v0, v1);
+    const int o = c0 + (vo - v0);
     double h = 0.0;
-    for (int o = o0 + b * 256 + (int)threadIdx.x; o < o1; o += CKB * 256)
-        h += half_rho(cams, pp, pts, cam_idx[o], pt_idx[o], uv[2 * (size_t)o], uv[2 * (size_t)o + 1],
-                      loss_s);
+    if (o < c1)
+        h = half_rho(cams, pp, pts, cam_idx[o], pt_idx[o], uv[2 * (size_t)o], uv[2 * (size_t)o + 1],
+                     loss_s);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) h += __shfl_down(h, off, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = h;
@@ -654,30 +675,12 @@ __global__ __launch_bounds__(256) void ba_cost_chunk_kernel(
     if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// One wave: chunk k's cost = its CKB block partials in order (lane-strided + shuffle tree);
-// exp = 0: cost[0] = the canonical tree over the chunks; exp = 1: cost[k] per chunk.
-__global__ __launch_bounds__(64) void ba_cost_chunk_final(int nck, int exp, const double* __restrict__ part,
-                                                          double* __restrict__ cost) {
-    const int lane = threadIdx.x;
-    double a[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        double v = 0.0;
-        if (k < nck) {
-            v = part[(size_t)k * CKB + lane];   // CKB == 64: one partial per lane
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-        }
-        a[k] = v;
-    }
-    if (lane != 0) return;
-    if (exp) {
-        for (int k = 0; k < nck; ++k) cost[k] = a[k];
-        return;
-    }
-    cost[0] = sfm::chunk_tree16(a);
+// One block of 16 waves: wave k forms chunk k's cost (chunk_cost_finish).
+__global__ __launch_bounds__(1024) void ba_cost_chunk_final(int nck, int exp, sfm::ChunkOff vst,
+                                                            const double* __restrict__ part,
+                                                            double* __restrict__ cost) {
+    chunk_cost_finish(nck, exp, vst, part, cost, 16);
 }
-static_assert(CKB == 64, "ba_cost_chunk_final: one block partial per lane");
 
 __global__ __launch_bounds__(256) void ba_chunk_tree_kernel(int nck, long long n,
                                                             const double* __restrict__ parts,
@@ -764,6 +767,35 @@ __global__ __launch_bounds__(256) void ba_update_kernel(int n_cam, const double*
     }
 }
 
+// Chunk mode: cobs = the chunks' observation offsets, vst = their starts in the virtual index
+// space in which every chunk begins at a 256-observation block boundary (so an observation wave /
+// block, and every order built on them, depends only on its chunk); returns the virtual count.
+// Chunk mode: camera waves per camera (each takes chunks g, g + G, ...): enough for
+// CHUNK_WAVE_TARGET waves in all (500 cameras x 8 chunks: one wave per chunk measured 119 us
+// per K3 call against 126 us for one wave per camera, profiles/r05/ba_jtj_chunk_ab.txt);
+// SFM_BA_CKW overrides (A/B).  Any G gives the same bits (a chunk's partial does not depend on
+// which wave forms it).
+constexpr int CHUNK_WAVE_TARGET = 4096;
+int chunk_waves(int nck, int n_cam) {
+    static const int env = [] {
+        const char* e = getenv("SFM_BA_CKW");
+        return e ? atoi(e) : 0;
+    }();
+    const int g = env > 0 ? env : (CHUNK_WAVE_TARGET + n_cam - 1) / std::max(n_cam, 1);
+    return std::max(1, std::min(nck, g));
+}
+
+int chunk_layout(const sfm_ctx* ctx, sfm::ChunkOff& cobs, sfm::ChunkOff& vst) {
+    const int nck = ctx->ba_nchunk;
+    vst.v[0] = 0;
+    for (int k = 0; k < nck; ++k) {
+        cobs.v[k] = ctx->ba_chunk_obs[k];
+        vst.v[k + 1] = vst.v[k] + ((ctx->ba_chunk_obs[k + 1] - ctx->ba_chunk_obs[k] + 255) & ~255);
+    }
+    cobs.v[nck] = ctx->ba_chunk_obs[nck];
+    return vst.v[nck];
+}
+
 }  // namespace
 
 extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double* pp,
@@ -797,42 +829,36 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
     SFM_REQUIRE(cams && pp && pts && cam_idx && pt_idx && uv && pt_ptr && cam_ptr && cam_obs && U &&
                     V && W && gc && gp && res,
                 "sfm_ba_jtj: NULL array");
-    // chunk mode: the observation waves tile a virtual index space in which every chunk starts at
-    // a multiple of 64 (obs_block); cobs / vst = the chunks' real / virtual starts
+    // chunk mode: the observation blocks tile a virtual index space in which every chunk starts at
+    // a multiple of 256 (obs_block); cobs / vst = the chunks' real / virtual starts
     sfm::ChunkOff cobs{}, vst{};
-    int n_vobs = n_obs;
-    if (ctx->ba_nchunk > 0) {
-        const int nck = ctx->ba_nchunk;
-        vst.v[0] = 0;
-        for (int k = 0; k < nck; ++k) {
-            cobs.v[k] = ctx->ba_chunk_obs[k];
-            vst.v[k + 1] = vst.v[k] + ((ctx->ba_chunk_obs[k + 1] - ctx->ba_chunk_obs[k] + 63) & ~63);
-        }
-        cobs.v[nck] = ctx->ba_chunk_obs[nck];
-        n_vobs = vst.v[nck];
-    }
+    const int n_vobs = ctx->ba_nchunk > 0 ? chunk_layout(ctx, cobs, vst) : n_obs;
     // workspace: segment records (2 per wave) | their point ids | cost per block | camera partials
     const int n_wave = (n_vobs + 63) / 64;
     const int n_obsb = (n_vobs + 255) / 256;
     // few cameras: split each camera's observations so the camera waves still fill the chip;
-    // chunk mode: one split per chunk (sfm_ba_set_chunks)
+    // chunk mode: G waves per camera, each a share of the chunks (camera_wave), at least
+    // SPLIT_TARGET camera waves in all
     const bool ck = ctx->ba_nchunk > 0;
-    const int splits = ck ? ctx->ba_nchunk
+    const int splits = ck ? chunk_waves(ctx->ba_nchunk, n_cam)
                           : std::max(1, std::min(16, (SPLIT_TARGET + n_cam - 1) / n_cam));
     SFM_REQUIRE(!ck || ctx->ba_cam_bounds, "sfm_ba_jtj: chunk mode without cam_bounds");
     const size_t sb = sfm::align_up(sizeof(double) * NV * 2 * (size_t)std::max(n_wave, 1), 256);
     const size_t ib = sfm::align_up(sizeof(int32_t) * 2 * (size_t)std::max(n_wave, 1), 256);
     const size_t cb = sfm::align_up(sizeof(double) * (size_t)std::max(n_obsb, 1), 256);
-    const size_t pb = sfm::align_up(sizeof(double) * NU * (size_t)n_cam * splits, 256);
-    const size_t kb = ck ? sizeof(double) * CKB * ctx->ba_nchunk : 0;   // chunk cost partials
-    char* ws = (char*)sfm::workspace(ctx, sb + ib + cb + pb + kb + 1024);
+    const size_t pb = sfm::align_up(sizeof(double) * NU * (size_t)n_cam * (ck ? ctx->ba_nchunk : splits), 256);
+    char* ws = (char*)sfm::workspace(ctx, sb + ib + cb + pb + 1024);
     if (!ws) return SFM_ERR_NOMEM;
     double* seg = (double*)ws;
     int32_t* seg_pt = (int32_t*)(ws + sb);
     double* cost_blk = (double*)(ws + sb + ib);
     double* part = (double*)(ws + sb + ib + cb);
     // camera waves (four per block) + observation blocks in one launch, then the finish blocks
+#ifdef BA_ABL_OBSONLY  // ablation (timing only): observation blocks alone
+    const int n_camw = 0;
+#else
     const int n_camw = n_cam * splits * CH;
+#endif
     const int n_camb = (n_camw + 3) / 4;
 #ifdef BA_ABL_CAMONLY  // ablation (timing only): camera waves alone
     const int n_ob_launch = 0;
@@ -854,25 +880,14 @@ extern "C" int sfm_ba_jtj(sfm_ctx* ctx, int32_t n_cam, const double* cams, const
 #endif
     SFM_HIP_CHECK(hipGetLastError());
     const int nw = n_obs > 0 ? n_wave : 0;
-    const int n_fin = std::max(std::max((nw + 255) / 256, (n_pt + 255) / 256), 1);
+    // chunk mode: the finish blocks also form U / g_c and the cost from the chunk partials (the
+    // canonical tree, or exported per chunk for the caller's exchange)
+    const int n_fin = std::max({(nw + 255) / 256, (n_pt + 255) / 256, ck ? (n_cam * NU + 255) / 256 : 0, 1});
     hipLaunchKernelGGL(ba_finish_kernel, dim3(n_fin), dim3(256), 0, st, nw, n_obs > 0 ? n_obsb : 0,
-                       n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost, ctx->ba_nchunk, cobs, vst);
+                       n_pt, pt_ptr, seg, seg_pt, V, gp, cost_blk, cost, ctx->ba_nchunk, cobs, vst,
+                       n_cam, ctx->ba_ntotal > 0 ? 1 : 0, part, U, gc);
     SFM_HIP_CHECK(hipGetLastError());
-    if (ck) {   // U / g_c and the cost from the chunk partials (tree, or exported for the caller)
-        const int exp = ctx->ba_ntotal > 0 ? 1 : 0;
-        hipLaunchKernelGGL(ba_chunk_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, st,
-                           n_cam, splits, exp, part, U, gc);
-        SFM_HIP_CHECK(hipGetLastError());
-        double* kpart = (double*)(ws + sb + ib + cb + pb);
-        sfm::ChunkOff co;
-        for (int k = 0; k <= splits; ++k) co.v[k] = ctx->ba_chunk_obs[k];
-        hipLaunchKernelGGL(ba_cost_chunk_kernel, dim3(splits * CKB), dim3(256), 0, st, co, cams,
-                           pp, pts, cam_idx, pt_idx, uv, loss_s, kpart);
-        SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(ba_cost_chunk_final, dim3(1), dim3(64), 0, st, splits, exp, kpart, cost);
-        SFM_HIP_CHECK(hipGetLastError());
-        return SFM_OK;
-    }
+    if (ck) return SFM_OK;
     if (splits > 1) {
         hipLaunchKernelGGL(ba_final_kernel, dim3((n_cam * NU + 255) / 256), dim3(256), 0, st,
                            n_cam, splits, part, U, gc);
@@ -897,15 +912,15 @@ extern "C" int sfm_ba_cost(sfm_ctx* ctx, int32_t n_cam, const double* cams, cons
     if (ctx->ba_nchunk > 0) {   // chunk mode (sfm_ba_set_chunks): chunk partials, tree or export
         const int nck = ctx->ba_nchunk;
         SFM_REQUIRE(ctx->ba_chunk_obs[nck] == n_obs, "sfm_ba_cost: chunk offsets do not match n_obs");
-        double* kpart = (double*)sfm::workspace(ctx, sizeof(double) * CKB * nck + 256);
+        sfm::ChunkOff cobs{}, vst{};
+        const int nvb = chunk_layout(ctx, cobs, vst) / 256;
+        double* kpart = (double*)sfm::workspace(ctx, sizeof(double) * (size_t)nvb + 256);
         if (!kpart) return SFM_ERR_NOMEM;
-        sfm::ChunkOff co;
-        for (int k = 0; k <= nck; ++k) co.v[k] = ctx->ba_chunk_obs[k];
-        hipLaunchKernelGGL(ba_cost_chunk_kernel, dim3(nck * CKB), dim3(256), 0, st, co, cams, pp,
-                           pts, cam_idx, pt_idx, uv, loss_s, kpart);
+        hipLaunchKernelGGL(ba_cost_chunk_kernel, dim3(nvb), dim3(256), 0, st, nck, cobs, vst, cams,
+                           pp, pts, cam_idx, pt_idx, uv, loss_s, kpart);
         SFM_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(ba_cost_chunk_final, dim3(1), dim3(64), 0, st, nck,
-                           ctx->ba_ntotal > 0 ? 1 : 0, kpart, cost);
+        hipLaunchKernelGGL(ba_cost_chunk_final, dim3(1), dim3(1024), 0, st, nck,
+                           ctx->ba_ntotal > 0 ? 1 : 0, vst, kpart, cost);
         SFM_HIP_CHECK(hipGetLastError());
         return SFM_OK;
     }

@@ -30,6 +30,12 @@ namespace {
 
 constexpr double DIAG_MIN = 1e-6, DIAG_MAX = 1e32;
 constexpr int CT = 256;  // threads per camera block
+// Chunk mode (sfm_ba_set_chunks) camera passes: the camera's chunks one after the other, each over
+// the whole block (block-strided from the chunk's start, then block_sum) — a camera's observations
+// sit in one or two chunks (points are chunked by id and a camera sees a local set), so spreading
+// the chunks over lane groups would leave most groups idle.  The association of a chunk's sum
+// depends only on that chunk (never on how many chunks the calling rank holds); empty chunks
+// are zero without a reduction.
 
 struct PcgState {
     double beta;    // β_k of the current iteration (published by the previous iteration's vector
@@ -44,22 +50,14 @@ struct PcgState {
 
 __device__ __forceinline__ double dclamp(double d) { return fmin(fmax(d, DIAG_MIN), DIAG_MAX); }
 
-// Fixed-order block sum over CT threads of n values per thread (shuffle tree in each wave, then
-// the 4 wave partials in order).  Result valid in `red[i]` for i < n after the call.
+// Fixed-order block sum over CT threads of n <= 64 values per thread (each wave's recursive-halving
+// sum, then the 4 wave partials in order).  Result in out[i] for i < n after the call.
 template <int N>
 __device__ __forceinline__ void block_sum(double (&a)[N], double (*red)[N], double* out) {
+    static_assert(CT == 256, "block_sum: four waves");
     const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        double v = a[i];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
-        a[i] = v;
-    }
-    if ((tid & 63) == 0) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) red[tid >> 6][i] = a[i];
-    }
+    int idx;
+    if (sfm::wave_halving_sum<N>(a, tid & 63, idx)) red[tid >> 6][idx] = a[0];
     __syncthreads();
     if (tid < N) out[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
     __syncthreads();
@@ -223,25 +221,18 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
                 tot[tid] = sfm::chunk_tree16(a);
             }
             __syncthreads();
-        } else {
-            const int wv = tid >> 6, lane = tid & 63;
-            for (int k = wv; k < nck; k += CT / 64) {
+        } else {   // the camera's chunks in turn, each block-wide (see CT above)
+            for (int k = 0; k < nck; ++k) {
+                const int e0 = cb[(size_t)c * (nck + 1) + k], e1 = cb[(size_t)c * (nck + 1) + k + 1];
+                if (e0 == e1) {   // block-uniform
+                    if (tid < N) cpart[k][tid] = 0.0;
+                    continue;
+                }
                 double acc[N];
 #pragma unroll
                 for (int i = 0; i < N; ++i) acc[i] = 0.0;
-                const int e1 = cb[(size_t)c * (nck + 1) + k + 1];
-                for (int e = cb[(size_t)c * (nck + 1) + k] + lane; e < e1; e += 64) accum(e, acc);
-#pragma unroll
-                for (int i = 0; i < N; ++i) {
-                    double v = acc[i];
-#pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-                    acc[i] = v;
-                }
-                if (lane == 0) {
-#pragma unroll
-                    for (int i = 0; i < N; ++i) cpart[k][i] = acc[i];
-                }
+                for (int e = e0 + tid; e < e1; e += CT) accum(e, acc);
+                block_sum<N>(acc, red, cpart[k]);
             }
             __syncthreads();
             if (phase == 1) {   // export: this rank's chunk partials, [chunk][camera][44]
@@ -625,25 +616,19 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
             acc[2 * i + 1] += v.y;
         }
     };
-    if (cb) {   // chunk mode: wave w sums chunks w, w + 4, ... (lane-strided, xor tree)
+    if (cb) {   // chunk mode: the camera's chunks in turn, each block-wide (see CT above)
+        static_assert(CC == CT, "bas_pcg_camera chunk mode: block_sum's four waves");
         if (phase != 2) {
-            const int wv = tid >> 6, lane = tid & 63;
-            for (int k = wv; k < nck; k += CC / 64) {
+            for (int k = 0; k < nck; ++k) {
+                const int e0 = cb[(size_t)c * (nck + 1) + k], e1 = cb[(size_t)c * (nck + 1) + k + 1];
+                if (e0 == e1) {   // block-uniform
+                    if (tid < 8) cpart[k][tid] = 0.0;
+                    continue;
+                }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) acc[i] = 0.0;
-                const int e1 = cb[(size_t)c * (nck + 1) + k + 1];
-                for (int e = cb[(size_t)c * (nck + 1) + k] + lane; e < e1; e += 64) add_obs(e);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    double v = acc[i];
-#pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-                    acc[i] = v;
-                }
-                if (lane == 0) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) cpart[k][i] = acc[i];
-                }
+                for (int e = e0 + tid; e < e1; e += CC) add_obs(e);
+                block_sum<8>(acc, red, cpart[k]);
             }
         }
     } else {

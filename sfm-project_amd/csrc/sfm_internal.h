@@ -34,6 +34,26 @@ namespace sfm {
 struct ChunkOff {
     int32_t v[17];
 };
+// Chunk of a (per-lane) index x in the monotone offsets off[0..nck] (off[k] <= x < off[k+1], the
+// last chunk for x >= off[nck - 1]): fully unrolled compares against the kernel-argument offsets at
+// compile-time positions (uniform scalar loads + selects) — a loop with a per-lane index into the
+// argument struct would turn into dependent per-lane memory loads.  Returns k; *a / *b receive
+// base[k] and base[k + 1] of a second offset table (may be the same).
+__device__ __forceinline__ int chunk_of(int x, int nck, const ChunkOff& off, const ChunkOff& base,
+                                        int& a, int& b) {
+    int k = 0;
+    a = base.v[0];
+    b = base.v[1];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+        if (i < nck && x >= off.v[i]) {
+            k = i;
+            a = base.v[i];
+            b = base.v[i + 1];
+        }
+    }
+    return k;
+}
 // The canonical pairwise tree over the chunk partials a[0..n) (n <= 16): a fixed 16-leaf tree with
 // the missing leaves 0 — the same as "a[i] = a[2i] + a[2i+1], an odd last one carried".
 __device__ __forceinline__ double chunk_tree16(double (&a)[16]) {
@@ -42,6 +62,44 @@ __device__ __forceinline__ double chunk_tree16(double (&a)[16]) {
 #pragma unroll
         for (int i = 0; i < w; ++i) a[i] = a[2 * i] + a[2 * i + 1];
     return a[0];
+}
+
+// Wave reduction of M <= 64 per-lane values by recursive halving: at the step with lane bit OFF,
+// the lane keeps one half of its (zero-padded) values and adds the partner's copy of that half,
+// so M values cost about M exchanges instead of the 6 M of M separate shuffle trees.  Afterwards
+// a[0] of lane l is the wave sum of value `idx` (the sum of the kept-half offsets) when the call
+// returns true; every value is held by exactly one such lane (a padding slot can carry an index
+// that is real elsewhere, so `rs`, the real length of the lane's current slice, decides).  The
+// association is fixed (a function of M).
+template <int M, int OFF>
+__device__ __forceinline__ void wave_halving_step(double* a, int lane, int& idx, int& rs) {
+    if constexpr (OFF >= 1) {
+        constexpr int H = (M + 1) / 2;
+        const bool up = (lane & OFF) != 0;
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            const double lo = a[i], hi = (H + i < M) ? a[H + i] : 0.0;
+            const double r = __shfl_xor(up ? lo : hi, OFF, 64);
+            a[i] = (up ? hi : lo) + r;
+        }
+        if (up) {
+            idx += H;
+            rs -= H;
+        } else if (rs > H) {
+            rs = H;
+        }
+        wave_halving_step<H, OFF / 2>(a, lane, idx, rs);
+    }
+}
+// LANES < 64: the same over each aligned group of LANES lanes (a power of two, M <= LANES).
+template <int M, int LANES = 64>
+__device__ __forceinline__ bool wave_halving_sum(double* a, int lane, int& idx) {
+    static_assert(LANES >= 2 && LANES <= 64 && (LANES & (LANES - 1)) == 0, "wave_halving_sum: lanes");
+    static_assert(M >= 1 && M <= LANES, "wave_halving_sum: 1..LANES values");
+    int rs = M;
+    idx = 0;
+    wave_halving_step<M, LANES / 2>(a, lane, idx, rs);
+    return rs > 0;
 }
 
 void set_error(const std::string& msg);

@@ -86,19 +86,23 @@ def shard_points(pt_ptr, rank: int, world: int):
     return int(cuts[rank]), int(cuts[rank + 1])
 
 
-def shard_cuts_device(pt_idx, n_pt: int, world: int):
+def shard_cuts_device(pt_idx, n_pt: int, world: int, ptr=None):
     """shard_points for every rank from a point-major device tensor pt_idx: the same cuts (float64
     searchsorted of the balanced observation targets in the point CSR, made monotone), computed
     on the GPU; returns host lists (point cuts [world + 1], observation cuts [world + 1]) — the
-    only device -> host read of the sharded set-up (2 (world + 1) integers)."""
+    only device -> host read of the sharded set-up (2 (world + 1) integers).  `ptr`: the point
+    CSR offsets [n_pt + 1] when the caller has them (saves a bincount and its sync)."""
     import torch
     dev = pt_idx.device
     n_obs = int(pt_idx.numel())
-    ptr = torch.zeros(n_pt + 1, dtype=torch.int64, device=dev)
-    if n_obs:
-        ptr[1:] = torch.cumsum(torch.bincount(pt_idx.long(), minlength=n_pt), 0)
     if world <= 1:
         return [0, n_pt], [0, n_obs]
+    if ptr is None:
+        ptr = torch.zeros(n_pt + 1, dtype=torch.int64, device=dev)
+        if n_obs:
+            ptr[1:] = torch.cumsum(torch.bincount(pt_idx.long(), minlength=n_pt), 0)
+    else:
+        ptr = ptr.long()
     tgt = n_obs * torch.arange(world + 1, dtype=torch.float64, device=dev) / world
     cuts = torch.searchsorted(ptr.double(), tgt, right=False)
     cuts[0], cuts[-1] = 0, n_pt
@@ -230,7 +234,7 @@ class BAProblem:
         self.chunks = None
         if chunks is not None and chunks != 0:
             if isinstance(chunks, int):
-                cpt, cob = shard_cuts_device(self.pt_idx, n_pt, chunks)
+                cpt, cob = shard_cuts_device(self.pt_idx, n_pt, chunks, ptr=self.pt_ptr)
                 n_total, k0 = 0, 0
             else:
                 cpt = [int(v) for v in chunks]
@@ -509,6 +513,10 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     import time
     import torch
     t_entry = time.perf_counter()
+    if info is not None:   # the caller's queued GPU work is not this call's set-up
+        torch.cuda.synchronize(device)
+        info["entry_wait_s"] = time.perf_counter() - t_entry
+        t_entry = time.perf_counter()
     n_cam, n_pt = len(cams), len(pts)
     allreduce = None
     world = 1
@@ -578,6 +586,9 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     else:
         prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, hi - lo, device, chunks=nchunk or None)
     f64 = torch.float64
+    if info is not None:
+        torch.cuda.synchronize(prob.dev)
+        info["problem_s"] = time.perf_counter() - t_entry   # BAProblem: CSR, chunk table
 
     def gather_chunks(part, width):
         """This shard's chunk partials [n_local, width] -> the canonical tree over all chunks

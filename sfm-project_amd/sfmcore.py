@@ -372,11 +372,13 @@ class Context:
         if spec is None:
             _check(self.lib.sfm_ba_set_chunks(self.handle, 0, None, None, 0, None))
             return
-        n = len(spec.chunk_pt) - 1
-        cpt = (C.c_int32 * (n + 1))(*[int(v) for v in spec.chunk_pt])
-        cob = (C.c_int32 * (n + 1))(*[int(v) for v in spec.chunk_obs])
-        _check(self.lib.sfm_ba_set_chunks(self.handle, n, cpt, cob, int(spec.n_total),
-                                          _ptr(spec.cam_bounds)))
+        args = getattr(spec, "_cargs", None)   # the ctypes arrays, built once per spec
+        if args is None:
+            n = len(spec.chunk_pt) - 1
+            args = spec._cargs = (n, (C.c_int32 * (n + 1))(*[int(v) for v in spec.chunk_pt]),
+                                  (C.c_int32 * (n + 1))(*[int(v) for v in spec.chunk_obs]),
+                                  int(spec.n_total), _ptr(spec.cam_bounds))
+        _check(self.lib.sfm_ba_set_chunks(self.handle, *args))
 
     def ba_chunk_tree(self, parts, out=None):
         """sfm_ba_chunk_tree: parts [n_total, ...] f64 device -> out [...] (the canonical tree)."""
