@@ -735,11 +735,17 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / n
-    jtj_ms = timed(lambda: P.linearize(c, p, 2.0), reps)
-    lin = P.linearize(c, p, 2.0)
-    s0 = timed(lambda: P.solve(lin, 1e-3, max_iter=0, tol=0.0), reps)
-    sn = timed(lambda: P.solve(lin, 1e-3, max_iter=cg, tol=0.0, poll=-1), max(reps // 4, 2))
-    it_ms = (sn - s0) / cg
+    def measure(P):
+        jtj = timed(lambda: P.linearize(c, p, 2.0), reps)
+        lin = P.linearize(c, p, 2.0)
+        s0 = timed(lambda: P.solve(lin, 1e-3, max_iter=0, tol=0.0), reps)
+        sn = timed(lambda: P.solve(lin, 1e-3, max_iter=cg, tol=0.0, poll=-1), max(reps // 4, 2))
+        return jtj, (sn - s0) / cg
+    jtj_ms, it_ms = measure(P)
+    # the production form: bundle_adjust's sharding-invariant chunk sums (reconstruction.BAChunks)
+    nck = R.ba_chunk_count()
+    jtj_ck, it_ck = measure(R.BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device,
+                                        chunks=nck)) if nck else (None, None)
     idx_b = 4 * (2 * n_obs + (n_pt + 1) + (n_cam + 1) + n_obs)     # cam/pt idx, CSR ptrs, cam_obs
     k3_b = (8 * (8 * n_cam + 2 * n_cam + 3 * n_pt + 2 * n_obs) + idx_b
             + 8 * (64 * n_cam + 9 * n_pt + 24 * n_obs + 8 * n_cam + 3 * n_pt + 2 * n_obs + 1))
@@ -750,6 +756,12 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
             "cg_iteration": {"ms": it_ms, "bytes": cg_b,
                              "achieved_GBs": cg_b / (it_ms * 1e-3) / 1e9 if it_ms > 0 else None,
                              "frac": cg_b / (it_ms * 1e-3) / PEAK_HBM if it_ms > 0 else None},
+            "chunked": None if jtj_ck is None else {
+                "chunks": nck, "note": "bundle_adjust's form (sharding-invariant chunk sums); "
+                                       "the same algorithmic bytes",
+                "k3": {"ms": jtj_ck, "frac": k3_b / (jtj_ck * 1e-3) / PEAK_HBM},
+                "cg_iteration": {"ms": it_ck,
+                                 "frac": cg_b / (it_ck * 1e-3) / PEAK_HBM if it_ck > 0 else None}},
             "peak_GBs": PEAK_HBM / 1e9}
 
 

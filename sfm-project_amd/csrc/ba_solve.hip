@@ -429,6 +429,23 @@ __device__ __forceinline__ Scalars read_scalars(const PcgState* __restrict__ st)
 #endif
 constexpr int PG = SFM_BA_PG;  // lanes per point in the point-major passes
 
+// u_o (8 doubles) of one observation.  BA_U_NT: non-temporal stores — u (64 B per observation,
+// 66 MB at 1 M observations) is read once, by the next kernel, and never fits the L2; plain
+// stores leave it dirty in L2 at the kernel boundary.
+#ifndef BA_U_NT
+#define BA_U_NT 1
+#endif
+__device__ __forceinline__ void store_u(double* __restrict__ dst, const double (&uo)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#if BA_U_NT
+        __builtin_nontemporal_store(uo[i], dst + i);
+#else
+        dst[i] = uo[i];
+#endif
+    }
+}
+
 // Wave per long-track point (more than LONG_OBS observations; listed by bas_point_setup): lane j
 // takes observations j, j+64, ... in order, a 64-lane xor butterfly combines them, then the lanes
 // write u_o = W_o t_p for their observations.  The waves of the lb long-track blocks stride over
@@ -479,9 +496,7 @@ __device__ __forceinline__ void pcg_point_long(int b, int lb, int n_obs,
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 uo[i] = Wo[(3 * i) * n] * t0 + Wo[(3 * i + 1) * n] * t1 + Wo[(3 * i + 2) * n] * t2;
-            double2* d = (double2*)(u + 8 * (size_t)o);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) d[i] = make_double2(uo[2 * i], uo[2 * i + 1]);
+            store_u(u + 8 * (size_t)o, uo);
         }
     }
 }
@@ -569,9 +584,7 @@ __global__ __launch_bounds__(256) void bas_pcg_point(
         double uo[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) uo[i] = wo[3 * i] * t0 + wo[3 * i + 1] * t1 + wo[3 * i + 2] * t2;
-        double2* d = (double2*)(u + 8 * (size_t)o);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) d[i] = make_double2(uo[2 * i], uo[2 * i + 1]);
+        store_u(u + 8 * (size_t)o, uo);
     };
     put(o0, w);
     for (int o = o0 + PG; o < o1; o += PG) {  // points with more than PG observations
@@ -582,6 +595,9 @@ __global__ __launch_bounds__(256) void bas_pcg_point(
 }
 
 constexpr int CC = SFM_BA_CC;  // threads per camera block in the CG camera pass
+#ifndef CAM_PCG_MLP
+#define CAM_PCG_MLP 4  // observations per lane whose loads the CG camera pass keeps in flight
+#endif
 
 // Block per camera: p_k stored; q_c = U_d p_c - Σ_o u_o (u_o = W_o t_p, bas_pcg_point); p_c·q_c.
 // Sharded solve: phase 1 writes the local Σ_o u_o to comm[8c..] and stops; after the
@@ -616,6 +632,29 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
             acc[2 * i + 1] += v.y;
         }
     };
+    // the lane's observations e, e + CC, ... < e1 in order; CAM_PCG_MLP of them per step have their
+    // cam_obs and u loads in flight together (500 camera blocks leave ~2 waves per SIMD: the pass
+    // is latency-bound), the sums still taken one observation after the other
+    auto sum_range = [&](int e, int e1) {
+        for (; e + (CAM_PCG_MLP - 1) * CC < e1; e += CAM_PCG_MLP * CC) {
+            int o[CAM_PCG_MLP];
+#pragma unroll
+            for (int m = 0; m < CAM_PCG_MLP; ++m) o[m] = cam_obs[e + m * CC];
+            double2 v[CAM_PCG_MLP][4];
+#pragma unroll
+            for (int m = 0; m < CAM_PCG_MLP; ++m)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[m][i] = ((const double2*)(u + 8 * (size_t)o[m]))[i];
+#pragma unroll
+            for (int m = 0; m < CAM_PCG_MLP; ++m)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    acc[2 * i] += v[m][i].x;
+                    acc[2 * i + 1] += v[m][i].y;
+                }
+        }
+        for (; e < e1; e += CC) add_obs(e);
+    };
     if (cb) {   // chunk mode: the camera's chunks in turn, each block-wide (see CT above)
         static_assert(CC == CT, "bas_pcg_camera chunk mode: block_sum's four waves");
         if (phase != 2) {
@@ -627,24 +666,14 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
                 }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) acc[i] = 0.0;
-                for (int e = e0 + tid; e < e1; e += CC) add_obs(e);
+                sum_range(e0 + tid, e1);
                 block_sum<8>(acc, red, cpart[k]);
             }
         }
     } else {
-    const int e_end = phase == 2 ? 0 : cam_ptr[c + 1];
-    for (int e = (phase == 2 ? 0 : cam_ptr[c]) + tid; e < e_end; e += CC) add_obs(e);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        double v = acc[i];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
-        acc[i] = v;
-    }
-    if ((tid & 63) == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) red[tid >> 6][i] = acc[i];
-    }
+    if (phase != 2) sum_range(cam_ptr[c] + tid, cam_ptr[c + 1]);
+    int idx;   // the wave's 8 sums by recursive halving; the waves' partials summed in order below
+    if (sfm::wave_halving_sum<8>(acc, tid & 63, idx)) red[tid >> 6][idx] = acc[0];
     }
     if (tid < 8) {
         const size_t kk = 8 * (size_t)c + tid;
