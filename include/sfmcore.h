@@ -258,6 +258,7 @@ int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
 #define SFM_BA_STAGE_BACKSUB 4
 #define SFM_BA_STAGE_MODEL 5
 #define SFM_BA_STAGE_POLL 6
+#define SFM_BA_STAGE_SCHUR 7   /* explicit S only (sfm_ba_set_schur): after SETUP, exports T's partials */
 int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_t n_cam, int32_t n_pt,
                        int32_t n_obs, const int32_t* cam_idx, const int32_t* pt_idx,
                        const int32_t* pt_ptr, const int32_t* cam_ptr, const int32_t* cam_obs,
@@ -309,6 +310,26 @@ int sfm_ba_update(sfm_ctx* ctx, int32_t n_cam, const double* cams, const double*
 int sfm_ba_set_chunks(sfm_ctx* ctx, int32_t n_chunk, const int32_t* chunk_pt,
                       const int32_t* chunk_obs, int32_t n_total, const int32_t* cam_bounds);
 int sfm_ba_chunk_tree(sfm_ctx* ctx, int32_t n_total, int64_t n, const double* parts, double* out);
+
+/* Explicit reduced camera system (sfm_version 4; needs chunk mode).  The solve forms the
+ * off-diagonal Schur blocks T_ij = Σ_p W_pi V_d,p⁻¹ W_pjᵀ once per solve (S_ij = -T_ij, i != j) and
+ * runs the CG on S directly — two launches per iteration over 64 B per camera-pair block instead of
+ * streaming W (192 B per observation) every iteration.  It pays when the camera-pair products are
+ * few against the CG iterations (short tracks); the caller decides (reconstruction.schur_rule).
+ *   sfm_ba_set_schur(ctx, n_slot, slot_cam, n_seg, seg, n_inst, inst, row_ptr, n_ent, row_ent):
+ *   slot_cam [n_slot][2] (ci <= cj): the camera pairs (slots) of the WHOLE problem, the same table
+ *   on every rank; inst [2][n_inst] (observation a, observation b of one point, LOCAL observation
+ *   indices; cam(a) = ci, cam(b) = cj of its slot; a pair within one camera appears as (a, b) and
+ *   (b, a)); seg [4][n_seg] (local chunk, slot, first instance, end instance): the instances
+ *   grouped by (chunk, slot), each group in point order — T's chunk partial of a slot is the fixed-
+ *   order sum over its group; row_ptr [n_cam + 1], row_ent [n_ent] = 2 slot + t: block row c of S
+ *   (t = 1: the slot's transpose), in a fixed order.  All device, caller-owned.  n_slot = 0 turns
+ *   it off.  The chunk partials of T follow the chunk rules above (exported to comm after the 44-sum
+ *   partials by SETUP of a shard, comm >= n_total * (44 n_cam + 64 n_slot) doubles); with it on,
+ *   ITER / ITER_FINISH of the sharded solve need no exchange (S is replicated after SETUP_FINISH). */
+int sfm_ba_set_schur(sfm_ctx* ctx, int32_t n_slot, const int32_t* slot_cam, int32_t n_seg,
+                     const int32_t* seg, int32_t n_inst, const int32_t* inst, const int32_t* row_ptr,
+                     int32_t n_ent, const int32_t* row_ent);
 
 /* ---- feature tracks ----------------------------------------------------------------------------
  * the verified match graph (sfm_graph_rows) -> tracks, the input of

@@ -175,7 +175,8 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
     double* __restrict__ Ud, double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ pv,
     double* __restrict__ rz_c, double* __restrict__ bb_c, int32_t* __restrict__ bad, int phase,
-    double* __restrict__ comm, const int32_t* __restrict__ cb, int nck, int ntot) {
+    double* __restrict__ comm, const int32_t* __restrict__ cb, int nck, int ntot,
+    double* __restrict__ Scc) {
     constexpr int N = 44;
     __shared__ double red[4][N];
     __shared__ double tot[N];
@@ -276,6 +277,10 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
                 S[8 * j + i] = S[8 * i + j];
                 ++t;
             }
+        if (Scc) {   // the explicit system's diagonal block (sfm_ba_set_schur)
+#pragma unroll
+            for (int k = 0; k < 64; ++k) Scc[64 * (size_t)c + k] = S[k];
+        }
         if (!inv8_spd(S, M)) {
             atomicOr(bad, 1);
 #pragma unroll
@@ -770,6 +775,127 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
     publish_next(k, n_cam, rzc, rrc, tol, st, gridDim.x, red4);
 }
 
+// ---- explicit reduced camera system (sfm_ba_set_schur) -------------------------------------------
+//
+// T_slot = Σ over the slot's camera-pair instances (a, b) of Y_a W_bᵀ, Y_a = W_a V_d⁻¹ (the point of
+// a), so the off-diagonal Schur blocks are S_ij = -T_ij; the diagonal blocks S_cc come from
+// bas_camera_setup.  Two waves per (chunk, slot) group, wave h the block's rows 4h .. 4h + 3:
+// lane-strided over the group's instances (an order that depends only on the group), 32
+// accumulators per lane, then the recursive-halving wave sum — lane t ends holding element
+// 32 h + t and stores it.  (All 64 rows in one wave: 262 registers, one wave per SIMD.)
+__global__ __launch_bounds__(256) void bas_schur_build(
+    int n_seg, int n_slot, int n_inst, const int32_t* __restrict__ seg,
+    const int32_t* __restrict__ inst, const int32_t* __restrict__ pt_idx,
+    const double* __restrict__ W, const double* __restrict__ Vinv, double* __restrict__ Tpart) {
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int s = wv >> 1, h = wv & 1;
+    if (s >= n_seg) return;   // wave-uniform
+    const int k = seg[s], slot = seg[n_seg + s], i0 = seg[2 * n_seg + s], i1 = seg[3 * n_seg + s];
+    double acc[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) acc[t] = 0.0;
+    for (int i = i0 + lane; i < i1; i += 64) {
+        const int a = inst[i], b = inst[n_inst + i];
+        const int p = pt_idx[a];
+        double wa[12], wb[24], vi[9];
+        const double2* Wa = (const double2*)(W + 24 * (size_t)a + 12 * h);   // rows 4h .. 4h + 3
+        const double2* Wb = (const double2*)(W + 24 * (size_t)b);
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            const double2 u = Wa[t];
+            wa[2 * t] = u.x; wa[2 * t + 1] = u.y;
+        }
+#pragma unroll
+        for (int t = 0; t < 12; ++t) {
+            const double2 v = Wb[t];
+            wb[2 * t] = v.x; wb[2 * t + 1] = v.y;
+        }
+        const double* Vi = Vinv + 9 * (size_t)p;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) vi[t] = Vi[t];
+        double y[12];   // rows 4h .. 4h + 3 of W_a V_d⁻¹, bas_camera_setup's expression
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                y[3 * i2 + j] = wa[3 * i2] * vi[j] + wa[3 * i2 + 1] * vi[3 + j] + wa[3 * i2 + 2] * vi[6 + j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[8 * r + c] += y[3 * r] * wb[3 * c] + y[3 * r + 1] * wb[3 * c + 1] + y[3 * r + 2] * wb[3 * c + 2];
+    }
+    int idx;
+    if (sfm::wave_halving_sum<32>(acc, lane, idx))
+        Tpart[((size_t)k * n_slot + slot) * 64 + 32 * h + idx] = acc[0];
+}
+
+// T = the canonical tree over the n_total chunk partials (parts [n_total][n]).
+__global__ __launch_bounds__(256) void bas_chunk_tree(int ntot, long long n,
+                                                      const double* __restrict__ parts,
+                                                      double* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double a[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] = k < ntot ? parts[(size_t)k * n + i] : 0.0;
+    out[i] = sfm::chunk_tree16(a);
+}
+
+// Explicit CG product (bas_point + bas_pcg_camera's role once S is formed): wave per block row c.
+// p_k = z_k + β_k p_{k-1} (p_{k-1} from the other parity slot of pv2, so no block reads what
+// another writes); the row's blocks in row_ent order, 8 lanes per block (lane r: row r of the
+// block, or column r for a transposed slot), blocks g, g + 8, ... per lane group, then a fixed
+// xor tree over the 8 groups; q_c = S_cc p_c - Σ T p_j, p_k stored, p·q per camera.
+__global__ __launch_bounds__(256) void bas_pcg_spmv(
+    int k, int n_cam, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ row_ent,
+    const int32_t* __restrict__ slot_cam, const double* __restrict__ T,
+    const double* __restrict__ Scc, const double* __restrict__ z, double* __restrict__ pv2,
+    const PcgState* __restrict__ st, double* __restrict__ q, double* __restrict__ pq) {
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (c >= n_cam) return;   // wave-uniform
+    const Scalars sc = read_scalars(st);
+    if (sc.done) return;
+    const double* pold = pv2 + (size_t)((k + 1) & 1) * 8 * n_cam;
+    double* pnew = pv2 + (size_t)(k & 1) * 8 * n_cam;
+    const int g = lane >> 3, r = lane & 7;
+    const int e0 = row_ptr[c], e1 = row_ptr[c + 1];
+    double s = 0.0;
+    for (int e = e0 + g; e < e1; e += 8) {
+        const int ent = row_ent[e];
+        const int slot = ent >> 1, tr = ent & 1;
+        const int j = slot_cam[2 * slot + (tr ? 0 : 1)];   // the other camera of the block
+        const double* Tb = T + 64 * (size_t)slot;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const double pj = z[8 * (size_t)j + m] + sc.beta * pold[8 * (size_t)j + m];
+            s += (tr ? Tb[8 * m + r] : Tb[8 * r + m]) * pj;
+        }
+    }
+    s += __shfl_xor(s, 8, 64);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    double pc[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) pc[m] = z[8 * (size_t)c + m] + sc.beta * pold[8 * (size_t)c + m];
+    double sp = 0.0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) sp += Scc[64 * (size_t)c + 8 * r + m] * pc[m];
+    const double qi = sp - s;
+    double pr = 0.0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) pr = (m == r) ? pc[m] : pr;
+    if (lane < 8) {
+        pnew[8 * (size_t)c + r] = pr;
+        q[8 * (size_t)c + r] = qi;
+    }
+    double v = pr * qi;
+    v += __shfl_down(v, 4, 8);
+    v += __shfl_down(v, 2, 8);
+    v += __shfl_down(v, 1, 8);
+    if (lane == 0) pq[c] = v;
+}
+
 // Largest camera count for which the sharded solve finishes an iteration in one launch
 // (bas_pcg_finish_vec keeps every camera's p·q in LDS and recomputes them in every block:
 // n_cam² · 11 B of L2 reads).  Mirrored by sfmcore.BA_FINISH_VEC_MAX_CAM.
@@ -1179,6 +1305,7 @@ static ChunkArgs chunk_args(const sfm_ctx* ctx) {
 
 struct SolveWs {
     double *Vinv, *vg, *Ud, *Mc, *r, *z, *pv, *q, *rzc, *rrc, *pq, *mpart, *mtot, *Wp, *u;
+    double *Scc = nullptr, *T = nullptr, *Tpart = nullptr, *pv2 = nullptr;   // explicit S only
     PcgState* state;
     int32_t* bad;
     int32_t* long_cnt;   // long-track points (bas_point_setup)
@@ -1202,8 +1329,17 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     const size_t b_part = sfm::align_up(sizeof(double) * n_part, 256);
     const size_t no = (size_t)std::max(n_obs, 1);
     const size_t b_soa = sfm::align_up(sizeof(double) * 32 * no + sizeof(int32_t) * no, 256);
-    char* ws = (char*)sfm::workspace(ctx, b_pt + b_cam + b_part + 512 + b_soa);
+    // explicit reduced camera system: S_cc, T, its chunk partials, p in two parity slots
+    const size_t ns = (size_t)ctx->ba_nslot, nck = (size_t)std::max(ctx->ba_nchunk, 1);
+    const size_t b_ex = ns > 0 ? sfm::align_up(sizeof(double) * (64 * nc + 64 * ns + 64 * ns * nck + 16 * nc), 256) : 0;
+    char* ws = (char*)sfm::workspace(ctx, b_pt + b_cam + b_part + 512 + b_soa + b_ex);
     if (!ws) return SFM_ERR_NOMEM;
+    if (ns > 0) {
+        w.Scc = (double*)(ws + b_pt + b_cam + b_part + 512 + b_soa);
+        w.T = w.Scc + 64 * nc;
+        w.Tpart = w.T + 64 * ns;
+        w.pv2 = w.Tpart + 64 * ns * nck;
+    }
     w.Vinv = (double*)ws;
     w.vg = w.Vinv + 9 * np;
     w.long_list = (int32_t*)(w.vg + 3 * np);
@@ -1249,7 +1385,7 @@ static int solve_setup(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, in
     }
     hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
                        w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
-                       w.rzc, w.rrc, w.bad, phase, comm, ck.cb, ck.nck, ck.ntot);
+                       w.rzc, w.rrc, w.bad, phase, comm, ck.cb, ck.nck, ck.ntot, w.Scc);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
@@ -1273,6 +1409,42 @@ static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, 
                        (const double*)nullptr, exp ? comm : w.mtot);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
+}
+
+// Explicit S: the local chunks' T partials (zeroed, then one wave per instance group) into
+// `out` ([n_chunk][n_slot][64]: Tpart, or a shard's export slot in comm).
+static int schur_build(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, const int32_t* pt_idx,
+                       const double* W, double* out) {
+    const size_t n = (size_t)ctx->ba_nchunk * ctx->ba_nslot * 64;
+    SFM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * n, st));
+    if (ctx->ba_nseg > 0) {
+        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg + 1) / 2), dim3(256), 0, st,
+                           ctx->ba_nseg, ctx->ba_nslot, ctx->ba_ninst, ctx->ba_seg, ctx->ba_inst,
+                           pt_idx, W, w.Vinv, out);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
+    return SFM_OK;
+}
+
+// Explicit S: T from n_total chunk partials (canonical tree) and the zeroed p_{-1} slot.
+static int schur_finish(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int32_t n_cam,
+                        int ntot, const double* parts) {
+    const long long n = (long long)ctx->ba_nslot * 64;
+    hipLaunchKernelGGL(bas_chunk_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, ntot, n, parts, w.T);
+    SFM_HIP_CHECK(hipGetLastError());
+    SFM_HIP_CHECK(hipMemsetAsync(w.pv2, 0, sizeof(double) * 16 * (size_t)n_cam, st));
+    return SFM_OK;
+}
+
+// One explicit CG iteration: the S product, then the vector update (p_k in parity slot k & 1).
+static void schur_iter(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int k, int32_t n_cam,
+                       double* dc, double tol) {
+    hipLaunchKernelGGL(bas_pcg_spmv, dim3((n_cam + 3) / 4), dim3(256), 0, st, k, n_cam,
+                       ctx->ba_row_ptr, ctx->ba_row_ent, ctx->ba_slot_cam, w.T, w.Scc, w.z, w.pv2,
+                       w.state, w.q, w.pq);
+    hipLaunchKernelGGL(bas_pcg_vec, dim3(w.vblk), dim3(256), 0, st, k, n_cam, w.Mc, dc, w.r, w.z,
+                       w.pv2 + (size_t)(k & 1) * 8 * n_cam, w.q, w.pq, w.rzc, w.rrc, w.state, tol);
 }
 
 static int solve_poll(sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int32_t* done) {
@@ -1312,9 +1484,15 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     SFM_REQUIRE(ck.ntot == 0, "sfm_ba_solve: chunk mode of a shard (n_total > 0) needs the stages");
     if (ck.cb)
         SFM_REQUIRE(ck.cpt.v[ck.nck] == n_pt, "sfm_ba_solve: chunk offsets do not match n_pt");
+    const bool ex = ctx->ba_nslot > 0;   // explicit reduced camera system (sfm_ba_set_schur)
+    SFM_REQUIRE(!ex || ck.cb, "sfm_ba_solve: the explicit Schur system needs chunk mode");
     const int rc = solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U,
                                V, W, gc, gp, lam, dc, 0, nullptr);
     if (rc != SFM_OK) return rc;
+    if (ex) {
+        if (schur_build(ctx, st, w, pt_idx, W, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
+        if (schur_finish(ctx, st, w, n_cam, ck.nck, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
+    }
     hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
     SFM_HIP_CHECK(hipGetLastError());
     // 0 (the zero-initialised struct) = every 8 iterations, the library default; < 0 = never
@@ -1333,6 +1511,10 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
             const int prc = solve_poll(ctx, st, w, &done);
             if (prc != SFM_OK) return prc;
             if (done) break;
+        }
+        if (ex) {
+            schur_iter(ctx, st, w, k, n_cam, dc, tol);
+            continue;
         }
         hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk + w.lblk), dim3(256), 0, st, k, n_pt, n_cam,
                            n_obs, pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol,
@@ -1365,7 +1547,7 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
                                   double* dc, double* dp, double* info, int32_t* done) {
     SFM_SOLVE_ARGS_CHECK("sfm_ba_solve_stage");
     SFM_REQUIRE(comm != nullptr, "sfm_ba_solve_stage: comm is NULL");
-    SFM_REQUIRE(stage >= SFM_BA_STAGE_SETUP && stage <= SFM_BA_STAGE_POLL,
+    SFM_REQUIRE(stage >= SFM_BA_STAGE_SETUP && stage <= SFM_BA_STAGE_SCHUR,
                 "sfm_ba_solve_stage: unknown stage");
     SFM_REQUIRE(stage != SFM_BA_STAGE_POLL || done != nullptr, "sfm_ba_solve_stage: done is NULL");
     SFM_REQUIRE(k >= 0, "sfm_ba_solve_stage: k must be >= 0");
@@ -1381,18 +1563,30 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
     SFM_REQUIRE(!ck.cb || ck.ntot > 0, "sfm_ba_solve_stage: chunk mode needs n_total > 0");
     if (ck.cb)
         SFM_REQUIRE(ck.cpt.v[ck.nck] == n_pt, "sfm_ba_solve_stage: chunk offsets do not match n_pt");
+    const bool ex = ctx->ba_nslot > 0;   // explicit reduced camera system (sfm_ba_set_schur)
+    SFM_REQUIRE(!ex || ck.cb, "sfm_ba_solve_stage: the explicit Schur system needs chunk mode");
+    SFM_REQUIRE(stage != SFM_BA_STAGE_SCHUR || ex, "sfm_ba_solve_stage: SCHUR without sfm_ba_set_schur");
     switch (stage) {
     case SFM_BA_STAGE_SETUP:  // -> comm[0, 44 n_cam) (chunk mode: [n_chunk][n_cam][44])
         return solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
                            W, gc, gp, lam, dc, 1, comm);
+    case SFM_BA_STAGE_SCHUR:  // explicit S: this shard's T partials -> comm [n_chunk][n_slot][64]
+        return schur_build(ctx, st, w, pt_idx, W, comm);
     case SFM_BA_STAGE_SETUP_FINISH:
         hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
                            w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z,
-                           w.pv, w.rzc, w.rrc, w.bad, 2, comm, ck.cb, ck.nck, ck.ntot);
+                           w.pv, w.rzc, w.rrc, w.bad, 2, comm, ck.cb, ck.nck, ck.ntot, w.Scc);
         SFM_HIP_CHECK(hipGetLastError());
+        if (ex && schur_finish(ctx, st, w, n_cam, ck.ntot,
+                               comm + (size_t)ck.ntot * 44 * n_cam) != SFM_OK)
+            return SFM_ERR_HIP;
         hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
         break;
     case SFM_BA_STAGE_ITER:  // -> comm[0, 8 n_cam)
+        if (ex) {   // S is replicated: the whole iteration locally, nothing to exchange
+            schur_iter(ctx, st, w, k, n_cam, dc, tol);
+            break;
+        }
         hipLaunchKernelGGL(bas_pcg_point, dim3(w.gblk + w.lblk), dim3(256), 0, st, k, n_pt, n_cam,
                            n_obs, pt_ptr, cam_idx, w.Wp, w.Vinv, w.z, w.pv, w.rzc, w.rrc, tol,
                            w.state, w.u, w.lblk, w.long_list, w.long_cnt);
@@ -1402,6 +1596,7 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
                            comm, ck.cb, ck.nck, ck.ntot);
         break;
     case SFM_BA_STAGE_ITER_FINISH:
+        if (ex) break;   // done by ITER
         if (fused) {
             hipLaunchKernelGGL(bas_pcg_finish_vec, dim3((8 * n_cam + FV - 1) / FV), dim3(FV), 0, st,
                                k, n_cam, w.q, comm, w.pv, w.Mc, dc, w.r, w.z, w.rzc, w.rrc,
@@ -1492,5 +1687,31 @@ extern "C" int sfm_ba_fix_params(sfm_ctx* ctx, int32_t n_cam, int32_t n_obs,
                            cam_idx, fixed, W);
         SFM_HIP_CHECK(hipGetLastError());
     }
+    return SFM_OK;
+}
+
+extern "C" int sfm_ba_set_schur(sfm_ctx* ctx, int32_t n_slot, const int32_t* slot_cam,
+                                int32_t n_seg, const int32_t* seg, int32_t n_inst,
+                                const int32_t* inst, const int32_t* row_ptr, int32_t n_ent,
+                                const int32_t* row_ent) {
+    SFM_REQUIRE(ctx != nullptr, "sfm_ba_set_schur: ctx is NULL");
+    SFM_REQUIRE(n_slot >= 0 && n_seg >= 0 && n_inst >= 0 && n_ent >= 0, "sfm_ba_set_schur: negative size");
+    if (n_slot == 0) {
+        ctx->ba_nslot = ctx->ba_nseg = ctx->ba_ninst = ctx->ba_nent = 0;
+        ctx->ba_slot_cam = ctx->ba_seg = ctx->ba_inst = ctx->ba_row_ptr = ctx->ba_row_ent = nullptr;
+        return SFM_OK;
+    }
+    SFM_REQUIRE(slot_cam && row_ptr && (n_seg == 0 || seg) && (n_inst == 0 || inst) &&
+                    (n_ent == 0 || row_ent),
+                "sfm_ba_set_schur: NULL array");
+    ctx->ba_nslot = n_slot;
+    ctx->ba_nseg = n_seg;
+    ctx->ba_ninst = n_inst;
+    ctx->ba_nent = n_ent;
+    ctx->ba_slot_cam = slot_cam;
+    ctx->ba_seg = seg;
+    ctx->ba_inst = inst;
+    ctx->ba_row_ptr = row_ptr;
+    ctx->ba_row_ent = row_ent;
     return SFM_OK;
 }

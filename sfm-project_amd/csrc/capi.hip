@@ -38,7 +38,7 @@ extern "C" {
 
 const char* sfm_last_error(void) { return g_err.c_str(); }
 
-int32_t sfm_version(void) { return 3; }  // 2: sfm_ba_solve_params.poll 0 = every 8; 3: BA chunk mode
+int32_t sfm_version(void) { return 4; }  // 2: sfm_ba_solve_params.poll 0 = every 8; 3: BA chunk mode; 4: explicit Schur
 
 int sfm_ctx_create(int32_t device, sfm_ctx** out) {
     SFM_REQUIRE(out != nullptr, "sfm_ctx_create: out is NULL");

@@ -194,6 +194,109 @@ def cam_bounds_device(cam_idx, cam_obs, n_cam: int, chunk_obs):
     return torch.searchsorted(key, q.reshape(-1)).to(torch.int32).reshape(n_cam, -1).contiguous()
 
 
+# Explicit reduced camera system (include/sfmcore.h sfm_ba_set_schur): the
+# off-diagonal Schur blocks formed once per solve from the camera-pair products of every point,
+# then the CG runs on S.  It pays when those products are few against the CG's per-iteration
+# stream of W (344 B per observation per iteration against 456 B per product per solve, the
+# iterations per solve 10-40): explicit iff products <= SCHUR_INST_PER_OBS * observations (short
+# tracks: cfg5's ~5 views per point give ~1.7; long tracks of 100 views give ~50).
+SCHUR_INST_PER_OBS = 4.0
+
+
+def schur_mode():
+    """SFM_BA_SCHUR: 'auto' (default, the rule above), '1' (always), '0' (never)."""
+    import os
+    return os.environ.get("SFM_BA_SCHUR", "auto")
+
+
+class SchurSpec:
+    """Structure of the explicit reduced camera system of one (local) problem: device int32
+    tensors slot_cam [n_slot, 2] (the WHOLE problem's camera pairs ci <= cj, sorted), seg [4, n_seg]
+    (local chunk, slot, first, end instance), inst [2, n_inst] (observation pairs, grouped by
+    (chunk, slot), point order inside a group), row_ptr [n_cam + 1] / row_ent [n_ent] (2 slot + t,
+    t = 1 for the slot's transpose: block row c of S)."""
+
+    def __init__(self, slot_cam, seg, inst, row_ptr, row_ent):
+        self.slot_cam, self.seg, self.inst = slot_cam, seg, inst
+        self.row_ptr, self.row_ent = row_ptr, row_ent
+        self.n_slot, self.n_seg = int(slot_cam.shape[0]), int(seg.shape[1])
+        self.n_inst, self.n_ent = int(inst.shape[1]), int(row_ent.numel())
+
+
+def schur_pair_count(pt_ptr):
+    """Camera-pair products of a point-major problem: Σ_p m_p (m_p - 1) / 2 (device int64 scalar)."""
+    import torch
+    m = (pt_ptr[1:] - pt_ptr[:-1]).long()
+    return (m * (m - 1) // 2).sum()
+
+
+def schur_instances(cam_idx, pt_idx, pt_ptr, n_cam, chunk_pt):
+    """The local camera-pair instances: for every point and every pair of its observations a < b
+    (observation order), oriented so that cam(a) <= cam(b); a pair within one camera also as
+    (b, a).  Returns (composite key chunk * n_cam^2 + ci * n_cam + cj, a, b) sorted stably by the
+    key — inside a (chunk, slot) group the instances stay in point order — plus the local keys."""
+    import torch
+    dev = cam_idx.device
+    n_obs = int(cam_idx.numel())
+    ptr = pt_ptr.long()
+    if n_obs == 0:
+        e = torch.zeros(0, dtype=torch.int64, device=dev)
+        return e, e, e
+    end = ptr[1:][pt_idx.long()]                               # end of each observation's point
+    o = torch.arange(n_obs, dtype=torch.int64, device=dev)
+    cnt = end - o - 1                                          # partners after o in its point
+    a = torch.repeat_interleave(o, cnt)
+    first = torch.cumsum(cnt, 0) - cnt
+    b = a + 1 + (torch.arange(a.numel(), dtype=torch.int64, device=dev)
+                 - torch.repeat_interleave(first, cnt))
+    cam = cam_idx.long()
+    ca, cb = cam[a], cam[b]
+    sw = ca > cb
+    a, b = torch.where(sw, b, a), torch.where(sw, a, b)
+    same = ca == cb
+    if bool(same.any()):
+        a, b = torch.cat([a, b[same]]), torch.cat([b, a[same]])
+    ci, cj = cam[a], cam[b]
+    cpt = torch.as_tensor(list(chunk_pt[1:]), dtype=torch.int64, device=dev)
+    k = torch.searchsorted(cpt, pt_idx.long()[a], right=True)
+    key = (k * n_cam + ci) * n_cam + cj
+    key, order = torch.sort(key, stable=True)
+    return key, a[order], b[order]
+
+
+def schur_spec(key, a, b, n_cam, slot_keys):
+    """SchurSpec from the sorted local instances and the WHOLE problem's slot keys
+    (ci * n_cam + cj, sorted unique int64, identical on every rank)."""
+    import torch
+    dev = slot_keys.device
+    i32 = torch.int32
+    nn = n_cam * n_cam
+    comp, cnt = torch.unique_consecutive(key, return_counts=True)
+    starts = torch.cumsum(cnt, 0) - cnt
+    seg = torch.stack([comp // nn, torch.searchsorted(slot_keys, comp % nn), starts,
+                       starts + cnt]).to(i32).contiguous()
+    ci, cj = slot_keys // n_cam, slot_keys % n_cam
+    slot_cam = torch.stack([ci, cj], 1).to(i32).contiguous()
+    s = torch.arange(slot_keys.numel(), dtype=torch.int64, device=dev)
+    off = ci != cj
+    rows = torch.cat([ci, cj[off]])
+    other = torch.cat([cj, ci[off]])
+    ent = torch.cat([2 * s, 2 * s[off] + 1])
+    order = torch.sort(rows * n_cam + other, stable=True).indices
+    rows, ent = rows[order], ent[order]
+    row_ptr = torch.zeros(n_cam + 1, dtype=torch.int64, device=dev)
+    if rows.numel():
+        row_ptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n_cam), 0)
+    inst = torch.stack([a, b]).to(i32).contiguous()
+    return SchurSpec(slot_cam, seg, inst, row_ptr.to(i32).contiguous(), ent.to(i32).contiguous())
+
+
+def torch_unique_keys(key, n_cam):
+    """The camera-pair keys (ci * n_cam + cj) of composite instance keys, sorted unique."""
+    import torch
+    return torch.unique(key % (n_cam * n_cam))
+
+
 class BAProblem:
     """Device-resident observations + CSR indices for repeated linearisation / solves."""
 
@@ -232,6 +335,7 @@ class BAProblem:
         self.n_cam, self.n_pt = n_cam, n_pt
         self.ctx = sfmcore.context(device)
         self.chunks = None
+        self.schur = None   # SchurSpec (set_schur), the explicit reduced camera system
         if chunks is not None and chunks != 0:
             if isinstance(chunks, int):
                 cpt, cob = shard_cuts_device(self.pt_idx, n_pt, chunks, ptr=self.pt_ptr)
@@ -243,15 +347,33 @@ class BAProblem:
             cb = cam_bounds_device(self.cam_idx, self.cam_obs, n_cam, cob)
             self.chunks = BAChunks(cpt, cob, cb, n_total, k0)
 
+    def set_schur(self, union=None):
+        """Turn the explicit reduced camera system on (needs chunk mode).  union: for a shard, maps
+        this shard's camera-pair keys (sorted unique int64 device tensor) to the WHOLE problem's
+        (a collective; the same result on every rank); None = this problem's own."""
+        if self.chunks is None:
+            raise ValueError("BAProblem.set_schur: the explicit Schur system needs chunk mode")
+        key, a, b = schur_instances(self.cam_idx, self.pt_idx, self.pt_ptr, self.n_cam,
+                                    self.chunks.chunk_pt)
+        slot_keys = torch_unique_keys(key, self.n_cam)
+        if union is not None:
+            slot_keys = union(slot_keys)
+        self.schur = schur_spec(key, a, b, self.n_cam, slot_keys)
+
     def _call(self, fn, *a, **kw):
-        """fn under this problem's chunk mode (set on the shared context, then cleared)."""
+        """fn under this problem's chunk mode and explicit-Schur structure (set on the shared
+        context, then cleared)."""
         if self.chunks is None:
             return fn(*a, **kw)
         self.ctx.ba_set_chunks(self.chunks)
+        if self.schur is not None:
+            self.ctx.ba_set_schur(self.schur)
         try:
             return fn(*a, **kw)
         finally:
             self.ctx.ba_set_chunks(None)
+            if self.schur is not None:
+                self.ctx.ba_set_schur(None)
 
     def _slots(self):
         ck = self.chunks
@@ -270,7 +392,7 @@ class BAProblem:
     def solve_sharded(self, lin, lam, allreduce, max_iter=100, tol=1e-10, **kw):
         return self._call(self.ctx.ba_solve_sharded, lin, self.cam_idx, self.pt_idx, self.pt_ptr,
                           self.cam_ptr, self.cam_obs, lam, allreduce, max_iter=max_iter, tol=tol,
-                          chunks=self.chunks, **kw)
+                          chunks=self.chunks, schur=self.schur, **kw)
 
     def cost(self, cams, pts, loss_s=0.0):
         return self._call(self.ctx.ba_cost, cams, self.pp, pts, self.cam_idx, self.pt_idx, self.uv,
@@ -586,7 +708,32 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     else:
         prob = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, hi - lo, device, chunks=nchunk or None)
     f64 = torch.float64
+    # explicit reduced camera system (SchurSpec) when the camera-pair products are few: the rule
+    # sees the WHOLE problem's counts, so every rank (and the single process) decides alike
+    use_schur = False
+    smode = schur_mode()
+    if nchunk > 0 and smode != "0":
+        tgt = full if full is not None else prob
+        cnt = schur_pair_count(tgt.pt_ptr).double().reshape(1)
+        n_obs_tot = len(tgt.cam_idx)
+        if allreduce is not None and full is None:
+            allreduce(cnt)
+            n_obs_tot = n_obs_all
+        use_schur = smode == "1" or float(cnt.item()) <= SCHUR_INST_PER_OBS * max(n_obs_tot, 1)
+        if use_schur:
+            if allreduce is not None and full is None:
+                def union(keys):   # every shard's camera pairs -> the whole problem's (sorted)
+                    nk = torch.zeros(world, dtype=f64, device=prob.dev)
+                    nk[rank] = keys.numel()
+                    allreduce(nk)
+                    g = _gather_rows(keys.double().reshape(-1, 1), [int(v) for v in nk.tolist()],
+                                     group)
+                    return torch.unique(g.reshape(-1).long())
+                prob.set_schur(union)
+            else:
+                tgt.set_schur()
     if info is not None:
+        info["schur"] = use_schur
         torch.cuda.synchronize(prob.dev)
         info["problem_s"] = time.perf_counter() - t_entry   # BAProblem: CSR, chunk table
 

@@ -27,7 +27,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
             "sfm_ransac_stats", "sfm_ransac_f_batch_f64", "sfm_graph_rows_packed",
             "sfm_graph_expand", "sfm_match_batch_both", "sfm_ransac_wave_stops",
-            "sfm_ba_set_chunks", "sfm_ba_chunk_tree"]
+            "sfm_ba_set_chunks", "sfm_ba_chunk_tree", "sfm_ba_set_schur"]
 
 
 class SfmCoreError(RuntimeError):
@@ -61,7 +61,7 @@ class RansacParams(C.Structure):
 
 # stages of sfm_ba_solve_stage (include/sfmcore.h)
 (BA_STAGE_SETUP, BA_STAGE_SETUP_FINISH, BA_STAGE_ITER, BA_STAGE_ITER_FINISH, BA_STAGE_BACKSUB,
- BA_STAGE_MODEL, BA_STAGE_POLL) = range(7)
+ BA_STAGE_MODEL, BA_STAGE_POLL, BA_STAGE_SCHUR) = range(8)
 # up to this many cameras ITER_FINISH is one k-free launch (ba_solve.hip FINISH_VEC_MAX_CAM)
 BA_FINISH_VEC_MAX_CAM = 1024
 
@@ -112,6 +112,7 @@ def load_library(path: str = LIB_PATH):
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
         L.sfm_ba_fix_params.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp]
         L.sfm_ba_set_chunks.argtypes = [vp, i32, vp, vp, i32, vp]
+        L.sfm_ba_set_schur.argtypes = [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp]
         L.sfm_ba_chunk_tree.argtypes = [vp, i32, i64, vp, vp]
         L.sfm_orb_batch.argtypes = [vp, vp, i32, i32, i32, C.POINTER(OrbParams), vp, vp, vp]
         L.sfm_register_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(RegisterParams),
@@ -380,6 +381,16 @@ class Context:
                                   int(spec.n_total), _ptr(spec.cam_bounds))
         _check(self.lib.sfm_ba_set_chunks(self.handle, *args))
 
+    def ba_set_schur(self, spec=None):
+        """spec = reconstruction.SchurSpec (the explicit reduced camera system's structure) or None
+        (off).  Applies to the next BA solves (sfm_ba_set_schur; needs chunk mode)."""
+        if spec is None:
+            _check(self.lib.sfm_ba_set_schur(self.handle, 0, None, 0, None, 0, None, None, 0, None))
+            return
+        _check(self.lib.sfm_ba_set_schur(self.handle, spec.n_slot, _ptr(spec.slot_cam), spec.n_seg,
+                                         _ptr(spec.seg), spec.n_inst, _ptr(spec.inst),
+                                         _ptr(spec.row_ptr), spec.n_ent, _ptr(spec.row_ent)))
+
     def ba_chunk_tree(self, parts, out=None):
         """sfm_ba_chunk_tree: parts [n_total, ...] f64 device -> out [...] (the canonical tree)."""
         torch = self.torch
@@ -505,7 +516,8 @@ class Context:
         return dc, dp, info
 
     def ba_solve_sharded(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, allreduce,
-                         max_iter=100, tol=1e-10, out=None, poll=8, graph=False, chunks=None):
+                         max_iter=100, tol=1e-10, out=None, poll=8, graph=False, chunks=None,
+                         schur=None):
         """ba_solve on this rank's point shard (lin: ba_jtj of the shard with U / gc already
         all-reduced), driving sfm_ba_solve_stage: allreduce(t) sums the f64 device tensor t over
         all ranks in place, ordered on the current stream (reconstruction.make_allreduce).
@@ -529,7 +541,12 @@ class Context:
         # it see every chunk's partial bit for bit, in chunk order
         nt = chunks.n_total if chunks is not None else 1
         k0 = chunks.k0 if chunks is not None else 0
-        comm = torch.zeros(nt * 44 * nc, dtype=torch.float64, device=dev)
+        # explicit S (schur = reconstruction.SchurSpec, set on this context): SETUP's 44-sum
+        # partials, then SCHUR's T partials [n_total][n_slot][64] behind them, ONE exchange; the
+        # CG iterations then run on every rank from the replicated S with no exchange
+        ns = schur.n_slot if schur is not None else 0
+        n_setup = nt * 44 * nc
+        comm = torch.zeros(n_setup + nt * 64 * ns, dtype=torch.float64, device=dev)
         prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll))
         done = C.c_int32(0)
         cptr = comm.data_ptr()
@@ -551,7 +568,13 @@ class Context:
                 comm[:n].zero_()
             stage(s, k, a)
             allreduce(comm[:n])
-        produce(BA_STAGE_SETUP, nt * 44 * nc, a_setup)
+        if ns:
+            comm.zero_()
+            stage(BA_STAGE_SETUP, 0, a_setup)
+            stage(BA_STAGE_SCHUR, 0, args(n_setup + k0 * 64 * ns))
+            allreduce(comm)
+        else:
+            produce(BA_STAGE_SETUP, n_setup, a_setup)
         stage(BA_STAGE_SETUP_FINISH)
         every = poll
         # windows of `poll` iterations between host polls.  With a capturable collective (RCCL)
@@ -559,7 +582,7 @@ class Context:
         # the iteration kernels depend on k only through its parity and k > 0 (the one-launch
         # finish counts iterations itself), so a window captured at k = poll replays at any
         # k = m·poll, poll even.
-        graph = (graph and getattr(allreduce, "graph_safe", False) and every > 0
+        graph = (graph and not ns and getattr(allreduce, "graph_safe", False) and every > 0
                  and every % 2 == 0 and nc <= BA_FINISH_VEC_MAX_CAM)
         win = every if every > 0 else max(max_iter, 1)
         g = None
@@ -587,6 +610,9 @@ class Context:
                     torch.cuda.current_stream(dev).wait_stream(cap)
                     self._bind_stream()
                 g.replay()
+            elif ns:
+                for j in range(k, k + n):   # replicated S: nothing to exchange
+                    stage(BA_STAGE_ITER, j)
             else:
                 for j in range(k, k + n):
                     produce(BA_STAGE_ITER, nt * 8 * nc, a_iter, j)

@@ -280,3 +280,95 @@ def test_c_abi_capture_with_zero_initialised_poll():
         torch.cuda.synchronize()
         for a, b in zip(out, ref):
             assert torch.equal(a, b), poll
+
+
+def _explicit_vs_oracle(prob, lam, loss_s, chunks=8):
+    """The explicit reduced camera system (SchurSpec, sfm_ba_set_schur) against the oracle's PCG,
+    the dense solve and the implicit chunked solve of the same problem."""
+    import torch
+    n_cam, n_pt = len(prob["cams"]), len(prob["pts"])
+    args = (prob["pp"], prob["cam_idx"], prob["pt_idx"], prob["uv"], n_cam, n_pt)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()
+    cams, pts = T(prob["cams"]), T(prob["pts"])
+    Pi = R.BAProblem(*args, chunks=chunks)
+    Pe = R.BAProblem(*args, chunks=chunks)
+    Pe.set_schur()
+    assert Pe.schur.n_slot > 0
+    out = []
+    for P in (Pi, Pe):
+        lin = P.linearize(cams, pts, loss_s)
+        dc, dp, info = P.solve(lin, lam, max_iter=500, tol=1e-12)
+        out.append((dc.cpu().numpy(), dp.cpu().numpy(), info.cpu().numpy()))
+    o = O.ba_jtj(prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"],
+                 prob["uv"], loss_s)
+    oargs = (o["U"], o["V"], o["W"], o["gc"], o["gp"], prob["cam_idx"], prob["pt_idx"])
+    odc, odp, oit, _ = L.schur_pcg(*oargs, lam, max_iter=500, tol=1e-12)
+    ddc, ddp = L.solve_dense(*oargs, lam)
+    dc, dp, info = out[1]
+    assert info[1] <= 1e-12 and abs(info[0] - oit) <= 3 and info[4] == 0
+    for a, b in ((dc, odc), (dc, ddc), (dc, out[0][0])):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-8 * np.abs(b).max())
+    for a, b in ((dp, odp), (dp, ddp), (dp, out[0][1])):
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-8 * np.abs(b).max())
+    gd, q = L.model_terms(*oargs[:5], prob["cam_idx"], prob["pt_idx"], dc, dp)
+    assert abs(info[2] - gd) <= 1e-11 * abs(gd) and abs(info[3] - q) <= 1e-11 * abs(q)
+    return Pe
+
+
+@pytest.mark.parametrize("lam,loss_s,chunks", [(1e-4, 0.0, 8), (1e-1, 0.0, 3), (1e-3, 2.0, 8)])
+def test_explicit_schur_solve_matches_oracle(lam, loss_s, chunks):
+    prob = synth.make_ba_problem(12, 400, obs_per_pt=4, seed=11, perturb=2e-3)
+    _explicit_vs_oracle(prob, lam, loss_s, chunks)
+
+
+def test_explicit_schur_duplicate_camera_and_long_tracks():
+    """A point seen twice by one camera (its cross term lands on the diagonal block, both
+    orientations), long tracks (many camera pairs per point) and an unobserved camera."""
+    counts = np.where(np.arange(60) % 9 == 0, 40, 3)
+    prob = synth.make_ba_problem(50, 60, obs_per_pt=counts, seed=31, perturb=2e-3)
+    o = np.nonzero(prob["pt_idx"] == 1)[0]
+    prob["cam_idx"] = prob["cam_idx"].copy()
+    prob["cam_idx"][o[1]] = prob["cam_idx"][o[0]]       # same camera twice for point 1
+    prob["cams"] = np.concatenate([prob["cams"], prob["cams"][:1]])
+    prob["pp"] = np.concatenate([prob["pp"], prob["pp"][:1]])
+    Pe = _explicit_vs_oracle(prob, 1e-3, 1.5)
+    sc = Pe.schur.slot_cam.cpu().numpy()
+    assert np.any(sc[:, 0] == sc[:, 1])                  # a diagonal slot from the duplicate
+
+
+def test_explicit_schur_sharded_world1_bit_identical():
+    """The explicit system through the sharded stages (SETUP + SCHUR, one exchange, local CG) in a
+    world-size-1 RCCL group: the same bits as sfm_ba_solve with it."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    prob = synth.make_ba_problem(20, 600, obs_per_pt=5, seed=17, perturb=2e-3)
+    n_cam, n_pt = len(prob["cams"]), len(prob["pts"])
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()
+    cams, pts = T(prob["cams"]), T(prob["pts"])
+    args = (prob["pp"], prob["cam_idx"], prob["pt_idx"], prob["uv"], n_cam, n_pt)
+    P = R.BAProblem(*args, chunks=8)
+    P.set_schur()
+    lin = P.linearize(cams, pts)
+    ref = [t.cpu().numpy() for t in P.solve(lin, 1e-3, max_iter=200, tol=1e-10)]
+    # the same problem as a 1-rank shard (export form: n_total = 8, k0 = 0)
+    S = R.BAProblem(*args, chunks=list(P.chunks.chunk_pt), n_total=8, k0=0)
+    S.set_schur()
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        ar = R.make_allreduce()
+        ls = S.linearize(cams, pts)
+        tot = S.ctx.ba_chunk_tree(torch.cat([ls["U"].reshape(8, -1), ls["gc"].reshape(8, -1)], 1))
+        ls["U"] = tot[:n_cam * 64].view(n_cam, 8, 8)
+        ls["gc"] = tot[n_cam * 64:].view(n_cam, 8)
+        got = [t.cpu().numpy() for t in S.solve_sharded(ls, 1e-3, ar, max_iter=200, tol=1e-10)]
+        R.release_allreduce()
+    finally:
+        dist.destroy_process_group()
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
