@@ -701,7 +701,8 @@ def cfg5_run(n_img, k, n_pts, steps, warmup, world, rank, local, pcg):
                     for kk, v in rec.timings.items()},
         "bundle_adjustments": rec.ba_log,
         "ba_phase_s": {k: round(float(sum(b.get(k, 0.0) for b in rec.ba_log)), 4)
-                       for k in ("select_s", "entry_wait_s", "setup_s", "problem_s", "lm_s", "post_s", "s")},
+                       for k in ("select_s", "entry_wait_s", "setup_s", "problem_s", "schur_s", "lm_s",
+                                 "post_s", "s")},
         "lm_steps": int(sum(b["lm_steps"] for b in rec.ba_log)),
         "cg_iters": int(sum(b["cg_iters"] for b in rec.ba_log)),
         "pcg_branches": sorted({b["pcg"] for b in rec.ba_log}),
@@ -742,10 +743,35 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
         sn = timed(lambda: P.solve(lin, 1e-3, max_iter=cg, tol=0.0, poll=-1), max(reps // 4, 2))
         return jtj, (sn - s0) / cg
     jtj_ms, it_ms = measure(P)
-    # the production form: bundle_adjust's sharding-invariant chunk sums (reconstruction.BAChunks)
+    # the production forms: bundle_adjust's sharding-invariant chunk sums (reconstruction.BAChunks)
+    # and, where schur_rule takes it, the explicit reduced camera system on top
     nck = R.ba_chunk_count()
     jtj_ck, it_ck = measure(R.BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device,
                                         chunks=nck)) if nck else (None, None)
+    explicit = None
+    if nck:
+        Pe = R.BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device, chunks=nck)
+        Pe.set_schur()
+        sp = Pe.schur
+        lin = Pe.linearize(c, p, 2.0)
+        s0e = timed(lambda: Pe.solve(lin, 1e-3, max_iter=0, tol=0.0), reps)
+        Pe.schur = None
+        s0i = timed(lambda: Pe.solve(lin, 1e-3, max_iter=0, tol=0.0), reps)
+        Pe.set_schur()
+        sne = timed(lambda: Pe.solve(lin, 1e-3, max_iter=cg, tol=0.0, poll=-1), max(reps // 4, 2))
+        build_ms = s0e - s0i            # T: the products + the tree, once per solve
+        tb = sp.n_inst * (192 + 192 + 72)
+        explicit = {"rule": R.schur_rule(sp.n_inst, sp.n_seg, sp.n_slot, n_obs),
+                    "n_inst": sp.n_inst, "n_slot": sp.n_slot, "n_seg": sp.n_seg,
+                    "schur_build": {"ms": build_ms, "bytes": tb,
+                                    "achieved_GBs": tb / (build_ms * 1e-3) / 1e9 if build_ms > 0 else None,
+                                    "frac": tb / (build_ms * 1e-3) / PEAK_HBM if build_ms > 0 else None,
+                                    "note": "per solve; algorithmic bytes = per camera-pair product "
+                                            "W_a + W_b rows + V_d^-1 (456 B)"},
+                    "cg_iteration": {"ms": (sne - s0e) / cg,
+                                     "bytes": 1024 * sp.n_slot + 8 * 16 * n_cam,
+                                     "note": "S blocks (both orientations, 1 KB per camera pair) "
+                                             "+ camera vectors: latency-bound, 2 launches"}}
     idx_b = 4 * (2 * n_obs + (n_pt + 1) + (n_cam + 1) + n_obs)     # cam/pt idx, CSR ptrs, cam_obs
     k3_b = (8 * (8 * n_cam + 2 * n_cam + 3 * n_pt + 2 * n_obs) + idx_b
             + 8 * (64 * n_cam + 9 * n_pt + 24 * n_obs + 8 * n_cam + 3 * n_pt + 2 * n_obs + 1))
@@ -762,6 +788,7 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
                 "k3": {"ms": jtj_ck, "frac": k3_b / (jtj_ck * 1e-3) / PEAK_HBM},
                 "cg_iteration": {"ms": it_ck,
                                  "frac": cg_b / (it_ck * 1e-3) / PEAK_HBM if it_ck > 0 else None}},
+            "explicit_schur": explicit,
             "peak_GBs": PEAK_HBM / 1e9}
 
 

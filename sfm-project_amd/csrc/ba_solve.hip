@@ -779,32 +779,34 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
 //
 // T_slot = Σ over the slot's camera-pair instances (a, b) of Y_a W_bᵀ, Y_a = W_a V_d⁻¹ (the point of
 // a), so the off-diagonal Schur blocks are S_ij = -T_ij; the diagonal blocks S_cc come from
-// bas_camera_setup.  Two waves per (chunk, slot) group, wave h the block's rows 4h .. 4h + 3:
-// lane-strided over the group's instances (an order that depends only on the group), 32
-// accumulators per lane, then the recursive-halving wave sum — lane t ends holding element
-// 32 h + t and stores it.  (All 64 rows in one wave: 262 registers, one wave per SIMD.)
+// bas_camera_setup.  SB_WAVES waves per (chunk, slot) group, wave h the block's rows
+// SB_ROWS h .. SB_ROWS (h + 1) - 1: lane-strided over the group's instances (an order that depends
+// only on the group), 8 SB_ROWS accumulators per lane, then the recursive-halving wave sum — lane t
+// ends holding element 8 SB_ROWS h + t and stores it.  (All 64 elements in one wave: 262 registers,
+// one wave per SIMD; 2 waves of 32: 178 registers, 0.216 ms per T at cfg5's final model.)
+#ifndef SB_WAVES
+#define SB_WAVES 2
+#endif
+constexpr int SB_ROWS = 8 / SB_WAVES, SB_N = 8 * SB_ROWS;
 __global__ __launch_bounds__(256) void bas_schur_build(
     int n_seg, int n_slot, int n_inst, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ inst, const int32_t* __restrict__ pt_idx,
     const double* __restrict__ W, const double* __restrict__ Vinv, double* __restrict__ Tpart) {
     const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int s = wv >> 1, h = wv & 1;
+    const int s = wv / SB_WAVES, h = wv % SB_WAVES;
     if (s >= n_seg) return;   // wave-uniform
     const int k = seg[s], slot = seg[n_seg + s], i0 = seg[2 * n_seg + s], i1 = seg[3 * n_seg + s];
-    double acc[32];
+    double acc[SB_N];
 #pragma unroll
-    for (int t = 0; t < 32; ++t) acc[t] = 0.0;
+    for (int t = 0; t < SB_N; ++t) acc[t] = 0.0;
     for (int i = i0 + lane; i < i1; i += 64) {
         const int a = inst[i], b = inst[n_inst + i];
         const int p = pt_idx[a];
-        double wa[12], wb[24], vi[9];
-        const double2* Wa = (const double2*)(W + 24 * (size_t)a + 12 * h);   // rows 4h .. 4h + 3
+        double wa[3 * SB_ROWS], wb[24], vi[9];
+        const double* Wa = W + 24 * (size_t)a + 3 * SB_ROWS * h;   // rows SB_ROWS h ..
         const double2* Wb = (const double2*)(W + 24 * (size_t)b);
 #pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            const double2 u = Wa[t];
-            wa[2 * t] = u.x; wa[2 * t + 1] = u.y;
-        }
+        for (int t = 0; t < 3 * SB_ROWS; ++t) wa[t] = Wa[t];
 #pragma unroll
         for (int t = 0; t < 12; ++t) {
             const double2 v = Wb[t];
@@ -813,21 +815,21 @@ __global__ __launch_bounds__(256) void bas_schur_build(
         const double* Vi = Vinv + 9 * (size_t)p;
 #pragma unroll
         for (int t = 0; t < 9; ++t) vi[t] = Vi[t];
-        double y[12];   // rows 4h .. 4h + 3 of W_a V_d⁻¹, bas_camera_setup's expression
+        double y[3 * SB_ROWS];   // rows of W_a V_d⁻¹, bas_camera_setup's expression
 #pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2)
+        for (int i2 = 0; i2 < SB_ROWS; ++i2)
 #pragma unroll
             for (int j = 0; j < 3; ++j)
                 y[3 * i2 + j] = wa[3 * i2] * vi[j] + wa[3 * i2 + 1] * vi[3 + j] + wa[3 * i2 + 2] * vi[6 + j];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < SB_ROWS; ++r)
 #pragma unroll
             for (int c = 0; c < 8; ++c)
                 acc[8 * r + c] += y[3 * r] * wb[3 * c] + y[3 * r + 1] * wb[3 * c + 1] + y[3 * r + 2] * wb[3 * c + 2];
     }
     int idx;
-    if (sfm::wave_halving_sum<32>(acc, lane, idx))
-        Tpart[((size_t)k * n_slot + slot) * 64 + 32 * h + idx] = acc[0];
+    if (sfm::wave_halving_sum<SB_N>(acc, lane, idx))
+        Tpart[((size_t)k * n_slot + slot) * 64 + SB_N * h + idx] = acc[0];
 }
 
 // T = the canonical tree over the n_total chunk partials (parts [n_total][n]).
@@ -1418,7 +1420,7 @@ static int schur_build(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, con
     const size_t n = (size_t)ctx->ba_nchunk * ctx->ba_nslot * 64;
     SFM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * n, st));
     if (ctx->ba_nseg > 0) {
-        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg + 1) / 2), dim3(256), 0, st,
+        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg * SB_WAVES + 3) / 4), dim3(256), 0, st,
                            ctx->ba_nseg, ctx->ba_nslot, ctx->ba_ninst, ctx->ba_seg, ctx->ba_inst,
                            pt_idx, W, w.Vinv, out);
         SFM_HIP_CHECK(hipGetLastError());

@@ -201,6 +201,19 @@ def cam_bounds_device(cam_idx, cam_obs, n_cam: int, chunk_obs):
 # iterations per solve 10-40): explicit iff products <= SCHUR_INST_PER_OBS * observations (short
 # tracks: cfg5's ~5 views per point give ~1.7; long tracks of 100 views give ~50).
 SCHUR_INST_PER_OBS = 4.0
+# ... and when the structure is dense enough to use: T is built by a wave pair per (chunk, slot)
+# group, which wants >= SCHUR_INST_PER_SEG products per group, and the product reads 1 KB per
+# camera pair per iteration, which must stay under SCHUR_S_FRACTION of the implicit iteration's
+# 344 B per observation (random visibility over 500 cameras: 4.4 products per group and every one
+# of the 124 750 pairs: 4.0 ms per T build and 87 us per iteration, tests/perf/ba_schur_time.py)
+SCHUR_INST_PER_SEG = 16.0
+SCHUR_S_FRACTION = 0.25
+
+
+def schur_rule(n_inst, n_seg, n_slot, n_obs):
+    """True when the explicit reduced camera system pays (whole-problem counts)."""
+    return (n_inst <= SCHUR_INST_PER_OBS * max(n_obs, 1) and n_inst >= SCHUR_INST_PER_SEG * n_seg
+            and 1024.0 * n_slot <= SCHUR_S_FRACTION * 344.0 * max(n_obs, 1))
 
 
 def schur_mode():
@@ -234,44 +247,58 @@ def schur_instances(cam_idx, pt_idx, pt_ptr, n_cam, chunk_pt):
     """The local camera-pair instances: for every point and every pair of its observations a < b
     (observation order), oriented so that cam(a) <= cam(b); a pair within one camera also as
     (b, a).  Returns (composite key chunk * n_cam^2 + ci * n_cam + cj, a, b) sorted stably by the
-    key — inside a (chunk, slot) group the instances stay in point order — plus the local keys."""
+    key — inside a (chunk, slot) group the instances stay in point order.  Two host syncs (the
+    instance count and the same-camera count)."""
     import torch
     dev = cam_idx.device
     n_obs = int(cam_idx.numel())
-    ptr = pt_ptr.long()
     if n_obs == 0:
         e = torch.zeros(0, dtype=torch.int64, device=dev)
         return e, e, e
+    ptr = pt_ptr.long()
     end = ptr[1:][pt_idx.long()]                               # end of each observation's point
     o = torch.arange(n_obs, dtype=torch.int64, device=dev)
     cnt = end - o - 1                                          # partners after o in its point
-    a = torch.repeat_interleave(o, cnt)
+    total = int(cnt.sum())
+    a = torch.repeat_interleave(o, cnt, output_size=total)
     first = torch.cumsum(cnt, 0) - cnt
-    b = a + 1 + (torch.arange(a.numel(), dtype=torch.int64, device=dev)
-                 - torch.repeat_interleave(first, cnt))
+    b = a + 1 + (torch.arange(total, dtype=torch.int64, device=dev)
+                 - torch.repeat_interleave(first, cnt, output_size=total))
     cam = cam_idx.long()
     ca, cb = cam[a], cam[b]
     sw = ca > cb
     a, b = torch.where(sw, b, a), torch.where(sw, a, b)
     same = ca == cb
-    if bool(same.any()):
+    if int(same.sum()):
         a, b = torch.cat([a, b[same]]), torch.cat([b, a[same]])
-    ci, cj = cam[a], cam[b]
     cpt = torch.as_tensor(list(chunk_pt[1:]), dtype=torch.int64, device=dev)
     k = torch.searchsorted(cpt, pt_idx.long()[a], right=True)
-    key = (k * n_cam + ci) * n_cam + cj
+    key = (k * n_cam + cam[a]) * n_cam + cam[b]
+    if len(chunk_pt) * n_cam * n_cam < 2 ** 31:
+        key = key.to(torch.int32)                              # a 32-bit sort
     key, order = torch.sort(key, stable=True)
-    return key, a[order], b[order]
+    return key.long(), a[order], b[order]
 
 
-def schur_spec(key, a, b, n_cam, slot_keys):
-    """SchurSpec from the sorted local instances and the WHOLE problem's slot keys
-    (ci * n_cam + cj, sorted unique int64, identical on every rank)."""
+def schur_groups(key):
+    """(composite keys of the (chunk, slot) groups, their sizes) of sorted instance keys."""
+    import torch
+    return torch.unique_consecutive(key, return_counts=True)
+
+
+def torch_unique_keys(comp, n_cam):
+    """The camera-pair keys (ci * n_cam + cj) of composite keys, sorted unique."""
+    import torch
+    return torch.unique(comp % (n_cam * n_cam))
+
+
+def schur_spec(comp, cnt, a, b, n_cam, slot_keys):
+    """SchurSpec from the (chunk, slot) groups of the sorted local instances and the WHOLE
+    problem's slot keys (ci * n_cam + cj, sorted unique int64, identical on every rank)."""
     import torch
     dev = slot_keys.device
     i32 = torch.int32
     nn = n_cam * n_cam
-    comp, cnt = torch.unique_consecutive(key, return_counts=True)
     starts = torch.cumsum(cnt, 0) - cnt
     seg = torch.stack([comp // nn, torch.searchsorted(slot_keys, comp % nn), starts,
                        starts + cnt]).to(i32).contiguous()
@@ -282,19 +309,11 @@ def schur_spec(key, a, b, n_cam, slot_keys):
     rows = torch.cat([ci, cj[off]])
     other = torch.cat([cj, ci[off]])
     ent = torch.cat([2 * s, 2 * s[off] + 1])
-    order = torch.sort(rows * n_cam + other, stable=True).indices
-    rows, ent = rows[order], ent[order]
-    row_ptr = torch.zeros(n_cam + 1, dtype=torch.int64, device=dev)
-    if rows.numel():
-        row_ptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n_cam), 0)
+    rk, order = torch.sort(rows * n_cam + other, stable=True)
+    row_ptr = torch.searchsorted(rk, torch.arange(n_cam + 1, dtype=torch.int64, device=dev) * n_cam)
     inst = torch.stack([a, b]).to(i32).contiguous()
-    return SchurSpec(slot_cam, seg, inst, row_ptr.to(i32).contiguous(), ent.to(i32).contiguous())
-
-
-def torch_unique_keys(key, n_cam):
-    """The camera-pair keys (ci * n_cam + cj) of composite instance keys, sorted unique."""
-    import torch
-    return torch.unique(key % (n_cam * n_cam))
+    return SchurSpec(slot_cam, seg, inst, row_ptr.to(i32).contiguous(),
+                     ent[order].to(i32).contiguous())
 
 
 class BAProblem:
@@ -355,10 +374,11 @@ class BAProblem:
             raise ValueError("BAProblem.set_schur: the explicit Schur system needs chunk mode")
         key, a, b = schur_instances(self.cam_idx, self.pt_idx, self.pt_ptr, self.n_cam,
                                     self.chunks.chunk_pt)
-        slot_keys = torch_unique_keys(key, self.n_cam)
+        comp, cnt = schur_groups(key)
+        slot_keys = torch_unique_keys(comp, self.n_cam)
         if union is not None:
             slot_keys = union(slot_keys)
-        self.schur = schur_spec(key, a, b, self.n_cam, slot_keys)
+        self.schur = schur_spec(comp, cnt, a, b, self.n_cam, slot_keys)
 
     def _call(self, fn, *a, **kw):
         """fn under this problem's chunk mode and explicit-Schur structure (set on the shared
@@ -721,7 +741,9 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             n_obs_tot = n_obs_all
         use_schur = smode == "1" or float(cnt.item()) <= SCHUR_INST_PER_OBS * max(n_obs_tot, 1)
         if use_schur:
-            if allreduce is not None and full is None:
+            t_s = time.perf_counter()
+            sharded_s = allreduce is not None and full is None
+            if sharded_s:
                 def union(keys):   # every shard's camera pairs -> the whole problem's (sorted)
                     nk = torch.zeros(world, dtype=f64, device=prob.dev)
                     nk[rank] = keys.numel()
@@ -732,6 +754,18 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                 prob.set_schur(union)
             else:
                 tgt.set_schur()
+            sp = tgt.schur
+            tot = torch.tensor([sp.n_inst, sp.n_seg], dtype=f64, device=prob.dev)
+            if sharded_s:
+                allreduce(tot)   # the whole problem's products and groups
+            n_inst_tot, n_seg_tot = (float(v) for v in tot.tolist())
+            if smode != "1" and not schur_rule(n_inst_tot, n_seg_tot, sp.n_slot, n_obs_tot):
+                tgt.schur = None
+                use_schur = False
+            if info is not None:
+                info["schur_terms"] = {"n_inst": n_inst_tot, "n_seg": n_seg_tot,
+                                       "n_slot": sp.n_slot, "n_obs": n_obs_tot}
+                info["schur_s"] = time.perf_counter() - t_s   # structure + rule (ends in a sync)
     if info is not None:
         info["schur"] = use_schur
         torch.cuda.synchronize(prob.dev)

@@ -167,9 +167,13 @@ def test_ba_sharded_three_ranks_with_an_empty_shard(tmp_path):
     assert len(d[2]["dp"]) == 0
 
 
-def test_ba_sharded_two_ranks(tmp_path):
+@pytest.mark.parametrize("schur", ["auto", "1"])
+def test_ba_sharded_two_ranks(tmp_path, monkeypatch, schur):
     """Two ranks (torch.distributed.run, gloo, both on GPU 0) shard the points: the ranks agree
-    bit for bit, and the sharded solve / LM match the single-process ones to fp64 reassociation."""
+    bit for bit, and the sharded solve / LM match the single-process ones to fp64 reassociation.
+    schur "1" forces the explicit reduced camera system (sfm_ba_set_schur) in both: the shards'
+    T partials are gathered once per solve and the CG runs on every rank without an exchange."""
+    monkeypatch.setenv("SFM_BA_SCHUR", schur)
     prob = problem()
     rdc, rdp, rinfo = _reference_solve(prob)
     args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])

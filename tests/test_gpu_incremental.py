@@ -95,14 +95,19 @@ def test_incremental_sharded_matching_two_ranks(tmp_path):
         np.testing.assert_array_equal(d["points"], ref.points)
 
 
-@pytest.mark.parametrize("n,pcg", [(2, "sharded"), (2, "replicated"), (3, "sharded"),
-                                   (3, "replicated")])
-def test_incremental_sharded_bundle_adjustment_is_sharding_invariant(tmp_path, n, pcg):
+@pytest.mark.parametrize("n,pcg,schur", [(2, "sharded", "auto"), (2, "replicated", "auto"),
+                                         (3, "sharded", "auto"), (3, "replicated", "auto"),
+                                         (2, "sharded", "1"), (3, "replicated", "1")])
+def test_incremental_sharded_bundle_adjustment_is_sharding_invariant(tmp_path, monkeypatch, n,
+                                                                     pcg, schur):
     """cfg5's multi-GPU form with the bundle adjustments sharded too (shard_ba: the points split
     over the ranks as runs of whole BA chunks; gloo ranks on GPU 0), both PCG branches, 2 and 3
     ranks: the reconstruction equals the single-process one BIT FOR BIT — cameras, points,
     has_point, registrations, tracks (every camera-space sum is a fixed tree
-    over fixed point chunks, reconstruction.BA_CHUNKS)."""
+    over fixed point chunks, reconstruction.BA_CHUNKS).  schur "1": the explicit reduced camera
+    system in every bundle adjustment (the arc scene's long tracks leave it to the rule's
+    implicit branch otherwise)."""
+    monkeypatch.setenv("SFM_BA_SCHUR", schur)
     import os
     import socket
     import subprocess

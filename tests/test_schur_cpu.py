@@ -49,8 +49,8 @@ def test_schur_structure_matches_brute_force(seed):
     ref = _brute(cam, pt, n_cam, chunk_pt)
     np.testing.assert_array_equal(a.numpy(), [r[3] for r in ref])
     np.testing.assert_array_equal(b.numpy(), [r[4] for r in ref])
-    slot_keys = R.torch_unique_keys(key, n_cam)
-    spec = R.schur_spec(key, a, b, n_cam, slot_keys)
+    comp, cnt = R.schur_groups(key)
+    spec = R.schur_spec(comp, cnt, a, b, n_cam, R.torch_unique_keys(comp, n_cam))
     sk = sorted({r[1] * n_cam + r[2] for r in ref})
     np.testing.assert_array_equal(spec.slot_cam.numpy(), [[k // n_cam, k % n_cam] for k in sk])
     # groups: (chunk, slot) runs in order
@@ -89,7 +89,8 @@ def test_schur_product_restatement_equals_dense():
     ptr = np.r_[np.searchsorted(pt, np.arange(n_pt)), n_obs].astype(np.int32)
     T_ = lambda a: torch.from_numpy(np.ascontiguousarray(a))
     key, a, b = R.schur_instances(T_(cam), T_(pt), T_(ptr), n_cam, [0, 20, n_pt])
-    spec = R.schur_spec(key, a, b, n_cam, R.torch_unique_keys(key, n_cam))
+    comp, cnt = R.schur_groups(key)
+    spec = R.schur_spec(comp, cnt, a, b, n_cam, R.torch_unique_keys(comp, n_cam))
     Tb = np.zeros((spec.n_slot, 8, 8))
     seg, inst = spec.seg.numpy(), spec.inst.numpy()
     for g in range(spec.n_seg):
