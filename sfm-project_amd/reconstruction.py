@@ -707,8 +707,18 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         if mode not in ("auto", "sharded", "replicated"):
             raise ValueError(f"bundle_adjust: pcg must be auto|sharded|replicated, got {mode!r}")
         if mode == "auto":
-            if world == 1:
+            # the explicit reduced camera system (schur_rule) has no exchange per CG iteration:
+            # then the sharded branch (one gather of T's chunk partials per solve) is the one;
+            # the pair count is the whole problem's, the same on every rank
+            likely_schur = False
+            if nchunk > 0 and schur_mode() != "0":
+                m = torch.bincount(pt_idx.long(), minlength=n_pt)
+                pairs = float((m * (m - 1) // 2).sum())
+                likely_schur = schur_mode() == "1" or pairs <= SCHUR_INST_PER_OBS * max(n_obs_all, 1)
+            if world == 1 or likely_schur:
                 mode = "sharded"
+                if info is not None and world > 1:
+                    info["rule"] = {"explicit_schur_candidate": True}
             else:
                 lat, bw = probe_collectives(allreduce, n_cam, device, group)
                 mode, terms = pcg_rule(len(pt_idx), n_pt, n_cam, world, lat, bw)

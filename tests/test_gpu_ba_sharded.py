@@ -258,11 +258,14 @@ def test_ba_auto_rule_reports_its_branch():
         dist.destroy_process_group()
 
 
-def test_ba_auto_mode_repeated_on_three_ranks(tmp_path):
+@pytest.mark.parametrize("schur", ["0", "auto"])
+def test_ba_auto_mode_repeated_on_three_ranks(tmp_path, monkeypatch, schur):
     """several sequential auto-mode bundle adjustments on 3 gloo ranks — the
     collective probe's cache key is the same on every rank (backend, group, device, path, n_cam),
     so every rank hits or misses it together and takes the same branch; the ranks agree bit for
-    bit and every call gives the same result."""
+    bit and every call gives the same result.  schur "0" keeps the explicit Schur candidate out of
+    the branch decision (so the probe runs); "auto" lets its pair count pick the sharded branch."""
+    monkeypatch.setenv("SFM_BA_SCHUR", schur)
     d = _run_ranks(tmp_path, 3, "std", "auto", "3")
     for k in (1, 2):
         for key in ("cams", "pts", "hist", "branches"):
