@@ -316,20 +316,27 @@ int sfm_ba_chunk_tree(sfm_ctx* ctx, int32_t n_total, int64_t n, const double* pa
  * runs the CG on S directly — two launches per iteration over 64 B per camera-pair block instead of
  * streaming W (192 B per observation) every iteration.  It pays when the camera-pair products are
  * few against the CG iterations (short tracks); the caller decides (reconstruction.schur_rule).
- *   sfm_ba_set_schur(ctx, n_slot, slot_cam, n_seg, seg, n_inst, inst, row_ptr, n_ent, row_ent):
+ *   sfm_ba_set_schur(ctx, n_slot, slot_cam, n_seg, seg, n_inst, inst, row_ptr, n_ent, row_ent,
+ *                    n_group, sg_ptr, sg, gk):
  *   slot_cam [n_slot][2] (ci <= cj): the camera pairs (slots) of the WHOLE problem, the same table
  *   on every rank; inst [2][n_inst] (observation a, observation b of one point, LOCAL observation
  *   indices; cam(a) = ci, cam(b) = cj of its slot; a pair within one camera appears as (a, b) and
- *   (b, a)); seg [4][n_seg] (local chunk, slot, first instance, end instance): the instances
- *   grouped by (chunk, slot), each group in point order — T's chunk partial of a slot is the fixed-
- *   order sum over its group; row_ptr [n_cam + 1], row_ent [n_ent] = 2 slot + t: block row c of S
- *   (t = 1: the slot's transpose), in a fixed order.  All device, caller-owned.  n_slot = 0 turns
- *   it off.  The chunk partials of T follow the chunk rules above (exported to comm after the 44-sum
- *   partials by SETUP of a shard, comm >= n_total * (44 n_cam + 64 n_slot) doubles); with it on,
- *   ITER / ITER_FINISH of the sharded solve need no exchange (S is replicated after SETUP_FINISH). */
+ *   (b, a)); seg [4][n_seg] (local chunk, slot, first instance, end instance): this problem's
+ *   instances grouped by (chunk, slot), each group in point order — a group's T partial is the
+ *   fixed-order sum over it; row_ptr [n_cam + 1], row_ent [n_ent] = 2 slot + t: block row c of S
+ *   (t = 1: the slot's transpose), in a fixed order.  The groups of the WHOLE problem (every rank's,
+ *   in chunk order: a shard's n_seg groups are a contiguous run of them): n_group of them, gk
+ *   [n_group] their chunk, sg_ptr [n_slot + 1] / sg [n_group] each slot's groups in chunk order.
+ *   T_slot = the canonical chunk tree over the slot's group partials (missing chunks 0).  All
+ *   device, caller-owned.  n_slot = 0 turns it off.  Sharded (n_total > 0): SCHUR (after SETUP)
+ *   writes the shard's group partials [n_seg][64] at its comm pointer (the caller passes comm +
+ *   n_total·44·n_cam + g0·64, g0 = the shard's first group); one exchange of n_total·44·n_cam +
+ *   n_group·64 doubles (zero-filled: an exact all-gather); SETUP_FINISH; then ITER / ITER_FINISH
+ *   need no exchange (S is replicated). */
 int sfm_ba_set_schur(sfm_ctx* ctx, int32_t n_slot, const int32_t* slot_cam, int32_t n_seg,
                      const int32_t* seg, int32_t n_inst, const int32_t* inst, const int32_t* row_ptr,
-                     int32_t n_ent, const int32_t* row_ent);
+                     int32_t n_ent, const int32_t* row_ent, int32_t n_group, const int32_t* sg_ptr,
+                     const int32_t* sg, const int32_t* gk);
 
 /* ---- feature tracks ----------------------------------------------------------------------------
  * the verified match graph (sfm_graph_rows) -> tracks, the input of

@@ -789,13 +789,13 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
 #endif
 constexpr int SB_ROWS = 8 / SB_WAVES, SB_N = 8 * SB_ROWS;
 __global__ __launch_bounds__(256) void bas_schur_build(
-    int n_seg, int n_slot, int n_inst, const int32_t* __restrict__ seg,
+    int n_seg, int n_inst, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ inst, const int32_t* __restrict__ pt_idx,
     const double* __restrict__ W, const double* __restrict__ Vinv, double* __restrict__ Tpart) {
     const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int s = wv / SB_WAVES, h = wv % SB_WAVES;
     if (s >= n_seg) return;   // wave-uniform
-    const int k = seg[s], slot = seg[n_seg + s], i0 = seg[2 * n_seg + s], i1 = seg[3 * n_seg + s];
+    const int i0 = seg[2 * n_seg + s], i1 = seg[3 * n_seg + s];
     double acc[SB_N];
 #pragma unroll
     for (int t = 0; t < SB_N; ++t) acc[t] = 0.0;
@@ -829,18 +829,29 @@ __global__ __launch_bounds__(256) void bas_schur_build(
     }
     int idx;
     if (sfm::wave_halving_sum<SB_N>(acc, lane, idx))
-        Tpart[((size_t)k * n_slot + slot) * 64 + SB_N * h + idx] = acc[0];
+        Tpart[(size_t)s * 64 + SB_N * h + idx] = acc[0];   // the group's row
 }
 
-// T = the canonical tree over the n_total chunk partials (parts [n_total][n]).
-__global__ __launch_bounds__(256) void bas_chunk_tree(int ntot, long long n,
+// T = per slot, the canonical chunk tree over its group partials (parts [n_group][64]; chunks
+// without a group are 0 leaves — the dense [n_total][n_slot] tree's bits).  Thread per element.
+__global__ __launch_bounds__(256) void bas_schur_tree(int n_slot, const int32_t* __restrict__ sg_ptr,
+                                                      const int32_t* __restrict__ sg,
+                                                      const int32_t* __restrict__ gk,
                                                       const double* __restrict__ parts,
                                                       double* __restrict__ out) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= (long long)n_slot * 64) return;
+    const int s = (int)(i >> 6), e = (int)(i & 63);
     double a[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) a[k] = k < ntot ? parts[(size_t)k * n + i] : 0.0;
+    for (int k = 0; k < 16; ++k) a[k] = 0.0;
+    for (int j = sg_ptr[s]; j < sg_ptr[s + 1]; ++j) {
+        const int g = sg[j];
+        const double v = parts[(size_t)g * 64 + e];
+        const int k = gk[g];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) a[q] = (q == k) ? v : a[q];
+    }
     out[i] = sfm::chunk_tree16(a);
 }
 
@@ -1332,15 +1343,15 @@ static int solve_ws(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs, So
     const size_t no = (size_t)std::max(n_obs, 1);
     const size_t b_soa = sfm::align_up(sizeof(double) * 32 * no + sizeof(int32_t) * no, 256);
     // explicit reduced camera system: S_cc, T, its chunk partials, p in two parity slots
-    const size_t ns = (size_t)ctx->ba_nslot, nck = (size_t)std::max(ctx->ba_nchunk, 1);
-    const size_t b_ex = ns > 0 ? sfm::align_up(sizeof(double) * (64 * nc + 64 * ns + 64 * ns * nck + 16 * nc), 256) : 0;
+    const size_t ns = (size_t)ctx->ba_nslot, ngr = (size_t)std::max(ctx->ba_ngroup, 1);
+    const size_t b_ex = ns > 0 ? sfm::align_up(sizeof(double) * (64 * nc + 64 * ns + 64 * ngr + 16 * nc), 256) : 0;
     char* ws = (char*)sfm::workspace(ctx, b_pt + b_cam + b_part + 512 + b_soa + b_ex);
     if (!ws) return SFM_ERR_NOMEM;
     if (ns > 0) {
         w.Scc = (double*)(ws + b_pt + b_cam + b_part + 512 + b_soa);
         w.T = w.Scc + 64 * nc;
         w.Tpart = w.T + 64 * ns;
-        w.pv2 = w.Tpart + 64 * ns * nck;
+        w.pv2 = w.Tpart + 64 * ngr;
     }
     w.Vinv = (double*)ws;
     w.vg = w.Vinv + 9 * np;
@@ -1413,27 +1424,24 @@ static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, 
     return SFM_OK;
 }
 
-// Explicit S: the local chunks' T partials (zeroed, then one wave per instance group) into
-// `out` ([n_chunk][n_slot][64]: Tpart, or a shard's export slot in comm).
+// Explicit S: this problem's group partials of T ([n_seg][64], one wave pair per group) into out.
 static int schur_build(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, const int32_t* pt_idx,
                        const double* W, double* out) {
-    const size_t n = (size_t)ctx->ba_nchunk * ctx->ba_nslot * 64;
-    SFM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * n, st));
     if (ctx->ba_nseg > 0) {
-        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg * SB_WAVES + 3) / 4), dim3(256), 0, st,
-                           ctx->ba_nseg, ctx->ba_nslot, ctx->ba_ninst, ctx->ba_seg, ctx->ba_inst,
-                           pt_idx, W, w.Vinv, out);
+        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg * SB_WAVES + 3) / 4), dim3(256), 0,
+                           st, ctx->ba_nseg, ctx->ba_ninst, ctx->ba_seg, ctx->ba_inst, pt_idx, W,
+                           w.Vinv, out);
         SFM_HIP_CHECK(hipGetLastError());
     }
     return SFM_OK;
 }
 
-// Explicit S: T from n_total chunk partials (canonical tree) and the zeroed p_{-1} slot.
+// Explicit S: T from the whole problem's group partials (slot trees) and the zeroed p_{-1} slot.
 static int schur_finish(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int32_t n_cam,
-                        int ntot, const double* parts) {
+                        const double* parts) {
     const long long n = (long long)ctx->ba_nslot * 64;
-    hipLaunchKernelGGL(bas_chunk_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       st, ntot, n, parts, w.T);
+    hipLaunchKernelGGL(bas_schur_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       ctx->ba_nslot, ctx->ba_sg_ptr, ctx->ba_sg, ctx->ba_gk, parts, w.T);
     SFM_HIP_CHECK(hipGetLastError());
     SFM_HIP_CHECK(hipMemsetAsync(w.pv2, 0, sizeof(double) * 16 * (size_t)n_cam, st));
     return SFM_OK;
@@ -1493,7 +1501,7 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     if (rc != SFM_OK) return rc;
     if (ex) {
         if (schur_build(ctx, st, w, pt_idx, W, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
-        if (schur_finish(ctx, st, w, n_cam, ck.nck, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
+        if (schur_finish(ctx, st, w, n_cam, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
     }
     hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
     SFM_HIP_CHECK(hipGetLastError());
@@ -1572,15 +1580,14 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
     case SFM_BA_STAGE_SETUP:  // -> comm[0, 44 n_cam) (chunk mode: [n_chunk][n_cam][44])
         return solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
                            W, gc, gp, lam, dc, 1, comm);
-    case SFM_BA_STAGE_SCHUR:  // explicit S: this shard's T partials -> comm [n_chunk][n_slot][64]
+    case SFM_BA_STAGE_SCHUR:  // explicit S: this shard's group partials of T -> comm [n_seg][64]
         return schur_build(ctx, st, w, pt_idx, W, comm);
     case SFM_BA_STAGE_SETUP_FINISH:
         hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
                            w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z,
                            w.pv, w.rzc, w.rrc, w.bad, 2, comm, ck.cb, ck.nck, ck.ntot, w.Scc);
         SFM_HIP_CHECK(hipGetLastError());
-        if (ex && schur_finish(ctx, st, w, n_cam, ck.ntot,
-                               comm + (size_t)ck.ntot * 44 * n_cam) != SFM_OK)
+        if (ex && schur_finish(ctx, st, w, n_cam, comm + (size_t)ck.ntot * 44 * n_cam) != SFM_OK)
             return SFM_ERR_HIP;
         hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
         break;
@@ -1695,25 +1702,33 @@ extern "C" int sfm_ba_fix_params(sfm_ctx* ctx, int32_t n_cam, int32_t n_obs,
 extern "C" int sfm_ba_set_schur(sfm_ctx* ctx, int32_t n_slot, const int32_t* slot_cam,
                                 int32_t n_seg, const int32_t* seg, int32_t n_inst,
                                 const int32_t* inst, const int32_t* row_ptr, int32_t n_ent,
-                                const int32_t* row_ent) {
+                                const int32_t* row_ent, int32_t n_group, const int32_t* sg_ptr,
+                                const int32_t* sg, const int32_t* gk) {
     SFM_REQUIRE(ctx != nullptr, "sfm_ba_set_schur: ctx is NULL");
-    SFM_REQUIRE(n_slot >= 0 && n_seg >= 0 && n_inst >= 0 && n_ent >= 0, "sfm_ba_set_schur: negative size");
+    SFM_REQUIRE(n_slot >= 0 && n_seg >= 0 && n_inst >= 0 && n_ent >= 0 && n_group >= 0,
+                "sfm_ba_set_schur: negative size");
     if (n_slot == 0) {
-        ctx->ba_nslot = ctx->ba_nseg = ctx->ba_ninst = ctx->ba_nent = 0;
+        ctx->ba_nslot = ctx->ba_nseg = ctx->ba_ninst = ctx->ba_nent = ctx->ba_ngroup = 0;
         ctx->ba_slot_cam = ctx->ba_seg = ctx->ba_inst = ctx->ba_row_ptr = ctx->ba_row_ent = nullptr;
+        ctx->ba_sg_ptr = ctx->ba_sg = ctx->ba_gk = nullptr;
         return SFM_OK;
     }
-    SFM_REQUIRE(slot_cam && row_ptr && (n_seg == 0 || seg) && (n_inst == 0 || inst) &&
-                    (n_ent == 0 || row_ent),
+    SFM_REQUIRE(n_seg <= n_group, "sfm_ba_set_schur: more local groups than the problem has");
+    SFM_REQUIRE(slot_cam && row_ptr && sg_ptr && (n_seg == 0 || seg) && (n_inst == 0 || inst) &&
+                    (n_ent == 0 || row_ent) && (n_group == 0 || (sg && gk)),
                 "sfm_ba_set_schur: NULL array");
     ctx->ba_nslot = n_slot;
     ctx->ba_nseg = n_seg;
     ctx->ba_ninst = n_inst;
     ctx->ba_nent = n_ent;
+    ctx->ba_ngroup = n_group;
     ctx->ba_slot_cam = slot_cam;
     ctx->ba_seg = seg;
     ctx->ba_inst = inst;
     ctx->ba_row_ptr = row_ptr;
     ctx->ba_row_ent = row_ent;
+    ctx->ba_sg_ptr = sg_ptr;
+    ctx->ba_sg = sg;
+    ctx->ba_gk = gk;
     return SFM_OK;
 }

@@ -27,9 +27,10 @@ struct sfm_ctx {
     int32_t ba_chunk_pt[17] = {0}, ba_chunk_obs[17] = {0};
     const int32_t* ba_cam_bounds = nullptr;
     // explicit reduced camera system (sfm_ba_set_schur): n_slot 0 = off
-    int ba_nslot = 0, ba_nseg = 0, ba_ninst = 0, ba_nent = 0;
+    int ba_nslot = 0, ba_nseg = 0, ba_ninst = 0, ba_nent = 0, ba_ngroup = 0;
     const int32_t *ba_slot_cam = nullptr, *ba_seg = nullptr, *ba_inst = nullptr,
-                  *ba_row_ptr = nullptr, *ba_row_ent = nullptr;
+                  *ba_row_ptr = nullptr, *ba_row_ent = nullptr, *ba_sg_ptr = nullptr,
+                  *ba_sg = nullptr, *ba_gk = nullptr;
 };
 
 namespace sfm {

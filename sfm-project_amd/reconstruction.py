@@ -225,15 +225,19 @@ def schur_mode():
 class SchurSpec:
     """Structure of the explicit reduced camera system of one (local) problem: device int32
     tensors slot_cam [n_slot, 2] (the WHOLE problem's camera pairs ci <= cj, sorted), seg [4, n_seg]
-    (local chunk, slot, first, end instance), inst [2, n_inst] (observation pairs, grouped by
-    (chunk, slot), point order inside a group), row_ptr [n_cam + 1] / row_ent [n_ent] (2 slot + t,
-    t = 1 for the slot's transpose: block row c of S)."""
+    (local chunk, slot, first, end instance: this problem's (chunk, slot) groups), inst [2, n_inst]
+    (observation pairs, grouped, point order inside a group), row_ptr [n_cam + 1] / row_ent [n_ent]
+    (2 slot + t, t = 1 for the slot's transpose: block row c of S); the WHOLE problem's groups:
+    n_group, gk [n_group] (their chunk), sg_ptr [n_slot + 1] / sg [n_group] (each slot's groups in
+    chunk order); g0 = this problem's first group among them."""
 
-    def __init__(self, slot_cam, seg, inst, row_ptr, row_ent):
+    def __init__(self, slot_cam, seg, inst, row_ptr, row_ent, sg_ptr, sg, gk, g0):
         self.slot_cam, self.seg, self.inst = slot_cam, seg, inst
         self.row_ptr, self.row_ent = row_ptr, row_ent
+        self.sg_ptr, self.sg, self.gk, self.g0 = sg_ptr, sg, gk, int(g0)
         self.n_slot, self.n_seg = int(slot_cam.shape[0]), int(seg.shape[1])
         self.n_inst, self.n_ent = int(inst.shape[1]), int(row_ent.numel())
+        self.n_group = int(gk.numel())
 
 
 def schur_pair_count(pt_ptr):
@@ -286,19 +290,16 @@ def schur_groups(key):
     return torch.unique_consecutive(key, return_counts=True)
 
 
-def torch_unique_keys(comp, n_cam):
-    """The camera-pair keys (ci * n_cam + cj) of composite keys, sorted unique."""
+def schur_spec(comp, cnt, a, b, n_cam, all_groups, k0=0):
+    """SchurSpec from this problem's (chunk, slot) groups (sorted local composite keys `comp`, sizes
+    `cnt`, the sorted instances a / b) and the WHOLE problem's group keys `all_groups` (global chunk
+    * n_cam^2 + ci * n_cam + cj, sorted, identical on every rank; this problem's chunks start at
+    global chunk k0)."""
     import torch
-    return torch.unique(comp % (n_cam * n_cam))
-
-
-def schur_spec(comp, cnt, a, b, n_cam, slot_keys):
-    """SchurSpec from the (chunk, slot) groups of the sorted local instances and the WHOLE
-    problem's slot keys (ci * n_cam + cj, sorted unique int64, identical on every rank)."""
-    import torch
-    dev = slot_keys.device
+    dev = all_groups.device
     i32 = torch.int32
     nn = n_cam * n_cam
+    slot_keys = torch.unique(all_groups % nn)
     starts = torch.cumsum(cnt, 0) - cnt
     seg = torch.stack([comp // nn, torch.searchsorted(slot_keys, comp % nn), starts,
                        starts + cnt]).to(i32).contiguous()
@@ -311,9 +312,17 @@ def schur_spec(comp, cnt, a, b, n_cam, slot_keys):
     ent = torch.cat([2 * s, 2 * s[off] + 1])
     rk, order = torch.sort(rows * n_cam + other, stable=True)
     row_ptr = torch.searchsorted(rk, torch.arange(n_cam + 1, dtype=torch.int64, device=dev) * n_cam)
+    # the whole problem's groups: chunk, slot; each slot's groups in chunk order
+    gk = all_groups // nn
+    gslot = torch.searchsorted(slot_keys, all_groups % nn)
+    gs_sorted, sg = torch.sort(gslot * 64 + gk, stable=True)
+    sg_ptr = torch.searchsorted(gs_sorted, torch.arange(slot_keys.numel() + 1, dtype=torch.int64,
+                                                        device=dev) * 64)
+    g0 = torch.searchsorted(all_groups, torch.tensor([k0 * nn], dtype=all_groups.dtype, device=dev))
     inst = torch.stack([a, b]).to(i32).contiguous()
     return SchurSpec(slot_cam, seg, inst, row_ptr.to(i32).contiguous(),
-                     ent[order].to(i32).contiguous())
+                     ent[order].to(i32).contiguous(), sg_ptr.to(i32).contiguous(),
+                     sg.to(i32).contiguous(), gk.to(i32).contiguous(), int(g0.item()))
 
 
 class BAProblem:
@@ -368,17 +377,18 @@ class BAProblem:
 
     def set_schur(self, union=None):
         """Turn the explicit reduced camera system on (needs chunk mode).  union: for a shard, maps
-        this shard's camera-pair keys (sorted unique int64 device tensor) to the WHOLE problem's
-        (a collective; the same result on every rank); None = this problem's own."""
+        this shard's group keys (global chunk * n_cam^2 + ci * n_cam + cj, sorted int64 device
+        tensor) to the WHOLE problem's (every rank's, sorted; a collective, the same result on
+        every rank); None = this problem's own."""
         if self.chunks is None:
             raise ValueError("BAProblem.set_schur: the explicit Schur system needs chunk mode")
         key, a, b = schur_instances(self.cam_idx, self.pt_idx, self.pt_ptr, self.n_cam,
                                     self.chunks.chunk_pt)
         comp, cnt = schur_groups(key)
-        slot_keys = torch_unique_keys(comp, self.n_cam)
-        if union is not None:
-            slot_keys = union(slot_keys)
-        self.schur = schur_spec(comp, cnt, a, b, self.n_cam, slot_keys)
+        k0 = self.chunks.k0
+        gkeys = comp + k0 * self.n_cam * self.n_cam
+        all_groups = union(gkeys) if union is not None else gkeys
+        self.schur = schur_spec(comp, cnt, a, b, self.n_cam, all_groups, k0)
 
     def _call(self, fn, *a, **kw):
         """fn under this problem's chunk mode and explicit-Schur structure (set on the shared
@@ -754,21 +764,21 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             t_s = time.perf_counter()
             sharded_s = allreduce is not None and full is None
             if sharded_s:
-                def union(keys):   # every shard's camera pairs -> the whole problem's (sorted)
+                def union(keys):   # every shard's (chunk, slot) groups -> the whole problem's
                     nk = torch.zeros(world, dtype=f64, device=prob.dev)
                     nk[rank] = keys.numel()
                     allreduce(nk)
                     g = _gather_rows(keys.double().reshape(-1, 1), [int(v) for v in nk.tolist()],
                                      group)
-                    return torch.unique(g.reshape(-1).long())
+                    return torch.sort(g.reshape(-1).long()).values
                 prob.set_schur(union)
             else:
                 tgt.set_schur()
             sp = tgt.schur
-            tot = torch.tensor([sp.n_inst, sp.n_seg], dtype=f64, device=prob.dev)
+            tot = torch.tensor([sp.n_inst], dtype=f64, device=prob.dev)
             if sharded_s:
-                allreduce(tot)   # the whole problem's products and groups
-            n_inst_tot, n_seg_tot = (float(v) for v in tot.tolist())
+                allreduce(tot)   # the whole problem's products
+            n_inst_tot, n_seg_tot = float(tot.item()), float(sp.n_group)
             if smode != "1" and not schur_rule(n_inst_tot, n_seg_tot, sp.n_slot, n_obs_tot):
                 tgt.schur = None
                 use_schur = False

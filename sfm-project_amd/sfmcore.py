@@ -112,7 +112,7 @@ def load_library(path: str = LIB_PATH):
         L.sfm_ba_update.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
         L.sfm_ba_fix_params.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp]
         L.sfm_ba_set_chunks.argtypes = [vp, i32, vp, vp, i32, vp]
-        L.sfm_ba_set_schur.argtypes = [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp]
+        L.sfm_ba_set_schur.argtypes = [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp, i32, vp, vp, vp]
         L.sfm_ba_chunk_tree.argtypes = [vp, i32, i64, vp, vp]
         L.sfm_orb_batch.argtypes = [vp, vp, i32, i32, i32, C.POINTER(OrbParams), vp, vp, vp]
         L.sfm_register_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(RegisterParams),
@@ -385,11 +385,14 @@ class Context:
         """spec = reconstruction.SchurSpec (the explicit reduced camera system's structure) or None
         (off).  Applies to the next BA solves (sfm_ba_set_schur; needs chunk mode)."""
         if spec is None:
-            _check(self.lib.sfm_ba_set_schur(self.handle, 0, None, 0, None, 0, None, None, 0, None))
+            _check(self.lib.sfm_ba_set_schur(self.handle, 0, None, 0, None, 0, None, None, 0, None,
+                                             0, None, None, None))
             return
         _check(self.lib.sfm_ba_set_schur(self.handle, spec.n_slot, _ptr(spec.slot_cam), spec.n_seg,
                                          _ptr(spec.seg), spec.n_inst, _ptr(spec.inst),
-                                         _ptr(spec.row_ptr), spec.n_ent, _ptr(spec.row_ent)))
+                                         _ptr(spec.row_ptr), spec.n_ent, _ptr(spec.row_ent),
+                                         spec.n_group, _ptr(spec.sg_ptr), _ptr(spec.sg),
+                                         _ptr(spec.gk)))
 
     def ba_chunk_tree(self, parts, out=None):
         """sfm_ba_chunk_tree: parts [n_total, ...] f64 device -> out [...] (the canonical tree)."""
@@ -542,11 +545,12 @@ class Context:
         nt = chunks.n_total if chunks is not None else 1
         k0 = chunks.k0 if chunks is not None else 0
         # explicit S (schur = reconstruction.SchurSpec, set on this context): SETUP's 44-sum
-        # partials, then SCHUR's T partials [n_total][n_slot][64] behind them, ONE exchange; the
+        # partials, then SCHUR's group partials of T [n_group][64] behind them, ONE exchange; the
         # CG iterations then run on every rank from the replicated S with no exchange
         ns = schur.n_slot if schur is not None else 0
         n_setup = nt * 44 * nc
-        comm = torch.zeros(n_setup + nt * 64 * ns, dtype=torch.float64, device=dev)
+        comm = torch.zeros(n_setup + (64 * schur.n_group if ns else 0), dtype=torch.float64,
+                           device=dev)
         prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll))
         done = C.c_int32(0)
         cptr = comm.data_ptr()
@@ -571,7 +575,7 @@ class Context:
         if ns:
             comm.zero_()
             stage(BA_STAGE_SETUP, 0, a_setup)
-            stage(BA_STAGE_SCHUR, 0, args(n_setup + k0 * 64 * ns))
+            stage(BA_STAGE_SCHUR, 0, args(n_setup + 64 * schur.g0))
             allreduce(comm)
         else:
             produce(BA_STAGE_SETUP, n_setup, a_setup)

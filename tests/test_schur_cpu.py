@@ -50,7 +50,7 @@ def test_schur_structure_matches_brute_force(seed):
     np.testing.assert_array_equal(a.numpy(), [r[3] for r in ref])
     np.testing.assert_array_equal(b.numpy(), [r[4] for r in ref])
     comp, cnt = R.schur_groups(key)
-    spec = R.schur_spec(comp, cnt, a, b, n_cam, R.torch_unique_keys(comp, n_cam))
+    spec = R.schur_spec(comp, cnt, a, b, n_cam, comp)
     sk = sorted({r[1] * n_cam + r[2] for r in ref})
     np.testing.assert_array_equal(spec.slot_cam.numpy(), [[k // n_cam, k % n_cam] for k in sk])
     # groups: (chunk, slot) runs in order
@@ -62,6 +62,12 @@ def test_schur_structure_matches_brute_force(seed):
         else:
             groups[-1][3] = i + 1
     np.testing.assert_array_equal(spec.seg.numpy().T, np.array(groups))
+    # the whole problem's groups (one process: its own): chunk of each, each slot's in chunk order
+    assert spec.n_group == len(groups) and spec.g0 == 0
+    np.testing.assert_array_equal(spec.gk.numpy(), [g[0] for g in groups])
+    for si in range(len(sk)):
+        mine = [gi for gi, g in enumerate(groups) if g[1] == si]
+        np.testing.assert_array_equal(spec.sg.numpy()[spec.sg_ptr[si]:spec.sg_ptr[si + 1]], mine)
     # rows: every slot once in its first camera's row, transposed in its second camera's row
     for c in range(n_cam):
         ents = spec.row_ent.numpy()[spec.row_ptr[c]:spec.row_ptr[c + 1]]
@@ -90,7 +96,7 @@ def test_schur_product_restatement_equals_dense():
     T_ = lambda a: torch.from_numpy(np.ascontiguousarray(a))
     key, a, b = R.schur_instances(T_(cam), T_(pt), T_(ptr), n_cam, [0, 20, n_pt])
     comp, cnt = R.schur_groups(key)
-    spec = R.schur_spec(comp, cnt, a, b, n_cam, R.torch_unique_keys(comp, n_cam))
+    spec = R.schur_spec(comp, cnt, a, b, n_cam, comp)
     Tb = np.zeros((spec.n_slot, 8, 8))
     seg, inst = spec.seg.numpy(), spec.inst.numpy()
     for g in range(spec.n_seg):
@@ -119,3 +125,40 @@ def test_schur_product_restatement_equals_dense():
             acc += (Tb[s].T if t else Tb[s]) @ pvec[8 * j:8 * j + 8]
         q[8 * c:8 * c + 8] = Scc[c] @ pvec[8 * c:8 * c + 8] - acc
     np.testing.assert_allclose(q, S @ pvec, rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("cuts", [[0, 2, 6], [0, 1, 3, 6], [0, 3, 3, 6]])
+def test_schur_structure_of_shards_equals_whole(cuts):
+    """The sharded form: each rank builds its groups from its run of chunks, the group keys are
+    gathered (rank order = chunk order), and every shard then holds the whole problem's slots,
+    groups and rows; its own groups are the whole problem's rows g0 .. g0 + n_seg, with the same
+    instances (as global observations)."""
+    cam, pt, n_cam, n_pt = _problem(7, n_pt=60)
+    chunk_pt = [0, 9, 20, 20, 33, 47, n_pt]        # 6 chunks, one empty
+    ptr = np.r_[np.searchsorted(pt, np.arange(n_pt)), len(pt)].astype(np.int32)
+    T_ = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    nn = n_cam * n_cam
+    key, a, b = R.schur_instances(T_(cam), T_(pt), T_(ptr), n_cam, chunk_pt)
+    comp, cnt = R.schur_groups(key)
+    whole = R.schur_spec(comp, cnt, a, b, n_cam, comp)
+    parts = []
+    for r in range(len(cuts) - 1):
+        k0, k1 = cuts[r], cuts[r + 1]
+        lo, hi = chunk_pt[k0], chunk_pt[k1]
+        o0, o1 = ptr[lo], ptr[hi]
+        lcpt = [c - lo for c in chunk_pt[k0:k1 + 1]]
+        lk, la, lb = R.schur_instances(T_(cam[o0:o1]), T_(pt[o0:o1] - lo), T_(ptr[lo:hi + 1] - o0),
+                                       n_cam, lcpt)
+        lc, ln = R.schur_groups(lk)
+        parts.append((k0, o0, lc, ln, la, lb))
+    all_groups = torch.sort(torch.cat([p[2] + p[0] * nn for p in parts])).values
+    np.testing.assert_array_equal(all_groups.numpy(), comp.numpy())
+    for k0, o0, lc, ln, la, lb in parts:
+        sp = R.schur_spec(lc, ln, la, lb, n_cam, all_groups, k0)
+        for name in ("slot_cam", "row_ptr", "row_ent", "sg_ptr", "sg", "gk"):
+            np.testing.assert_array_equal(getattr(sp, name).numpy(), getattr(whole, name).numpy())
+        g = slice(sp.g0, sp.g0 + sp.n_seg)
+        np.testing.assert_array_equal(sp.seg.numpy()[1], whole.seg.numpy()[1][g])       # slots
+        np.testing.assert_array_equal(sp.seg.numpy()[0] + k0, whole.seg.numpy()[0][g])  # chunks
+        wi0, wi1 = whole.seg.numpy()[2][g][0] if sp.n_seg else 0, whole.seg.numpy()[3][g][-1] if sp.n_seg else 0
+        np.testing.assert_array_equal(sp.inst.numpy() + o0, whole.inst.numpy()[:, wi0:wi1])
