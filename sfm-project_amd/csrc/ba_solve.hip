@@ -779,34 +779,35 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
 //
 // T_slot = Σ over the slot's camera-pair instances (a, b) of Y_a W_bᵀ, Y_a = W_a V_d⁻¹ (the point of
 // a), so the off-diagonal Schur blocks are S_ij = -T_ij; the diagonal blocks S_cc come from
-// bas_camera_setup.  SB_WAVES waves per (chunk, slot) group, wave h the block's rows
-// SB_ROWS h .. SB_ROWS (h + 1) - 1: lane-strided over the group's instances (an order that depends
-// only on the group), 8 SB_ROWS accumulators per lane, then the recursive-halving wave sum — lane t
-// ends holding element 8 SB_ROWS h + t and stores it.  (All 64 elements in one wave: 262 registers,
-// one wave per SIMD; 2 waves of 32: 178 registers, 0.216 ms per T at cfg5's final model.)
-#ifndef SB_WAVES
-#define SB_WAVES 2
-#endif
-constexpr int SB_ROWS = 8 / SB_WAVES, SB_N = 8 * SB_ROWS;
+// bas_camera_setup.  One wave per (chunk, slot) group, a lane PAIR per instance: lane 2j + h takes
+// rows 4h .. 4h + 3 of the 8x8 block for instances j, j + 32, ... of the group (an order that
+// depends only on the group) — the pair reads the same W_b and V_d⁻¹ in one wave instruction, so
+// they are fetched once.  32 accumulators per lane, then the recursive-halving sum over the lanes
+// of the same h: lane 2j + h ends holding element 32 h + j and stores it.  (Two waves per group,
+// each half the rows for every instance, fetched W_b and V_d⁻¹ twice: 0.22 ms at cfg5's final
+// model; 1 / 4 / 8 waves per group 0.25 / 0.31 / 0.57.)
 __global__ __launch_bounds__(256) void bas_schur_build(
     int n_seg, int n_inst, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ inst, const int32_t* __restrict__ pt_idx,
     const double* __restrict__ W, const double* __restrict__ Vinv, double* __restrict__ Tpart) {
-    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int s = wv / SB_WAVES, h = wv % SB_WAVES;
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (s >= n_seg) return;   // wave-uniform
+    const int h = lane & 1, j = lane >> 1;
     const int i0 = seg[2 * n_seg + s], i1 = seg[3 * n_seg + s];
-    double acc[SB_N];
+    double acc[32];
 #pragma unroll
-    for (int t = 0; t < SB_N; ++t) acc[t] = 0.0;
-    for (int i = i0 + lane; i < i1; i += 64) {
+    for (int t = 0; t < 32; ++t) acc[t] = 0.0;
+    for (int i = i0 + j; i < i1; i += 32) {
         const int a = inst[i], b = inst[n_inst + i];
         const int p = pt_idx[a];
-        double wa[3 * SB_ROWS], wb[24], vi[9];
-        const double* Wa = W + 24 * (size_t)a + 3 * SB_ROWS * h;   // rows SB_ROWS h ..
+        double wa[12], wb[24], vi[9];
+        const double2* Wa = (const double2*)(W + 24 * (size_t)a + 12 * h);   // rows 4h .. 4h + 3
         const double2* Wb = (const double2*)(W + 24 * (size_t)b);
 #pragma unroll
-        for (int t = 0; t < 3 * SB_ROWS; ++t) wa[t] = Wa[t];
+        for (int t = 0; t < 6; ++t) {
+            const double2 u = Wa[t];
+            wa[2 * t] = u.x; wa[2 * t + 1] = u.y;
+        }
 #pragma unroll
         for (int t = 0; t < 12; ++t) {
             const double2 v = Wb[t];
@@ -815,21 +816,21 @@ __global__ __launch_bounds__(256) void bas_schur_build(
         const double* Vi = Vinv + 9 * (size_t)p;
 #pragma unroll
         for (int t = 0; t < 9; ++t) vi[t] = Vi[t];
-        double y[3 * SB_ROWS];   // rows of W_a V_d⁻¹, bas_camera_setup's expression
+        double y[12];   // rows 4h .. 4h + 3 of W_a V_d⁻¹, bas_camera_setup's expression
 #pragma unroll
-        for (int i2 = 0; i2 < SB_ROWS; ++i2)
+        for (int i2 = 0; i2 < 4; ++i2)
 #pragma unroll
-            for (int j = 0; j < 3; ++j)
-                y[3 * i2 + j] = wa[3 * i2] * vi[j] + wa[3 * i2 + 1] * vi[3 + j] + wa[3 * i2 + 2] * vi[6 + j];
+            for (int c = 0; c < 3; ++c)
+                y[3 * i2 + c] = wa[3 * i2] * vi[c] + wa[3 * i2 + 1] * vi[3 + c] + wa[3 * i2 + 2] * vi[6 + c];
 #pragma unroll
-        for (int r = 0; r < SB_ROWS; ++r)
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int c = 0; c < 8; ++c)
                 acc[8 * r + c] += y[3 * r] * wb[3 * c] + y[3 * r + 1] * wb[3 * c + 1] + y[3 * r + 2] * wb[3 * c + 2];
     }
     int idx;
-    if (sfm::wave_halving_sum<SB_N>(acc, lane, idx))
-        Tpart[(size_t)s * 64 + SB_N * h + idx] = acc[0];   // the group's row
+    if (sfm::wave_halving_sum_strided<32, 2>(acc, lane, idx))
+        Tpart[(size_t)s * 64 + 32 * h + idx] = acc[0];   // the group's row
 }
 
 // T = per slot, the canonical chunk tree over its group partials (parts [n_group][64]; chunks
@@ -1428,7 +1429,7 @@ static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, 
 static int schur_build(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, const int32_t* pt_idx,
                        const double* W, double* out) {
     if (ctx->ba_nseg > 0) {
-        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg * SB_WAVES + 3) / 4), dim3(256), 0,
+        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg + 3) / 4), dim3(256), 0,
                            st, ctx->ba_nseg, ctx->ba_ninst, ctx->ba_seg, ctx->ba_inst, pt_idx, W,
                            w.Vinv, out);
         SFM_HIP_CHECK(hipGetLastError());

@@ -76,9 +76,9 @@ __device__ __forceinline__ double chunk_tree16(double (&a)[16]) {
 // returns true; every value is held by exactly one such lane (a padding slot can carry an index
 // that is real elsewhere, so `rs`, the real length of the lane's current slice, decides).  The
 // association is fixed (a function of M).
-template <int M, int OFF>
+template <int M, int OFF, int MINOFF = 1>
 __device__ __forceinline__ void wave_halving_step(double* a, int lane, int& idx, int& rs) {
-    if constexpr (OFF >= 1) {
+    if constexpr (OFF >= MINOFF) {
         constexpr int H = (M + 1) / 2;
         const bool up = (lane & OFF) != 0;
 #pragma unroll
@@ -93,8 +93,18 @@ __device__ __forceinline__ void wave_halving_step(double* a, int lane, int& idx,
         } else if (rs > H) {
             rs = H;
         }
-        wave_halving_step<H, OFF / 2>(a, lane, idx, rs);
+        wave_halving_step<H, OFF / 2, MINOFF>(a, lane, idx, rs);
     }
+}
+// The same over the lanes that share lane bits below MINOFF (e.g. MINOFF 2: even lanes with even
+// lanes, odd with odd), M <= 64 / MINOFF values.
+template <int M, int MINOFF>
+__device__ __forceinline__ bool wave_halving_sum_strided(double* a, int lane, int& idx) {
+    static_assert(M >= 1 && M <= 64 / MINOFF, "wave_halving_sum_strided: too many values");
+    int rs = M;
+    idx = 0;
+    wave_halving_step<M, 32, MINOFF>(a, lane, idx, rs);
+    return rs > 0;
 }
 // LANES < 64: the same over each aligned group of LANES lanes (a power of two, M <= LANES).
 template <int M, int LANES = 64>
