@@ -755,14 +755,18 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
         sp = Pe.schur
         lin = Pe.linearize(c, p, 2.0)
         s0e = timed(lambda: Pe.solve(lin, 1e-3, max_iter=0, tol=0.0), reps)
-        Pe.schur = None
-        s0i = timed(lambda: Pe.solve(lin, 1e-3, max_iter=0, tol=0.0), reps)
-        Pe.set_schur()
+        # the same set-up with the group list emptied: no products are formed (the tree and the
+        # rest run as before), so the difference is the product kernel alone
+        full_n_seg = sp.n_seg
+        sp.n_seg = 0
+        s0z = timed(lambda: Pe.solve(lin, 1e-3, max_iter=0, tol=0.0), reps)
+        sp.n_seg = full_n_seg
         sne = timed(lambda: Pe.solve(lin, 1e-3, max_iter=cg, tol=0.0, poll=-1), max(reps // 4, 2))
-        build_ms = s0e - s0i            # T: the products + the tree, once per solve
+        build_ms = s0e - s0z            # T's products (bas_schur_build), once per solve
         tb = sp.n_inst * (192 + 192 + 72)
         explicit = {"rule": R.schur_rule(sp.n_inst, sp.n_seg, sp.n_slot, n_obs),
                     "n_inst": sp.n_inst, "n_slot": sp.n_slot, "n_seg": sp.n_seg,
+                    "setup_backsub_ms": s0e,
                     "schur_build": {"ms": build_ms, "bytes": tb,
                                     "achieved_GBs": tb / (build_ms * 1e-3) / 1e9 if build_ms > 0 else None,
                                     "frac": tb / (build_ms * 1e-3) / PEAK_HBM if build_ms > 0 else None,

@@ -118,12 +118,14 @@ __global__ __launch_bounds__(256) void bas_soa(int n_obs, const int32_t* __restr
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n_obs) return;
     const size_t n = (size_t)n_obs;
-    const double2* a = (const double2*)(W + 24 * (size_t)e);
+    if (Wp) {   // nullptr: the explicit Schur solve (no CG point pass; backsub reads W row-major)
+        const double2* a = (const double2*)(W + 24 * (size_t)e);
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const double2 v = a[k];
-        Wp[(2 * k) * n + e] = v.x;
-        Wp[(2 * k + 1) * n + e] = v.y;
+        for (int k = 0; k < 12; ++k) {
+            const double2 v = a[k];
+            Wp[(2 * k) * n + e] = v.x;
+            Wp[(2 * k + 1) * n + e] = v.y;
+        }
     }
     ptc[e] = pt_idx[cam_obs[e]];
 }
@@ -866,48 +868,49 @@ __global__ __launch_bounds__(256) void bas_pcg_spmv(
     const int32_t* __restrict__ slot_cam, const double* __restrict__ T,
     const double* __restrict__ Scc, const double* __restrict__ z, double* __restrict__ pv2,
     const PcgState* __restrict__ st, double* __restrict__ q, double* __restrict__ pq) {
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (c >= n_cam) return;   // wave-uniform
     const Scalars sc = read_scalars(st);
-    if (sc.done) return;
-    const double* pold = pv2 + (size_t)((k + 1) & 1) * 8 * n_cam;
-    double* pnew = pv2 + (size_t)(k & 1) * 8 * n_cam;
-    const int g = lane >> 3, r = lane & 7;
-    const int e0 = row_ptr[c], e1 = row_ptr[c + 1];
-    double s = 0.0;
-    for (int e = e0 + g; e < e1; e += 8) {
-        const int ent = row_ent[e];
-        const int slot = ent >> 1, tr = ent & 1;
-        const int j = slot_cam[2 * slot + (tr ? 0 : 1)];   // the other camera of the block
-        const double* Tb = T + 64 * (size_t)slot;
+    if (sc.done) return;   // the same for every block (published before the launch)
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (c < n_cam) {
+        const double* pold = pv2 + (size_t)((k + 1) & 1) * 8 * n_cam;
+        double* pnew = pv2 + (size_t)(k & 1) * 8 * n_cam;
+        const int g = lane >> 3, r = lane & 7;
+        const int e0 = row_ptr[c], e1 = row_ptr[c + 1];
+        double s = 0.0;
+        for (int e = e0 + g; e < e1; e += 8) {
+            const int ent = row_ent[e];
+            const int slot = ent >> 1, tr = ent & 1;
+            const int j = slot_cam[2 * slot + (tr ? 0 : 1)];   // the other camera of the block
+            const double* Tb = T + 64 * (size_t)slot;
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const double pj = z[8 * (size_t)j + m] + sc.beta * pold[8 * (size_t)j + m];
-            s += (tr ? Tb[8 * m + r] : Tb[8 * r + m]) * pj;
+            for (int m = 0; m < 8; ++m) {
+                const double pj = z[8 * (size_t)j + m] + sc.beta * pold[8 * (size_t)j + m];
+                s += (tr ? Tb[8 * m + r] : Tb[8 * r + m]) * pj;
+            }
         }
+        s += __shfl_xor(s, 8, 64);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        double pc[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) pc[m] = z[8 * (size_t)c + m] + sc.beta * pold[8 * (size_t)c + m];
+        double sp = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) sp += Scc[64 * (size_t)c + 8 * r + m] * pc[m];
+        const double qi = sp - s;
+        double pr = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) pr = (m == r) ? pc[m] : pr;
+        if (lane < 8) {
+            pnew[8 * (size_t)c + r] = pr;
+            q[8 * (size_t)c + r] = qi;
+        }
+        double v = pr * qi;
+        v += __shfl_down(v, 4, 8);
+        v += __shfl_down(v, 2, 8);
+        v += __shfl_down(v, 1, 8);
+        if (lane == 0) pq[c] = v;
     }
-    s += __shfl_xor(s, 8, 64);
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    double pc[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) pc[m] = z[8 * (size_t)c + m] + sc.beta * pold[8 * (size_t)c + m];
-    double sp = 0.0;
-#pragma unroll
-    for (int m = 0; m < 8; ++m) sp += Scc[64 * (size_t)c + 8 * r + m] * pc[m];
-    const double qi = sp - s;
-    double pr = 0.0;
-#pragma unroll
-    for (int m = 0; m < 8; ++m) pr = (m == r) ? pc[m] : pr;
-    if (lane < 8) {
-        pnew[8 * (size_t)c + r] = pr;
-        q[8 * (size_t)c + r] = qi;
-    }
-    double v = pr * qi;
-    v += __shfl_down(v, 4, 8);
-    v += __shfl_down(v, 2, 8);
-    v += __shfl_down(v, 1, 8);
-    if (lane == 0) pq[c] = v;
 }
 
 // Largest camera count for which the sharded solve finishes an iteration in one launch
@@ -1132,7 +1135,11 @@ __global__ __launch_bounds__(256) void bas_backsub(int n_pt, int n_obs,
 // per-point code) and accumulates each lane's model terms in that order; then the wave trees and
 // the 4 waves in order -> mpart[(k BPB + b)][2].  The order depends only on the chunk.
 constexpr int BPB = 64;
+// W element m of observation o at Wp[o * so + m * sm]: the SoA planes (so 1, sm n_obs) or K3's
+// row-major W (so 24, sm 1; the explicit Schur solve skips the SoA copy) — the same values, the same
+// sums.
 __global__ __launch_bounds__(256) void bas_backsub_ck(sfm::ChunkOff cpt, int n_obs,
+                                                      long long so, long long sm,
                                                       const int32_t* __restrict__ pt_ptr,
                                                       const int32_t* __restrict__ cam_idx,
                                                       const double* __restrict__ Wp,
@@ -1147,7 +1154,6 @@ __global__ __launch_bounds__(256) void bas_backsub_ck(sfm::ChunkOff cpt, int n_o
     const int k = blockIdx.x / BPB, b = blockIdx.x - k * BPB;
     const int p0 = cpt.v[k], p1 = cpt.v[k + 1];
     const int j = threadIdx.x % PG;
-    const size_t n = (size_t)n_obs;
     double m0 = 0.0, m1 = 0.0;
     for (int gb = p0 + b * (256 / PG); gb < p1; gb += BPB * (256 / PG)) {
         const int g = gb + threadIdx.x / PG;
@@ -1155,14 +1161,14 @@ __global__ __launch_bounds__(256) void bas_backsub_ck(sfm::ChunkOff cpt, int n_o
         double s0 = 0.0, s1 = 0.0, s2 = 0.0;
         const int o1 = valid ? pt_ptr[g + 1] : 0;
         for (int o = (valid ? pt_ptr[g] : 0) + j; o < o1; o += PG) {
-            const double* Wo = Wp + o;
+            const double* Wo = Wp + o * so;
             const double* x = dc + 8 * (size_t)cam_idx[o];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const double xi = x[i];
-                s0 += Wo[(3 * i) * n] * xi;
-                s1 += Wo[(3 * i + 1) * n] * xi;
-                s2 += Wo[(3 * i + 2) * n] * xi;
+                s0 += Wo[(3 * i) * sm] * xi;
+                s1 += Wo[(3 * i + 1) * sm] * xi;
+                s2 += Wo[(3 * i + 2) * sm] * xi;
             }
         }
 #pragma unroll
@@ -1385,7 +1391,7 @@ static int solve_setup(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, in
                        const int32_t* pt_idx, const int32_t* pt_ptr, const int32_t* cam_ptr,
                        const int32_t* cam_obs, const double* U, const double* V, const double* W,
                        const double* gc, const double* gp, double lam, double* dc, int phase,
-                       double* comm) {
+                       double* comm, bool soa = true) {
     SFM_HIP_CHECK(hipMemsetAsync(w.bad, 0, 2 * sizeof(int32_t), st));  // bad flag, long count
     if (n_pt > 0) {
         hipLaunchKernelGGL(bas_point_setup, dim3(w.pblk), dim3(256), 0, st, n_pt, pt_ptr, V, gp,
@@ -1394,7 +1400,7 @@ static int solve_setup(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, in
     }
     if (n_obs > 0) {
         hipLaunchKernelGGL(bas_soa, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs, cam_obs,
-                           pt_idx, W, w.Wp, w.ptc);
+                           pt_idx, W, soa ? w.Wp : nullptr, w.ptc);
         SFM_HIP_CHECK(hipGetLastError());
     }
     hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
@@ -1409,15 +1415,17 @@ static int solve_setup(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, in
 static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, int32_t n_pt,
                          int32_t n_obs, const int32_t* pt_ptr, const int32_t* cam_idx,
                          const double* V, const double* gp, const double* dc, double* dp, bool exp,
-                         double* comm) {
+                         double* comm, const double* W = nullptr) {
     if (!ck.cb) {
         hipLaunchKernelGGL(bas_backsub, dim3(w.gblk), dim3(256), 0, st, n_pt, n_obs, pt_ptr,
                            cam_idx, w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
         SFM_HIP_CHECK(hipGetLastError());
         return SFM_OK;
     }
-    hipLaunchKernelGGL(bas_backsub_ck, dim3(ck.nck * BPB), dim3(256), 0, st, ck.cpt, n_obs, pt_ptr,
-                       cam_idx, w.Wp, V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
+    // W given: row-major (the explicit Schur solve made no SoA copy)
+    hipLaunchKernelGGL(bas_backsub_ck, dim3(ck.nck * BPB), dim3(256), 0, st, ck.cpt, n_obs,
+                       W ? 24LL : 1LL, W ? 1LL : (long long)n_obs, pt_ptr, cam_idx, W ? W : w.Wp,
+                       V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bas_mchunk, dim3(1), dim3(64), 0, st, ck.nck, exp ? 1 : 0, 0, w.mpart,
                        (const double*)nullptr, exp ? comm : w.mtot);
@@ -1498,7 +1506,7 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     const bool ex = ctx->ba_nslot > 0;   // explicit reduced camera system (sfm_ba_set_schur)
     SFM_REQUIRE(!ex || ck.cb, "sfm_ba_solve: the explicit Schur system needs chunk mode");
     const int rc = solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U,
-                               V, W, gc, gp, lam, dc, 0, nullptr);
+                               V, W, gc, gp, lam, dc, 0, nullptr, !ex);
     if (rc != SFM_OK) return rc;
     if (ex) {
         if (schur_build(ctx, st, w, pt_idx, W, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
@@ -1537,7 +1545,8 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
                            w.z, w.pv, w.q, w.pq, w.rzc, w.rrc, w.state, tol);
     }
     SFM_HIP_CHECK(hipGetLastError());
-    if (solve_backsub(st, w, ck, n_pt, n_obs, pt_ptr, cam_idx, V, gp, dc, dp, false, nullptr) != SFM_OK)
+    if (solve_backsub(st, w, ck, n_pt, n_obs, pt_ptr, cam_idx, V, gp, dc, dp, false, nullptr,
+                      ex ? W : nullptr) != SFM_OK)
         return SFM_ERR_HIP;
     hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, ck.cb ? 1 : w.gblk, U, gc, dc,
                        ck.cb ? w.mtot : w.mpart, w.rrc, w.state, w.bad, info);
@@ -1580,7 +1589,7 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
     switch (stage) {
     case SFM_BA_STAGE_SETUP:  // -> comm[0, 44 n_cam) (chunk mode: [n_chunk][n_cam][44])
         return solve_setup(st, w, ck, n_cam, n_pt, n_obs, pt_idx, pt_ptr, cam_ptr, cam_obs, U, V,
-                           W, gc, gp, lam, dc, 1, comm);
+                           W, gc, gp, lam, dc, 1, comm, !ex);
     case SFM_BA_STAGE_SCHUR:  // explicit S: this shard's group partials of T -> comm [n_seg][64]
         return schur_build(ctx, st, w, pt_idx, W, comm);
     case SFM_BA_STAGE_SETUP_FINISH:
@@ -1622,7 +1631,8 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
         break;
     case SFM_BA_STAGE_BACKSUB:  // -> comm[0, 2) (chunk mode: [n_chunk][2])
         if (ck.cb) {
-            if (solve_backsub(st, w, ck, n_pt, n_obs, pt_ptr, cam_idx, V, gp, dc, dp, true, comm) != SFM_OK)
+            if (solve_backsub(st, w, ck, n_pt, n_obs, pt_ptr, cam_idx, V, gp, dc, dp, true, comm,
+                              ex ? W : nullptr) != SFM_OK)
                 return SFM_ERR_HIP;
             break;
         }
