@@ -71,6 +71,20 @@ class Reconstruction:
         self.n_verified = 0        # rows of the verified match graph
         self.obs_d = None          # device (obs_track, timg, obs_xy) of the track observations
         self.gauge = None          # (reference camera, scale camera) of the initial pair
+        self._tracks_d = None      # device (ptr, img, kp) of the tracks; host copies on first use
+        self._tracks = None
+
+    @property
+    def tracks(self):
+        """(ptr [n_tr + 1], img [n_obs], kp [n_obs]) host arrays of the tracks (copied from the
+        device on first use: the reconstruction itself never reads them on the host)."""
+        if self._tracks is None and self._tracks_d is not None:
+            self._tracks = tuple(t.cpu().numpy() for t in self._tracks_d)
+        return self._tracks
+
+    @tracks.setter
+    def tracks(self, v):
+        self._tracks, self._tracks_d = v, None
 
 
 def _match_graph(gb, pairs, pairs_t, n_kp, group):
@@ -196,27 +210,30 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     rows, inl = _match_graph(gb, pairs, pairs_t, n_kp, group)
     tk = lap("match_verify", tk)
     ptr_t, timg_t, tkp_t = match_graph.build_tracks(rows, pairs_t, n_kp, min_track, device)
-    tptr, timg, tkp = (t.cpu().numpy() for t in (ptr_t, timg_t, tkp_t))
-    n_tr = len(tptr) - 1
-    kps_np = np.asarray(kps)  # converted to f64 per gathered row (exact), not as a whole
-    obs_track = np.repeat(np.arange(n_tr), np.diff(tptr))
-    # one flat row gather (np.take is ~4x faster than the 2-D fancy index at 2 M observations)
-    obs_xy = np.take(kps_np.reshape(-1, 2), timg.astype(np.int64) * kps_np.shape[1] + tkp,
-                     axis=0).astype(np.float64)
+    n_tr = int(ptr_t.numel()) - 1
+    n_obs = int(timg_t.numel())
+    kps_np = np.asarray(kps)
+    # the observation arrays, built on the device (every bundle adjustment, registration and
+    # triangulation selects its observations there; the host numpy build of the 1.4 M cfg5
+    # observations took ~25 ms): track id per observation, image, and the keypoint as f64 (exact
+    # from the caller's dtype; the builder's f32 copy when that is the caller's)
+    kps_d = gb.kps if kps_np.dtype == np.float32 else torch.from_numpy(
+        np.ascontiguousarray(kps_np)).to(dev)
+    timg_l = timg_t.long()
+    obs_d = (torch.repeat_interleave(torch.arange(n_tr, dtype=torch.int64, device=dev),
+                                     (ptr_t[1:] - ptr_t[:-1]).long(), output_size=n_obs),
+             timg_l,
+             kps_d.reshape(-1, 2)[timg_l * kps_np.shape[1] + tkp_t.long()].to(torch.float64))
     say(f"graph: {len(rows)} verified matches, {n_tr} tracks")
-    # device copies of the observation arrays: every bundle adjustment selects its observations
-    # on the GPU (1.5 M observations at cfg5: ~50 ms of host masking per round otherwise)
-    obs_d = (torch.from_numpy(obs_track.astype(np.int64)).to(dev),
-             torch.from_numpy(timg.astype(np.int64)).to(dev), torch.from_numpy(obs_xy).to(dev))
 
     rec = Reconstruction(n_img)
     rec.obs_d = obs_d
     rec.timings = tim
     rec.n_verified = int(rows.shape[0])
+    rec._tracks_d = (ptr_t, timg_t, tkp_t)
     tk = lap("tracks", tk)
     rec.points = np.zeros((n_tr, 3))
     rec.has_point = np.zeros(n_tr, bool)
-    rec.tracks = (tptr, timg, tkp)
     rec.cams[:, 6:8] = intr[:, :2]
 
     # ---- initial pair: most verified inliers; relative pose from that pair's RANSAC-verified
@@ -234,7 +251,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             continue
         xa = _undistort(kps_np[a, r[:, 1]].astype(np.float64), intr[a])
         xb = _undistort(kps_np[b, r[:, 2]].astype(np.float64), intr[b])
-        common = np.intersect1d(obs_track[timg == a], obs_track[timg == b])
+        ta, tb = obs_d[0][obs_d[1] == a], obs_d[0][obs_d[1] == b]
+        common = torch.unique(ta[torch.isin(ta, tb)]).cpu().numpy()   # sorted, as intersect1d
         best = None
         for R, t in relative_pose(xa, xb):
             cams = rec.cams.copy()
@@ -260,8 +278,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     if not rec.registered.any():
         raise RuntimeError("reconstruct: no initial pair with enough well-conditioned matches")
     tk = lap("initial_pair", tk)
-    _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-            shard_ba, group, ba_cg_tol, ba_pcg, ba_ftol)
+    _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba, group, ba_cg_tol, ba_pcg,
+            ba_ftol)
     tk = lap("bundle_adjust", tk)
     tim["rounds"] = 0
 
@@ -295,8 +313,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             break
         _triangulate_new(rec, ctx, intr, max_err)
         tk = lap("triangulate", tk)
-        _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-                shard_ba, group, ba_cg_tol, ba_pcg, ba_ftol)
+        _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba, group, ba_cg_tol,
+                ba_pcg, ba_ftol)
         tk = lap("bundle_adjust", tk)
     return rec
 
@@ -336,13 +354,13 @@ def _triangulate_new(rec, ctx, intr, max_err):
     rec.has_point[todo[ok]] = True
 
 
-def _bundle(rec, intr, obs_track, timg, obs_xy, loss_s, ba_iter, max_err, device,
-            shard_ba=False, group=None, cg_tol=0.1, pcg="auto", ftol=1e-6):
+def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=None, cg_tol=0.1,
+            pcg="auto", ftol=1e-6):
     """Global LM over the registered cameras and the triangulated points (GPU), then drop points
     whose mean reprojection error stays above max_err.  Gauge: the initial pair's first camera
     keeps its pose and the second one translation coordinate (the scale); the intrinsics are
     known, so f and k1 are held too (reconstruction.gauge_mask).  The observations are selected
-    on the device from rec.obs_d (the same arrays as obs_track / timg / obs_xy on the host)."""
+    on the device from rec.obs_d = (obs_track, timg, obs_xy)."""
     import time
     import torch
     t0 = time.perf_counter()

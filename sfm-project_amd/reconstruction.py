@@ -247,12 +247,13 @@ def schur_pair_count(pt_ptr):
     return (m * (m - 1) // 2).sum()
 
 
-def schur_instances(cam_idx, pt_idx, pt_ptr, n_cam, chunk_pt):
+def schur_instances(cam_idx, pt_idx, pt_ptr, n_cam, chunk_pt, total=None):
     """The local camera-pair instances: for every point and every pair of its observations a < b
     (observation order), oriented so that cam(a) <= cam(b); a pair within one camera also as
     (b, a).  Returns (composite key chunk * n_cam^2 + ci * n_cam + cj, a, b) sorted stably by the
     key — inside a (chunk, slot) group the instances stay in point order.  Two host syncs (the
-    instance count and the same-camera count)."""
+    instance count, unless the caller passes it as `total` — schur_pair_count — and the
+    same-camera count)."""
     import torch
     dev = cam_idx.device
     n_obs = int(cam_idx.numel())
@@ -263,7 +264,7 @@ def schur_instances(cam_idx, pt_idx, pt_ptr, n_cam, chunk_pt):
     end = ptr[1:][pt_idx.long()]                               # end of each observation's point
     o = torch.arange(n_obs, dtype=torch.int64, device=dev)
     cnt = end - o - 1                                          # partners after o in its point
-    total = int(cnt.sum())
+    total = int(cnt.sum()) if total is None else int(total)
     a = torch.repeat_interleave(o, cnt, output_size=total)
     first = torch.cumsum(cnt, 0) - cnt
     b = a + 1 + (torch.arange(total, dtype=torch.int64, device=dev)
@@ -318,11 +319,12 @@ def schur_spec(comp, cnt, a, b, n_cam, all_groups, k0=0):
     gs_sorted, sg = torch.sort(gslot * 64 + gk, stable=True)
     sg_ptr = torch.searchsorted(gs_sorted, torch.arange(slot_keys.numel() + 1, dtype=torch.int64,
                                                         device=dev) * 64)
-    g0 = torch.searchsorted(all_groups, torch.tensor([k0 * nn], dtype=all_groups.dtype, device=dev))
+    g0 = 0 if k0 == 0 else int(torch.searchsorted(
+        all_groups, torch.tensor([k0 * nn], dtype=all_groups.dtype, device=dev)).item())
     inst = torch.stack([a, b]).to(i32).contiguous()
     return SchurSpec(slot_cam, seg, inst, row_ptr.to(i32).contiguous(),
                      ent[order].to(i32).contiguous(), sg_ptr.to(i32).contiguous(),
-                     sg.to(i32).contiguous(), gk.to(i32).contiguous(), int(g0.item()))
+                     sg.to(i32).contiguous(), gk.to(i32).contiguous(), g0)
 
 
 class BAProblem:
@@ -358,7 +360,7 @@ class BAProblem:
             T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dt)).to(self.dev)
             self.cam_idx, self.pt_idx, self.uv = T(cam_idx), T(pt_idx), T(uv)
         self.pp = torch.from_numpy(np.ascontiguousarray(pp, np.float64)).to(self.dev)
-        self.pt_ptr, _ = sfmcore.csr_by_device(self.pt_idx, n_pt)
+        self.pt_ptr = sfmcore.csr_ptr_device(self.pt_idx, n_pt, ascending=True)   # point-major
         self.cam_ptr, self.cam_obs = sfmcore.csr_by_device(self.cam_idx, n_cam)
         self.n_cam, self.n_pt = n_cam, n_pt
         self.ctx = sfmcore.context(device)
@@ -375,15 +377,16 @@ class BAProblem:
             cb = cam_bounds_device(self.cam_idx, self.cam_obs, n_cam, cob)
             self.chunks = BAChunks(cpt, cob, cb, n_total, k0)
 
-    def set_schur(self, union=None):
+    def set_schur(self, union=None, n_pairs=None):
         """Turn the explicit reduced camera system on (needs chunk mode).  union: for a shard, maps
         this shard's group keys (global chunk * n_cam^2 + ci * n_cam + cj, sorted int64 device
         tensor) to the WHOLE problem's (every rank's, sorted; a collective, the same result on
-        every rank); None = this problem's own."""
+        every rank); None = this problem's own.  n_pairs: this problem's schur_pair_count when
+        the caller already read it (saves a host sync)."""
         if self.chunks is None:
             raise ValueError("BAProblem.set_schur: the explicit Schur system needs chunk mode")
         key, a, b = schur_instances(self.cam_idx, self.pt_idx, self.pt_ptr, self.n_cam,
-                                    self.chunks.chunk_pt)
+                                    self.chunks.chunk_pt, total=n_pairs)
         comp, cnt = schur_groups(key)
         k0 = self.chunks.k0
         gkeys = comp + k0 * self.n_cam * self.n_cam
@@ -755,11 +758,13 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     if nchunk > 0 and smode != "0":
         tgt = full if full is not None else prob
         cnt = schur_pair_count(tgt.pt_ptr).double().reshape(1)
+        own = cnt.clone()
         n_obs_tot = len(tgt.cam_idx)
         if allreduce is not None and full is None:
             allreduce(cnt)
             n_obs_tot = n_obs_all
-        use_schur = smode == "1" or float(cnt.item()) <= SCHUR_INST_PER_OBS * max(n_obs_tot, 1)
+        cnt, own = (float(v) for v in torch.cat([cnt, own]).tolist())   # one host read
+        use_schur = smode == "1" or cnt <= SCHUR_INST_PER_OBS * max(n_obs_tot, 1)
         if use_schur:
             t_s = time.perf_counter()
             sharded_s = allreduce is not None and full is None
@@ -771,14 +776,16 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                     g = _gather_rows(keys.double().reshape(-1, 1), [int(v) for v in nk.tolist()],
                                      group)
                     return torch.sort(g.reshape(-1).long()).values
-                prob.set_schur(union)
+                prob.set_schur(union, n_pairs=own)
             else:
-                tgt.set_schur()
+                tgt.set_schur(n_pairs=own)
             sp = tgt.schur
-            tot = torch.tensor([sp.n_inst], dtype=f64, device=prob.dev)
+            n_inst_tot = float(sp.n_inst)
             if sharded_s:
+                tot = torch.tensor([sp.n_inst], dtype=f64, device=prob.dev)
                 allreduce(tot)   # the whole problem's products
-            n_inst_tot, n_seg_tot = float(tot.item()), float(sp.n_group)
+                n_inst_tot = float(tot.item())
+            n_seg_tot = float(sp.n_group)
             if smode != "1" and not schur_rule(n_inst_tot, n_seg_tot, sp.n_slot, n_obs_tot):
                 tgt.schur = None
                 use_schur = False

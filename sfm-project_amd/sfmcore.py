@@ -671,14 +671,27 @@ def context(device: int = 0) -> Context:
 
 def csr_by_device(index, n: int):
     """csr_by on a device tensor (torch's stable sort on the GPU): the same (ptr, order) as
-    csr_by, int32 device tensors, without a host sort of every observation."""
+    csr_by, int32 device tensors, without a host sort of every observation (and without a host
+    sync: the counts are an index_add into n slots, not a bincount sized by the maximum)."""
     import torch
     idx = index.long()
     order = torch.argsort(idx, stable=True).to(torch.int32)
-    ptr = torch.zeros(n + 1, dtype=torch.int32, device=index.device)
-    if idx.numel():
-        ptr[1:] = torch.cumsum(torch.bincount(idx, minlength=n), 0).to(torch.int32)
-    return ptr, order
+    return csr_ptr_device(idx, n), order
+
+
+def csr_ptr_device(index, n: int, ascending: bool = False):
+    """The CSR offsets [n + 1] (int32 device) of the values 0..n-1 of a device index tensor, with no
+    host sync; ascending=True (index non-decreasing): a searchsorted instead of a count."""
+    import torch
+    idx = index.long()
+    dev = index.device
+    if ascending:
+        return torch.searchsorted(idx, torch.arange(n + 1, dtype=torch.int64, device=dev)).to(torch.int32)
+    cnt = torch.zeros(n, dtype=torch.int64, device=dev)
+    cnt.index_add_(0, idx, torch.ones_like(idx))
+    ptr = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+    ptr[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+    return ptr
 
 
 def csr_by(index: np.ndarray, n: int):

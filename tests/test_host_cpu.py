@@ -173,6 +173,10 @@ def test_csr_by_device_equals_host_csr():
         dptr, dorder = sfmcore.csr_by_device(torch.from_numpy(idx), n)
         np.testing.assert_array_equal(dptr.numpy(), ptr)
         np.testing.assert_array_equal(dorder.numpy(), order)
+        # the point CSR of a point-major problem (ascending index: a searchsorted)
+        sidx = np.sort(idx)
+        np.testing.assert_array_equal(
+            sfmcore.csr_ptr_device(torch.from_numpy(sidx), n, ascending=True).numpy(), ptr)
 
 
 @pytest.mark.parametrize("kw,digest", [
