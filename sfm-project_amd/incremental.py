@@ -64,8 +64,8 @@ class Reconstruction:
         self.timings = {}          # wall seconds per stage (each stage ends in a device sync)
         self.cams = np.zeros((n_img, 8))
         self.registered = np.zeros(n_img, bool)
-        self.points = None
-        self.has_point = None
+        self.pts_d = None          # device [n_tr, 3] f64 points and [n_tr] bool flags: the driver
+        self.has_d = None          # keeps them on the GPU; .points / .has_point are host copies
         self.history = []
         self.ba_log = []           # per bundle adjustment: size, LM / CG iterations, PCG branch
         self.n_verified = 0        # rows of the verified match graph
@@ -85,6 +85,16 @@ class Reconstruction:
     @tracks.setter
     def tracks(self, v):
         self._tracks, self._tracks_d = v, None
+
+    @property
+    def points(self):
+        """[n_tr, 3] host copy of the track points (valid where has_point)."""
+        return None if self.pts_d is None else self.pts_d.cpu().numpy()
+
+    @property
+    def has_point(self):
+        """[n_tr] bool host copy: the track has a triangulated point."""
+        return None if self.has_d is None else self.has_d.cpu().numpy()
 
 
 def _match_graph(gb, pairs, pairs_t, n_kp, group):
@@ -232,8 +242,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     rec.n_verified = int(rows.shape[0])
     rec._tracks_d = (ptr_t, timg_t, tkp_t)
     tk = lap("tracks", tk)
-    rec.points = np.zeros((n_tr, 3))
-    rec.has_point = np.zeros(n_tr, bool)
+    rec.pts_d = torch.zeros((n_tr, 3), dtype=torch.float64, device=dev)
+    rec.has_d = torch.zeros(n_tr, dtype=torch.bool, device=dev)
     rec.cams[:, 6:8] = intr[:, :2]
 
     # ---- initial pair: most verified inliers; relative pose from that pair's RANSAC-verified
@@ -259,7 +269,8 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
             cams[a, :6] = 0.0
             cams[b, :3] = _angle_axis(R)
             cams[b, 3:6] = t
-            pts, st = _triangulate(ctx, cams, intr, [a, b], common, rec.obs_d, n_tr)
+            pts, st = (t.cpu().numpy() for t in
+                       _triangulate(ctx, cams, intr, [a, b], common, rec.obs_d, n_tr))
             good = int(np.sum((st[:, 3] == 0) & (st[:, 0] < max_err)))
             if best is None or good > best[0]:
                 best = (good, cams, pts, st)
@@ -269,8 +280,9 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         # (neighbouring views of a dense sequence) cannot seed the model
         if good >= 30 and int(ok.sum()) >= 30:
             rec.cams = cams_b
-            rec.points[common[ok]] = pts[ok]
-            rec.has_point[common[ok]] = True
+            sel = torch.from_numpy(common[ok]).to(dev)
+            rec.pts_d[sel] = torch.from_numpy(np.ascontiguousarray(pts[ok])).to(dev)
+            rec.has_d[sel] = True
             rec.registered[[a, b]] = True
             rec.gauge = (a, b)
             say(f"initial pair ({a}, {b}): {len(r)} verified matches, {int(ok.sum())} points")
@@ -289,12 +301,12 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
         # image (ascending) and ascending observation index within an image: one pass
         # (selected on the device from rec.obs_d: ~1.5 M observations at cfg5)
         otr_d, timg_d, oxy_d = obs_d
-        sel, ids, cptr = registration_obs(otr_d, timg_d, torch.from_numpy(rec.has_point).to(dev),
+        sel, ids, cptr = registration_obs(otr_d, timg_d, rec.has_d,
                                           torch.from_numpy(rec.registered).to(dev))
         if len(ids) == 0:
             break
         T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
-        pts_d = T(rec.points, np.float64)
+        pts_d = rec.pts_d
         cams_r, cnt, _, _ = ctx.register_batch(T(cptr, np.int32), oxy_d[sel].contiguous(),
                                                pts_d[otr_d[sel]].contiguous(),
                                                T(intr[ids], np.float64), T(ids, np.int32),
@@ -320,19 +332,20 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
 
 
 def _triangulate(ctx, cams, intr, imgs, tracks, obs_d, n_tr):
-    """Triangulate `tracks` (ascending ids) from their observations in the images `imgs` (GPU
-    kernel; the observations are selected on the device from obs_d = (obs_track, timg, obs_xy))."""
+    """Triangulate `tracks` (ascending ids: host array or device tensor) from their observations
+    in the images `imgs` (GPU kernel; the observations are selected on the device from obs_d =
+    (obs_track, timg, obs_xy)).  Returns device (pts [n, 3], stats [n, 4]) f64 tensors."""
     import torch
     otr_d, timg_d, oxy_d = obs_d
     dev = otr_d.device
     in_img = torch.zeros(len(cams), dtype=torch.bool, device=dev)
     in_img[torch.as_tensor(np.asarray(imgs, np.int64), device=dev)] = True
-    o, ptr = track_obs(otr_d, timg_d, n_tr, torch.as_tensor(np.asarray(tracks, np.int64),
-                                                             device=dev), in_img)
+    tr = (tracks.long() if isinstance(tracks, torch.Tensor) else
+          torch.as_tensor(np.asarray(tracks, np.int64), device=dev))
+    o, ptr = track_obs(otr_d, timg_d, n_tr, tr, in_img)
     T = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x, dt)).to(dev)
-    pts, st = ctx.triangulate(T(cams, np.float64), T(intr[:, 2:4], np.float64), ptr,
-                              timg_d[o].to(torch.int32), oxy_d[o].contiguous())
-    return pts.cpu().numpy(), st.cpu().numpy()
+    return ctx.triangulate(T(cams, np.float64), T(intr[:, 2:4], np.float64), ptr,
+                           timg_d[o].to(torch.int32), oxy_d[o].contiguous())
 
 
 def _triangulate_new(rec, ctx, intr, max_err):
@@ -340,18 +353,19 @@ def _triangulate_new(rec, ctx, intr, max_err):
     import torch
     otr_d, timg_d, _ = rec.obs_d
     dev = otr_d.device
-    n_tr = len(rec.has_point)
+    n_tr = int(rec.has_d.numel())
     reg_d = torch.from_numpy(rec.registered).to(dev)
-    n_reg = torch.bincount(otr_d[reg_d[timg_d]], minlength=n_tr)
-    todo_d = torch.nonzero(~torch.from_numpy(rec.has_point).to(dev) & (n_reg >= 2)).squeeze(1)
-    todo = todo_d.cpu().numpy()
-    if len(todo) == 0:
+    n_reg = torch.zeros(n_tr, dtype=torch.int64, device=dev)
+    sel = otr_d[reg_d[timg_d]]
+    n_reg.index_add_(0, sel, torch.ones_like(sel))
+    todo_d = torch.nonzero(~rec.has_d & (n_reg >= 2)).squeeze(1)
+    if todo_d.numel() == 0:
         return
-    pts, st = _triangulate(ctx, rec.cams, intr, np.nonzero(rec.registered)[0], todo, rec.obs_d,
+    pts, st = _triangulate(ctx, rec.cams, intr, np.nonzero(rec.registered)[0], todo_d, rec.obs_d,
                            n_tr)
     ok = (st[:, 3] == 0) & (st[:, 0] < max_err) & (st[:, 1] > 1.0)
-    rec.points[todo[ok]] = pts[ok]
-    rec.has_point[todo[ok]] = True
+    rec.pts_d[todo_d[ok]] = pts[ok]
+    rec.has_d[todo_d[ok]] = True
 
 
 def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=None, cg_tol=0.1,
@@ -367,8 +381,7 @@ def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=N
     otr_d, timg_d, oxy_d = rec.obs_d
     dev = otr_d.device
     reg_d = torch.from_numpy(rec.registered).to(dev)
-    has_d = torch.from_numpy(rec.has_point).to(dev)
-    use = torch.nonzero(reg_d[timg_d] & has_d[otr_d]).squeeze(1)   # the one sizing sync
+    use = torch.nonzero(reg_d[timg_d] & rec.has_d[otr_d]).squeeze(1)   # the one sizing sync
     n_use = int(use.shape[0])
     if n_use == 0:
         return
@@ -377,26 +390,27 @@ def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=N
     tr = otr_d[use]   # non-decreasing (track-major): unique tracks by run starts
     first = torch.ones(n_use, dtype=torch.bool, device=dev)
     first[1:] = tr[1:] != tr[:-1]
-    pts_ids = tr[first].cpu().numpy()
+    pts_ids = tr[first]     # device: the BA's points, gathered and scattered on the GPU
     pt_idx_d = torch.cumsum(first, 0, dtype=torch.int32) - 1
     info = {}
     t_sel = time.perf_counter() - t0    # observation selection (ends in host syncs)
-    cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.points[pts_ids],
+    cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.pts_d[pts_ids],
                                                    timg_d[use].to(torch.int32), pt_idx_d,
                                                    oxy_d[use], loss_s=loss_s, max_iter=ba_iter,
                                                    cg_tol=cg_tol, ftol=ftol, device=device,
                                                    fixed=fixed, shard=shard_ba, group=group,
-                                                   pcg=pcg, info=info, reproj_err="device")
+                                                   pcg=pcg, info=info, reproj_err="device",
+                                                   device_out=True)
     err_d = info.pop("err")   # device, at the returned parameters (bundle_adjust reproj_err)
-    rec.ba_log.append(dict(info, n_cam=int(rec.registered.sum()), n_pt=int(len(pts_ids)),
+    rec.ba_log.append(dict(info, n_cam=int(rec.registered.sum()), n_pt=int(pts_ids.numel()),
                            n_obs=n_use, lm_steps=len(hist),
                            cg_iters=int(sum(h[3] for h in hist))))
     reg = rec.registered
     rec.cams[reg] = cams[reg]
-    rec.points[pts_ids] = pts
+    rec.pts_d[pts_ids] = pts
     mean = point_mean(err_d, first)
-    rec.has_point[pts_ids[(mean > max_err).cpu().numpy()]] = False
+    rec.has_d[pts_ids[mean > max_err]] = False
     rec.ba_log[-1]["s"] = time.perf_counter() - t0   # setup + LM + reprojection filter
     rec.ba_log[-1]["select_s"] = t_sel
-    rec.history.append((int(reg.sum()), int(rec.has_point.sum()),
+    rec.history.append((int(reg.sum()), int(rec.has_d.sum()),
                         float(hist[-1][0]) if hist else float("nan")))

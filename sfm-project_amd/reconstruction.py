@@ -629,7 +629,7 @@ def _gather_rows(t, counts, group):
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
                   lam0: float = 1e-4, ftol: float = 1e-12, max_cg: int = 200,
                   cg_tol: float = 1e-10, device: int = 0, fixed=None, shard: bool = False,
-                  group=None, pcg: str = "auto", info=None, reproj_err=False):
+                  group=None, pcg: str = "auto", info=None, reproj_err=False, device_out=False):
     """Levenberg-Marquardt on paper eq. (1): every step on the GPU
     (J^TJ build, Schur-complement PCG, update, trial cost); the host reads 7 scalars per step to
     accept / reject it.  cam_idx / pt_idx / uv may be device tensors (used in place).
@@ -662,6 +662,9 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     sharded: each rank's shard summed into a zero-padded vector), instead of a second host ->
     device copy of the whole problem through reprojection_errors.  reproj_err="device" leaves
     `err` as an f64 device tensor (same order) instead of a host array.
+
+    pts may be a device tensor (used without a host round trip); device_out=True returns pts as
+    an f64 device tensor instead of a host array.
 
     Returns (cams [n_cam,8], pts [n_pt,3], history [(cost, λ, accepted, cg_iterations)])."""
     import os
@@ -806,10 +809,12 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         slot[k0:k0 + nl] = part.reshape(nl, width)
         allreduce(slot.view(-1))
         return prob.ctx.ba_chunk_tree(slot)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(prob.dev)
+    T = lambda a: (a.to(prob.dev, torch.float64).contiguous() if isinstance(a, torch.Tensor)
+                   else torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(prob.dev))
     cams_d = T(cams)
     # replicated: every rank keeps all points (the solve's δp is whole); the shard is a view
-    pts_d = T(pts) if full is not None else T(np.asarray(pts, np.float64)[lo:hi])
+    pts_d = T(pts) if full is not None else T(pts[lo:hi] if isinstance(pts, torch.Tensor)
+                                              else np.asarray(pts, np.float64)[lo:hi])
     shard_of = (lambda p: p[lo:hi]) if full is not None else (lambda p: p)
     fixed_d = None
     if fixed is not None and np.any(fixed):
@@ -911,7 +916,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         allp[lo:hi] = pts_d
         allreduce(allp.view(-1))
         pts_d = allp
-    out = cams_d.cpu().numpy(), pts_d.cpu().numpy(), hist
+    out = cams_d.cpu().numpy(), (pts_d if device_out else pts_d.cpu().numpy()), hist
     if info is not None:
         info["post_s"] = time.perf_counter() - t_lm - info["lm_s"]   # errors + results to host
     return out
