@@ -131,6 +131,19 @@ def _match_graph(gb, pairs, pairs_t, n_kp, group):
     return graph, inl.cpu().numpy()
 
 
+def track_observations(ptr, img, kp, kps):
+    """The observation arrays of the tracks (torch tensors of one device): (track id int64, image
+    int64, keypoint [n, 2] f64) per observation, track-major — from the tracks CSR (ptr [T + 1],
+    img / kp [n]) and the keypoints kps [n_img, K, 2] (any float dtype; f64 is exact)."""
+    import torch
+    n_tr, n_obs = int(ptr.numel()) - 1, int(img.numel())
+    img_l = img.long()
+    otr = torch.repeat_interleave(torch.arange(n_tr, dtype=torch.int64, device=ptr.device),
+                                  (ptr[1:] - ptr[:-1]).long(), output_size=n_obs)
+    xy = kps.reshape(-1, 2)[img_l * kps.shape[1] + kp.long()].to(torch.float64)
+    return otr, img_l, xy
+
+
 def track_obs(otr, timg, n_tr, tracks, in_img):
     """Observations of `tracks` (ascending track ids) whose image is flagged in `in_img`, as the
     triangulation kernel's CSR: (o, ptr) with o the observation indices in track order, ascending
@@ -221,7 +234,6 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     tk = lap("match_verify", tk)
     ptr_t, timg_t, tkp_t = match_graph.build_tracks(rows, pairs_t, n_kp, min_track, device)
     n_tr = int(ptr_t.numel()) - 1
-    n_obs = int(timg_t.numel())
     kps_np = np.asarray(kps)
     # the observation arrays, built on the device (every bundle adjustment, registration and
     # triangulation selects its observations there; the host numpy build of the 1.4 M cfg5
@@ -229,11 +241,7 @@ def reconstruct(desc, kps, n_kp, intr, min_track=2, n_hyp=1024, reg_thr=4.0, max
     # from the caller's dtype; the builder's f32 copy when that is the caller's)
     kps_d = gb.kps if kps_np.dtype == np.float32 else torch.from_numpy(
         np.ascontiguousarray(kps_np)).to(dev)
-    timg_l = timg_t.long()
-    obs_d = (torch.repeat_interleave(torch.arange(n_tr, dtype=torch.int64, device=dev),
-                                     (ptr_t[1:] - ptr_t[:-1]).long(), output_size=n_obs),
-             timg_l,
-             kps_d.reshape(-1, 2)[timg_l * kps_np.shape[1] + tkp_t.long()].to(torch.float64))
+    obs_d = track_observations(ptr_t, timg_t, tkp_t, kps_d)
     say(f"graph: {len(rows)} verified matches, {n_tr} tracks")
 
     rec = Reconstruction(n_img)

@@ -367,3 +367,26 @@ def test_shard_cuts_device_equals_shard_points():
             exp = [reconstruction.shard_points(ptr, r, world) for r in range(world)]
             assert [(cuts[r], cuts[r + 1]) for r in range(world)] == exp
             assert ocuts == [int(ptr[c]) for c in cuts]
+
+
+def test_track_observations_equal_host_build():
+    """incremental.track_observations (the driver's device build of the track observation arrays)
+    gives the host numpy build it replaced — np.repeat of the track ids, np.take of the keypoint
+    rows as f64 — element for element (CPU tensors here), for f32 and f64 keypoints."""
+    import torch
+    import incremental
+    rng = np.random.default_rng(9)
+    n_img, K = 7, 50
+    lens = rng.integers(2, 6, 40)
+    ptr = np.r_[0, np.cumsum(lens)].astype(np.int32)
+    img = rng.integers(0, n_img, ptr[-1]).astype(np.int32)
+    kp = rng.integers(0, K, ptr[-1]).astype(np.int32)
+    for dt in (np.float32, np.float64):
+        kps = (rng.random((n_img, K, 2)) * 1000).astype(dt)
+        otr, oimg, oxy = incremental.track_observations(torch.from_numpy(ptr), torch.from_numpy(img),
+                                                        torch.from_numpy(kp), torch.from_numpy(kps))
+        np.testing.assert_array_equal(otr.numpy(), np.repeat(np.arange(len(lens)), lens))
+        np.testing.assert_array_equal(oimg.numpy(), img.astype(np.int64))
+        ref = np.take(kps.reshape(-1, 2), img.astype(np.int64) * K + kp, axis=0).astype(np.float64)
+        np.testing.assert_array_equal(oxy.numpy(), ref)
+        assert oxy.dtype == torch.float64
