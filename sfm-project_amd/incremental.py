@@ -88,13 +88,22 @@ class Reconstruction:
 
     @property
     def points(self):
-        """[n_tr, 3] host copy of the track points (valid where has_point)."""
-        return None if self.pts_d is None else self.pts_d.cpu().numpy()
+        """[n_tr, 3] host copy of the track points (valid where has_point); read-only — the model
+        lives in pts_d, so writing to a copy would be lost (write to pts_d instead)."""
+        return _host_copy(self.pts_d)
 
     @property
     def has_point(self):
-        """[n_tr] bool host copy: the track has a triangulated point."""
-        return None if self.has_d is None else self.has_d.cpu().numpy()
+        """[n_tr] bool host copy: the track has a triangulated point (read-only, see points)."""
+        return _host_copy(self.has_d)
+
+
+def _host_copy(t):
+    if t is None:
+        return None
+    a = t.cpu().numpy()
+    a.setflags(write=False)
+    return a
 
 
 def _match_graph(gb, pairs, pairs_t, n_kp, group):

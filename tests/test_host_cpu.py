@@ -390,3 +390,20 @@ def test_track_observations_equal_host_build():
         ref = np.take(kps.reshape(-1, 2), img.astype(np.int64) * K + kp, axis=0).astype(np.float64)
         np.testing.assert_array_equal(oxy.numpy(), ref)
         assert oxy.dtype == torch.float64
+
+
+def test_reconstruction_host_views_are_read_only_copies():
+    """The driver keeps points / flags on the device (Reconstruction.pts_d / has_d); .points and
+    .has_point are host copies that refuse writes (a write to a copy would be lost)."""
+    import torch
+    import incremental
+    rec = incremental.Reconstruction(3)
+    assert rec.points is None and rec.has_point is None
+    rec.pts_d = torch.arange(12, dtype=torch.float64).reshape(4, 3)
+    rec.has_d = torch.tensor([True, False, True, False])
+    np.testing.assert_array_equal(rec.points, np.arange(12.0).reshape(4, 3))
+    np.testing.assert_array_equal(rec.has_point, [True, False, True, False])
+    with pytest.raises(ValueError):
+        rec.points[0, 0] = 1.0
+    with pytest.raises(ValueError):
+        rec.has_point[1] = True
