@@ -162,8 +162,11 @@ def track_obs(otr, timg, n_tr, tracks, in_img):
     want = torch.zeros(n_tr, dtype=torch.bool, device=otr.device)
     want[tracks] = True
     o = torch.nonzero(want[otr] & in_img[timg]).squeeze(1)
+    cnt = torch.zeros(n_tr, dtype=torch.int64, device=otr.device)   # index_add: no sizing sync
+    sel = otr[o]
+    cnt.index_add_(0, sel, torch.ones_like(sel))
     ptr = torch.zeros(len(tracks) + 1, dtype=torch.int32, device=otr.device)
-    ptr[1:] = torch.cumsum(torch.bincount(otr[o], minlength=n_tr)[tracks], 0)
+    ptr[1:] = torch.cumsum(cnt[tracks], 0)
     return o, ptr
 
 
