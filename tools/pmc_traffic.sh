@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 # launches per step: one per step at the bench default --chunk (131072), for both configs
 if [ $CFG = cfg3 ]; then NI=50; K=2048; PER=1; else NI=500; K=4096; PER=1; fi
 STEPS=2
-B="python3 bench.py --config $CFG --steps $STEPS --warmup 1 --no-cpu-baseline --no-cfg3 --no-cfg5 --no-fp64"
+B="python3 bench.py --config $CFG --steps $STEPS --warmup 1 --no-cpu-baseline --no-cfg3 --no-cfg5 --no-fp64 --no-local"
 RX="mfma_prep_kernel|mfma_mutual_kernel|mutual_finalize_kernel|ransac_prep_kernel|ransac_fit_kernel|ransac_order_kernel|ransac_score_kernel|ransac_final_kernel|graph_rows_kernel"
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
