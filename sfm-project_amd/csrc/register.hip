@@ -5,10 +5,12 @@
 // Spec: oracle/sfm_oracle_reg.c header (mirrored op-for-op here; only +, -, *, /, sqrt in the
 // RANSAC part and no FMA contraction on either side, so counts, the winning hypothesis and the
 // inlier mask are bit-identical to the CPU).  Kernels:
-//   reg_hyp_kernel    lane per hypothesis (grid: hypothesis blocks x images): Philox sample of 3
-//                     correspondences, Grunert P3P (Durand-Kerner quartic roots), every pose scored
-//                     over the image's correspondences; 64-bit key (count+1) << 32 | ~(4h + root)
-//                     -> wave max -> atomicMax per image
+//   reg_hyp_kernel    lane per (hypothesis, correspondence slice) (grid: hypothesis blocks x
+//                     slices x images): Philox sample of 3 correspondences, Grunert P3P (Durand-
+//                     Kerner quartic roots), every pose scored over the slice; integer counts
+//                     summed per hypothesis by atomics
+//   reg_key_kernel    lane per hypothesis: 64-bit key (count+1) << 32 | ~(4h + root) -> wave max
+//                     -> atomicMax per image
 //   reg_final_kernel  block per image: the winner's pose again, inlier mask and count, then 10
 //                     Gauss-Newton steps on the inliers (left rotation increment, as the BA
 //                     Jacobians; fixed-order sums; 6x6 Cholesky), pose -> (angle-axis, t, f, k1)
@@ -20,6 +22,13 @@ namespace {
 constexpr int REG_UNDISTORT = 10;
 constexpr int REG_DK_ITERS = 48;
 constexpr int REG_GN_ITERS = 10;
+// Correspondence slices per hypothesis (reg_hyp_kernel): 1024 hypotheses x the candidate images
+// are fewer waves than the chip has SIMDs, so every hypothesis' correspondences are cut into
+// REG_SPLIT slices scored by REG_SPLIT lanes (each solves the P3P again) and the integer counts
+// are summed by atomics — exact in any order — before the key kernel picks the winner.
+#ifndef REG_SPLIT
+#define REG_SPLIT 4
+#endif
 
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1, uint32_t out[4]) {
@@ -214,26 +223,73 @@ __device__ void hypothesis(uint64_t seed, uint32_t img, uint32_t h, int n,
 __global__ __launch_bounds__(256) void reg_hyp_kernel(
     const int32_t* __restrict__ corr_ptr, const double* __restrict__ xy,
     const double* __restrict__ X, const double* __restrict__ intr_all,
-    const int32_t* __restrict__ img_id, uint64_t seed, double thr2,
-    unsigned long long* __restrict__ best) {
+    const int32_t* __restrict__ img_id, uint64_t seed, double thr2, int n_hyp,
+    unsigned long long* __restrict__ best, int32_t* __restrict__ cnt_g,
+    uint8_t* __restrict__ ok_g) {
     const int im = blockIdx.y;
     const int c0 = corr_ptr[im], n = corr_ptr[im + 1] - c0;
     if (n < 3) return;
-    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    const int sl = (int)blockIdx.x % REG_SPLIT;   // this lane's correspondence slice
+    const uint32_t h = (blockIdx.x / REG_SPLIT) * blockDim.x + threadIdx.x;
     const double* intr = intr_all + 4 * (size_t)im;
     const double* xyi = xy + 2 * (size_t)c0;
     const double* Xi = X + 3 * (size_t)c0;
     double Rs[4][9], ts[4][3];
     bool ok[4];
     hypothesis(seed, (uint32_t)img_id[im], h, n, xyi, Xi, intr, Rs, ts, ok);
+    // the poses of a hypothesis scored together, one pass over the slice: each correspondence is
+    // loaded once and the (up to) four independent division chains overlap (reg_hyp 21.6 ->
+    // 17.1 ms per cfg5 reconstruction before the slices).  Per-evaluation arithmetic as the spec.
+    const int m0 = (int)((long long)n * sl / REG_SPLIT), m1 = (int)((long long)n * (sl + 1) / REG_SPLIT);
+    int cnt[4] = {0, 0, 0, 0};
+    const bool any0 = __any(ok[0]), any1 = __any(ok[1]), any2 = __any(ok[2]), any3 = __any(ok[3]);
+    for (int m = m0; m < m1; ++m) {  // wave-uniform correspondence loads
+        const double x = xyi[2 * m], y = xyi[2 * m + 1];
+        const double* Xm = Xi + 3 * m;
+        if (any0) cnt[0] += (ok[0] && inlier(Rs[0], ts[0], intr, x, y, Xm, thr2)) ? 1 : 0;
+        if (any1) cnt[1] += (ok[1] && inlier(Rs[1], ts[1], intr, x, y, Xm, thr2)) ? 1 : 0;
+        if (any2) cnt[2] += (ok[2] && inlier(Rs[2], ts[2], intr, x, y, Xm, thr2)) ? 1 : 0;
+        if (any3) cnt[3] += (ok[3] && inlier(Rs[3], ts[3], intr, x, y, Xm, thr2)) ? 1 : 0;
+    }
+    if (REG_SPLIT > 1) {   // slice counts -> the hypothesis' totals (reg_key_kernel takes over)
+        int32_t* cg = cnt_g + ((size_t)im * n_hyp + h) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (ok[k] && cnt[k]) atomicAdd(cg + k, cnt[k]);
+        if (sl == 0)
+            ok_g[(size_t)im * n_hyp + h] = (uint8_t)(ok[0] | (ok[1] << 1) | (ok[2] << 2) | (ok[3] << 3));
+        return;
+    }
     unsigned long long key = 0ull;
     for (int k = 0; k < 4; ++k) {
         if (!ok[k]) continue;
-        int cnt = 0;
-        for (int m = 0; m < n; ++m)  // wave-uniform correspondence loads
-            cnt += inlier(Rs[k], ts[k], intr, xyi[2 * m], xyi[2 * m + 1], Xi + 3 * m, thr2) ? 1 : 0;
-        const unsigned long long kk =
-            ((unsigned long long)(cnt + 1) << 32) | (unsigned long long)(0xFFFFFFFFu - (4u * h + k));
+        const unsigned long long kk = ((unsigned long long)(cnt[k] + 1) << 32) |
+                                      (unsigned long long)(0xFFFFFFFFu - (4u * h + k));
+        key = key > kk ? key : kk;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(key, off, 64);
+        key = key > o ? key : o;
+    }
+    if ((threadIdx.x & 63) == 0 && key) atomicMax(best + im, key);
+}
+
+// REG_SPLIT > 1: the winner key per image from the summed slice counts (lane per hypothesis).
+__global__ __launch_bounds__(256) void reg_key_kernel(const int32_t* __restrict__ corr_ptr,
+                                                      int n_hyp, const int32_t* __restrict__ cnt_g,
+                                                      const uint8_t* __restrict__ ok_g,
+                                                      unsigned long long* __restrict__ best) {
+    const int im = blockIdx.y;
+    if (corr_ptr[im + 1] - corr_ptr[im] < 3) return;
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    const int okb = ok_g[(size_t)im * n_hyp + h];
+    const int32_t* cg = cnt_g + ((size_t)im * n_hyp + h) * 4;
+    unsigned long long key = 0ull;
+    for (int k = 0; k < 4; ++k) {
+        if (!((okb >> k) & 1)) continue;
+        const unsigned long long kk = ((unsigned long long)(cg[k] + 1) << 32) |
+                                      (unsigned long long)(0xFFFFFFFFu - (4u * h + k));
         key = key > kk ? key : kk;
     }
 #pragma unroll
@@ -449,14 +505,27 @@ extern "C" int sfm_register_batch(sfm_ctx* ctx, int32_t n_img, const int32_t* co
                 "sfm_register_batch: NULL array");
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    unsigned long long* best =
-        (unsigned long long*)sfm::workspace(ctx, sizeof(unsigned long long) * (size_t)n_img);
-    if (!best) return SFM_ERR_NOMEM;
-    SFM_HIP_CHECK(hipMemsetAsync(best, 0, sizeof(unsigned long long) * (size_t)n_img, st));
+    // workspace: best keys [n_img] u64, then (REG_SPLIT > 1) slice-count sums [n_img][n_hyp][4]
+    // i32 and pose flags [n_img][n_hyp] u8; keys and sums zeroed in one memset
+    const size_t bb = sfm::align_up(sizeof(unsigned long long) * (size_t)n_img, 256);
+    const size_t cb = REG_SPLIT > 1 ? sizeof(int32_t) * 4 * (size_t)n_img * prm->n_hyp : 0;
+    const size_t ob = REG_SPLIT > 1 ? (size_t)n_img * prm->n_hyp : 0;
+    char* ws = (char*)sfm::workspace(ctx, bb + cb + ob);
+    if (!ws) return SFM_ERR_NOMEM;
+    unsigned long long* best = (unsigned long long*)ws;
+    int32_t* cnt_g = (int32_t*)(ws + bb);
+    uint8_t* ok_g = (uint8_t*)(ws + bb + cb);
+    SFM_HIP_CHECK(hipMemsetAsync(ws, 0, bb + cb, st));
     const double thr2 = prm->thr * prm->thr;
-    hipLaunchKernelGGL(reg_hyp_kernel, dim3(prm->n_hyp / 256, n_img), dim3(256), 0, st, corr_ptr,
-                       xy, X, intr, img_id, (uint64_t)prm->seed, thr2, best);
+    hipLaunchKernelGGL(reg_hyp_kernel, dim3(prm->n_hyp / 256 * REG_SPLIT, n_img), dim3(256), 0, st,
+                       corr_ptr, xy, X, intr, img_id, (uint64_t)prm->seed, thr2, prm->n_hyp, best,
+                       cnt_g, ok_g);
     SFM_HIP_CHECK(hipGetLastError());
+    if (REG_SPLIT > 1) {
+        hipLaunchKernelGGL(reg_key_kernel, dim3(prm->n_hyp / 256, n_img), dim3(256), 0, st,
+                           corr_ptr, prm->n_hyp, cnt_g, ok_g, best);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
     hipLaunchKernelGGL(reg_final_kernel, dim3(n_img), dim3(256), 0, st, corr_ptr, xy, X, intr,
                        img_id, (uint64_t)prm->seed, thr2, prm->refine, best, out_cams, out_count,
                        out_key, out_mask);
