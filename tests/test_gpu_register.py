@@ -45,8 +45,10 @@ def _gpu(images, ids, n_hyp=512, thr=3.0, refine=True):
 
 def test_register_matches_oracle_bitwise():
     rng = np.random.default_rng(0)
-    images = [_image(rng, n) for n in (300, 50, 1000, 7)]
-    ids = np.array([3, 11, 5, 8], np.int32)
+    # sizes around the scoring kernel's correspondence slices (REG_SPLIT 4): 3 and 5 leave empty
+    # or one-correspondence slices, 1000 is many per slice
+    images = [_image(rng, n) for n in (300, 50, 1000, 7, 3, 5)]
+    ids = np.array([3, 11, 5, 8, 2, 9], np.int32)
     cams, cnt, key, mask, ptr = _gpu(images, ids)
     for i, im in enumerate(images):
         o = O.reg_ransac(im["xy"], im["X"], im["intr"], img=int(ids[i]), n_hyp=512, seed=42,
