@@ -558,6 +558,10 @@ def pairs_main(args, world, rank, local, dist_info):
         torch.cuda.empty_cache()
         if args.config != "cfg3" and not args.no_cfg3:
             result["cfg3"] = cfg3_side(args.n_hyp, args.chunk)
+            try:   # a side leg: its failure is recorded, the line stands
+                result["cfg2"] = cfg2_side()
+            except Exception as e:  # noqa: BLE001
+                result["cfg2"] = {"error": f"{type(e).__name__}: {e}"}
         if args.config == "cfg4" and not args.no_local:
             torch.cuda.empty_cache()
             try:   # a side leg: its failure is recorded, the cfg4 line stands
@@ -1079,6 +1083,42 @@ def cfg3_side(n_hyp, chunk):
                             "frac_of_practical": tops / PRACTICAL_I8_TOPS,
                             "frac": tops / PEAK_I8_TOPS,
                             "traffic": pmc_traffic("mfma_mutual_kernel", "cfg3", 50, 2048, 1)}}
+
+
+def cfg2_side(reps=20):
+    """BASELINE configs[1] (cfg2): the 1225 pairs of cfg3's scene, L2 match with the fused ratio
+    test (4/5) and no cross check — the dispatcher's ratio path (forward MFMA scan + exact
+    recovery) — per call on this GPU (HIP events on the launch stream, `reps` calls after one)."""
+    import numpy as np
+    import torch
+    import sfmcore
+    import synth
+    s = synth.make_scene(50, 2048, seed=0)
+    pairs = synth.unordered_pairs(50)
+    ctx = sfmcore.context(torch.cuda.current_device())
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)
+    ops = 2.0 * 128 * float(sum(int(s["n_kp"][a]) * int(s["n_kp"][b]) for a, b in pairs))
+    out = ctx.match_batch(desc, n_kp, pr, cross_check=0, ratio=(4, 5))
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        out = ctx.match_batch(desc, n_kp, pr, cross_check=0, ratio=(4, 5), out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    tops = ops / (ms * 1e-3) / 1e12
+    return {"workload": "cfg2: all 1225 unordered pairs of 50 synthetic images x 2048 128-D u8 "
+                        "descriptors; L2 match with the fused ratio test 4/5, no cross check "
+                        "(ratio path: forward MFMA scan + exact recovery)",
+            "ms_per_call": ms, "matches": int(out[0].sum().item()),
+            "k1_roofline": {"achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOP/s (i8)",
+                            "frac": tops / PEAK_I8_TOPS,
+                            "frac_of_practical": tops / PRACTICAL_I8_TOPS,
+                            "mfma_busy_pmc": 0.52,
+                            "mfma_busy_note": "scan kernel, PMC SQ_VALU_MFMA_BUSY_CYCLES over "
+                                              "the SIMD cycles, profiles/r05/k1_cfg2/"}}
 
 
 if __name__ == "__main__":
