@@ -191,6 +191,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 side measurement")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 side measurement")
+    ap.add_argument("--cfg5-n-img", type=int, default=0,
+                    help="cfg4 line's cfg5 leg: override its image count (tests; default 500)")
+    ap.add_argument("--cfg5-k", type=int, default=0,
+                    help="cfg4 line's cfg5 leg: override its keypoints/image (tests; default 4096)")
     ap.add_argument("--no-fp64", action="store_true", help="skip the fp64-K2 side measurement")
     ap.add_argument("--no-local", action="store_true",
                     help="skip the cfg4_local side measurement (local-visibility scene)")
@@ -568,13 +572,21 @@ def pairs_main(args, world, rank, local, dist_info):
                 result["cfg4_local"] = cfg4_local_side(n_img, k, args.n_hyp, args.chunk)
             except Exception as e:  # noqa: BLE001
                 result["cfg4_local"] = {"error": f"{type(e).__name__}: {e}"}
-        if args.config == "cfg4" and not args.no_cfg5:
-            torch.cuda.empty_cache()
-            try:   # a side leg: its failure is recorded, the cfg4 line stands
-                result["cfg5"] = cfg5_run(CONFIGS["cfg5"]["n_img"], CONFIGS["cfg5"]["k"],
-                                          None, 2, 1, 1, 0, local, "auto")
-            except Exception as e:  # noqa: BLE001
-                result["cfg5"] = {"error": f"{type(e).__name__}: {e}"}
+    if args.config == "cfg4" and not args.no_cfg5:
+        # BASELINE configs[4] beside the cfg4 line: at N = 1 on rank 0, at N > 1 on every rank
+        # (pair-sharded matching + graph all-gather, point-sharded BA over the group's all-reduce
+        # with the PCG branch chosen by reconstruction.pcg_rule on probed latency / bandwidth)
+        if world > 1:
+            del run, graph
+        torch.cuda.empty_cache()
+        try:   # a side leg: its failure is recorded, the cfg4 line stands
+            r5 = cfg5_run(args.cfg5_n_img or CONFIGS["cfg5"]["n_img"],
+                          args.cfg5_k or CONFIGS["cfg5"]["k"], None,
+                          2 if world == 1 else 1, 1, world, rank, local, "auto")
+        except Exception as e:  # noqa: BLE001
+            r5 = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            result["cfg5"] = r5
     return result
 
 
@@ -712,6 +724,15 @@ def cfg5_run(n_img, k, n_pts, steps, warmup, world, rank, local, pcg):
         "pcg_branches": sorted({b["pcg"] for b in rec.ba_log}),
         "shard_ba": world > 1, "n_gpus": world,
     }
+    rules = [dict(b["rule"], n_cam=b["n_cam"]) for b in rec.ba_log if isinstance(b.get("rule"), dict)
+             and "allreduce_us" in b["rule"]]
+    if rules:   # pcg_rule's probed all-reduce latency / bus bandwidth and its verdicts
+        out["pcg_rule"] = {"probes": len(rules), "allreduce_us_first": rules[0]["allreduce_us"],
+                           "busbw_GBs_first": rules[0]["busbw_GBs"],
+                           "allreduce_us_last": rules[-1]["allreduce_us"],
+                           "busbw_GBs_last": rules[-1]["busbw_GBs"],
+                           "branch_counts": {m: sum(b["pcg"] == m for b in rec.ba_log)
+                                             for m in ("sharded", "replicated")}}
     if rank == 0:
         out["ba_rooflines"] = ba_rooflines(scene["pp"], rec.cams, rec.points[pts_ids],
                                            timg[use].astype(np.int32), pt_idx, uv, local)

@@ -8,6 +8,11 @@ namespace sfm {
 void set_error(const std::string& msg) { g_err = msg; }
 
 void* workspace(sfm_ctx* ctx, size_t bytes) {
+    // every workspace user may overwrite (or, growing, free) the counted RANSAC batch's wave
+    // words: sfm_ransac_wave_stops then fails cleanly instead of reading stale or freed memory
+    // (the RANSAC call re-arms it after its own workspace request)
+    ctx->rs_last_w = nullptr;
+    ctx->rs_last_pairs = ctx->rs_last_hyp = 0;
     if (bytes <= ctx->ws_bytes) return ctx->ws;
     // growing frees and reallocates (a device-wide synchronisation): illegal inside a HIP-graph
     // capture of the context's stream — the caller runs the call once uncaptured to size it

@@ -51,13 +51,17 @@ constexpr int SCAN_THREADS = 64 * WAVES;
 constexpr int QT = L2FR_QT;                  // query tiles (32 queries) per wave: 4, or 2
 constexpr int QB = WAVES * QT * 32;          // queries per workgroup (1024 resp. 512)
 constexpr int SCAN_MIN_WAVES = 8 / QT;       // waves per SIMD the scan kernel is built for (2 or 4)
-constexpr int CHUNK = 256;                   // train rows per LDS stage
+#ifndef L2FR_CHUNK
+#define L2FR_CHUNK 256
+#endif
+constexpr int CHUNK = L2FR_CHUNK;            // train rows per LDS stage of the scan (256 or 512)
+constexpr int GROUP = 256;                   // train rows per recovery group (8 tiles)
 constexpr int NT = CHUNK / 32;               // tiles per stage
-constexpr int NK = D / 32;                   // MFMA k-steps per tile
+constexpr int NK = D / 32;                   // MFMA k-steps per tile (32x32x32 form)
 constexpr int SLOTS = D / 16;                // 16-B slots per row
 constexpr int PIECES = CHUNK * D / 1024 / WAVES;
 constexpr int RPP = 1024 / D;                // rows per 1 KB DMA piece
-constexpr int KALIGN = 256;
+constexpr int KALIGN = CHUNK > GROUP ? CHUNK : GROUP;
 constexpr int KMAX = 4096;
 constexpr int PAD_INIT = -(1 << 30);         // accumulator init of a padded train row
 constexpr int E_VALID = -(1 << 23);          // e of a real element is > -2^22
@@ -134,10 +138,15 @@ __global__ void l2fr_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
 
 // Pair orders by streamed image, counting sort in LDS: block 0 orders by pairs[p][1] (forward
 // scan) into order_f, block 1 by pairs[p][0] (reverse scan) into order_r.
+// Block 0 also cuts order_f into recovery ranges: runs of at most REC_R consecutive entries with
+// the same train image, rng[r] = (first entry, length), *n_rng of them.
+constexpr int REC_R = 4;  // pairs (sharing their train image) per recovery block
 __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restrict__ pairs,
                                                           int n_pairs, int n_img,
                                                           int32_t* __restrict__ order_f,
-                                                          int32_t* __restrict__ order_r) {
+                                                          int32_t* __restrict__ order_r,
+                                                          int2* __restrict__ rng,
+                                                          int32_t* __restrict__ n_rng) {
     extern __shared__ int hist[];
     const int tid = threadIdx.x, col = blockIdx.x == 0 ? 1 : 0;
     int32_t* order = blockIdx.x == 0 ? order_f : order_r;
@@ -145,10 +154,25 @@ __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restr
     __syncthreads();
     for (int p = tid; p < n_pairs; p += 1024) atomicAdd(&hist[pairs[2 * p + col]], 1);
     __syncthreads();
+    int* roff = hist + n_img;  // block 0: first recovery range of each train image
     if (tid == 0) {
-        int off = 0;
-        for (int i = 0; i < n_img; ++i) { const int c = hist[i]; hist[i] = off; off += c; }
+        int off = 0, nr = 0;
+        for (int i = 0; i < n_img; ++i) {
+            const int c = hist[i];
+            roff[i] = nr;
+            nr += (c + REC_R - 1) / REC_R;
+            hist[i] = off;
+            off += c;
+        }
+        if (blockIdx.x == 0) *n_rng = nr;
     }
+    __syncthreads();
+    if (blockIdx.x == 0)
+        for (int i = tid; i < n_img; i += 1024) {
+            const int c = (i + 1 < n_img ? hist[i + 1] : n_pairs) - hist[i];
+            for (int k = 0; k < c; k += REC_R)
+                rng[roff[i] + k / REC_R] = make_int2(hist[i] + k, min(REC_R, c - k));
+        }
     __syncthreads();
     for (int p = tid; p < n_pairs; p += 1024) order[atomicAdd(&hist[pairs[2 * p + col]], 1)] = p;
 }
@@ -170,8 +194,21 @@ struct FwdCls {
     int rnum, rden;          // ratio num/den
     long long max_dist;
     int4* qst;               // [P][k_pad] DROP / SLOW statuses
-    uint8_t* cls;            // [P][k_pad] tile group (e1 tile / 8) of a candidate, 0xFF otherwise
+    uint8_t* cls;            // [P][k_pad] e1 tile of a candidate (< 128), 0xFF otherwise
 };
+
+#ifdef L2FR_CLOCK
+// Diagnostic build only (-DL2FR_CLOCK): per forward-scan block, wave 0 stamps (realtime entry,
+// realtime after the prologue barrier, memtime there, realtime at the end of each chunk (16),
+// memtime and realtime at the loop end, realtime at exit, HW_ID, XCC_ID).
+constexpr int L2FR_CLOCK_SLOTS = 1 << 16;
+constexpr int L2FR_CLOCK_W = 24;
+__device__ unsigned long long g_l2fr_clock[L2FR_CLOCK_W * L2FR_CLOCK_SLOTS];
+#define L2FR_STAMP(i, v) \
+    if (!REV && tid == 0 && blockIdx.x < L2FR_CLOCK_SLOTS) g_l2fr_clock[L2FR_CLOCK_W * (size_t)blockIdx.x + (i)] = (v)
+#else
+#define L2FR_STAMP(i, v)
+#endif
 
 // The MFMA scan.  Forward (REV = false): queries = image pairs[p][0] rows 0..n-1, streamed trains =
 // image pairs[p][1].  Reverse (REV = true): queries = the survivor list's j1 rows of image
@@ -208,6 +245,7 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
     const int nb = n_kp[ti];
     if (qb * QB >= nq || nb <= 0) return;  // block-uniform
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+    L2FR_STAMP(0, __builtin_amdgcn_s_memrealtime());
 
     const uint8_t* db = desc + (size_t)ti * k_max * D;
     const int32_t* cib = cinit + (size_t)ti * k_pad;
@@ -223,17 +261,115 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
             const uint8_t* src = (j < nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
             __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
         }
-        if (wave == 0 && lane < CHUNK / 4) {
-            const int32_t* src = cib + ch * CHUNK + lane * 4;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D), 16, 0, 0);
+        if (tid < CHUNK / 4) {  // the chunk's accumulator init: whole waves 0 (.. 1)
+            const int32_t* src = cib + ch * CHUNK + tid * 4;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D + wave * 1024),
+                                             16, 0, 0);
         }
     };
 
     const int qbase = qb * QB + wave * QT * 32;
     const bool active = qbase < nq;  // wave-uniform
+    const uint8_t* da = desc + (size_t)qi * k_max * D;
+
+    // One query's record (e1, e2, tile of e1) -> out, and the forward scan's ratio classification.
+    auto emit = [&](int e, int e1, int e2, int t) {
+        const int4 rec = make_int4(e1, e2, t, 0);
+        out[(size_t)p * k_pad + e] = rec;
+        if (!REV) {  // ratio bounds: drop / slow now, candidates go to the recovery
+            const unsigned char st =
+                classify(rec, fc.norm[(size_t)qi * k_pad + e], fc.rnum, fc.rden, fc.max_dist);
+            fc.cls[(size_t)p * k_pad + e] = st == ST_CAND ? (uint8_t)t : (uint8_t)0xFF;
+            if (st != ST_CAND) fc.qst[(size_t)p * k_pad + e] = make_int4(st, 0, 0, 0);
+        }
+    };
+
+#if L2FR_MFMA16
+    // v_mfma_i32_16x16x64_i8 form: the wave's 4*32 queries as 8 subtiles of 16 (B fragments: lane
+    // l holds query row l%16, bytes 32*(l/16) + 16*s of k-step s), a 32-train tile as 2 subtiles of
+    // 16 (A fragments, same byte map).  Accumulator register r of lane l is train row
+    // 16*u + 4*(l/16) + r of the tile, query l%16 of the subtile; lanes l, l^16, l^32, l^48 share a
+    // query.  Same matrix cycles per tile (32 MFMAs of 16 instead of 16 of 32).
+    constexpr int QS = 2 * QT;
+    const int g4 = lane >> 4, r16 = lane & 15;
+    v4i bq[QS][2];
+    int tb[QS], ts[QS], t1[QS];
+#pragma unroll
+    for (int c = 0; c < QS; ++c) {
+        const int e = qbase + c * 16 + r16;
+        int row = -1;
+        if (e < nq) row = REV ? qlist[(size_t)p * k_pad + e].y : e;
+        const v4i* src = (const v4i*)((row >= 0) ? da + (size_t)row * D + 32 * g4 : zero_row + 32 * g4);
+        bq[c][0] = src[0];
+        bq[c][1] = src[1];
+        tb[c] = INT_MIN; ts[c] = INT_MIN; t1[c] = 0;
+    }
+    v4i acc[QS][2];
+    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
+#ifndef L2FR_ABL_NOSTAGE
+        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
+#endif
+        const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
+        if (active) {
+            const int* Ci = (const int*)(cur + CHUNK * D);
+            auto load_tile = [&](int tt, v4i (&af)[2][2], v4i (&init)[2]) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int row = tt * 32 + 16 * u + r16;
+                    const int sw = swz(row);
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+#ifdef L2FR_ABL_NOLDS
+                        af[u][s] = bq[(tt + u + s) & (QS - 1)][s];
+#else
+                        af[u][s] = *(const v4i*)(cur + row * D + (((2 * g4 + s) ^ sw) << 4));
+#endif
+#ifdef L2FR_ABL_NOLDS
+                    init[u] = v4i{tt, u, tt, u};
+#else
+                    init[u] = *(const v4i*)(Ci + tt * 32 + 16 * u + 4 * g4);
+#endif
+                }
+            };
+            v4i af[2][2], init[2];
+            load_tile(0, af, init);
+            for (int tt = 0; tt < nt; ++tt) {
+                const int gt = ch * NT + tt;
+#ifndef L2FR_NO_MPRIO  // the MFMA block at raised priority (its issue wins over the partner's VALU)
+                __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int c = 0; c < QS; ++c)
+                            acc[c][u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                af[u][s], bq[c][s], s == 0 ? init[u] : acc[c][u], 0, 0, 0);
+#ifndef L2FR_NO_MPRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
+                if (tt + 1 < nt) load_tile(tt + 1, af, init);
+#pragma unroll
+                for (int c = 0; c < QS; ++c) {
+                    const int o = tb[c];
+#ifdef L2FR_ABL_NOEPI
+                    tb[c] = max(tb[c], acc[c][0][0] ^ acc[c][1][3]);
+#else
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        top2_insert(tb[c], ts[c], acc[c][u][0], acc[c][u][1]);
+                        top2_insert(tb[c], ts[c], acc[c][u][2], acc[c][u][3]);
+                    }
+#endif
+                    t1[c] = (tb[c] != o) ? gt : t1[c];
+                }
+            }
+        }
+    };
+#else
     v4i bq[QT][NK];
     int tb[QT], ts[QT], t1[QT];
-    const uint8_t* da = desc + (size_t)qi * k_max * D;
 #pragma unroll
     for (int c = 0; c < QT; ++c) {
         const int e = qbase + c * 32 + r32;
@@ -262,7 +398,9 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
     };
 
     auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
+#ifndef L2FR_ABL_NOSTAGE
         if (ch + 1 < n_chunk) stage(ch + 1, nxt);
+#endif
         const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
         if (active) {
             const int* Ci = (const int*)(cur + CHUNK * D);
@@ -273,10 +411,18 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
                 const int sw = swz(row);
 #pragma unroll
                 for (int s = 0; s < NK; ++s)
+#ifdef L2FR_ABL_NOLDS
+                    af[s] = bq[(tt + s) & (QT - 1)][s];
+#else
                     af[s] = *(const v4i*)(cur + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
+#endif
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
+#ifdef L2FR_ABL_NOLDS
+                    const v4i cv = v4i{tt, g, tt, g};
+#else
                     const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
+#endif
                     init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
                     init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
                 }
@@ -286,27 +432,63 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
             load_tile(0, af, init);
             for (int tt = 0; tt < nt; ++tt) {
                 const int gt = ch * NT + tt;
-#pragma unroll
-                for (int c = 0; c < QT; ++c) acc[c] = init;
+#ifndef L2FR_NO_MPRIO
+                __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
                 for (int s = 0; s < NK; ++s)
 #pragma unroll
                     for (int c = 0; c < QT; ++c)
-                        acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc[c], 0, 0, 0);
+                        acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s],
+                                                                        s == 0 ? init : acc[c], 0, 0, 0);
+#ifndef L2FR_NO_MPRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
                 if (tt + 1 < nt) load_tile(tt + 1, af, init);
                 epi_all(gt);
             }
         }
     };
+#endif
+
     if (n_chunk > 0) stage(0, lds0);
     __syncthreads();
+    L2FR_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    L2FR_STAMP(2, __builtin_amdgcn_s_memtime());
+#ifdef L2FR_PRIO  // static priority for the second-dispatched half (MI355X_MICROARCH.md, item 4)
+    if (wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef L2FR_ABL_NOSTAGE  // ablation: every chunk reads chunk 0's stage, no barriers in the loop
+    for (int ch = 0; ch < n_chunk; ++ch) process(ch, lds0, lds1);
+#else
     for (int ch = 0; ch < n_chunk; ch += 2) {
         process(ch, lds0, lds1);
         __syncthreads();
+        if (ch < 16) L2FR_STAMP(3 + ch, __builtin_amdgcn_s_memrealtime());
         if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
         __syncthreads();
+        if (ch + 1 < 16) L2FR_STAMP(4 + ch, __builtin_amdgcn_s_memrealtime());
     }
+#endif
+    L2FR_STAMP(19, __builtin_amdgcn_s_memtime());
+    L2FR_STAMP(20, __builtin_amdgcn_s_memrealtime());
     if (active) {
+#if L2FR_MFMA16
+#pragma unroll
+        for (int c = 0; c < QS; ++c) {
+            // lanes l, l^16, l^32, l^48 hold four row groups of every tile of the same query
+            int e1 = tb[c], e2 = ts[c], t = t1[c];
+#pragma unroll
+            for (int m = 16; m <= 32; m <<= 1) {
+                const int P1 = __shfl_xor(e1, m), P2 = __shfl_xor(e2, m), PT = __shfl_xor(t, m);
+                e2 = max(min(e1, P1), max(e2, P2));
+                t = e1 > P1 ? t : (P1 > e1 ? PT : min(t, PT));
+                e1 = max(e1, P1);
+            }
+            const int e = qbase + c * 16 + r16;
+            if (g4 == 0 && e < nq) emit(e, e1, e2, t);
+        }
+#else
 #pragma unroll
         for (int c = 0; c < QT; ++c) {
             // lanes l and l^32 hold the two 16-row halves of every tile of the same query
@@ -316,18 +498,15 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
             const int e2 = max(min(tb[c], P1), max(ts[c], P2));
             const int t = tb[c] > P1 ? t1[c] : (P1 > tb[c] ? PT : min(t1[c], PT));
             const int e = qbase + c * 32 + r32;
-            if (h == 0 && e < nq) {
-                const int4 rec = make_int4(e1, e2, t, 0);
-                out[(size_t)p * k_pad + e] = rec;
-                if (!REV) {  // ratio bounds: drop / slow now, candidates go to the recovery
-                    const unsigned char st =
-                        classify(rec, fc.norm[(size_t)qi * k_pad + e], fc.rnum, fc.rden, fc.max_dist);
-                    fc.cls[(size_t)p * k_pad + e] = st == ST_CAND ? (uint8_t)(t >> 3) : (uint8_t)0xFF;
-                    if (st != ST_CAND) fc.qst[(size_t)p * k_pad + e] = make_int4(st, 0, 0, 0);
-                }
-            }
+            if (h == 0 && e < nq) emit(e, e1, e2, t);
         }
+#endif
     }
+#ifdef L2FR_CLOCK
+    L2FR_STAMP(21, __builtin_amdgcn_s_memrealtime());
+    L2FR_STAMP(22, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));   // HW_ID
+    L2FR_STAMP(23, (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20));  // XCC_ID
+#endif
 }
 
 // Exact (d1, j1, d2) of one query over all trains (multiset second, lowest-index j1), block-wide.
@@ -397,8 +576,8 @@ __global__ __launch_bounds__(256) void l2fr_recover_kernel(
     const int32_t* __restrict__ pairs, const int4* __restrict__ fwd,
     const uint8_t* __restrict__ cls, int rnum, int rden, long long max_dist,
     int4* __restrict__ qst) {
-    __shared__ uint4 tiles[CHUNK * SLOTS];   // 256 train rows, slot s of row r at s ^ (r & 7)
-    __shared__ int tci[CHUNK], tnb[CHUNK];   // their accumulator init and |y'|^2
+    __shared__ uint4 tiles[GROUP * SLOTS];   // 256 train rows, slot s of row r at s ^ (r & 7)
+    __shared__ int tci[GROUP], tnb[GROUP];   // their accumulator init and |y'|^2
     __shared__ uint4 qrows[64 * SLOTS];      // a batch of 64 candidate query rows
     __shared__ int4 crec[64];
     __shared__ int cq[64], cA[64];
@@ -438,7 +617,7 @@ __global__ __launch_bounds__(256) void l2fr_recover_kernel(
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int q = tid * 16 + k;
-        if (q < na && ((cw[k >> 2] >> (8 * (k & 3))) & 0xFF) == (unsigned)grp)
+        if (q < na && ((cw[k >> 2] >> (8 * (k & 3))) & 0xFF) >> 3 == (unsigned)grp)
             clist[atomicAdd(&ccount, 1)] = (short)q;
     }
     __syncthreads();
@@ -491,6 +670,229 @@ __global__ __launch_bounds__(256) void l2fr_recover_kernel(
             }
         }
         __syncthreads();
+    }
+}
+
+// Per recovery range, its pairs: rinfo[r][e] = (p, a, b, n_kp[a] | n_kp[b] << 16), p = -1 past
+// the range's length (one thread per range).
+__global__ void l2fr_range_kernel(const int32_t* __restrict__ pairs, const int32_t* __restrict__ n_kp,
+                                  const int32_t* __restrict__ order_f, const int2* __restrict__ rng,
+                                  const int32_t* __restrict__ n_rng, int4* __restrict__ rinfo) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= *n_rng) return;
+    const int2 g = rng[r];
+#pragma unroll
+    for (int e = 0; e < REC_R; ++e) {
+        int4 v = make_int4(-1, 0, 0, 0);
+        if (e < g.y) {
+            const int p = order_f[g.x + e], a = pairs[2 * p], b = pairs[2 * p + 1];
+            v = make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
+        }
+        rinfo[(size_t)r * REC_R + e] = v;
+    }
+}
+
+// Recovery, MFMA form: one block of 256 (4 waves) per (range of up to REC_R pairs that share
+// their train image b, group of 8 train tiles of b).  A gather: ~1.2 M candidates at cfg2, each
+// needing its query row and one 32-train tile, so the kernel is built for few dependent round
+// trips (3), one load of b's train rows per REC_R pairs, no LDS atomics and no LDS staging of
+// query rows:
+//   1. the range's pairs (rinfo); then one round of independent loads: the pairs' candidate
+//      classes (cls, written by the forward scan: the e1 tile of a candidate), wave w's train
+//      tiles 2w, 2w+1 of the group as A fragments, the group's accumulator inits
+//      -ceil(|y'|^2/2) and norm parities (LDS);
+//   2. the group's candidates of all the pairs, sorted by tile (a block prefix sum of packed
+//      per-thread tile counts): wave w's are those of its two tiles;
+//   3. per wave, one round of loads for up to 4 sub-batches of 32 of its candidates: query rows
+//      straight into B fragments, forward records and |x'|^2; per sub-batch e = x'.y' -
+//      ceil(|y'|^2/2) for the 2 tiles x 32 candidates (8 MFMAs: ~1 % of the scan's matrix work).
+// A candidate's nearest neighbour j1 is the unique train of its e1 tile with e == e1 (e1 > e2 for
+// every candidate); the lane finds the row by compares, d1 = |x'|^2 - 2 e1 - (|y'_j1|^2 mod 2)
+// exactly, and the ratio test is decided exactly where d2's unit ambiguity allows:
+// qst[p][q] = (status, j1, d1).
+constexpr int REC_SB = 4;  // sub-batches of 32 candidates per wave and load round
+__global__ __launch_bounds__(256, 2) void l2fr_recover_mfma_kernel(
+    const uint8_t* __restrict__ desc, int k_max, int k_pad, const int32_t* __restrict__ norm,
+    const int32_t* __restrict__ cinit, const int4* __restrict__ rinfo,
+    const int32_t* __restrict__ n_rng, const int4* __restrict__ fwd,
+    const uint8_t* __restrict__ cls, int rnum, int rden, long long max_dist,
+    int4* __restrict__ qst) {
+    __shared__ unsigned short clist[REC_R * KMAX];  // (pair in range) << 12 | query, by tile
+    __shared__ __attribute__((aligned(16))) int gini[GROUP];
+    __shared__ unsigned char gpar[GROUP];
+    __shared__ unsigned long long wlo[4], whi[4];
+    __shared__ int toff[9];
+    const int ri = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
+    if (ri >= *n_rng) return;  // block-uniform
+    const int wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+    int4 pi[REC_R];
+#pragma unroll
+    for (int e = 0; e < REC_R; ++e) pi[e] = rinfo[(size_t)ri * REC_R + e];
+    const int b = pi[0].z, nb = pi[0].w >> 16;
+    const int ntiles = (nb + 31) >> 5, tg = grp * 8;
+    if (nb <= 0 || tg >= ntiles) return;  // block-uniform
+    const uint8_t* db = desc + (size_t)b * k_max * D;
+
+    // 1. independent loads
+    uint4 cv[REC_R];
+#pragma unroll
+    for (int e = 0; e < REC_R; ++e) {
+        cv[e] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (pi[e].x >= 0 && tid * 16 < (pi[e].w & 0xFFFF))
+            cv[e] = ((const uint4*)(cls + (size_t)pi[e].x * k_pad))[tid];
+    }
+    v4i af[2][NK];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int row = (tg + 2 * wave + u) * 32 + r32;
+#pragma unroll
+        for (int s = 0; s < NK; ++s)
+            af[u][s] = row < nb ? *(const v4i*)(db + (size_t)row * D + 64 * h + 16 * s) : v4i{0, 0, 0, 0};
+    }
+    {
+        const size_t o = (size_t)b * k_pad + tg * 32 + tid;  // < k_pad: k_pad is a multiple of 256
+        gini[tid] = cinit[o];
+        gpar[tid] = (unsigned char)(norm[o] & 1);
+    }
+    // 2. the group's candidates by tile, in (pair, query) order within a tile: per-thread tile
+    //    counts packed as 16-bit fields (tiles 0-3 in lo, 4-7 in hi), one block prefix sum
+    unsigned long long lo = 0, hi = 0;
+#pragma unroll
+    for (int e = 0; e < REC_R; ++e) {
+        const int na = pi[e].x >= 0 ? (pi[e].w & 0xFFFF) : 0;
+        const unsigned cw[4] = {cv[e].x, cv[e].y, cv[e].z, cv[e].w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const unsigned c = (cw[k >> 2] >> (8 * (k & 3))) & 0xFF;
+            if (tid * 16 + k < na && c >> 3 == (unsigned)grp) {
+                const unsigned long long one = 1ull << (16 * (c & 3));
+                if (c & 4) hi += one; else lo += one;
+            }
+        }
+    }
+    unsigned long long plo = lo, phi = hi;  // inclusive wave prefix
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long vl = __shfl_up(plo, d), vh = __shfl_up(phi, d);
+        if (lane >= d) { plo += vl; phi += vh; }
+    }
+    if (lane == 63) { wlo[wave] = plo; whi[wave] = phi; }
+    __syncthreads();
+    unsigned long long blo = 0, bhi = 0, tlo = 0, thi = 0;  // before this wave; block totals
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        blo += w < wave ? wlo[w] : 0ull;
+        bhi += w < wave ? whi[w] : 0ull;
+        tlo += wlo[w];
+        thi += whi[w];
+    }
+    int pos[8];  // this thread's first slot per tile
+    {
+        int o = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const unsigned long long tot = t < 4 ? tlo : thi, bef = t < 4 ? blo : bhi,
+                                     mine = t < 4 ? plo - lo : phi - hi;
+            const int sh = 16 * (t & 3);
+            pos[t] = o + (int)((bef >> sh) & 0xFFFF) + (int)((mine >> sh) & 0xFFFF);
+            if (tid == 0) toff[t] = o;
+            o += (int)((tot >> sh) & 0xFFFF);
+        }
+        if (tid == 0) toff[8] = o;
+    }
+#pragma unroll
+    for (int e = 0; e < REC_R; ++e) {
+        const int na = pi[e].x >= 0 ? (pi[e].w & 0xFFFF) : 0;
+        const unsigned cw[4] = {cv[e].x, cv[e].y, cv[e].z, cv[e].w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const unsigned c = (cw[k >> 2] >> (8 * (k & 3))) & 0xFF;
+            if (tid * 16 + k < na && c >> 3 == (unsigned)grp) {
+                int slot = pos[0];
+#pragma unroll
+                for (int t = 1; t < 8; ++t) slot = (c & 7) == (unsigned)t ? pos[t] : slot;
+                clist[slot] = (unsigned short)((e << 12) | (tid * 16 + k));
+#pragma unroll
+                for (int t = 0; t < 8; ++t) pos[t] += (c & 7) == (unsigned)t;
+            }
+        }
+    }
+    __syncthreads();
+    // 3. this wave's candidates: those of tiles 2w, 2w+1
+    const int w0 = toff[2 * wave], w1 = toff[2 * wave + 2];
+    const int t0 = tg + 2 * wave;
+    for (int c0 = w0; c0 < w1; c0 += 32 * REC_SB) {
+        v4i bf[REC_SB][NK];
+        int4 rc[REC_SB];
+        int qq[REC_SB], pp[REC_SB], AA[REC_SB];
+#pragma unroll
+        for (int k = 0; k < REC_SB; ++k) {
+            const int c = c0 + 32 * k + r32;
+            qq[k] = -1;
+            if (c < w1) {
+                const int en = clist[c], e = en >> 12, q = en & 0xFFF;
+                int p = pi[0].x, a = pi[0].y;
+#pragma unroll
+                for (int f = 1; f < REC_R; ++f) {
+                    p = e == f ? pi[f].x : p;
+                    a = e == f ? pi[f].y : a;
+                }
+                const uint8_t* xr = desc + ((size_t)a * k_max + q) * D + 64 * h;
+#pragma unroll
+                for (int s = 0; s < NK; ++s) bf[k][s] = *(const v4i*)(xr + 16 * s);
+                rc[k] = fwd[(size_t)p * k_pad + q];
+                AA[k] = norm[(size_t)a * k_pad + q];
+                qq[k] = q;
+                pp[k] = p;
+            } else {
+#pragma unroll
+                for (int s = 0; s < NK; ++s) bf[k][s] = v4i{0, 0, 0, 0};
+                rc[k] = make_int4(0, 0, -1, 0);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < REC_SB; ++k) {
+            if (c0 + 32 * k >= w1) break;  // wave-uniform
+            const int4 r = rc[k];
+            const int mine = r.z - t0;  // 0 / 1: the candidate's tile (always one of the wave's)
+            int hit = -1;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                v16i acc;
+                const int* gi = gini + (2 * wave + u) * 32 + 4 * h;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const v4i c4 = *(const v4i*)(gi + 8 * g);
+                    acc[4 * g + 0] = c4.x; acc[4 * g + 1] = c4.y;
+                    acc[4 * g + 2] = c4.z; acc[4 * g + 3] = c4.w;
+                }
+#pragma unroll
+                for (int s = 0; s < NK; ++s)
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[u][s], bf[k][s], acc, 0, 0, 0);
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr)
+                    hit = (mine == u && acc[rr] == r.x) ? 8 * (rr >> 2) + 4 * h + (rr & 3) : hit;
+            }
+            hit = max(hit, __shfl_xor(hit, 32));
+            if (h == 0 && qq[k] >= 0) {
+                int4* qs = qst + (size_t)pp[k] * k_pad;
+                if (hit < 0) {
+                    qs[qq[k]] = make_int4(ST_SLOW, 0, 0, 0);  // defensive
+                } else {
+                    const int jg = (2 * wave + mine) * 32 + hit;  // row in the group
+                    const long long A = AA[k];
+                    const long long d1 = A - 2LL * r.x - gpar[jg];
+                    const long long d2lo = r.y > E_VALID ? A - 2LL * r.y - 1 : sfm::DIST_INF;
+                    const long long d2hi = r.y > E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
+                    int st;
+                    if (max_dist >= 0 && !(d1 < max_dist)) st = ST_DROP;
+                    else if (sfm::ratio_ok(d1, d2lo, rnum, rden, true)) st = ST_PASS;
+                    else if (!sfm::ratio_ok(d1, d2hi, rnum, rden, true)) st = ST_DROP;
+                    else st = ST_SLOW;
+                    qs[qq[k]] = make_int4(st, tg * 32 + jg, (int)d1, 0);
+                }
+            }
+        }
     }
 }
 
@@ -660,8 +1062,12 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     const size_t cntb = sfm::align_up(sizeof(int32_t) * (size_t)n_pairs, 256);
     const size_t descb = sfm::align_up((size_t)n_img * k_max * D, 256);
     const size_t ordb = sfm::align_up(sizeof(int32_t) * (size_t)n_pairs, 256);
-    const size_t clsb = (size_t)n_pairs * k_pad;
-    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + 3 * recb + cntb + descb + 2 * ordb + clsb);
+    const size_t clsb = sfm::align_up((size_t)n_pairs * k_pad, 256);
+    const int n_rng_max = n_pairs / REC_R + n_img + 1;  // recovery ranges (runs per train image)
+    const size_t rngb = sfm::align_up(sizeof(int2) * (size_t)n_rng_max, 256);
+    const size_t rinfob = sizeof(int4) * (size_t)n_rng_max * REC_R;
+    char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + 3 * recb + cntb + descb + 2 * ordb + clsb +
+                                              256 + rngb + rinfob);
     if (!ws) return SFM_ERR_NOMEM;
     char* w = ws;
     uint8_t* zero_row = (uint8_t*)w; w += 256;
@@ -674,7 +1080,10 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     uint8_t* desc_i8 = (uint8_t*)w; w += descb;
     int32_t* ord_f = (int32_t*)w; w += ordb;
     int32_t* ord_r = (int32_t*)w; w += ordb;
-    uint8_t* cls = (uint8_t*)w;
+    uint8_t* cls = (uint8_t*)w; w += clsb;
+    int32_t* n_rng = (int32_t*)w; w += 256;
+    int2* rng = (int2*)w; w += rngb;
+    int4* rinfo = (int4*)w;
     const int ppx = (n_pairs + 7) / 8;  // pairs per XCD run (scan kernel block order)
     const int n_blk = n_pairs;
     const int grid = 8 * ppx * n_qblk;
@@ -684,7 +1093,11 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
                        k_max, k_pad, norm, cinit, zero_row, (uint4*)desc_i8);
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(l2fr_order_kernel, dim3(mutual ? 2 : 1), dim3(1024),
-                       sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img, ord_f, ord_r);
+                       2 * sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img, ord_f, ord_r, rng,
+                       n_rng);
+    SFM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(l2fr_range_kernel, dim3((n_rng_max + 255) / 256), dim3(256), 0, st, pairs, n_kp,
+                       ord_f, (const int2*)rng, (const int32_t*)n_rng, rinfo);
     SFM_HIP_CHECK(hipGetLastError());
     // qst (per-query status of the recovery) shares the reverse scan's output buffer: it is
     // consumed by the compaction before the reverse scan writes there.
@@ -702,9 +1115,16 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
                            out_dist);
         return SFM_OK;
     }
-    hipLaunchKernelGGL(l2fr_recover_kernel, dim3(n_pairs, k_pad / CHUNK), dim3(256), 0, st, desc_i8,
+#ifdef L2FR_RECOVER_VALU
+    hipLaunchKernelGGL(l2fr_recover_kernel, dim3(n_pairs, k_pad / GROUP), dim3(256), 0, st, desc_i8,
                        n_kp, k_max, k_pad, norm, cinit, pairs, fwd, (const uint8_t*)cls,
                        prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, qst);
+#else
+    hipLaunchKernelGGL(l2fr_recover_mfma_kernel, dim3(n_rng_max, k_pad / GROUP), dim3(256), 0, st,
+                       desc_i8, k_max, k_pad, norm, cinit, (const int4*)rinfo, (const int32_t*)n_rng,
+                       (const int4*)fwd, (const uint8_t*)cls, prm->ratio_num, prm->ratio_den,
+                       (long long)prm->max_dist, qst);
+#endif
     SFM_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(l2fr_compact_kernel, dim3(n_pairs), dim3(256), 0, st, desc_i8, n_kp, k_max,
                        k_pad, norm, pairs, (const int4*)qst, prm->ratio_num, prm->ratio_den,
@@ -734,3 +1154,13 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
+
+#ifdef L2FR_CLOCK
+// Diagnostic build only: the stamps of the last forward scan (L2FR_CLOCK_W per block).
+extern "C" int sfm_debug_l2fr_stamps(unsigned long long* host, int32_t n_blocks) {
+    const size_t n = L2FR_CLOCK_W * (size_t)std::min(n_blocks, L2FR_CLOCK_SLOTS);
+    SFM_HIP_CHECK(hipDeviceSynchronize());
+    SFM_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_l2fr_clock), n * sizeof(unsigned long long)));
+    return SFM_OK;
+}
+#endif

@@ -161,6 +161,7 @@ def build_jtj_sharded(cams, pp, pts, cam_idx, pt_idx, uv, rank: int, world: int,
 # combined by one canonical tree, so 1 to BA_CHUNKS ranks (a rank = a run of whole chunks) give the
 # same bits.  SFM_BA_CHUNKS=0 selects the round-4 sums (A/B only; not sharding-invariant).
 BA_CHUNKS = 8
+BA_MAX_CHUNKS = 16   # SFM_BA_MAX_CHUNKS (include/sfmcore.h)
 
 
 def ba_chunk_count():
@@ -709,7 +710,13 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             # the whole problem's chunks (balanced by observations); rank r takes chunks
             # [r C / N, (r + 1) C / N): every rank a run of whole chunks, so the sums match N = 1
             if world > nchunk:
-                raise ValueError(f"bundle_adjust: {world} ranks > {nchunk} BA chunks")
+                # every rank needs a whole chunk: raise the count to the rank count (the chunk
+                # sums then differ from a run with BA_CHUNKS chunks in the last bits), or beyond
+                # SFM_BA_MAX_CHUNKS fall back to the plain per-shard sums (no chunk table)
+                nchunk = world if world <= BA_MAX_CHUNKS else 0
+                if info is not None:
+                    info["chunks_adjusted"] = {"world": world, "nchunk": nchunk}
+        if nchunk > 0:
             gcuts, gocuts = shard_cuts_device(pt_idx, n_pt, nchunk)
             kr = [r * nchunk // world for r in range(world + 1)]
             cuts, ocuts = [gcuts[k] for k in kr], [gocuts[k] for k in kr]
@@ -736,8 +743,11 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                 if info is not None and world > 1:
                     info["rule"] = {"explicit_schur_candidate": True}
             else:
-                lat, bw = probe_collectives(allreduce, n_cam, device, group)
+                # the chunked sharded CG all-reduces nchunk camera-vector partials per iteration
+                # (ADVICE r5): probe and price that payload, not one camera vector
+                lat, bw = probe_collectives(allreduce, n_cam * max(nchunk, 1), device, group)
                 mode, terms = pcg_rule(len(pt_idx), n_pt, n_cam, world, lat, bw)
+                terms["allreduce_doubles"] = 8 * n_cam * max(nchunk, 1)
                 if info is not None:
                     info["rule"] = terms
         if mode == "replicated":

@@ -42,7 +42,8 @@ def main():
     dc, dp, info, lo, hi = shard_solve(prob, rank, world, R.make_allreduce())
     np.savez(f"{out}.rank{rank}.npz", cams=cams, pts=pts, hist=np.array(hist, np.float64),
              dc=dc, dp=dp, info=info, lo=lo, hi=hi, pcg=np.array(binfo["pcg"]),
-             branches=np.array(branches))
+             branches=np.array(branches),
+             nchunk_adj=np.array(binfo.get("chunks_adjusted", {}).get("nchunk", -1)))
     dist.barrier()
     dist.destroy_process_group()
 

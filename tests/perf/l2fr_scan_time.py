@@ -1,5 +1,5 @@
 """Times the forward MFMA scan of the ratio-test L2 path alone (SFM_L2FR_DEBUG=1 stops the launch
-after prep + order + scan + a record dump) on the cfg3 workload.  Usage (variants via SFMCORE_LIB):
+after prep + order + scan + a record dump) on the cfg3 workload (N_IMG, K override).  Usage (variants via SFMCORE_LIB):
 python tests/perf/l2fr_scan_time.py"""
 import os
 import sys
@@ -15,8 +15,9 @@ import synth
 
 
 def main():
-    s = synth.make_scene(50, 2048, seed=0)
-    pairs = synth.unordered_pairs(50)
+    n_img, K = int(os.environ.get("N_IMG", "50")), int(os.environ.get("K", "2048"))
+    s = synth.make_scene(n_img, K, seed=0)
+    pairs = synth.unordered_pairs(n_img)
     ctx = sfmcore.context(0)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     desc, n_kp, pr = T(s["desc"]), T(s["n_kp"]), T(pairs)

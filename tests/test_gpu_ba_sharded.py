@@ -127,7 +127,7 @@ def test_ba_sharded_world1_graph_and_launch_modes():
         dist.destroy_process_group()
 
 
-def _run_ranks(tmp_path, n, *extra):
+def _run_ranks(tmp_path, n, *extra, env_extra=None):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -135,7 +135,7 @@ def _run_ranks(tmp_path, n, *extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(root, "tests", "dist_ba_worker.py"), out, *extra]
-    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env = dict(os.environ, OMP_NUM_THREADS="4", **(env_extra or {}))
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return [np.load(f"{out}.rank{k}.npz") for k in range(n)]
@@ -165,6 +165,32 @@ def test_ba_sharded_three_ranks_with_an_empty_shard(tmp_path):
     np.testing.assert_array_equal(d[0]["cams"], rcams)
     np.testing.assert_array_equal(d[0]["pts"], rpts)
     assert len(d[2]["dp"]) == 0
+
+
+def test_ba_sharded_more_ranks_than_chunks(tmp_path):
+    """three ranks with SFM_BA_CHUNKS=2 (more ranks than chunks): bundle_adjust raises
+    the chunk count to the rank count instead of failing, says so in info, and the ranks agree bit
+    for bit and match a single process that uses 3 chunks."""
+    prob = problem()
+    args = (prob["cams"], prob["pp"], prob["pts"], prob["cam_idx"], prob["pt_idx"], prob["uv"])
+    fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
+    d = _run_ranks(tmp_path, 3, env_extra={"SFM_BA_CHUNKS": "2"})
+    for k in (1, 2):
+        for key in ("cams", "pts", "hist"):
+            np.testing.assert_array_equal(d[0][key], d[k][key])
+    assert all(int(d[k]["nchunk_adj"]) == 3 for k in range(3))
+    old = os.environ.get("SFM_BA_CHUNKS")
+    os.environ["SFM_BA_CHUNKS"] = "3"
+    try:
+        rcams, rpts, rhist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed)
+    finally:
+        if old is None:
+            os.environ.pop("SFM_BA_CHUNKS")
+        else:
+            os.environ["SFM_BA_CHUNKS"] = old
+    np.testing.assert_array_equal(d[0]["hist"], np.array(rhist, np.float64))
+    np.testing.assert_array_equal(d[0]["cams"], rcams)
+    np.testing.assert_array_equal(d[0]["pts"], rpts)
 
 
 @pytest.mark.parametrize("schur", ["auto", "1"])

@@ -118,6 +118,32 @@ def test_bench_self_launch_two_ranks():
     assert d["graph_checksum"] == d1["graph_checksum"]
 
 
+def test_bench_cfg4_line_carries_cfg5_at_two_ranks():
+    """at N > 1 the cfg4 line runs its cfg5 leg (BASELINE configs[4]) on every
+    rank — pair-sharded matching, point-sharded BA with the PCG branch from pcg_rule — so the
+    driver's multi-GPU run times it.  A 2-rank gloo rehearsal through the self-launcher on small
+    scenes: the N = 2 line's cfg5 reconstruction equals N = 1's bit for bit (points, registered
+    views, median and mean reprojection error), and its BAs ran sharded."""
+    base = ["--config", "cfg4", "--n-img", "12", "--k", "512", "--n-hyp", "1024", "--steps", "1",
+            "--warmup", "1", "--no-cpu-baseline", "--no-fp64", "--no-cfg3", "--no-local",
+            "--cfg5-n-img", "16", "--cfg5-k", "1024"]
+    one = _bench(base)
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = json.loads([l for l in one.stdout.splitlines() if l.strip()][-1])
+    two = _bench(base + ["--gpus", "2", "--dist-backend", "gloo", "--ranks-per-gpu", "2"])
+    assert two.returncode == 0, two.stderr[-3000:]
+    d2 = json.loads([l for l in two.stdout.splitlines() if l.strip()][-1])
+    c1, c2 = d1["cfg5"], d2["cfg5"]
+    assert "error" not in c1 and "error" not in c2, (c1, c2)
+    assert c1["n_gpus"] == 1 and c2["n_gpus"] == 2 and c2["shard_ba"] is True
+    for key in ("points", "registered", "observations", "verified_matches", "median_reproj_px",
+                "mean_reproj_px"):
+        assert c1[key] == c2[key], (key, c1[key], c2[key])
+    assert c1["registered"] >= 14 and c2["s_per_reconstruction"] > 0
+    assert set(c2["pcg_branches"]) <= {"sharded", "replicated"}
+    assert d2["graph_checksum"] == d1["graph_checksum"]
+
+
 def test_bench_refuses_more_gpus_than_the_box_has():
     """`--gpus N` with fewer than N visible GPUs exits non-zero with a clear message and no JSON
     line (the box has one MI355X)."""

@@ -91,6 +91,32 @@ def test_cfg3_full_launch_every_pair():
     assert rows.shape[0] > 500_000              # the bench's ~554 k verified matches
 
 
+def test_cfg2_ratio_rule_every_pair(ctx):
+    """BASELINE configs[1] (cfg2) at full size, its own rule: all 1225 pairs of 50 x 2048 128-D,
+    L2 with the fused ratio test 4/5 and no cross check — the dispatcher's ratio path (forward
+    MFMA scan, MFMA recovery, exact slow path, compaction). Every pair's count, (query, train)
+    indices and d^2 equal the oracle's (oracle_match, the rule of code/feature_matching.py:48-58
+    without crossCheck plus the exact ratio test), bit for bit."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    scene = synth.make_scene(50, 2048, seed=0)
+    pairs = synth.unordered_pairs(50)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    cnt, mt, dist = ctx.match_batch(T(scene["desc"]), T(scene["n_kp"]), T(pairs), cross_check=0,
+                                    ratio=(4, 5))
+    torch.cuda.synchronize()
+    cnt, mt, dist = cnt.cpu().numpy(), mt.cpu().numpy(), dist.cpu().numpy()
+    d = scene["desc"]
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:   # ctypes releases the GIL
+        ref = list(ex.map(lambda ab: O.match(d[ab[0]], d[ab[1]], 0, 0, (4, 5)), pairs))
+    for p, (q, t, dd) in enumerate(ref):
+        assert cnt[p] == len(q), f"pair {p}"
+        np.testing.assert_array_equal(mt[p, :cnt[p], 0], q, err_msg=f"pair {p}")
+        np.testing.assert_array_equal(mt[p, :cnt[p], 1], t, err_msg=f"pair {p}")
+        np.testing.assert_array_equal(dist[p, :cnt[p]], dd, err_msg=f"pair {p}")
+    assert cnt.sum() > 1_000_000                # 1 170 943 tentative matches (k1_cfg2_time.py)
+
+
 def test_cfg4_shard_sample():
     scene = synth.make_scene(500, 4096, seed=0)
     pairs = synth.unordered_pairs(500)

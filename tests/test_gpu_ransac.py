@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+import sfmcore
 import synth
 
 pytestmark = pytest.mark.gpu
@@ -290,3 +291,11 @@ def test_ransac_stats_identity(ctx):
         assert torch.equal(out[k], ref[k])
     for p in range(len(pairs)):
         assert torch.equal(out["mask"][p, :M[p]], ref["mask"][p, :M[p]])
+    # any later workspace user invalidates the counted batch's wave words, and the
+    # read-back then fails cleanly (no stale or freed device memory is read)
+    ctx.ransac_stats(enable=True, read=True)
+    ctx.ransac_batch(kps, pr, cnt, mt, n_hyp=H, seed=42, thr=1.0)
+    ctx.match_batch(desc, torch.from_numpy(s["n_kp"]).cuda(), pr, ratio=(4, 5))
+    ctx.ransac_stats(enable=False, read=True)
+    with pytest.raises(sfmcore.SfmCoreError):
+        ctx.ransac_wave_stops(len(pairs), H)
