@@ -451,6 +451,10 @@ def pairs_main(args, world, rank, local, dist_info):
         run.step(xr)
     torch.cuda.synchronize()
     run.ctx.ransac_stats(enable=True, read=True)
+    # this box's i8 matrix ceiling, measured in the same run right before the
+    # timed steps (an MFMA-only launch of ~200 ms on every CU), so K1's fraction can be read
+    # against the box it ran on; not inside the timed region
+    calib = run.ctx.calib_mfma_i8(200.0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -479,7 +483,7 @@ def pairs_main(args, world, rank, local, dist_info):
     per_rank = gather_ranks(world, {
         "rank": rank, "device": local, "pairs": int(hi - lo),
         "shard_ms_per_step": t_own / args.steps * 1e3, "match_ms": match_ms,
-        "ransac_ms": ransac_ms})
+        "ransac_ms": ransac_ms, "calib_tops": calib["tops"], "calib_clock_ghz": calib["clock_ghz"]})
     k1_tops = run.k1_ops / (match_ms * 1e-3) / 1e12
     value = verified_per_step * args.steps / elapsed
     result = {
@@ -512,10 +516,15 @@ def pairs_main(args, world, rank, local, dist_info):
                      "traffic_unit": f"HBM bytes per step (all launches), PMC, "
                                      f"profiles/traffic_{args.config}.json",
                      "ms": match_ms, "ops_per_step": run.k1_ops,
-                     "practical_peak": PRACTICAL_I8_TOPS,
-                     "frac_of_practical": k1_tops / PRACTICAL_I8_TOPS,
-                     "practical_peak_note": "i8 MFMA-only loop on random operands holds ~1.75 GHz "
-                                            "(profiles/r02/mfma_peak_i8.json, tools/mfma_peak.hip)"},
+                     "practical_peak": calib["tops"],
+                     "frac_of_practical": k1_tops / calib["tops"],
+                     "practical_peak_note": "this run's calib probe (below): an i8 MFMA-only launch "
+                                            "on random operands on every CU of this box",
+                     "practical_peak_recorded": PRACTICAL_I8_TOPS},
+        "calib": dict(calib, probe="sfm_calib_mfma_i8: v_mfma_i32_32x32x32_i8 on register "
+                                   "operands, random data, 2 waves per SIMD on every CU, ~200 ms, "
+                                   "run right before the timed steps (rank 0's device)",
+                      nominal_tops=PEAK_I8_TOPS),
         "stages": {"match_ms": match_ms, "ransac_ms": ransac_ms,
                    "graph_ms": elapsed / args.steps * 1e3 - match_ms - ransac_ms,
                    "ransac_roofline": {
@@ -561,9 +570,9 @@ def pairs_main(args, world, rank, local, dist_info):
         del run, graph   # the side legs below build their own buffers
         torch.cuda.empty_cache()
         if args.config != "cfg3" and not args.no_cfg3:
-            result["cfg3"] = cfg3_side(args.n_hyp, args.chunk)
+            result["cfg3"] = cfg3_side(args.n_hyp, args.chunk, calib["tops"])
             try:   # a side leg: its failure is recorded, the line stands
-                result["cfg2"] = cfg2_side()
+                result["cfg2"] = cfg2_side(calib["tops"])
             except Exception as e:  # noqa: BLE001
                 result["cfg2"] = {"error": f"{type(e).__name__}: {e}"}
         if args.config == "cfg4" and not args.no_local:
@@ -1075,7 +1084,7 @@ def cfg1_timing():
     return out
 
 
-def cfg3_side(n_hyp, chunk):
+def cfg3_side(n_hyp, chunk, practical):
     """cfg3 (50 x 2048, 1225 pairs) on this GPU: the north_star's 2048 x 128 K1 kernel and the
     cfg3 step, 10 timed steps after 3 warmups."""
     import numpy as np
@@ -1101,15 +1110,16 @@ def cfg3_side(n_hyp, chunk):
             "value": graph.shape[0] * 10 / el, "unit": "verified matches/s",
             "ms_per_step": el / 10 * 1e3, "match_ms": m, "ransac_ms": r,
             "k1_roofline": {"achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOP/s (i8)",
-                            "frac_of_practical": tops / PRACTICAL_I8_TOPS,
+                            "frac_of_practical": tops / practical, "practical_peak": practical,
                             "frac": tops / PEAK_I8_TOPS,
                             "traffic": pmc_traffic("mfma_mutual_kernel", "cfg3", 50, 2048, 1)}}
 
 
-def cfg2_side(reps=20):
+def cfg2_side(practical, reps=20):
     """BASELINE configs[1] (cfg2): the 1225 pairs of cfg3's scene, L2 match with the fused ratio
     test (4/5) and no cross check — the dispatcher's ratio path (forward MFMA scan + exact
-    recovery) — per call on this GPU (HIP events on the launch stream, `reps` calls after one)."""
+    recovery) — per call on this GPU (HIP events on the launch stream, `reps` calls after one);
+    frac_of_practical against this run's calib probe."""
     import numpy as np
     import torch
     import sfmcore
@@ -1136,11 +1146,8 @@ def cfg2_side(reps=20):
             "ms_per_call": ms, "matches": int(out[0].sum().item()),
             "k1_roofline": {"achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOP/s (i8)",
                             "frac": tops / PEAK_I8_TOPS,
-                            "frac_of_practical": tops / PRACTICAL_I8_TOPS,
-                            "mfma_busy_recorded": 0.52,
-                            "mfma_busy_note": "not measured in this run: the scan kernel's PMC "
-                                              "record (SQ_VALU_MFMA_BUSY_CYCLES over the SIMD "
-                                              "cycles), profiles/r05/k1_cfg2/"}}
+                            "frac_of_practical": tops / practical,
+                            "practical_peak": practical}}
 
 
 if __name__ == "__main__":

@@ -409,6 +409,14 @@ int sfm_orb_batch(sfm_ctx* ctx, const uint8_t* images, int32_t n_img, int32_t H,
                   const sfm_orb_params* prm, float* out_kp, uint8_t* out_desc,
                   int32_t* out_count);
 
+/* ---- measurement: the device's i8 matrix ceiling right now ------------------------------------
+ * Not a reference interface: the bench line's calibration probe (bench.py "calib"), so that K1's
+ * roofline fraction can be read against the ceiling of the box it ran on.  Every CU runs MFMA-only
+ * waves (v_mfma_i32_32x32x32_i8, register operands, random data, 2 waves per SIMD) for about
+ * target_ms (0 < target_ms <= 5000).  out[4]: wall ms of the measured launch, i8 TOP/s, median
+ * in-kernel clock (GHz), fraction of the nominal dense-i8 peak.  Synchronises the stream. */
+int sfm_calib_mfma_i8(sfm_ctx* ctx, float target_ms, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsfmcore.so")
-SOURCES = ["capi.hip", "match_mfma.hip", "match_l2fr.hip", "match_hamming.hip", "ransac.hip", "ba.hip", "ba_solve.hip", "graph.hip", "tracks.hip", "triangulate.hip", "register.hip", "orb.hip"]
+SOURCES = ["capi.hip", "match_mfma.hip", "match_l2fr.hip", "match_hamming.hip", "ransac.hip", "ba.hip", "ba_solve.hip", "graph.hip", "tracks.hip", "triangulate.hip", "register.hip", "orb.hip", "calib.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: RANSAC follows the oracle's op sequence bit-for-bit (explicit fmaf only).
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",

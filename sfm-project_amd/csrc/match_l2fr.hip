@@ -139,14 +139,16 @@ __global__ void l2fr_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
 // Pair orders by streamed image, counting sort in LDS: block 0 orders by pairs[p][1] (forward
 // scan) into order_f, block 1 by pairs[p][0] (reverse scan) into order_r.
 // Block 0 also cuts order_f into recovery ranges: runs of at most REC_R consecutive entries with
-// the same train image, rng[r] = (first entry, length), *n_rng of them.
+// the same train image, rng[r] = (first entry, length), *n_rng of them, and their pairs (rinfo).
 constexpr int REC_R = 4;  // pairs (sharing their train image) per recovery block
 __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restrict__ pairs,
                                                           int n_pairs, int n_img,
                                                           int32_t* __restrict__ order_f,
                                                           int32_t* __restrict__ order_r,
                                                           int2* __restrict__ rng,
-                                                          int32_t* __restrict__ n_rng) {
+                                                          int32_t* __restrict__ n_rng,
+                                                          const int32_t* __restrict__ n_kp,
+                                                          int4* __restrict__ rinfo) {
     extern __shared__ int hist[];
     const int tid = threadIdx.x, col = blockIdx.x == 0 ? 1 : 0;
     int32_t* order = blockIdx.x == 0 ? order_f : order_r;
@@ -174,7 +176,26 @@ __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restr
                 rng[roff[i] + k / REC_R] = make_int2(hist[i] + k, min(REC_R, c - k));
         }
     __syncthreads();
+    __syncthreads();
     for (int p = tid; p < n_pairs; p += 1024) order[atomicAdd(&hist[pairs[2 * p + col]], 1)] = p;
+    if (blockIdx.x != 0) return;
+    // the recovery ranges' pairs: rinfo[r][e] = (p, a, b, n_kp[a] | n_kp[b] << 16), p = -1 past
+    // the range's length (order_f and rng come from this block: visible after the barrier)
+    __threadfence_block();
+    __syncthreads();
+    const int nr = *n_rng;
+    for (int r = tid; r < nr; r += 1024) {
+        const int2 g = rng[r];
+#pragma unroll
+        for (int e = 0; e < REC_R; ++e) {
+            int4 v = make_int4(-1, 0, 0, 0);
+            if (e < g.y) {
+                const int p = order[g.x + e], a = pairs[2 * p], b = pairs[2 * p + 1];
+                v = make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
+            }
+            rinfo[(size_t)r * REC_R + e] = v;
+        }
+    }
 }
 
 // Ratio bounds of one forward record: DROP (cannot pass even at the favourable ends of the d1, d2
@@ -673,25 +694,6 @@ __global__ __launch_bounds__(256) void l2fr_recover_kernel(
     }
 }
 
-// Per recovery range, its pairs: rinfo[r][e] = (p, a, b, n_kp[a] | n_kp[b] << 16), p = -1 past
-// the range's length (one thread per range).
-__global__ void l2fr_range_kernel(const int32_t* __restrict__ pairs, const int32_t* __restrict__ n_kp,
-                                  const int32_t* __restrict__ order_f, const int2* __restrict__ rng,
-                                  const int32_t* __restrict__ n_rng, int4* __restrict__ rinfo) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= *n_rng) return;
-    const int2 g = rng[r];
-#pragma unroll
-    for (int e = 0; e < REC_R; ++e) {
-        int4 v = make_int4(-1, 0, 0, 0);
-        if (e < g.y) {
-            const int p = order_f[g.x + e], a = pairs[2 * p], b = pairs[2 * p + 1];
-            v = make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
-        }
-        rinfo[(size_t)r * REC_R + e] = v;
-    }
-}
-
 // Recovery, MFMA form: one block of 256 (4 waves) per (range of up to REC_R pairs that share
 // their train image b, group of 8 train tiles of b).  A gather: ~1.2 M candidates at cfg2, each
 // needing its query row and one 32-train tile, so the kernel is built for few dependent round
@@ -710,8 +712,11 @@ __global__ void l2fr_range_kernel(const int32_t* __restrict__ pairs, const int32
 // every candidate); the lane finds the row by compares, d1 = |x'|^2 - 2 e1 - (|y'_j1|^2 mod 2)
 // exactly, and the ratio test is decided exactly where d2's unit ambiguity allows:
 // qst[p][q] = (status, j1, d1).
-constexpr int REC_SB = 4;  // sub-batches of 32 candidates per wave and load round
-__global__ __launch_bounds__(256, 2) void l2fr_recover_mfma_kernel(
+#ifndef L2FR_REC_SB
+#define L2FR_REC_SB 2
+#endif
+constexpr int REC_SB = L2FR_REC_SB;  // sub-batches of 32 candidates per wave and load round
+__global__ __launch_bounds__(256, REC_SB > 2 ? 2 : 3) void l2fr_recover_mfma_kernel(
     const uint8_t* __restrict__ desc, int k_max, int k_pad, const int32_t* __restrict__ norm,
     const int32_t* __restrict__ cinit, const int4* __restrict__ rinfo,
     const int32_t* __restrict__ n_rng, const int4* __restrict__ fwd,
@@ -754,20 +759,32 @@ __global__ __launch_bounds__(256, 2) void l2fr_recover_mfma_kernel(
         gini[tid] = cinit[o];
         gpar[tid] = (unsigned char)(norm[o] & 1);
     }
-    // 2. the group's candidates by tile, in (pair, query) order within a tile: per-thread tile
-    //    counts packed as 16-bit fields (tiles 0-3 in lo, 4-7 in hi), one block prefix sum
+    // 2. the group's candidates by tile, in (pair, query) order within a tile: a SWAR byte match
+    //    gives each thread its candidate mask (cls >> 3 == group), per-thread tile counts packed
+    //    as 16-bit fields (tiles 0-3 in lo, 4-7 in hi), one block prefix sum
+    unsigned msk[REC_R];
     unsigned long long lo = 0, hi = 0;
+    const unsigned g8 = 0x01010101u * ((unsigned)grp << 3);
 #pragma unroll
     for (int e = 0; e < REC_R; ++e) {
         const int na = pi[e].x >= 0 ? (pi[e].w & 0xFFFF) : 0;
         const unsigned cw[4] = {cv[e].x, cv[e].y, cv[e].z, cv[e].w};
+        unsigned m = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const unsigned c = (cw[k >> 2] >> (8 * (k & 3))) & 0xFF;
-            if (tid * 16 + k < na && c >> 3 == (unsigned)grp) {
-                const unsigned long long one = 1ull << (16 * (c & 3));
-                if (c & 4) hi += one; else lo += one;
-            }
+        for (int k = 0; k < 4; ++k) {
+            const unsigned t = (cw[k] ^ g8) & 0xF8F8F8F8u;                      // 0 byte: match
+            const unsigned nz = ((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t;           // bit 7: byte != 0
+            const unsigned z = ~nz & 0x80808080u;
+            m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+        }
+        const int lim = na - tid * 16;   // queries past na are not candidates
+        m &= lim >= 16 ? 0xFFFFu : (lim <= 0 ? 0u : (1u << lim) - 1u);
+        msk[e] = m;
+        for (unsigned mm = m; mm; mm &= mm - 1) {
+            const int k = __builtin_ctz(mm);
+            const unsigned c = (cw[k >> 2] >> (8 * (k & 3))) & 7u;
+            const unsigned long long one = 1ull << (16 * (c & 3));
+            if (c & 4) hi += one; else lo += one;
         }
     }
     unsigned long long plo = lo, phi = hi;  // inclusive wave prefix
@@ -786,7 +803,8 @@ __global__ __launch_bounds__(256, 2) void l2fr_recover_mfma_kernel(
         tlo += wlo[w];
         thi += whi[w];
     }
-    int pos[8];  // this thread's first slot per tile
+    // this thread's first slot per tile, packed as 16-bit fields like the counts
+    unsigned long long slo = 0, shi = 0;
     {
         int o = 0;
 #pragma unroll
@@ -794,7 +812,9 @@ __global__ __launch_bounds__(256, 2) void l2fr_recover_mfma_kernel(
             const unsigned long long tot = t < 4 ? tlo : thi, bef = t < 4 ? blo : bhi,
                                      mine = t < 4 ? plo - lo : phi - hi;
             const int sh = 16 * (t & 3);
-            pos[t] = o + (int)((bef >> sh) & 0xFFFF) + (int)((mine >> sh) & 0xFFFF);
+            const unsigned long long v =
+                (unsigned long long)(o + (int)((bef >> sh) & 0xFFFF) + (int)((mine >> sh) & 0xFFFF)) << sh;
+            if (t < 4) slo |= v; else shi |= v;
             if (tid == 0) toff[t] = o;
             o += (int)((tot >> sh) & 0xFFFF);
         }
@@ -802,19 +822,14 @@ __global__ __launch_bounds__(256, 2) void l2fr_recover_mfma_kernel(
     }
 #pragma unroll
     for (int e = 0; e < REC_R; ++e) {
-        const int na = pi[e].x >= 0 ? (pi[e].w & 0xFFFF) : 0;
         const unsigned cw[4] = {cv[e].x, cv[e].y, cv[e].z, cv[e].w};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const unsigned c = (cw[k >> 2] >> (8 * (k & 3))) & 0xFF;
-            if (tid * 16 + k < na && c >> 3 == (unsigned)grp) {
-                int slot = pos[0];
-#pragma unroll
-                for (int t = 1; t < 8; ++t) slot = (c & 7) == (unsigned)t ? pos[t] : slot;
-                clist[slot] = (unsigned short)((e << 12) | (tid * 16 + k));
-#pragma unroll
-                for (int t = 0; t < 8; ++t) pos[t] += (c & 7) == (unsigned)t;
-            }
+        for (unsigned mm = msk[e]; mm; mm &= mm - 1) {
+            const int k = __builtin_ctz(mm);
+            const unsigned c = (cw[k >> 2] >> (8 * (k & 3))) & 7u;
+            const int sh = 16 * (c & 3);
+            const unsigned long long cur = (c & 4) ? shi : slo, inc = 1ull << sh;
+            clist[(int)((cur >> sh) & 0xFFFF)] = (unsigned short)((e << 12) | (tid * 16 + k));
+            if (c & 4) shi += inc; else slo += inc;
         }
     }
     __syncthreads();
@@ -1092,19 +1107,24 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     hipLaunchKernelGGL(l2fr_prep_kernel, dim3(k_pad / 256, n_img), dim3(256), 0, st, desc, n_kp,
                        k_max, k_pad, norm, cinit, zero_row, (uint4*)desc_i8);
     SFM_HIP_CHECK(hipGetLastError());
+#ifdef L2FR_QORDER  // A/B: the scans' XCD runs share the QUERY image (prologue loads L2-served)
+    const int32_t* sord_f = ord_r;
+    const int32_t* sord_r = ord_f;
+    hipLaunchKernelGGL(l2fr_order_kernel, dim3(2), dim3(1024),
+#else
+    const int32_t* sord_f = ord_f;
+    const int32_t* sord_r = ord_r;
     hipLaunchKernelGGL(l2fr_order_kernel, dim3(mutual ? 2 : 1), dim3(1024),
+#endif
                        2 * sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img, ord_f, ord_r, rng,
-                       n_rng);
-    SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(l2fr_range_kernel, dim3((n_rng_max + 255) / 256), dim3(256), 0, st, pairs, n_kp,
-                       ord_f, (const int2*)rng, (const int32_t*)n_rng, rinfo);
+                       n_rng, n_kp, rinfo);
     SFM_HIP_CHECK(hipGetLastError());
     // qst (per-query status of the recovery) shares the reverse scan's output buffer: it is
     // consumed by the compaction before the reverse scan writes there.
     int4* qst = rev;
     const FwdCls fc{norm, prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, qst, cls};
     hipLaunchKernelGGL(l2fr_scan_kernel<false>, dim3(grid), dim3(SCAN_THREADS), 0, st, desc_i8, n_kp, k_max,
-                       k_pad, cinit, zero_row, pairs, n_qblk, ord_f, n_blk, (const int4*)nullptr,
+                       k_pad, cinit, zero_row, pairs, n_qblk, sord_f, n_blk, (const int4*)nullptr,
                        (const int32_t*)nullptr, fwd, fc);
     SFM_HIP_CHECK(hipGetLastError());
     const char* dbg = getenv("SFM_L2FR_DEBUG");
@@ -1138,7 +1158,7 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     }
     if (mutual) {
         hipLaunchKernelGGL(l2fr_scan_kernel<true>, dim3(grid), dim3(SCAN_THREADS), 0, st, desc_i8, n_kp,
-                           k_max, k_pad, cinit, zero_row, pairs, n_qblk, ord_r, n_blk,
+                           k_max, k_pad, cinit, zero_row, pairs, n_qblk, sord_r, n_blk,
                            (const int4*)surv, (const int32_t*)scount, rev, fc);
         SFM_HIP_CHECK(hipGetLastError());
     }

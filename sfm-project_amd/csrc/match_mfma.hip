@@ -645,11 +645,17 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
 #pragma unroll
                 for (int c = 0; c < QT; c += 2) {
                     v16i acc0 = init, acc1 = init;
+#ifdef MU_MPRIO  // A/B: the MFMA group at raised priority (as the ratio path's scan)
+                    __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
                     for (int s = 0; s < NK; ++s) {
                         acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
                         acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
                     }
+#ifdef MU_MPRIO
+                    __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll
                     for (int r = 0; r < 16; r += 2) {
                         if constexpr (ROWS) {
@@ -734,261 +740,6 @@ __global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_kernel(
     if (tid == 0 && blockIdx.x < MU_CLOCK_SLOTS)
         g_mu_clock[MU_CLOCK_W * (size_t)blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
-}
-
-// ---- Mutual cross check, round 5: group-max rows + an LDS column reduction -----
-//
-// The same contraction, accumulator init and column key as mfma_mutual_kernel; two epilogue
-// changes cut the VALU work per element (the kernel is VALU-issue bound: PMC r04, 16.5 VALU per
-// MFMA, of which the row top-2 network was 1.5 per element and the column transpose 0.65):
-//  * rows: per query tile and 32-train tile a lane reduces its 16 values to their MAXIMUM (a max3
-//    chain, 0.5 per element) and keeps (best, second-best GROUP maximum, group of the best) — four
-//    instructions per group.  best = e1 exactly; the second-best group maximum is the exact
-//    maximum of e over every train outside the best group.  The one thing left unknown is the
-//    runner-up INSIDE the best group: mutual_grp_finalize_kernel recomputes that group's 16 dot
-//    products exactly (16 lanes per query, only for queries that survive the mutual test and the
-//    ratio bound) — an exact recheck, so the outputs are the same bits as the exhaustive rule.
-//  * columns: after the max over the wave's query tiles, each lane stores its 16 train-row keys to
-//    a per-wave LDS image [half][row][32 lanes] (ds_write_b32, conflict-free) and reads back the 16
-//    partial keys of ONE train row (4 ds_read_b128 with a per-row rotation: conflict-free in all
-//    four lane groups); a max3 chain and one ds_swizzle (lane ^ 16) finish the 32-lane maximum —
-//    about 10 VALU instead of the 40-instruction permlane/DPP transpose.  The per-workgroup column
-//    state is u32 (value 23 bits + query-in-workgroup 9 bits: d^2 <= 128 * 255^2 < 2^23), so the
-//    extra 16 KB of images fit beside the stages at two workgroups per CU.
-// Row record (8 B per query): w0 = (e1 + 2^22) << 9 | tile << 1 | half, w1 = second-best group
-// maximum (|e| < 2^22 for real elements; tile < 256 for k_max <= 8192).
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-}
-__device__ __forceinline__ void lds_max_u32(unsigned addr, unsigned v) {
-    asm volatile("ds_max_u32 %0, %1" : : "v"(addr), "v"(v) : "memory");
-}
-
-template <int D>
-__global__ __launch_bounds__(64 * MU_WAVES, MU_MINW) void mfma_mutual_grp_kernel(
-    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
-    const int32_t* __restrict__ norm, const int32_t* __restrict__ cinit,
-    const uint8_t* __restrict__ zero_row, const int32_t* __restrict__ pairs, int n_qblk,
-    const int32_t* __restrict__ pair_order, int n_blk, int2* __restrict__ rowres,
-    unsigned long long* __restrict__ colpart) {
-    constexpr int QT = Geo<D>::QT, QB = mu_qb<D>(), CHUNK = MU_CHUNK_BYTES / D, NK = Geo<D>::NK;
-    constexpr int SLOTS = Geo<D>::SLOTS, NT = CHUNK / 32, NTHR = 64 * MU_WAVES;
-    constexpr int PIECES = CHUNK * D / 1024 / MU_WAVES, RPP = 1024 / D;
-    static_assert(PIECES >= 1 && CHUNK % 32 == 0 && CHUNK / 4 <= 64, "stage geometry");
-    static_assert(QB <= 512, "u32 column state: 9-bit query-in-workgroup field");
-    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
-    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
-    __shared__ __attribute__((aligned(16))) int red[MU_WAVES][2 * 16 * 32];  // [half][row][lane]
-    extern __shared__ unsigned int lds_colw[];  // [k_pad] u32 column state, dynamic
-
-    const int per_xcd = (int)(gridDim.x >> 3);
-    const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
-    if (sblk >= n_blk) return;  // block-uniform, before any barrier
-    const int qb = sblk % n_qblk;
-    const int p = pair_order[sblk / n_qblk];
-    const int a = pairs[2 * p], b = pairs[2 * p + 1];
-    const int na = n_kp[a], nb = n_kp[b];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
-    for (int j = tid; j < k_pad; j += NTHR) lds_colw[j] = 0u;
-
-    const uint8_t* db = desc + (size_t)b * k_max * D;
-    const int32_t* cib = cinit + (size_t)b * k_pad;
-    const int n_chunk = (nb + CHUNK - 1) / CHUNK;
-    auto stage = [&](int ch, unsigned char* dst) {
-#pragma unroll
-        for (int i = 0; i < PIECES; ++i) {
-            const int piece = wave * PIECES + i;
-            const int row = piece * RPP + lane / SLOTS;
-            const int slot = (lane % SLOTS) ^ swz<D>(row);
-            const int j = ch * CHUNK + row;
-            const uint8_t* src = (j < nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
-        }
-        if (wave == 0 && lane < CHUNK / 4) {
-            const int32_t* src = cib + ch * CHUNK + lane * 4;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D), 16, 0, 0);
-        }
-    };
-
-    const int qbase = qb * QB + wave * QT * 32;
-    const bool active = qbase < na;  // wave-uniform
-    v4i bq[QT][NK];
-    int ccol[QT], tb[QT], ts[QT], pos[QT];
-    const uint8_t* da = desc + (size_t)a * k_max * D;
-#pragma unroll
-    for (int c = 0; c < QT; ++c) {
-        const int q = qbase + c * 32 + r32;
-        const v4i* src = (const v4i*)((q < na) ? da + (size_t)q * D + (D / 2) * h : zero_row + (D / 2) * h);
-#pragma unroll
-        for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
-        ccol[c] = (q < na) ? (-128 * norm[(size_t)a * k_pad + q] + 127 - (c * 32 + r32)) : MU_COL_PAD;
-        tb[c] = INT_MIN; ts[c] = INT_MIN; pos[c] = 0;
-    }
-    // LDS column image of this wave: writer lane (h, r32) stores row r at [h][r][r32]; reader lane
-    // (h, m = r32) reduces train register rr = m & 15 over lanes 16 sg .. 16 sg + 15 (sg = m >> 4):
-    // four ds_read_b128, piece k' = (i + (rr >> 1)) & 3 in step i (conflict-free rotation)
-    const unsigned red_w = lds_addr(&red[wave][0]) + h * 2048 + r32 * 4;
-    const int rr = r32 & 15, sg = r32 >> 4;
-    const unsigned red_r = lds_addr(&red[wave][0]) + h * 2048 + rr * 128 + sg * 64;
-    unsigned red_ra[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) red_ra[i] = red_r + 16 * ((i + (rr >> 1)) & 3);
-    const int jrow = 8 * (rr >> 2) + 4 * h + (rr & 3);       // the reader's train row in a tile
-    const int kbase = 511 - 127 - wave * QT * 32;            // 511 - q_wg = kbase + (key & 127)
-    const unsigned colw_base = lds_addr(lds_colw);
-
-    // the 16 partial keys of the reader's train row (4 ds_read_b128 in flight) -> its maximum over
-    // the wave's 128 queries -> the u32 column state
-    auto consume = [&](v4i (&g)[4], int j) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]));
-        int k = vmax3(g[0].x, g[0].y, g[0].z);
-        k = vmax3(k, g[0].w, g[1].x);
-        k = vmax3(k, g[1].y, g[1].z);
-        k = vmax3(k, g[1].w, g[2].x);
-        k = vmax3(k, g[2].y, g[2].z);
-        k = vmax3(k, g[2].w, g[3].x);
-        k = vmax3(k, g[3].y, g[3].z);
-        k = max(k, g[3].w);
-        k = max(k, __builtin_amdgcn_ds_swizzle(k, 0x401F));  // lane ^ 16: the other segment
-        if (sg == 0 && j < nb) {
-            // u32 state: (0x7FFFFF - d^2 - p_j) << 9 | (511 - query in workgroup)
-            const unsigned kw = ((unsigned)((k >> 7) + 0x7FFFFF) << 9) + (unsigned)(kbase + (k & 127));
-            lds_max_u32(colw_base + 4u * (unsigned)j, kw);
-        }
-    };
-    v4i gq[4];
-    int jq = 0;
-
-    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
-        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
-        const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
-        if (active) {
-            const unsigned char* A = cur;
-            const int* Ci = (const int*)(cur + CHUNK * D);
-            auto load_tile = [&](int tt, v4i (&af)[NK], v16i& init) {
-                const int row = tt * 32 + r32;
-                const int sw = swz<D>(row);
-#pragma unroll
-                for (int s = 0; s < NK; ++s)
-                    af[s] = *(const v4i*)(A + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
-                    init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
-                    init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
-                }
-            };
-            v4i af[NK];
-            v16i init;
-            for (int tt = 0; tt < nt; ++tt) {
-                load_tile(tt, af, init);
-                const int cur_t = ch * NT + tt;  // global tile index (wave-uniform)
-                int colacc[16];
-#pragma unroll
-                for (int c = 0; c < QT; c += 2) {
-                    v16i acc0 = init, acc1 = init;
-#pragma unroll
-                    for (int s = 0; s < NK; ++s) {
-                        acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s], acc0, 0, 0, 0);
-                        acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c + 1][s], acc1, 0, 0, 0);
-                    }
-                    int m0 = 0, m1 = 0;
-#pragma unroll
-                    for (int r = 0; r < 16; r += 2) {
-                        // column keys: 256 e + ccol (wraps only for padded-train rows, never merged)
-                        const int a0 = (int)(((unsigned)acc0[r] << 8) + (unsigned)ccol[c]);
-                        const int a1 = (int)(((unsigned)acc1[r] << 8) + (unsigned)ccol[c + 1]);
-                        const int b0 = (int)(((unsigned)acc0[r + 1] << 8) + (unsigned)ccol[c]);
-                        const int b1 = (int)(((unsigned)acc1[r + 1] << 8) + (unsigned)ccol[c + 1]);
-                        // group maxima (rows): one v_max3 per two elements, issued after the key
-                        // builds that take the MFMA -> VALU hazard padding (vmax3_after)
-                        if (r == 0) {
-                            m0 = max(acc0[0], acc0[1]);
-                            m1 = max(acc1[0], acc1[1]);
-                        } else {
-                            m0 = vmax3_after(m0, acc0[r], acc0[r + 1], a0, b0);
-                            m1 = vmax3_after(m1, acc1[r], acc1[r + 1], a1, b1);
-                        }
-                        colacc[r] = (c == 0) ? max(a0, a1) : vmax3(colacc[r], a0, a1);
-                        colacc[r + 1] = (c == 0) ? max(b0, b1) : vmax3(colacc[r + 1], b0, b1);
-                    }
-                    // (best, second-best group maximum, tile of the best): ts <= tb always
-                    pos[c] = m0 > tb[c] ? cur_t : pos[c];
-                    ts[c] = vmed3(ts[c], tb[c], m0);
-                    tb[c] = max(tb[c], m0);
-                    pos[c + 1] = m1 > tb[c + 1] ? cur_t : pos[c + 1];
-                    ts[c + 1] = vmed3(ts[c + 1], tb[c + 1], m1);
-                    tb[c + 1] = max(tb[c + 1], m1);
-                }
-#ifdef MU_GRP_XPOSE  // A/B build only: round 4's permlane16_swap / DPP transpose for the column side
-                {
-                    const int key = transpose_max16(colacc, lane);
-                    const int xr = ((lane >> 1) & 1) * 8 + ((lane >> 2) & 1) * 4 +
-                                   ((lane >> 3) & 1) * 2 + ((lane >> 4) & 1);
-                    const int j = ch * CHUNK + tt * 32 + (xr & 3) + 8 * (xr >> 2) + 4 * h;
-                    if (!(lane & 1) && j < nb)
-                        lds_max_u32(colw_base + 4u * (unsigned)j,
-                                    ((unsigned)((key >> 7) + 0x7FFFFF) << 9) +
-                                        (unsigned)(kbase + (key & 127)));
-                }
-#else
-#ifdef MU_GRP_PIPE   // A/B build only: the previous tile's column reads consumed one tile later
-                if (tt > 0) consume(gq, jq);
-#endif
-                // column maximum over the wave's 128 queries of each train row, through LDS
-                // (asm: the compiler neither sees these as aliasing the in-flight stage DMA nor
-                // reorders them — volatile asm keeps program order; the wait carries the data)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(red_w), "v"(colacc[r]),
-                                 "i"(r * 128));
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    asm volatile("ds_read_b128 %0, %1" : "=v"(gq[i]) : "v"(red_ra[i]));
-                jq = ch * CHUNK + tt * 32 + jrow;
-#ifndef MU_GRP_PIPE
-                consume(gq, jq);
-#endif
-#endif
-            }
-#if defined(MU_GRP_PIPE) && !defined(MU_GRP_XPOSE)
-            if (nt > 0) consume(gq, jq);
-#endif
-        }
-    };
-    if (n_chunk > 0) stage(0, lds0);
-    __syncthreads();
-    for (int ch = 0; ch < n_chunk; ch += 2) {
-        process(ch, lds0, lds1);
-        __syncthreads();
-        if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
-        __syncthreads();
-    }
-    if (active) {
-#pragma unroll
-        for (int c = 0; c < QT; ++c) {
-            const int P1 = __shfl_xor(tb[c], 32), P2 = __shfl_xor(ts[c], 32);
-            const int Pp = __shfl_xor(pos[c], 32);
-            const int e1 = max(tb[c], P1);
-            const int e2 = max(min(tb[c], P1), max(ts[c], P2));
-            const bool mine = tb[c] > P1 || (tb[c] == P1 && h == 0);
-            const int gsel = mine ? (pos[c] << 1 | h) : (Pp << 1 | (h ^ 1));
-            const int q = qbase + c * 32 + r32;
-            if (h == 0 && q < na)
-                rowres[(size_t)p * k_pad + q] =
-                    make_int2((int)(((unsigned)(e1 + (1 << 22)) << 9) | (unsigned)gsel), e2);
-        }
-    }
-    if (qb * QB < na) {   // the block holds real queries: every real train has a real key
-        unsigned long long* dst = colpart + (size_t)p * k_pad;
-        for (int j = tid; j < nb; j += NTHR) {
-            const unsigned kw = lds_colw[j];
-            const int nd = (int)(kw >> 9) - 0x7FFFFF;           // 2e - |x'_q|^2 = -d^2 - p_j
-            const unsigned gq = (unsigned)(qb * QB + 511 - (int)(kw & 511));
-            atomicMax(dst + j, ((unsigned long long)((unsigned)nd ^ 0x80000000u) << 32) |
-                                   (unsigned long long)(0xFFFFFFFFu - gq));
-        }
-    }
 }
 
 // ---- Hamming with the key built by the MFMA itself (sfm_match_batch_both's Hamming path) ----------
@@ -1329,181 +1080,6 @@ __global__ __launch_bounds__(MU_FT) void mutual_finalize_kernel(
     if (tid == 0) out_count[p] = base;
 }
 
-
-// Finalize of mfma_mutual_grp_kernel: mutual_finalize_kernel's rule with the group recheck.  A
-// query that survives the mutual test (its best proposal D* <= |x'|^2 - 2 e1) and the ratio bound
-// at the favourable end gets the exact e and d of the 16 trains of its best group (16 lanes per
-// query, one train each): a second e1 in the group means the nearest neighbour is not unique (->
-// exact row scan); else d2 = min(group runner-up d, outside bound [A - 2 e2 - 1, A - 2 e2]) and
-// the ratio test is decided exactly or, when the outside parity straddles it, by the row scan.
-// Grid: 8 * ceil(P / 8) blocks; XCD x (block b -> XCD b mod 8) takes the x-th contiguous run of
-// the pairs ordered by train image (pair_order), so the pairs one XCD finalises together share the
-// train descriptors the group rechecks read: they stay in that XCD's L2.
-template <int D>
-__global__ __launch_bounds__(MU_FT) void mutual_grp_finalize_kernel(
-    const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
-    const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs,
-    const int32_t* __restrict__ pair_order, int n_pairs,
-    const int2* __restrict__ rowres, const unsigned long long* __restrict__ colpart, int rnum,
-    int rden, long long max_dist, int32_t* __restrict__ out_count, int32_t* __restrict__ out_match,
-    int32_t* __restrict__ out_dist) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_best[];
-    __shared__ int wsum[MU_FT / 64], slow[MU_FT], nslow, rck[MU_FT], nrck;
-    __shared__ long long rb1[MU_FT], rb2[MU_FT];
-    __shared__ int rj1[MU_FT];
-    __shared__ unsigned char keepx[MU_FT];
-    __shared__ int jx[MU_FT], dx[MU_FT];
-    const int per_xcd = (int)(gridDim.x >> 3);
-    const int sblk = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
-    if (sblk >= n_pairs) return;  // block-uniform, before any barrier
-    const int p = pair_order[sblk], tid = threadIdx.x;
-    const int a = pairs[2 * p], b = pairs[2 * p + 1];
-    const int na = n_kp[a], nb = n_kp[b];
-    if (na <= 0 || nb <= 0) {
-        if (tid == 0) out_count[p] = 0;
-        return;
-    }
-    const unsigned long long* cp = colpart + (size_t)p * k_pad;
-    const int32_t* na_norm = norm + (size_t)a * k_pad;
-    const int32_t* nb_norm = norm + (size_t)b * k_pad;
-    const int2* rw = rowres + (size_t)p * k_pad;
-    constexpr bool SQ = D == 128;
-    constexpr int RS = D / 16;
-    const uint4* qa = (const uint4*)(desc + (size_t)a * k_max * D);
-    const uint4* dbv = (const uint4*)(desc + (size_t)b * k_max * D);
-    int32_t* om = out_match + (size_t)p * k_max * 2;
-    int32_t* od = out_dist + (size_t)p * k_max;
-    for (int i = tid; i < na; i += MU_FT) lds_best[i] = ~0ull;
-    __syncthreads();
-    for (int j = tid; j < nb; j += MU_FT) {
-        const unsigned long long best = cp[j];
-        if (best == 0) continue;
-        const int nd = (int)((unsigned)(best >> 32) ^ 0x80000000u);
-        const int gq = (int)(0xFFFFFFFFu - (unsigned)best);
-        if (gq < 0 || gq >= na) continue;  // defensive: a column winner is always a query
-        const long long d = -(long long)nd - (nb_norm[j] & 1);
-        atomicMin(&lds_best[gq], ((unsigned long long)d << 32) | (unsigned)j);
-    }
-    __syncthreads();
-    int base = 0;
-    for (int i0 = 0; i0 < na; i0 += MU_FT) {
-        const int i = i0 + tid;
-        bool sl = false, rc = false;
-        if (tid == 0) { nslow = 0; nrck = 0; }
-        if (i < na) {
-            const int2 r = rw[i];
-            const long long e1 = (long long)((unsigned)r.x >> 9) - (1 << 22);
-            const long long A = na_norm[i];
-            const unsigned long long e = lds_best[i];
-            const long long Dp = e != ~0ull ? (long long)(e >> 32) : sfm::DIST_INF;
-            const long long d1lo = max(A - 2 * e1 - 1, 0LL);
-            const long long d2hi = r.y > MU_E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
-            if (Dp <= A - 2 * e1 && sfm::ratio_ok(d1lo, d2hi, rnum, rden, SQ) &&
-                (max_dist < 0 || d1lo < max_dist)) {
-                if (e1 == r.y) sl = true;   // a tie across groups: exact row scan
-                else rc = true;             // group recheck
-            }
-        }
-        keepx[tid] = 0;
-        __syncthreads();
-        if (sl) slow[atomicAdd(&nslow, 1)] = tid;
-        if (rc) rck[atomicAdd(&nrck, 1)] = tid;
-        __syncthreads();
-        const int nr = nrck;
-        for (int g0 = 0; g0 < nr; g0 += MU_FT / 16) {   // 16 lanes per rechecked query
-            const int gi = g0 + (tid >> 4), k = tid & 15;
-            int ek = INT_MIN;
-            long long dk = sfm::DIST_INF;
-            if (gi < nr) {
-                const int q = i0 + rck[gi];
-                const unsigned w0 = (unsigned)rw[q].x;
-                const int t = (int)((w0 >> 1) & 255), hh = (int)(w0 & 1);
-                const int j = 32 * t + 8 * (k >> 2) + 4 * hh + (k & 3);
-                if (j < nb) {
-                    uint4 x[RS];
-#pragma unroll
-                    for (int u = 0; u < RS; ++u) x[u] = qa[(size_t)q * RS + u];
-                    const int dot = mu_dot<D>(x, dbv + (size_t)j * RS);
-                    ek = dot - ((nb_norm[j] + 1) >> 1);      // the kernel's e (accumulator init)
-                    dk = (long long)na_norm[q] + nb_norm[j] - 2LL * dot;
-                }
-            }
-            rb1[tid] = dk;
-            rj1[tid] = ek;
-            __syncthreads();
-            if (k == 0 && gi < nr) {
-                const int who = rck[gi], q = i0 + who;
-                const int2 r = rw[q];
-                const int e1 = (int)((unsigned)r.x >> 9) - (1 << 22);
-                int n1 = 0;
-                long long d2g = sfm::DIST_INF;
-                for (int u = 0; u < 16; ++u) {
-                    if (rj1[tid + u] == e1) ++n1;
-                    else d2g = min(d2g, rb1[tid + u]);
-                }
-                if (n1 != 1) {
-                    slow[atomicAdd(&nslow, 1)] = who;   // nearest not unique in e: row scan
-                } else {
-                    const long long A = na_norm[q];
-                    const unsigned long long e = lds_best[q];
-                    const long long d1 = (long long)(e >> 32);
-                    const long long o2lo = r.y > MU_E_VALID ? A - 2LL * r.y - 1 : sfm::DIST_INF;
-                    const long long o2hi = r.y > MU_E_VALID ? A - 2LL * r.y : sfm::DIST_INF;
-                    const long long d2lo = min(d2g, o2lo), d2hi = min(d2g, o2hi);
-                    if (sfm::ratio_ok(d1, d2lo, rnum, rden, SQ)) {
-                        keepx[who] = max_dist < 0 || d1 < max_dist;
-                        jx[who] = (int)(unsigned)e;
-                        dx[who] = (int)d1;
-                    } else if (sfm::ratio_ok(d1, d2hi, rnum, rden, SQ)) {
-                        slow[atomicAdd(&nslow, 1)] = who;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-        const int ns = nslow;
-        for (int s = 0; s < ns; ++s) {  // exact row scan of query i0 + slow[s] (rare)
-            const int who = slow[s], q = i0 + who;
-            uint4 x[RS];
-#pragma unroll
-            for (int u = 0; u < RS; ++u) x[u] = qa[(size_t)q * RS + u];
-            long long b1 = sfm::DIST_INF, b2 = sfm::DIST_INF;
-            int j1 = INT_MAX;
-            for (int j = tid; j < nb; j += MU_FT) {
-                const long long d = (long long)na_norm[q] + nb_norm[j] - 2LL * mu_dot<D>(x, dbv + (size_t)j * RS);
-                if (d < b1) { b2 = b1; b1 = d; j1 = j; } else if (d < b2) { b2 = d; }
-            }
-            rb1[tid] = b1; rb2[tid] = b2; rj1[tid] = j1;
-            __syncthreads();
-            for (int st = MU_FT / 2; st > 0; st >>= 1) {
-                if (tid < st) {
-                    const long long ob1 = rb1[tid + st], ob2 = rb2[tid + st];
-                    const int oj = rj1[tid + st];
-                    const bool other = ob1 < rb1[tid] || (ob1 == rb1[tid] && oj < rj1[tid]);
-                    const long long m2 = min(min(rb2[tid], ob2), other ? rb1[tid] : ob1);
-                    if (other) { rb1[tid] = ob1; rj1[tid] = oj; }
-                    rb2[tid] = m2;
-                }
-                __syncthreads();
-            }
-            if (tid == 0) {
-                const int n1 = rj1[0];
-                unsigned long long cw = (n1 >= 0 && n1 < nb) ? cp[n1] : 0ull;
-                bool kk = cw != 0ull && (int)(0xFFFFFFFFu - (unsigned)cw) == q;
-                kk = kk && sfm::ratio_ok(rb1[0], rb2[0], rnum, rden, SQ);
-                kk = kk && (max_dist < 0 || rb1[0] < max_dist);
-                keepx[who] = kk;
-                jx[who] = n1;
-                dx[who] = (int)rb1[0];
-            }
-            __syncthreads();
-        }
-        const bool kk = i < na && keepx[tid];
-        base = sfm::compact_n<MU_FT>(kk, i, jx[tid], dx[tid], base, wsum, om, od);
-    }
-    if (tid == 0) out_count[p] = base;
-}
-
 // Finalize of the column-only kernel, the OpenCV cross-check rule (oracle_match cross_check 2, the
 // reference's BFMatcher(crossCheck=True), code/feature_matching.py:48): every train j proposes
 // (d, j) to its nearest query; each query keeps the smallest proposal (lowest j on ties).
@@ -1747,8 +1323,6 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
                              (const void*)mfma_mutual_kernel<256, false>,
                              (const void*)mutual_finalize_kernel<128>,
                              (const void*)mutual_finalize_kernel<256>,
-                             (const void*)mutual_grp_finalize_kernel<128>,
-                             (const void*)mutual_grp_finalize_kernel<256>,
                              (const void*)opencv_finalize_kernel};
         for (const void* f : fns)
             SFM_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, want));
@@ -1777,49 +1351,6 @@ static int mfma_mutual_launch(sfm_ctx* ctx, int metric, const uint8_t* desc, con
     }();
     // whole pairs per XCD (blocks of one pair never straddle two XCDs' ranges)
     const int grid = 8 * ((n_pairs + 7) / 8) * n_qblk;
-    // mutual rule: the round-4 top-2 kernel (default) or the round-5 group-max kernel
-    // (SFM_K1_GRP=1: bit-identical, measured slower — DESIGN.md §4.1 "Round 5")
-    const char* grp_env = getenv("SFM_K1_GRP");
-    const bool grp = rows && grp_env && grp_env[0] == '1';
-    if (grp) {
-        SFM_HIP_CHECK(hipMemsetAsync(colpart, 0, sizeof(unsigned long long) * (size_t)n_pairs * k_pad, st));
-        hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(1024), sizeof(int) * (size_t)n_img, st,
-                           pairs, n_pairs, n_img, pair_order, pair_order + n_pairs);
-        SFM_HIP_CHECK(hipGetLastError());
-        if (l2)
-            hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_L2, true>), dim3(k_pad / 256, n_img),
-                               dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row,
-                               (uint4*)desc_i8);
-        else
-            hipLaunchKernelGGL((mfma_prep_kernel<SFM_METRIC_HAMMING, true>), dim3(k_pad / 256, n_img),
-                               dim3(256), 0, st, desc, n_kp, k_max, k_pad, norm, cinit, zero_row,
-                               (uint4*)desc_i8);
-        SFM_HIP_CHECK(hipGetLastError());
-        int2* rw2 = (int2*)rowres;
-        if (l2) {
-            hipLaunchKernelGGL(mfma_mutual_grp_kernel<128>, dim3(grid), dim3(64 * MU_WAVES),
-                               (size_t)k_pad * 4, st, desc_i8, n_kp, k_max, k_pad, norm, cinit,
-                               zero_row, pairs, n_qblk, pair_order, n_blk, rw2, colpart);
-            SFM_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(mutual_grp_finalize_kernel<128>, dim3(8 * ((n_pairs + 7) / 8)),
-                               dim3(MU_FT), (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad,
-                               norm, pairs, pair_order, n_pairs, rw2, colpart, prm->ratio_num,
-                               prm->ratio_den,
-                               (long long)prm->max_dist, out_count, out_match, out_dist);
-        } else {
-            hipLaunchKernelGGL(mfma_mutual_grp_kernel<256>, dim3(grid), dim3(64 * MU_WAVES),
-                               (size_t)k_pad * 4, st, desc_i8, n_kp, k_max, k_pad, norm, cinit,
-                               zero_row, pairs, n_qblk, pair_order, n_blk, rw2, colpart);
-            SFM_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(mutual_grp_finalize_kernel<256>, dim3(8 * ((n_pairs + 7) / 8)),
-                               dim3(MU_FT), (size_t)k_pad * 8, st, desc_i8, n_kp, k_max, k_pad,
-                               norm, pairs, pair_order, n_pairs, rw2, colpart, prm->ratio_num,
-                               prm->ratio_den,
-                               (long long)prm->max_dist, out_count, out_match, out_dist);
-        }
-        SFM_HIP_CHECK(hipGetLastError());
-        return SFM_OK;
-    }
     const int fin_qblk = col_atomic ? 1 : n_qblk;
     if (col_atomic)
         SFM_HIP_CHECK(hipMemsetAsync(colpart, 0, sizeof(unsigned long long) * (size_t)n_pairs * k_pad, st));

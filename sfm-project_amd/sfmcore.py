@@ -27,7 +27,7 @@ EXPORTED = ["sfm_ctx_create", "sfm_ctx_destroy", "sfm_ctx_set_stream", "sfm_ctx_
             "sfm_ba_fix_params", "sfm_orb_batch", "sfm_ransac_counts", "sfm_ba_solve_stage",
             "sfm_ransac_stats", "sfm_ransac_f_batch_f64", "sfm_graph_rows_packed",
             "sfm_graph_expand", "sfm_match_batch_both", "sfm_ransac_wave_stops",
-            "sfm_ba_set_chunks", "sfm_ba_chunk_tree", "sfm_ba_set_schur"]
+            "sfm_ba_set_chunks", "sfm_ba_chunk_tree", "sfm_ba_set_schur", "sfm_calib_mfma_i8"]
 
 
 class SfmCoreError(RuntimeError):
@@ -102,6 +102,7 @@ def load_library(path: str = LIB_PATH):
                                         C.POINTER(RansacParams), vp, vp, vp, vp]
         L.sfm_ransac_stats.argtypes = [vp, i32, vp]
         L.sfm_ransac_wave_stops.argtypes = [vp, i32, i32, vp]
+        L.sfm_calib_mfma_i8.argtypes = [vp, C.c_float, vp]
         L.sfm_ba_jtj.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp,
                                  vp, vp, vp, vp, vp, vp]
         L.sfm_ba_solve.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -324,6 +325,16 @@ class Context:
         _check(self.lib.sfm_ransac_wave_stops(self.handle, int(n_pairs), int(n_hyp),
                                               out.ctypes.data_as(C.c_void_p)))
         return out
+
+    def calib_mfma_i8(self, target_ms=200.0):
+        """sfm_calib_mfma_i8: the device's i8 MFMA ceiling right now — dict(ms, tops, clock_ghz,
+        frac_nominal) of an MFMA-only launch of about target_ms on every CU (synchronises)."""
+        out = np.zeros(4, np.float64)
+        self._bind_stream()
+        _check(self.lib.sfm_calib_mfma_i8(self.handle, float(target_ms),
+                                          out.ctypes.data_as(C.c_void_p)))
+        return {"ms": float(out[0]), "tops": float(out[1]), "clock_ghz": float(out[2]),
+                "frac_nominal": float(out[3])}
 
     # ---- verified match graph --------------------------------------------------------------
     def graph_rows(self, pair_base, count, match, inl_count, mask, min_inliers=15,

@@ -40,6 +40,11 @@ def test_bench_json_contract():
     assert r["bound"] in ("hbm", "mfma")
     assert abs(r["frac"] - r["achieved"] / r["peak"]) <= 1e-9
     assert 0.0 < r["frac"] < 1.0
+    # the box's i8 ceiling measured in the same run, and K1 read against it
+    c = d["calib"]
+    assert 1000.0 < c["tops"] < r["peak"] and 1.0 < c["clock_ghz"] < 3.0 and c["ms"] > 50.0
+    assert abs(r["practical_peak"] - c["tops"]) <= 1e-9
+    assert abs(r["frac_of_practical"] - r["achieved"] / c["tops"]) <= 1e-9
     # the cfg3 verified graph is fixed by the oracle-checked kernels (tests/test_gpu_fullsize.py);
     # 554 010 before round 3's rank-2 step (8 squarings of adj(F^T F))
     assert d["verified_matches_per_step"] == 554009

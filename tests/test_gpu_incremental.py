@@ -95,6 +95,35 @@ def test_incremental_sharded_matching_two_ranks(tmp_path):
         np.testing.assert_array_equal(d["points"], ref.points)
 
 
+def test_incremental_bench_cfg5_scene():
+    """the scene bench.py's cfg5 leg reconstructs (bench.local_scene: 500 x
+    4096 on a sphere-cap view grid, ~5 neighbouring views per point) asserted here, not only in
+    bench records: every view registered, median reprojection error under 0.5 px, camera centres
+    within 0.1 % of the grid radius after the similarity alignment, and the point / observation
+    counts of every recorded run (258 144 / 1 024 123, profiles/r04-r05 bench_cfg*.json)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    scene, _ = bench.local_scene(500, 4096)
+    intr = np.c_[scene["cams"][:, 6:8], scene["pp"]]
+    rec = incremental.reconstruct(scene["desc"], scene["kps"], scene["n_kp"], intr, device=0)
+    assert rec.registered.all()
+    tptr, timg, tkp = rec.tracks
+    obs_track = np.repeat(np.arange(len(tptr) - 1), np.diff(tptr))
+    has = rec.has_point
+    use = has[obs_track] & rec.registered[timg]
+    assert int(has.sum()) == 258144 and int(use.sum()) == 1024123
+    pts_ids, pt_idx = np.unique(obs_track[use], return_inverse=True)
+    err = R.reprojection_errors(rec.cams, scene["pp"], rec.points[pts_ids], timg[use],
+                                pt_idx.astype(np.int32), scene["kps"][timg[use], tkp[use]])
+    assert np.median(err) < 0.5
+    c_est, c_true = _centres(rec.cams), _centres(scene["cams"])
+    s, Rm, t = _umeyama(c_est, c_true)
+    aligned = (s * (Rm @ c_est.T)).T + t
+    assert np.abs(aligned - c_true).max() < 0.001 * 8.0   # 0.1 % of the grid radius
+
+
 @pytest.mark.parametrize("n,pcg,schur", [(2, "sharded", "auto"), (2, "replicated", "auto"),
                                          (3, "sharded", "auto"), (3, "replicated", "auto"),
                                          (2, "sharded", "1"), (3, "replicated", "1")])

@@ -300,12 +300,13 @@ def test_both_orders_rejects_ratio_and_large_k(ctx):
 
 @pytest.mark.parametrize("ratio", [(4, 5), (1, 1), None])
 @pytest.mark.parametrize("metric", [0, 1])
-def test_group_kernel_equals_top2_kernel_and_oracle(ctx, ratio, metric):
-    """Round 5's K1 (mfma_mutual_grp_kernel: group-max rows, exact recheck of the best group in
-    the finalize, LDS column reduction) against round 4's top-2 kernel (SFM_K1_GRP=0) and the
-    oracle: identical outputs, including the cases the recheck exists for — a tie of the nearest
-    value inside one 16-train group (trains 0/1, 8/9: same lane half, same tile), a tie across
-    tiles (trains 2 and 34), the runner-up inside the best group, ragged sizes, tie-heavy sets."""
+def test_mutual_rule_planted_ties_vs_oracle(ctx, ratio, metric):
+    """The mutual rule's kernels against the oracle on planted cases (kept from round 5's group-
+    kernel test; that kernel measured slower and left the library, its record is in
+    profiles/r05/): a tie of the nearest value inside one 16-train group (trains 0/1, 8/9: same
+    lane half, same tile), a tie across tiles (trains 2 and 34), the runner-up one unit away in
+    the same group, ragged sizes, tie-heavy sets.  L2 with a ratio test also runs the ratio path
+    (SFM_L2_PATH=fr: forward scan, MFMA recovery, reverse scan): both equal the oracle."""
     import os
     rng = np.random.default_rng(321 + metric)
     k, dim = 700, (128 if metric == 0 else 32)
@@ -322,22 +323,11 @@ def test_group_kernel_equals_top2_kernel_and_oracle(ctx, ratio, metric):
     desc[2, 100:110] = desc[0, 5]
     n_kp = np.array([k, k - 3, 65, k, 33], np.int32)
     pairs = np.array([[a, b] for a in range(5) for b in range(5) if a != b], np.int32)
-    outs = []
-    if metric == 1:     # Hamming runs the mutual-rule kernels only on request
-        os.environ["SFM_HAMMING_PATH"] = "mutual"
-    try:
-        for v in ("0", "1"):
-            os.environ["SFM_K1_GRP"] = v
-            try:
-                outs.append(_gpu_match(ctx, desc, n_kp, pairs, metric=metric, cross_check=1,
-                                       ratio=ratio))
-            finally:
-                os.environ.pop("SFM_K1_GRP", None)
-    finally:
-        os.environ.pop("SFM_HAMMING_PATH", None)
-    (c0, m0, d0), (c1, m1, d1) = outs
-    np.testing.assert_array_equal(c0, c1)
-    for p in range(len(pairs)):
-        np.testing.assert_array_equal(m0[p, :c0[p]], m1[p, :c1[p]])
-        np.testing.assert_array_equal(d0[p, :c0[p]], d1[p, :c1[p]])
-    _check_pairs(ctx, desc, n_kp, pairs, metric=metric, cross_check=1, ratio=ratio)
+    paths = ["mutual", "fr"] if (metric == 0 and ratio is not None) else ["mutual"]
+    for path in paths:
+        env = "SFM_L2_PATH" if metric == 0 else "SFM_HAMMING_PATH"
+        os.environ[env] = path
+        try:
+            _check_pairs(ctx, desc, n_kp, pairs, metric=metric, cross_check=1, ratio=ratio)
+        finally:
+            os.environ.pop(env, None)
