@@ -89,13 +89,27 @@ class Reconstruction:
     @property
     def points(self):
         """[n_tr, 3] host copy of the track points (valid where has_point); read-only — the model
-        lives in pts_d, so writing to a copy would be lost (write to pts_d instead)."""
-        return _host_copy(self.pts_d)
+        lives in pts_d, so writing to a copy would be lost (write to pts_d instead).  The copy is
+        cached until pts_d is replaced or changed in place (repeated reads cost one
+        device-to-host copy, not one each)."""
+        return self._host("pts", self.pts_d)
 
     @property
     def has_point(self):
-        """[n_tr] bool host copy: the track has a triangulated point (read-only, see points)."""
-        return _host_copy(self.has_d)
+        """[n_tr] bool host copy: the track has a triangulated point (read-only and cached, see
+        points)."""
+        return self._host("has", self.has_d)
+
+    def _host(self, name, t):
+        if t is None:
+            return None
+        key = (id(t), t.data_ptr(), t._version)   # _version: bumped by every in-place write
+        cache = self.__dict__.setdefault("_host_cache", {})
+        c = cache.get(name)
+        if c is None or c[0] != key or c[2] is not t:
+            c = (key, _host_copy(t), t)
+            cache[name] = c
+        return c[1]
 
 
 def _host_copy(t):

@@ -145,3 +145,23 @@ def test_reg_ransac_finds_pose_with_outliers():
     np.testing.assert_allclose(r["R"], R, atol=5e-3)
     assert np.abs(r["t"] - t).max() < 0.05 * np.linalg.norm(t)
     assert r["mask"][~out].mean() > 0.95 and r["mask"][out].mean() < 0.05
+
+
+def test_reconstruction_host_copies_are_cached_until_the_model_changes():
+    """Reconstruction.points / has_point copy the device model once per change, not
+    once per read; a replaced tensor or an in-place write gives a fresh copy."""
+    import torch
+    import incremental
+    rec = incremental.Reconstruction(3)
+    assert rec.points is None and rec.has_point is None
+    rec.pts_d = torch.zeros(4, 3, dtype=torch.float64)
+    rec.has_d = torch.zeros(4, dtype=torch.bool)
+    p1, p2 = rec.points, rec.points
+    assert p1 is p2 and not p1.flags.writeable
+    rec.pts_d[1, 2] = 5.0                      # in place
+    p3 = rec.points
+    assert p3 is not p1 and p3[1, 2] == 5.0   # (a CPU tensor's copy is a view; on the GPU a copy)
+    rec.has_d[2] = True
+    assert rec.has_point[2] and rec.has_point is rec.has_point
+    rec.pts_d = torch.ones(2, 3, dtype=torch.float64)   # replaced
+    assert rec.points.shape == (2, 3) and rec.points[0, 0] == 1.0
