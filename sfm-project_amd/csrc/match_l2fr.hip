@@ -552,197 +552,6 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
 #endif
 }
 
-// Persistent forward scan (32x32 form, 8 waves x 4 query tiles; -DL2FR_PERSIST builds it as the
-// forward scan).  One block per CU walks the units (pair, query block) of the non-persistent
-// grid with stride gridDim.x (a multiple of 8, so unit v runs on the XCD the hardware would have
-// given block v, keeping the train-image runs per XCD).  Per unit the work is the scan's; what
-// changes is the switch between units, which in the one-block-per-CU launch is exposed (the
-// block's 1024 query rows into registers + the first train stage: 8 % of a block's life at cfg2,
-// profiles/r06/k1_study): during the current unit's last chunk the block stages the next unit's
-// first train chunk into the free buffer and waves 0-3 stage their next 128 query rows each into
-// LDS (64 KB, slot-swizzled), so at the switch waves 0-3 read their query fragments from LDS and
-// only waves 4-7 load theirs from global memory, while waves 0-3 already compute.
-constexpr int PQ_WAVES = 4;  // waves whose next query rows are staged in LDS
-template <int DUMMY>
-__global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_persist_kernel(
-    const uint8_t* __restrict__ desc, int k_max, int k_pad, const int32_t* __restrict__ cinit,
-    const uint8_t* __restrict__ zero_row, int n_qblk, int n_units, const int4* __restrict__ sinfo,
-    int n_blk, int4* __restrict__ out, FwdCls fc) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
-    __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
-    __shared__ __attribute__((aligned(16))) unsigned char qbuf[PQ_WAVES * QT * 32 * D];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
-    const int ppx = (n_units >> 3) / n_qblk;
-    struct Unit { int p, qi, ti, nq, nb, qb; };
-    auto decode = [&](int v, Unit& u) -> bool {   // block-uniform
-        const int l = v >> 3;
-        const int pos = (v & 7) * ppx + l % ppx;
-        u.qb = l / ppx;
-        if (pos >= n_blk) return false;
-        const int4 r = sinfo[pos];
-        u.p = r.x; u.qi = r.y; u.ti = r.z; u.nq = r.w & 0xFFFF; u.nb = r.w >> 16;
-        return u.qb * QB < u.nq && u.nb > 0;
-    };
-    auto next_valid = [&](int v, Unit& u) -> int {
-        for (; v < n_units; v += (int)gridDim.x)
-            if (decode(v, u)) return v;
-        return n_units;
-    };
-    Unit cur, nxt;
-    int v = next_valid((int)blockIdx.x, cur);
-    if (v >= n_units) return;  // block-uniform
-
-    auto stage = [&](const Unit& u, int ch, unsigned char* dst) {
-        const uint8_t* db = desc + (size_t)u.ti * k_max * D;
-#pragma unroll
-        for (int i = 0; i < PIECES; ++i) {
-            const int piece = wave * PIECES + i;
-            const int row = piece * RPP + lane / SLOTS;
-            const int slot = (lane % SLOTS) ^ swz(row);
-            const int j = ch * CHUNK + row;
-            const uint8_t* src = (j < u.nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
-        }
-        if (tid < CHUNK / 4) {
-            const int32_t* src = cinit + (size_t)u.ti * k_pad + ch * CHUNK + tid * 4;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D + wave * 1024),
-                                             16, 0, 0);
-        }
-    };
-    // this wave's 128 query rows of unit u into qbuf (waves < PQ_WAVES): row r, slot s at
-    // s ^ (r & 7), 16 DMA pieces of 8 rows
-    auto stage_queries = [&](const Unit& u) {
-        const uint8_t* da = desc + (size_t)u.qi * k_max * D;
-        const int qbase = u.qb * QB + wave * QT * 32;
-        unsigned char* dst = qbuf + wave * (QT * 32 * D);
-#pragma unroll 1
-        for (int i = 0; i < QT * 32 * D / 1024; ++i) {
-            const int row = i * RPP + lane / SLOTS;
-            const int slot = (lane % SLOTS) ^ (row & 7);
-            const int e = qbase + row;
-            const uint8_t* src = (e < u.nq) ? da + (size_t)e * D + slot * 16 : zero_row + slot * 16;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + i * 1024), 16, 0, 0);
-        }
-    };
-    v4i bq[QT][NK];
-    int tb[QT], ts[QT], t1[QT];
-    auto load_queries_global = [&](const Unit& u) {
-        const uint8_t* da = desc + (size_t)u.qi * k_max * D;
-        const int qbase = u.qb * QB + wave * QT * 32;
-#pragma unroll
-        for (int c = 0; c < QT; ++c) {
-            const int e = qbase + c * 32 + r32;
-            const v4i* src = (const v4i*)((e < u.nq) ? da + (size_t)e * D + (D / 2) * h
-                                                     : zero_row + (D / 2) * h);
-#pragma unroll
-            for (int s = 0; s < NK; ++s) bq[c][s] = src[s];
-        }
-    };
-    auto load_queries_lds = [&]() {
-        const unsigned char* src = qbuf + wave * (QT * 32 * D);
-#pragma unroll
-        for (int c = 0; c < QT; ++c) {
-            const int row = c * 32 + r32;
-#pragma unroll
-            for (int s = 0; s < NK; ++s)
-                bq[c][s] = *(const v4i*)(src + row * D + ((((SLOTS / 2) * h + s) ^ (row & 7)) << 4));
-        }
-    };
-    // the first unit: everything from global memory
-    load_queries_global(cur);
-    stage(cur, 0, lds0);
-    __syncthreads();
-    int buf = 0;  // stage buffer of the current chunk
-    v16i acc[QT];
-    for (;;) {
-        const int vn = next_valid(v + (int)gridDim.x, nxt);
-        const bool more = vn < n_units;
-        const int qbase = cur.qb * QB + wave * QT * 32;
-        const bool active = qbase < cur.nq;  // wave-uniform
-#pragma unroll
-        for (int c = 0; c < QT; ++c) { tb[c] = INT_MIN; ts[c] = INT_MIN; t1[c] = 0; }
-        const int n_chunk = (cur.nb + CHUNK - 1) / CHUNK;
-        for (int ch = 0; ch < n_chunk; ++ch) {
-            unsigned char* curb = buf ? lds1 : lds0;
-            unsigned char* nxtb = buf ? lds0 : lds1;
-            if (ch + 1 < n_chunk) {
-                stage(cur, ch + 1, nxtb);
-            } else if (more) {   // the next unit's first chunk and (waves 0-3) its query rows
-                stage(nxt, 0, nxtb);
-                if (wave < PQ_WAVES) stage_queries(nxt);
-            }
-            const int nt = min(NT, (cur.nb - ch * CHUNK + 31) >> 5);
-            if (active) {
-                const int* Ci = (const int*)(curb + CHUNK * D);
-                auto load_tile = [&](int tt, v4i (&af)[NK], v16i& init) {
-                    const int row = tt * 32 + r32;
-                    const int sw = swz(row);
-#pragma unroll
-                    for (int s = 0; s < NK; ++s)
-                        af[s] = *(const v4i*)(curb + row * D + ((((SLOTS / 2) * h + s) ^ sw) << 4));
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const v4i cv = *(const v4i*)(Ci + tt * 32 + 8 * g + 4 * h);
-                        init[4 * g + 0] = cv.x; init[4 * g + 1] = cv.y;
-                        init[4 * g + 2] = cv.z; init[4 * g + 3] = cv.w;
-                    }
-                };
-                v4i af[NK];
-                v16i init;
-                load_tile(0, af, init);
-                for (int tt = 0; tt < nt; ++tt) {
-                    const int gt = ch * NT + tt;
-                    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                    for (int s = 0; s < NK; ++s)
-#pragma unroll
-                        for (int c = 0; c < QT; ++c)
-                            acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[c][s],
-                                                                            s == 0 ? init : acc[c], 0, 0, 0);
-                    __builtin_amdgcn_s_setprio(0);
-                    if (tt + 1 < nt) load_tile(tt + 1, af, init);
-#pragma unroll
-                    for (int u = 0; u < QT; ++u) {
-                        const int o = tb[u];
-#pragma unroll
-                        for (int r = 0; r < 16; r += 2) top2_insert(tb[u], ts[u], acc[u][r], acc[u][r + 1]);
-                        t1[u] = (tb[u] != o) ? gt : t1[u];
-                    }
-                }
-            }
-            __syncthreads();
-            buf ^= 1;
-        }
-        if (active) {
-#pragma unroll
-            for (int c = 0; c < QT; ++c) {
-                const int P1 = __shfl_xor(tb[c], 32), P2 = __shfl_xor(ts[c], 32),
-                          PT = __shfl_xor(t1[c], 32);
-                const int e1 = max(tb[c], P1);
-                const int e2 = max(min(tb[c], P1), max(ts[c], P2));
-                const int t = tb[c] > P1 ? t1[c] : (P1 > tb[c] ? PT : min(t1[c], PT));
-                const int e = qbase + c * 32 + r32;
-                if (h == 0 && e < cur.nq) {
-                    const int4 rec = make_int4(e1, e2, t, 0);
-                    out[(size_t)cur.p * k_pad + e] = rec;
-                    const unsigned char st = classify(rec, fc.norm[(size_t)cur.qi * k_pad + e],
-                                                      fc.rnum, fc.rden, fc.max_dist);
-                    fc.cls[(size_t)cur.p * k_pad + e] = st == ST_CAND ? (uint8_t)t : (uint8_t)0xFF;
-                    if (st != ST_CAND) fc.qst[(size_t)cur.p * k_pad + e] = make_int4(st, 0, 0, 0);
-                }
-            }
-        }
-        if (!more) break;
-        // the switch: the next unit's first chunk is in the other buffer (landed: the last
-        // chunk's barrier waited for every wave's DMA); query fragments from LDS (waves 0-3) or
-        // global memory (waves 4-7, whose loads overlap waves 0-3's first tiles)
-        if (wave < PQ_WAVES) load_queries_lds();
-        else load_queries_global(nxt);
-        cur = nxt;
-        v = vn;
-    }
-}
-
 // Exact (d1, j1, d2) of one query over all trains (multiset second, lowest-index j1), block-wide.
 // Returns through LDS slot `res` (valid for every thread after the call).
 struct Top2 { long long b1; int j1; long long b2; };
@@ -1332,19 +1141,10 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     // consumed by the compaction before the reverse scan writes there.
     int4* qst = rev;
     const FwdCls fc{norm, prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, qst, cls};
-#if defined(L2FR_PERSIST) && !L2FR_MFMA16 && L2FR_WAVES == 8 && L2FR_QT == 4
-    {   // one block per CU (VGPR-bound), a multiple of 8 blocks
-        const int pgrid = std::max(8, std::min(grid, ctx->n_cu / 8 * 8));
-        hipLaunchKernelGGL(l2fr_scan_persist_kernel<0>, dim3(pgrid), dim3(SCAN_THREADS), 0, st, desc_i8,
-                           k_max, k_pad, cinit, zero_row, n_qblk, grid, (const int4*)sinfo_f, n_blk,
-                           fwd, fc);
-    }
-#else
     hipLaunchKernelGGL(l2fr_scan_kernel<false>, dim3(grid), dim3(SCAN_THREADS), 0, st, desc_i8, n_kp, k_max,
                        k_pad, cinit, zero_row, pairs, n_qblk, sord_f, (const int4*)sinfo_f, n_blk,
                        (const int4*)nullptr,
                        (const int32_t*)nullptr, fwd, fc);
-#endif
     SFM_HIP_CHECK(hipGetLastError());
     const char* dbg = getenv("SFM_L2FR_DEBUG");
     const int dmode = dbg ? atoi(dbg) : 0;
