@@ -770,6 +770,35 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / n
+    def timed_graph(fn, n):
+        """fn captured once in a HIP graph (torch.cuda.graph; the library launches on torch's
+        current stream, which is the capturing one), then replayed n times between events: the
+        GPU time of fn's kernels without the host's per-call launch overhead (eager K3 calls are
+        host-bound in chunk mode: ~20 Python / ctypes calls per linearisation).  None if the
+        capture fails."""
+        try:
+            fn()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                fn()                      # warm on the side stream (sizes the workspace)
+                with torch.cuda.graph(g, stream=s):
+                    fn()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g.replay()
+            e0.record()
+            for _ in range(n):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / n
+        except Exception:  # noqa: BLE001
+            return None
+
     def measure(P):
         jtj = timed(lambda: P.linearize(c, p, 2.0), reps)
         lin = P.linearize(c, p, 2.0)
@@ -777,11 +806,13 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
         sn = timed(lambda: P.solve(lin, 1e-3, max_iter=cg, tol=0.0, poll=-1), max(reps // 4, 2))
         return jtj, (sn - s0) / cg
     jtj_ms, it_ms = measure(P)
+    jtj_graph = timed_graph(lambda: P.linearize(c, p, 2.0), reps)
     # the production forms: bundle_adjust's sharding-invariant chunk sums (reconstruction.BAChunks)
     # and, where schur_rule takes it, the explicit reduced camera system on top
     nck = R.ba_chunk_count()
-    jtj_ck, it_ck = measure(R.BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device,
-                                        chunks=nck)) if nck else (None, None)
+    Pck = R.BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device, chunks=nck) if nck else None
+    jtj_ck, it_ck = measure(Pck) if nck else (None, None)
+    jtj_ck_graph = timed_graph(lambda: Pck.linearize(c, p, 2.0), reps) if nck else None
     explicit = None
     if nck:
         Pe = R.BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device, chunks=nck)
@@ -816,14 +847,22 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
     cg_b = n_obs * (192 + 128 + 8) + n_pt * (72 + 4) + n_cam * (64 * 8 + 4 * 8 * 8)
     return {"n_cam": n_cam, "n_pt": n_pt, "n_obs": n_obs,
             "k3": {"ms": jtj_ms, "bytes": k3_b, "achieved_GBs": k3_b / (jtj_ms * 1e-3) / 1e9,
-                   "frac": k3_b / (jtj_ms * 1e-3) / PEAK_HBM},
+                   "frac": k3_b / (jtj_ms * 1e-3) / PEAK_HBM,
+                   "graph_ms": jtj_graph,
+                   "graph_frac": k3_b / (jtj_graph * 1e-3) / PEAK_HBM if jtj_graph else None},
             "cg_iteration": {"ms": it_ms, "bytes": cg_b,
                              "achieved_GBs": cg_b / (it_ms * 1e-3) / 1e9 if it_ms > 0 else None,
                              "frac": cg_b / (it_ms * 1e-3) / PEAK_HBM if it_ms > 0 else None},
             "chunked": None if jtj_ck is None else {
                 "chunks": nck, "note": "bundle_adjust's form (sharding-invariant chunk sums); "
                                        "the same algorithmic bytes",
-                "k3": {"ms": jtj_ck, "frac": k3_b / (jtj_ck * 1e-3) / PEAK_HBM},
+                "k3": {"ms": jtj_ck, "frac": k3_b / (jtj_ck * 1e-3) / PEAK_HBM,
+                       "graph_ms": jtj_ck_graph,
+                       "graph_frac": (k3_b / (jtj_ck_graph * 1e-3) / PEAK_HBM
+                                      if jtj_ck_graph else None),
+                       "note": "ms: eager calls (host-bound in chunk mode: the Python / ctypes "
+                               "launch path of one linearisation outlasts its kernels); graph_ms: "
+                               "the same call replayed as a HIP graph = its kernels' GPU time"},
                 "cg_iteration": {"ms": it_ck,
                                  "frac": cg_b / (it_ck * 1e-3) / PEAK_HBM if it_ck > 0 else None}},
             "explicit_schur": explicit,

@@ -728,6 +728,44 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
 
 // Thread per (camera, component): α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera
 // r·z (slot (k+1)&1) and r·r (slot (k+1)&1).  A breakdown (p·q <= 0) stops the iteration.
+// One camera component of the CG vector update (thread gi = 8 c + i; the 8 components of a camera
+// are 8 consecutive lanes): x += α p; r -= α q; z = M r; the camera's r·z and r·r into slot
+// (k+1)&1 (rr = 0 on a breakdown).  Shared by bas_pcg_vec and the one-workgroup CG.
+__device__ __forceinline__ void pcg_vec_component(int gi, int k, int n_cam, const double* __restrict__ Mc,
+                                                  double* __restrict__ x, double* __restrict__ r,
+                                                  double* __restrict__ z, const double* __restrict__ pv,
+                                                  const double* __restrict__ q, double alpha,
+                                                  bool breakdown, double* __restrict__ rzc,
+                                                  double* __restrict__ rrc) {
+    const int c = gi >> 3, i = gi & 7;
+    const bool valid = c < n_cam;
+    const int s1 = (k + 1) & 1;
+    double ri = 0.0;
+    if (valid) {
+        const size_t kk = 8 * (size_t)c + i;
+        x[kk] += alpha * pv[kk];
+        ri = r[kk] - alpha * q[kk];
+        r[kk] = ri;
+    }
+    double zi = 0.0;
+    const double* M = Mc + 64 * (size_t)(valid ? c : 0) + 8 * i;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zi += M[j] * __shfl(ri, (threadIdx.x & ~7) + j, 64);
+    double rz = ri * zi, rr = ri * ri;
+    rz += __shfl_down(rz, 4, 8); rr += __shfl_down(rr, 4, 8);
+    rz += __shfl_down(rz, 2, 8); rr += __shfl_down(rr, 2, 8);
+    rz += __shfl_down(rz, 1, 8); rr += __shfl_down(rr, 1, 8);
+    if (valid) {
+        z[8 * (size_t)c + i] = zi;
+        if (i == 0) {
+            rzc[(size_t)s1 * n_cam + c] = rz;
+            rrc[(size_t)s1 * n_cam + c] = breakdown ? 0.0 : rr;
+        }
+    }
+}
+
+// Thread per (camera, component): α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera
+// r·z (slot (k+1)&1) and r·r (slot (k+1)&1).  A breakdown (p·q <= 0) stops the iteration.
 __global__ __launch_bounds__(256) void bas_pcg_vec(
     int k, int n_cam, const double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, const double* __restrict__ pv,
@@ -751,28 +789,7 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
     const double pqs = canon_sum(pq, n_cam, red4);
     const bool breakdown = !(pqs > 0.0);
     const double alpha = breakdown ? 0.0 : rz_k / pqs;
-    double ri = 0.0;
-    if (valid) {
-        const size_t kk = 8 * (size_t)c + i;
-        x[kk] += alpha * pv[kk];
-        ri = r[kk] - alpha * q[kk];
-        r[kk] = ri;
-    }
-    double zi = 0.0;
-    const double* M = Mc + 64 * (size_t)(valid ? c : 0) + 8 * i;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) zi += M[j] * __shfl(ri, (threadIdx.x & ~7) + j, 64);
-    double rz = ri * zi, rr = ri * ri;
-    rz += __shfl_down(rz, 4, 8); rr += __shfl_down(rr, 4, 8);
-    rz += __shfl_down(rz, 2, 8); rr += __shfl_down(rr, 2, 8);
-    rz += __shfl_down(rz, 1, 8); rr += __shfl_down(rr, 1, 8);
-    if (valid) {
-        z[8 * (size_t)c + i] = zi;
-        if (i == 0) {
-            rzc[(size_t)s1 * n_cam + c] = rz;
-            rrc[(size_t)s1 * n_cam + c] = breakdown ? 0.0 : rr;
-        }
-    }
+    pcg_vec_component(gi, k, n_cam, Mc, x, r, z, pv, q, alpha, breakdown, rzc, rrc);
     if (gi == 0) st->iter = k + 1;
     publish_next(k, n_cam, rzc, rrc, tol, st, gridDim.x, red4);
 }
@@ -863,6 +880,60 @@ __global__ __launch_bounds__(256) void bas_schur_tree(int n_slot, const int32_t*
 // another writes); the row's blocks in row_ent order, 8 lanes per block (lane r: row r of the
 // block, or column r for a transposed slot), blocks g, g + 8, ... per lane group, then a fixed
 // xor tree over the 8 groups; q_c = S_cc p_c - Σ T p_j, p_k stored, p·q per camera.
+// One block row c of the explicit product (one wave; shared by bas_pcg_spmv and the one-workgroup
+// CG): p_k = z_k + β_k p_{k-1} (p_{k-1} from the other parity slot of pv2), the row's blocks in
+// row_ent order, 8 lanes per block (lane r: row r of the block, or column r for a transposed
+// slot), blocks g, g + 8, ... per lane group, then a fixed xor tree over the 8 groups;
+// q_c = S_cc p_c - Σ T p_j, p_k stored, p·q of the camera.
+__device__ __forceinline__ void schur_spmv_row(int c, int lane, int k, int n_cam, double beta,
+                                               const int32_t* __restrict__ row_ptr,
+                                               const int32_t* __restrict__ row_ent,
+                                               const int32_t* __restrict__ slot_cam,
+                                               const double* __restrict__ T,
+                                               const double* __restrict__ Scc,
+                                               const double* __restrict__ z, double* __restrict__ pv2,
+                                               double* __restrict__ q, double* __restrict__ pq) {
+    const double* pold = pv2 + (size_t)((k + 1) & 1) * 8 * n_cam;
+    double* pnew = pv2 + (size_t)(k & 1) * 8 * n_cam;
+    const int g = lane >> 3, r = lane & 7;
+    const int e0 = row_ptr[c], e1 = row_ptr[c + 1];
+    double s = 0.0;
+    for (int e = e0 + g; e < e1; e += 8) {
+        const int ent = row_ent[e];
+        const int slot = ent >> 1, tr = ent & 1;
+        const int j = slot_cam[2 * slot + (tr ? 0 : 1)];   // the other camera of the block
+        const double* Tb = T + 64 * (size_t)slot;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const double pj = z[8 * (size_t)j + m] + beta * pold[8 * (size_t)j + m];
+            s += (tr ? Tb[8 * m + r] : Tb[8 * r + m]) * pj;
+        }
+    }
+    s += __shfl_xor(s, 8, 64);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    double pc[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) pc[m] = z[8 * (size_t)c + m] + beta * pold[8 * (size_t)c + m];
+    double sp = 0.0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) sp += Scc[64 * (size_t)c + 8 * r + m] * pc[m];
+    const double qi = sp - s;
+    double pr = 0.0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) pr = (m == r) ? pc[m] : pr;
+    if (lane < 8) {
+        pnew[8 * (size_t)c + r] = pr;
+        q[8 * (size_t)c + r] = qi;
+    }
+    double v = pr * qi;
+    v += __shfl_down(v, 4, 8);
+    v += __shfl_down(v, 2, 8);
+    v += __shfl_down(v, 1, 8);
+    if (lane == 0) pq[c] = v;
+}
+
+// Explicit CG product (bas_point + bas_pcg_camera's role once S is formed): wave per block row.
 __global__ __launch_bounds__(256) void bas_pcg_spmv(
     int k, int n_cam, const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ row_ent,
     const int32_t* __restrict__ slot_cam, const double* __restrict__ T,
@@ -871,45 +942,45 @@ __global__ __launch_bounds__(256) void bas_pcg_spmv(
     const Scalars sc = read_scalars(st);
     if (sc.done) return;   // the same for every block (published before the launch)
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (c < n_cam) {
-        const double* pold = pv2 + (size_t)((k + 1) & 1) * 8 * n_cam;
-        double* pnew = pv2 + (size_t)(k & 1) * 8 * n_cam;
-        const int g = lane >> 3, r = lane & 7;
-        const int e0 = row_ptr[c], e1 = row_ptr[c + 1];
-        double s = 0.0;
-        for (int e = e0 + g; e < e1; e += 8) {
-            const int ent = row_ent[e];
-            const int slot = ent >> 1, tr = ent & 1;
-            const int j = slot_cam[2 * slot + (tr ? 0 : 1)];   // the other camera of the block
-            const double* Tb = T + 64 * (size_t)slot;
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const double pj = z[8 * (size_t)j + m] + sc.beta * pold[8 * (size_t)j + m];
-                s += (tr ? Tb[8 * m + r] : Tb[8 * r + m]) * pj;
-            }
+    if (c < n_cam)
+        schur_spmv_row(c, lane, k, n_cam, sc.beta, row_ptr, row_ent, slot_cam, T, Scc, z, pv2, q, pq);
+}
+
+// The whole explicit CG in ONE workgroup (small reduced systems, n_cam <= CG1_MAX_CAM): the same
+// per-row product, per-component update and canonical sums as bas_pcg_spmv + bas_pcg_vec +
+// publish_next, in the same association, so the iterates, the iteration count and the state are
+// the same bits — without two launches per iteration and the host polls between them (16 waves:
+// 16 block rows per pass of the product, 128 cameras per pass of the update).
+constexpr int CG1_MAX_CAM = 256;
+__global__ __launch_bounds__(1024) void bas_schur_cg1(
+    int max_iter, int n_cam, const int32_t* __restrict__ row_ptr,
+    const int32_t* __restrict__ row_ent, const int32_t* __restrict__ slot_cam,
+    const double* __restrict__ T, const double* __restrict__ Scc, const double* __restrict__ Mc,
+    double* __restrict__ x, double* __restrict__ r, double* __restrict__ z,
+    double* __restrict__ pv2, double* __restrict__ q, double* __restrict__ pq,
+    double* __restrict__ rzc, double* __restrict__ rrc, PcgState* __restrict__ st, double tol) {
+    __shared__ double red4[12];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    Scalars sc = read_scalars(st);   // iteration 0's, from bas_pcg_init
+    const int n8 = (8 * n_cam + 1023) & ~1023;   // whole passes: every 8-lane group is one camera
+    for (int k = 0; k < max_iter && !sc.done; ++k) {
+        for (int c = wave; c < n_cam; c += 16)
+            schur_spmv_row(c, lane, k, n_cam, sc.beta, row_ptr, row_ent, slot_cam, T, Scc, z, pv2, q, pq);
+        __syncthreads();
+        const double pqs = canon_sum(pq, n_cam, red4);
+        const bool breakdown = !(pqs > 0.0);
+        const double alpha = breakdown ? 0.0 : sc.rz / pqs;
+        const double* pv = pv2 + (size_t)(k & 1) * 8 * n_cam;
+        for (int gi = tid; gi < n8; gi += 1024)
+            pcg_vec_component(gi, k, n_cam, Mc, x, r, z, pv, q, alpha, breakdown, rzc, rrc);
+        __syncthreads();
+        sc = pcg_scalars(k + 1, n_cam, rzc, rrc, st->bb, tol, red4);
+        if (tid == 0) {
+            st->iter = k + 1;
+            st->beta = sc.beta;
+            st->rz = sc.rz;
+            st->done = sc.done ? 1 : 0;
         }
-        s += __shfl_xor(s, 8, 64);
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        double pc[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) pc[m] = z[8 * (size_t)c + m] + sc.beta * pold[8 * (size_t)c + m];
-        double sp = 0.0;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) sp += Scc[64 * (size_t)c + 8 * r + m] * pc[m];
-        const double qi = sp - s;
-        double pr = 0.0;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) pr = (m == r) ? pc[m] : pr;
-        if (lane < 8) {
-            pnew[8 * (size_t)c + r] = pr;
-            q[8 * (size_t)c + r] = qi;
-        }
-        double v = pr * qi;
-        v += __shfl_down(v, 4, 8);
-        v += __shfl_down(v, 2, 8);
-        v += __shfl_down(v, 1, 8);
-        if (lane == 0) pq[c] = v;
     }
 }
 
@@ -1522,6 +1593,17 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     SFM_HIP_CHECK(hipStreamIsCapturing(st, &cap));
     const int poll = cap != hipStreamCaptureStatusNone ? -1
                    : prm->poll == 0 ? SFM_BA_POLL_DEFAULT : prm->poll;
+    // a small explicit system: the whole CG in one workgroup, one launch, no polls (same bits)
+    static const bool cg1_off = [] {
+        const char* e = getenv("SFM_BA_CG1");
+        return e && e[0] == '0';
+    }();
+    if (ex && n_cam <= CG1_MAX_CAM && !cg1_off && prm->max_iter > 0) {
+        hipLaunchKernelGGL(bas_schur_cg1, dim3(1), dim3(1024), 0, st, prm->max_iter, n_cam,
+                           ctx->ba_row_ptr, ctx->ba_row_ent, ctx->ba_slot_cam, w.T, w.Scc, w.Mc, dc,
+                           w.r, w.z, w.pv2, w.q, w.pq, w.rzc, w.rrc, w.state, tol);
+        SFM_HIP_CHECK(hipGetLastError());
+    } else
     for (int k = 0; k < prm->max_iter; ++k) {
         // state->done is set by bas_pcg_point of the first iteration after convergence: once it
         // reads 1, every later iteration would exit at once, so stop enqueueing them

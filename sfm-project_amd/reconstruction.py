@@ -11,6 +11,8 @@ next-view registration remain "next".
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 
 import sfmcore
@@ -367,6 +369,7 @@ class BAProblem:
         self.ctx = sfmcore.context(device)
         self.chunks = None
         self.schur = None   # SchurSpec (set_schur), the explicit reduced camera system
+        self._bound = False
         if chunks is not None and chunks != 0:
             if isinstance(chunks, int):
                 cpt, cob = shard_cuts_device(self.pt_idx, n_pt, chunks, ptr=self.pt_ptr)
@@ -396,8 +399,8 @@ class BAProblem:
 
     def _call(self, fn, *a, **kw):
         """fn under this problem's chunk mode and explicit-Schur structure (set on the shared
-        context, then cleared)."""
-        if self.chunks is None:
+        context, then cleared; inside bind() they stay set)."""
+        if self.chunks is None or self._bound:
             return fn(*a, **kw)
         self.ctx.ba_set_chunks(self.chunks)
         if self.schur is not None:
@@ -405,6 +408,26 @@ class BAProblem:
         try:
             return fn(*a, **kw)
         finally:
+            self.ctx.ba_set_chunks(None)
+            if self.schur is not None:
+                self.ctx.ba_set_schur(None)
+
+    @contextlib.contextmanager
+    def bind(self):
+        """Keep this problem's chunk mode / Schur structure set on the shared context for a
+        block of calls (an LM loop: 4 ctypes calls fewer per linearise / solve / cost).  No other
+        BAProblem may use the context inside the block."""
+        if self.chunks is None or self._bound:
+            yield self
+            return
+        self.ctx.ba_set_chunks(self.chunks)
+        if self.schur is not None:
+            self.ctx.ba_set_schur(self.schur)
+        self._bound = True
+        try:
+            yield self
+        finally:
+            self._bound = False
             self.ctx.ba_set_chunks(None)
             if self.schur is not None:
                 self.ctx.ba_set_schur(None)
@@ -625,6 +648,41 @@ def _gather_rows(t, counts, group):
     pad[:t.shape[0]] = t
     g = match_graph._gather(pad.reshape(-1), world, group).reshape((world, mx) + tuple(inner))
     return torch.cat([g[r, :counts[r]] for r in range(world)]).contiguous()
+
+
+def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
+    """bundle_adjust's Levenberg-Marquardt iterations (the step rule in its docstring); one host
+    read of 7 scalars per step.  Returns (cams, pts, history)."""
+    import torch
+    lam, nu = lam0, 2.0
+    hist = []
+    old = float(cost(cams_d, pts_d).item())
+    lin = linearize(cams_d, pts_d)
+    for _ in range(max_iter):
+        dc, dp, sinfo = solve(lin, lam)
+        c2, p2 = upd.update(cams_d, dc, pts_d, dp)
+        new_t = cost(c2, p2)
+        vals = torch.cat([sinfo, new_t]).cpu().numpy()      # the one host sync of the step
+        it, gd, q, new = int(vals[0]), float(vals[2]), float(vals[3]), float(vals[5])
+        pred = -(gd + 0.5 * q)
+        if new < old and pred > 0:
+            rho = (old - new) / pred
+            cams_d, pts_d = c2, p2
+            lam *= max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3)
+            nu = 2.0
+            hist.append((new, lam, True, it))
+            done = old - new <= ftol * old
+            old = new
+            if done:
+                break
+            lin = linearize(cams_d, pts_d)
+        else:
+            lam *= nu
+            nu *= 2.0
+            hist.append((old, lam, False, it))
+            if lam > 1e16:
+                break
+    return cams_d, pts_d, hist
 
 
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
@@ -871,34 +929,12 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
         torch.cuda.synchronize(prob.dev)
         t_lm = time.perf_counter()
         info["setup_s"] = t_lm - t_entry    # problem upload / CSR build before the first LM step
-    lam, nu = lam0, 2.0
-    hist = []
-    old = float(cost(cams_d, pts_d).item())
-    lin = linearize(cams_d, pts_d)
-    for _ in range(max_iter):
-        dc, dp, sinfo = solve(lin, lam)
-        c2, p2 = upd.update(cams_d, dc, pts_d, dp)
-        new_t = cost(c2, p2)
-        vals = torch.cat([sinfo, new_t]).cpu().numpy()      # the one host sync of the step
-        it, gd, q, new = int(vals[0]), float(vals[2]), float(vals[3]), float(vals[5])
-        pred = -(gd + 0.5 * q)
-        if new < old and pred > 0:
-            rho = (old - new) / pred
-            cams_d, pts_d = c2, p2
-            lam *= max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3)
-            nu = 2.0
-            hist.append((new, lam, True, it))
-            done = old - new <= ftol * old
-            old = new
-            if done:
-                break
-            lin = linearize(cams_d, pts_d)
-        else:
-            lam *= nu
-            nu *= 2.0
-            hist.append((old, lam, False, it))
-            if lam > 1e16:
-                break
+    # one problem on the context for the whole loop (replicated: two alternate, so per call)
+    bound = (prob.bind() if full is None and os.environ.get("SFM_BA_BIND", "1") != "0"
+             else contextlib.nullcontext())
+    with bound:
+        cams_d, pts_d, hist = _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0,
+                                       max_iter, ftol)
     if info is not None:
         info["lm_s"] = time.perf_counter() - t_lm   # the loop ends in a host sync (the last step)
     if reproj_err and info is not None:

@@ -165,6 +165,7 @@ class Context:
         h = C.c_void_p()
         _check(self.lib.sfm_ctx_create(device, C.byref(h)))
         self.handle = h
+        self._stream = None   # the torch stream last set on the context (_bind_stream)
 
     def close(self):
         if getattr(self, "handle", None):
@@ -178,8 +179,12 @@ class Context:
             pass
 
     def _bind_stream(self):
+        # only this wrapper sets the context's stream, so an unchanged torch stream is a no-op
+        # (sfm_ctx_set_stream returns at once for it) and skips the ctypes call
         s = self.torch.cuda.current_stream(self.device).cuda_stream
-        _check(self.lib.sfm_ctx_set_stream(self.handle, C.c_void_p(s)))
+        if s != self._stream:
+            _check(self.lib.sfm_ctx_set_stream(self.handle, C.c_void_p(s)))
+            self._stream = s
 
     def sync(self):
         _check(self.lib.sfm_ctx_sync(self.handle))

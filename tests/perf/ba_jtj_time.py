@@ -1,7 +1,7 @@
 """Times K3 (sfm_ba_jtj) and the trial cost, unchunked and in chunk mode, at one BA size.
 
 Usage: python tests/perf/ba_jtj_time.py [n_cam n_pt obs_per_pt]   (SFM_BA_CKW: camera waves per
-camera in chunk mode).  Prints one JSON line; the chunked U / g_c / V / cost are checked equal to
+camera in chunk mode; BA_JTJ_ONLY=plain|chunked times one form only, for PMC passes).  Prints one JSON line; the chunked U / g_c / V / cost are checked equal to
 the unchunked ones within 1e-9 relative (the sums associate differently)."""
 import json
 import os
@@ -38,6 +38,11 @@ def main():
     Pc = R.BAProblem(*args, chunks=R.BA_CHUNKS)
     T = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float64)).cuda()
     cams, pts = T(prob["cams"]), T(prob["pts"])
+    only = os.environ.get("BA_JTJ_ONLY")   # "plain" / "chunked": one form only (PMC passes)
+    if only:
+        Q = P if only == "plain" else Pc
+        print(json.dumps({"only": only, "jtj_ms": timed(lambda: Q.linearize(cams, pts), 20)}))
+        return
     out = {"n_cam": n_cam, "n_pt": n_pt, "n_obs": len(prob["cam_idx"]),
            "ckw": os.environ.get("SFM_BA_CKW", "default"),
            "jtj_ms": timed(lambda: P.linearize(cams, pts), 20),

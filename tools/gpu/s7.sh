@@ -31,3 +31,13 @@ PY
 done
 cat $O/pmc.txt
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/test_gpu_bench.py::test_bench_cfg4_line_carries_cfg5_at_two_ranks tests/test_gpu_ba_sharded.py::test_ba_sharded_more_ranks_than_chunks tests/test_gpu_ransac.py::test_ransac_stats_identity > $O/pytest_new.log 2>&1; echo "new tests rc=$?"; grep -E "PASS|FAIL|Error|error" $O/pytest_new.log | tail -20
+for r in 1 2; do
+  for v in base mumprio; do
+    SFMCORE_LIB=$(lib $v) K1_ONLY_BENCH_RULE=1 timeout -k 10 120 python tests/perf/k1_time.py 2>&1 | grep "xc=" | sed "s/^/$v cfg3 /" >> $O/mu_ab.txt || exit 1
+  done
+done
+cat $O/mu_ab.txt
+for v in base mumprio m16w4; do
+  SFMCORE_LIB=$(lib $v) timeout -k 10 300 python tests/perf/k1_mutual_ab.py >> $O/mutual_fr_cfg4.jsonl || exit 1
+done
+cat $O/mutual_fr_cfg4.jsonl
