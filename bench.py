@@ -773,9 +773,8 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
     def timed_graph(fn, n):
         """fn captured once in a HIP graph (torch.cuda.graph; the library launches on torch's
         current stream, which is the capturing one), then replayed n times between events: the
-        GPU time of fn's kernels without the host's per-call launch overhead (eager K3 calls are
-        host-bound in chunk mode: ~20 Python / ctypes calls per linearisation).  None if the
-        capture fails."""
+        GPU time of fn's kernels without the host's per-call launch path (a cross-check that the
+        eager timing is not host-bound).  None if the capture fails."""
         try:
             fn()
             torch.cuda.synchronize()
@@ -860,9 +859,8 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
                        "graph_ms": jtj_ck_graph,
                        "graph_frac": (k3_b / (jtj_ck_graph * 1e-3) / PEAK_HBM
                                       if jtj_ck_graph else None),
-                       "note": "ms: eager calls (host-bound in chunk mode: the Python / ctypes "
-                               "launch path of one linearisation outlasts its kernels); graph_ms: "
-                               "the same call replayed as a HIP graph = its kernels' GPU time"},
+                       "note": "ms: eager calls; graph_ms: the same call replayed as a HIP "
+                               "graph (its kernels' GPU time, no host launch path)"},
                 "cg_iteration": {"ms": it_ck,
                                  "frac": cg_b / (it_ck * 1e-3) / PEAK_HBM if it_ck > 0 else None}},
             "explicit_schur": explicit,

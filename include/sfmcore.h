@@ -226,6 +226,10 @@ typedef struct sfm_ba_solve_params {
                          capturable in a hip graph (all max_iter iterations are enqueued, the
                          converged ones exit at once).  Results are identical either way.
                          (sfm_version 1 read 0 as "never"; version 2 restores 0 = poll.) */
+    int32_t poll_first; /* > 0: the first poll at iteration poll_first, then every `poll` (a
+                         caller that expects about as many iterations as its previous solve took
+                         polls once, there, instead of at every multiple of `poll`); 0 = at
+                         `poll` (sfm_version 5; earlier versions had no such field) */
 } sfm_ba_solve_params;
 #define SFM_BA_POLL_DEFAULT 8
 
@@ -244,7 +248,8 @@ int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n_obs,
  * no other sfm_* call on this context in between — the stages share its workspace):
  *   SETUP           -> all-reduce comm[0, 44 n_cam)  -> SETUP_FINISH
  *   for k = 0 .. max_iter-1:
- *     [every prm->poll > 0 iterations, k > 0: POLL -> *done (host int32); stop if 1]
+ *     [every prm->poll > 0 iterations, k > 0 (from prm->poll_first when > 0): POLL -> *done
+ *      (host int32); stop if 1]
  *     ITER(k)       -> all-reduce comm[0, 8 n_cam)   -> ITER_FINISH(k)
  *   BACKSUB         -> all-reduce comm[0, 2)         -> MODEL   (dc, dp, info as sfm_ba_solve)
  * After each all-reduce every camera-space value is replicated, so every rank takes the same CG

@@ -301,11 +301,13 @@ __device__ __forceinline__ void camera_wave(
     double acc[NU];  // entries outside [hw*NUH, hw*NUH + NUH) are dead when CH > 1
     const double* cam = cams + 8 * (size_t)c;
     double R[9];
+    auto rotation = [&]() {
 #ifdef BA_ABL_NOROT  // ablation (timing only)
-    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
 #else
-    rotmat(cam[0], cam[1], cam[2], R);
+        rotmat(cam[0], cam[1], cam[2], R);
 #endif
+    };
     // CAM_MLP observations per step: the dependent gathers (cam_obs -> pt_idx -> point, uv) of
     // all of them are issued before any is used (memory-level parallelism; latency-bound waves)
     auto accumulate = [&](int e0, int e1) {
@@ -354,14 +356,30 @@ __device__ __forceinline__ void camera_wave(
     constexpr int NR = CH == 1 ? NU : NUH;  // live sums of this wave
     const int t0 = CH == 1 ? 0 : hw * NUH;
     if (cb) {   // chunk mode: chunks s, s + G, ... (sfm_ba_set_chunks)
+        // A camera without observations in a chunk stores its zero partial directly, and the
+        // rotation is formed only by a wave with work: with local visibility (cfg5: a camera's
+        // observations in 1.06 of 8 chunks) 7 of 8 waves are such, and their rotation, empty
+        // sweep and 44-sum tree made chunk mode's camera half 34 % slower than the plain one
+        // (profiles/r06/ba_study/s15_jtj_local.jsonl).  The same bits: an empty sweep's sum is +0.
+        bool rot = false;
         for (int k = s; k < nck; k += splits) {
-            accumulate(cb[(size_t)c * (nck + 1) + k], cb[(size_t)c * (nck + 1) + k + 1]);
+            const int e0 = cb[(size_t)c * (nck + 1) + k], e1 = cb[(size_t)c * (nck + 1) + k + 1];
+            double* dst = part + ((size_t)c * nck + k) * NU + t0;
+            if (e0 == e1) {   // wave-uniform
+                if (lane < NR) dst[lane] = 0.0;
+                continue;
+            }
+            if (!rot) {
+                rotation();
+                rot = true;
+            }
+            accumulate(e0, e1);
             int idx;
-            if (sfm::wave_halving_sum<NR>(acc, lane, idx))
-                part[((size_t)c * nck + k) * NU + t0 + idx] = acc[0];
+            if (sfm::wave_halving_sum<NR>(acc, lane, idx)) dst[idx] = acc[0];
         }
         return;
     }
+    rotation();
     const int c0 = cam_ptr[c], c1 = cam_ptr[c + 1];
     const int len = (c1 - c0 + splits - 1) / splits;
     const int e0 = c0 + s * len;
@@ -771,11 +789,15 @@ __global__ __launch_bounds__(256) void ba_update_kernel(int n_cam, const double*
 // space in which every chunk begins at a 256-observation block boundary (so an observation wave /
 // block, and every order built on them, depends only on its chunk); returns the virtual count.
 // Chunk mode: camera waves per camera (each takes chunks g, g + G, ...): enough for
-// CHUNK_WAVE_TARGET waves in all (500 cameras x 8 chunks: one wave per chunk measured 119 us
-// per K3 call against 126 us for one wave per camera, profiles/r05/ba_jtj_chunk_ab.txt);
-// SFM_BA_CKW overrides (A/B).  Any G gives the same bits (a chunk's partial does not depend on
-// which wave forms it).
-constexpr int CHUNK_WAVE_TARGET = 4096;
+// CHUNK_WAVE_TARGET waves in all, as the plain form's SPLIT_TARGET (so G = 1 from 256 cameras on).
+// Round 6: with cfg5's local visibility (a camera's observations in 1.06 of 8 chunks) G = 8 kept
+// 8 waves per camera, 7 of them idle, occupying the CU slots the observation stream needs: the
+// final model's K3 0.120-0.125 ms at G = 8, 0.117-0.118 at G = 2, 0.107-0.108 at G = 1
+// (plain 0.101-0.107); random visibility, where every camera touches every chunk, 0.117 / 0.110 /
+// 0.118 (profiles/r06/ba_study/s17_*).  (Round 5's 4096 target measured 119 vs 126 us on the
+// random-visibility problem.)  SFM_BA_CKW overrides (A/B).  Any G gives the same bits (a chunk's
+// partial does not depend on which wave forms it).
+constexpr int CHUNK_WAVE_TARGET = 256;
 int chunk_waves(int nck, int n_cam) {
     static const int env = [] {
         const char* e = getenv("SFM_BA_CKW");

@@ -130,40 +130,6 @@ __global__ __launch_bounds__(256) void bas_soa(int n_obs, const int32_t* __restr
     ptc[e] = pt_idx[cam_obs[e]];
 }
 
-// 8x8 SPD inverse via Cholesky (one thread; 500-ish cameras).  Returns false if not SPD.
-__device__ bool inv8_spd(const double (&S)[64], double (&M)[64]) {
-    double L[64];
-#pragma unroll
-    for (int k = 0; k < 64; ++k) L[k] = 0.0;
-    for (int j = 0; j < 8; ++j) {
-        double s = S[8 * j + j];
-        for (int k = 0; k < j; ++k) s -= L[8 * j + k] * L[8 * j + k];
-        if (!(s > 0.0)) return false;
-        const double ljj = sqrt(s);
-        L[8 * j + j] = ljj;
-        for (int i = j + 1; i < 8; ++i) {
-            double t = S[8 * i + j];
-            for (int k = 0; k < j; ++k) t -= L[8 * i + k] * L[8 * j + k];
-            L[8 * i + j] = t / ljj;
-        }
-    }
-    // M = L^-T L^-1, column by column: solve L y = e_c, then L^T m = y
-    for (int c = 0; c < 8; ++c) {
-        double y[8];
-        for (int i = 0; i < 8; ++i) {
-            double t = (i == c) ? 1.0 : 0.0;
-            for (int k = 0; k < i; ++k) t -= L[8 * i + k] * y[k];
-            y[i] = t / L[8 * i + i];
-        }
-        for (int i = 7; i >= 0; --i) {
-            double t = y[i];
-            for (int k = i + 1; k < 8; ++k) t -= L[8 * k + i] * M[8 * k + c];
-            M[8 * i + c] = t / L[8 * i + i];
-        }
-    }
-    return true;
-}
-
 // Block per camera: S_cc = U_d - Σ_o W_o V_d⁻¹ W_oᵀ (upper triangle, 36 sums) and
 // b_c = -g_c + Σ_o W_o v_g (8 sums) over the camera's observations (cam_obs order, lane-strided,
 // fixed tree); then the preconditioner block M_c = S_cc⁻¹ and the CG start.
@@ -265,53 +231,83 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
     }
     block_sum<N>(acc, red, tot);
     }
-    if (tid == 0) {
-        const double* Uc = U + 64 * (size_t)c;
-        double S[64], M[64], ud[64];
-#pragma unroll
-        for (int k = 0; k < 64; ++k) ud[k] = Uc[k];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ud[9 * i] += lam * dclamp(Uc[9 * i]);
-        int t = 0;
-        for (int i = 0; i < 8; ++i)
-            for (int j = i; j < 8; ++j) {
-                S[8 * i + j] = ud[8 * i + j] - tot[t];
-                S[8 * j + i] = S[8 * i + j];
-                ++t;
+    // The block's tail, spread over the first wave (it was one thread: the 8x8 Cholesky and the
+    // inverse's 128 fp64 divisions in series, ~13 us per block, twice over at 500 cameras on 256
+    // CUs).  Every value is the serial code's expression in its order: lane (i, j) forms S_ij
+    // from the upper triangle, lane 0 each diagonal of L, lanes below it the column, lane c
+    // column c of M = L^-T L^-1, so the bits are the single thread's.
+    __shared__ double Ssh[64], Lsh[64], Msh[64], bsh[8], zsh[8];
+    __shared__ int spd;
+    const double* Uc = U + 64 * (size_t)c;
+    if (tid < 64) {
+        const int i = tid >> 3, j = tid & 7, a = min(i, j), b2 = max(i, j);
+        double u = Uc[tid];
+        if (i == j) u += lam * dclamp(Uc[tid]);
+        Ud[64 * (size_t)c + tid] = u;
+        double uab = Uc[8 * a + b2];
+        if (a == b2) uab += lam * dclamp(Uc[8 * a + b2]);
+        const double sv = uab - tot[8 * a - a * (a - 1) / 2 + (b2 - a)];
+        Ssh[tid] = sv;
+        if (Scc) Scc[64 * (size_t)c + tid] = sv;   // the explicit system's diagonal block
+        Lsh[tid] = 0.0;
+        if (tid == 0) spd = 1;
+    }
+    __syncthreads();
+    for (int j = 0; j < 8; ++j) {   // Cholesky, column j (inv8_spd's order)
+        if (tid == 0) {
+            double sv = Ssh[8 * j + j];
+            for (int k = 0; k < j; ++k) sv -= Lsh[8 * j + k] * Lsh[8 * j + k];
+            if (!(sv > 0.0)) spd = 0;
+            Lsh[8 * j + j] = sqrt(sv);
+        }
+        __syncthreads();
+        if (tid > j && tid < 8) {
+            double t = Ssh[8 * tid + j];
+            for (int k = 0; k < j; ++k) t -= Lsh[8 * tid + k] * Lsh[8 * j + k];
+            Lsh[8 * tid + j] = t / Lsh[8 * j + j];
+        }
+        __syncthreads();
+    }
+    const bool ok = spd != 0;
+    if (tid < 8) {   // column tid of M: solve L y = e_c, then L^T m = y
+        const int cc = tid;
+        double m[8];
+        if (ok) {
+            double y[8];
+            for (int i = 0; i < 8; ++i) {
+                double t = (i == cc) ? 1.0 : 0.0;
+                for (int k = 0; k < i; ++k) t -= Lsh[8 * i + k] * y[k];
+                y[i] = t / Lsh[8 * i + i];
             }
-        if (Scc) {   // the explicit system's diagonal block (sfm_ba_set_schur)
-#pragma unroll
-            for (int k = 0; k < 64; ++k) Scc[64 * (size_t)c + k] = S[k];
+            for (int i = 7; i >= 0; --i) {
+                double t = y[i];
+                for (int k = i + 1; k < 8; ++k) t -= Lsh[8 * k + i] * m[k];
+                m[i] = t / Lsh[8 * i + i];
+            }
+        } else {   // not SPD: the diagonal preconditioner
+            for (int i = 0; i < 8; ++i) m[i] = i == cc ? 1.0 / fmax(Ssh[9 * cc], DIAG_MIN) : 0.0;
+            if (cc == 0) atomicOr(bad, 1);
         }
-        if (!inv8_spd(S, M)) {
-            atomicOr(bad, 1);
-#pragma unroll
-            for (int k = 0; k < 64; ++k) M[k] = 0.0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) M[9 * i] = 1.0 / fmax(S[9 * i], DIAG_MIN);
-        }
-        double* ud_o = Ud + 64 * (size_t)c;
-        double* m_o = Mc + 64 * (size_t)c;
-#pragma unroll
-        for (int k = 0; k < 64; ++k) { ud_o[k] = ud[k]; m_o[k] = M[k]; }
-        double b[8], zz[8], rz = 0.0, bb = 0.0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) b[i] = tot[36 + i] - gc[8 * (size_t)c + i];
-#pragma unroll
+        for (int i = 0; i < 8; ++i) Msh[8 * i + cc] = m[i];
+        bsh[cc] = tot[36 + cc] - gc[8 * (size_t)c + cc];
+    }
+    __syncthreads();
+    if (tid < 64) Mc[64 * (size_t)c + tid] = Msh[tid];
+    if (tid < 8) {
+        double sz = 0.0;
+        for (int j = 0; j < 8; ++j) sz += Msh[8 * tid + j] * bsh[j];
+        zsh[tid] = sz;
+        x[8 * (size_t)c + tid] = 0.0;
+        r[8 * (size_t)c + tid] = bsh[tid];
+        z[8 * (size_t)c + tid] = sz;
+        pv[8 * (size_t)c + tid] = 0.0;  // p_{-1}: p_0 = z_0 + 0 * p_{-1}
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double rz = 0.0, bb = 0.0;
         for (int i = 0; i < 8; ++i) {
-            double s = 0.0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s += M[8 * i + j] * b[j];
-            zz[i] = s;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            x[8 * (size_t)c + i] = 0.0;
-            r[8 * (size_t)c + i] = b[i];
-            z[8 * (size_t)c + i] = zz[i];
-            pv[8 * (size_t)c + i] = 0.0;  // p_{-1}: p_0 = z_0 + 0 * p_{-1}
-            rz += b[i] * zz[i];
-            bb += b[i] * b[i];
+            rz += bsh[i] * zsh[i];
+            bb += bsh[i] * bsh[i];
         }
         rz_c[c] = rz;   // parity slot 0: rz_0
         bb_c[c] = bb;   // |b|^2 share, also rr_0 (parity slot 0 of the rr partials)
@@ -730,7 +726,7 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
 // r·z (slot (k+1)&1) and r·r (slot (k+1)&1).  A breakdown (p·q <= 0) stops the iteration.
 // One camera component of the CG vector update (thread gi = 8 c + i; the 8 components of a camera
 // are 8 consecutive lanes): x += α p; r -= α q; z = M r; the camera's r·z and r·r into slot
-// (k+1)&1 (rr = 0 on a breakdown).  Shared by bas_pcg_vec and the one-workgroup CG.
+// (k+1)&1 (rr = 0 on a breakdown).
 __device__ __forceinline__ void pcg_vec_component(int gi, int k, int n_cam, const double* __restrict__ Mc,
                                                   double* __restrict__ x, double* __restrict__ r,
                                                   double* __restrict__ z, const double* __restrict__ pv,
@@ -875,13 +871,8 @@ __global__ __launch_bounds__(256) void bas_schur_tree(int n_slot, const int32_t*
     out[i] = sfm::chunk_tree16(a);
 }
 
-// Explicit CG product (bas_point + bas_pcg_camera's role once S is formed): wave per block row c.
-// p_k = z_k + β_k p_{k-1} (p_{k-1} from the other parity slot of pv2, so no block reads what
-// another writes); the row's blocks in row_ent order, 8 lanes per block (lane r: row r of the
-// block, or column r for a transposed slot), blocks g, g + 8, ... per lane group, then a fixed
-// xor tree over the 8 groups; q_c = S_cc p_c - Σ T p_j, p_k stored, p·q per camera.
-// One block row c of the explicit product (one wave; shared by bas_pcg_spmv and the one-workgroup
-// CG): p_k = z_k + β_k p_{k-1} (p_{k-1} from the other parity slot of pv2), the row's blocks in
+// One block row c of the explicit CG product (one wave; bas_point + bas_pcg_camera's role once S
+// is formed): p_k = z_k + β_k p_{k-1} (p_{k-1} from the other parity slot of pv2), the row's blocks in
 // row_ent order, 8 lanes per block (lane r: row r of the block, or column r for a transposed
 // slot), blocks g, g + 8, ... per lane group, then a fixed xor tree over the 8 groups;
 // q_c = S_cc p_c - Σ T p_j, p_k stored, p·q of the camera.
@@ -944,44 +935,6 @@ __global__ __launch_bounds__(256) void bas_pcg_spmv(
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (c < n_cam)
         schur_spmv_row(c, lane, k, n_cam, sc.beta, row_ptr, row_ent, slot_cam, T, Scc, z, pv2, q, pq);
-}
-
-// The whole explicit CG in ONE workgroup (small reduced systems, n_cam <= CG1_MAX_CAM): the same
-// per-row product, per-component update and canonical sums as bas_pcg_spmv + bas_pcg_vec +
-// publish_next, in the same association, so the iterates, the iteration count and the state are
-// the same bits — without two launches per iteration and the host polls between them (16 waves:
-// 16 block rows per pass of the product, 128 cameras per pass of the update).
-constexpr int CG1_MAX_CAM = 256;
-__global__ __launch_bounds__(1024) void bas_schur_cg1(
-    int max_iter, int n_cam, const int32_t* __restrict__ row_ptr,
-    const int32_t* __restrict__ row_ent, const int32_t* __restrict__ slot_cam,
-    const double* __restrict__ T, const double* __restrict__ Scc, const double* __restrict__ Mc,
-    double* __restrict__ x, double* __restrict__ r, double* __restrict__ z,
-    double* __restrict__ pv2, double* __restrict__ q, double* __restrict__ pq,
-    double* __restrict__ rzc, double* __restrict__ rrc, PcgState* __restrict__ st, double tol) {
-    __shared__ double red4[12];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    Scalars sc = read_scalars(st);   // iteration 0's, from bas_pcg_init
-    const int n8 = (8 * n_cam + 1023) & ~1023;   // whole passes: every 8-lane group is one camera
-    for (int k = 0; k < max_iter && !sc.done; ++k) {
-        for (int c = wave; c < n_cam; c += 16)
-            schur_spmv_row(c, lane, k, n_cam, sc.beta, row_ptr, row_ent, slot_cam, T, Scc, z, pv2, q, pq);
-        __syncthreads();
-        const double pqs = canon_sum(pq, n_cam, red4);
-        const bool breakdown = !(pqs > 0.0);
-        const double alpha = breakdown ? 0.0 : sc.rz / pqs;
-        const double* pv = pv2 + (size_t)(k & 1) * 8 * n_cam;
-        for (int gi = tid; gi < n8; gi += 1024)
-            pcg_vec_component(gi, k, n_cam, Mc, x, r, z, pv, q, alpha, breakdown, rzc, rrc);
-        __syncthreads();
-        sc = pcg_scalars(k + 1, n_cam, rzc, rrc, st->bb, tol, red4);
-        if (tid == 0) {
-            st->iter = k + 1;
-            st->beta = sc.beta;
-            st->rz = sc.rz;
-            st->done = sc.done ? 1 : 0;
-        }
-    }
 }
 
 // Largest camera count for which the sharded solve finishes an iteration in one launch
@@ -1537,6 +1490,20 @@ static void schur_iter(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int
                        w.pv2 + (size_t)(k & 1) * 8 * n_cam, w.q, w.pq, w.rzc, w.rrc, w.state, tol);
 }
 
+// Iterations enqueued after a poll's flag copy before the host waits for it (sfm_ba_solve).
+constexpr int POLL_AHEAD = 2;
+
+// The flag copy of a look-ahead poll: state->done -> pinned[0], then ctx->poll_ev.
+static int solve_poll_issue(sfm_ctx* ctx, hipStream_t st, const SolveWs& w) {
+    if (!ctx->pinned)
+        SFM_HIP_CHECK(hipHostMalloc((void**)&ctx->pinned, 64, hipHostMallocDefault));
+    if (!ctx->poll_ev) SFM_HIP_CHECK(hipEventCreateWithFlags(&ctx->poll_ev, hipEventDisableTiming));
+    SFM_HIP_CHECK(hipMemcpyAsync(ctx->pinned, &w.state->done, sizeof(int32_t),
+                                 hipMemcpyDeviceToHost, st));
+    SFM_HIP_CHECK(hipEventRecord(ctx->poll_ev, st));
+    return SFM_OK;
+}
+
 static int solve_poll(sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int32_t* done) {
     if (!ctx->pinned)
         SFM_HIP_CHECK(hipHostMalloc((void**)&ctx->pinned, 64, hipHostMallocDefault));
@@ -1593,25 +1560,34 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     SFM_HIP_CHECK(hipStreamIsCapturing(st, &cap));
     const int poll = cap != hipStreamCaptureStatusNone ? -1
                    : prm->poll == 0 ? SFM_BA_POLL_DEFAULT : prm->poll;
-    // a small explicit system: the whole CG in one workgroup, one launch, no polls (same bits)
-    static const bool cg1_off = [] {
-        const char* e = getenv("SFM_BA_CG1");
-        return e && e[0] == '0';
+    const int first = prm->poll_first > 0 ? prm->poll_first : std::max(poll, 1);
+    // Look-ahead poll: at a poll point the flag is copied to pinned memory behind an event and
+    // POLL_AHEAD more iterations are enqueued before the host waits on that event, so the GPU
+    // runs them while the host wakes up instead of idling through the round trip (a converged
+    // flag makes them empty launches; bas_model reads the last real iteration's slot).
+    static const int ahead = [] {
+        const char* e = getenv("SFM_BA_POLL_AHEAD");
+        return e ? std::max(0, atoi(e)) : POLL_AHEAD;
     }();
-    if (ex && n_cam <= CG1_MAX_CAM && !cg1_off && prm->max_iter > 0) {
-        hipLaunchKernelGGL(bas_schur_cg1, dim3(1), dim3(1024), 0, st, prm->max_iter, n_cam,
-                           ctx->ba_row_ptr, ctx->ba_row_ent, ctx->ba_slot_cam, w.T, w.Scc, w.Mc, dc,
-                           w.r, w.z, w.pv2, w.q, w.pq, w.rzc, w.rrc, w.state, tol);
-        SFM_HIP_CHECK(hipGetLastError());
-    } else
+    int check_at = -1;   // iteration at which the pending flag copy is read
     for (int k = 0; k < prm->max_iter; ++k) {
         // state->done is set by bas_pcg_point of the first iteration after convergence: once it
         // reads 1, every later iteration would exit at once, so stop enqueueing them
-        if (poll > 0 && k > 0 && k % poll == 0) {
-            int32_t done = 0;
-            const int prc = solve_poll(ctx, st, w, &done);
-            if (prc != SFM_OK) return prc;
-            if (done) break;
+        if (poll > 0 && k >= first && (k - first) % poll == 0 && check_at < 0) {
+            if (ahead == 0) {
+                int32_t done = 0;
+                const int prc = solve_poll(ctx, st, w, &done);
+                if (prc != SFM_OK) return prc;
+                if (done) break;
+            } else {
+                if (solve_poll_issue(ctx, st, w) != SFM_OK) return SFM_ERR_HIP;
+                check_at = k + ahead;
+            }
+        }
+        if (k == check_at) {
+            SFM_HIP_CHECK(hipEventSynchronize(ctx->poll_ev));
+            check_at = -1;
+            if (ctx->pinned[0]) break;
         }
         if (ex) {
             schur_iter(ctx, st, w, k, n_cam, dc, tol);

@@ -43,7 +43,7 @@ extern "C" {
 
 const char* sfm_last_error(void) { return g_err.c_str(); }
 
-int32_t sfm_version(void) { return 4; }  // 2: sfm_ba_solve_params.poll 0 = every 8; 3: BA chunk mode; 4: explicit Schur
+int32_t sfm_version(void) { return 5; }  // 2: sfm_ba_solve_params.poll 0 = every 8; 3: BA chunk mode; 4: explicit Schur; 5: poll_first
 
 int sfm_ctx_create(int32_t device, sfm_ctx** out) {
     SFM_REQUIRE(out != nullptr, "sfm_ctx_create: out is NULL");
@@ -85,6 +85,7 @@ int sfm_ctx_destroy(sfm_ctx* ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->poll_ev) (void)hipEventDestroy(ctx->poll_ev);
     if (ctx->rs_acc) (void)hipFree(ctx->rs_acc);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;

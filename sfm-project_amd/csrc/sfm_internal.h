@@ -14,6 +14,7 @@ struct sfm_ctx {
     size_t ws_bytes = 0;
     hipEvent_t handoff = nullptr;  // orders the workspace across sfm_ctx_set_stream switches
     int32_t* pinned = nullptr;     // small pinned host buffer (device -> host flag reads)
+    hipEvent_t poll_ev = nullptr;  // the BA solve's look-ahead convergence poll (lazily created)
     int n_cu = 256;
     // RANSAC execution statistics (sfm_ransac_stats): on/off and the accumulated (executed,
     // algorithmic, pairs) evaluation counters; the per-wave counts live in the batch workspace

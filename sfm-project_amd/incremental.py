@@ -13,6 +13,8 @@ Cameras: angle-axis, t, f, k1 with known intrinsics (f, k1, principal point) per
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 import match_graph
@@ -421,6 +423,21 @@ def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=N
         return
     ref, second = rec.gauge
     fixed = reconstruction.gauge_mask(rec.cams, ref=ref, second=second, fix_intrinsics=True)
+    # the registered cameras only, renumbered 0 .. n_reg - 1 in image order (an unregistered
+    # camera has no observation here: it only added an empty block row to every kernel's camera
+    # side — 500 camera blocks per setup at the first bundle adjustment of two views)
+    reg_idx = np.nonzero(rec.registered)[0]
+    timg_use = timg_d[use]
+    if os.environ.get("SFM_BA_COMPACT", "1") != "0":
+        remap = torch.full((len(rec.registered),), -1, dtype=torch.int32, device=dev)
+        remap[torch.from_numpy(reg_idx).to(dev)] = torch.arange(len(reg_idx), dtype=torch.int32,
+                                                                device=dev)
+        ba_cams, ba_pp, ba_fixed = rec.cams[reg_idx], intr[reg_idx, 2:4], fixed[reg_idx]
+        cam_sel = remap[timg_use.long()]
+    else:
+        reg_idx = None
+        ba_cams, ba_pp, ba_fixed = rec.cams, intr[:, 2:4], fixed
+        cam_sel = timg_use.to(torch.int32)
     tr = otr_d[use]   # non-decreasing (track-major): unique tracks by run starts
     first = torch.ones(n_use, dtype=torch.bool, device=dev)
     first[1:] = tr[1:] != tr[:-1]
@@ -428,11 +445,11 @@ def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=N
     pt_idx_d = torch.cumsum(first, 0, dtype=torch.int32) - 1
     info = {}
     t_sel = time.perf_counter() - t0    # observation selection (ends in host syncs)
-    cams, pts, hist = reconstruction.bundle_adjust(rec.cams, intr[:, 2:4], rec.pts_d[pts_ids],
-                                                   timg_d[use].to(torch.int32), pt_idx_d,
+    cams, pts, hist = reconstruction.bundle_adjust(ba_cams, ba_pp, rec.pts_d[pts_ids],
+                                                   cam_sel, pt_idx_d,
                                                    oxy_d[use], loss_s=loss_s, max_iter=ba_iter,
                                                    cg_tol=cg_tol, ftol=ftol, device=device,
-                                                   fixed=fixed, shard=shard_ba, group=group,
+                                                   fixed=ba_fixed, shard=shard_ba, group=group,
                                                    pcg=pcg, info=info, reproj_err="device",
                                                    device_out=True)
     err_d = info.pop("err")   # device, at the returned parameters (bundle_adjust reproj_err)
@@ -440,7 +457,10 @@ def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=N
                            n_obs=n_use, lm_steps=len(hist),
                            cg_iters=int(sum(h[3] for h in hist))))
     reg = rec.registered
-    rec.cams[reg] = cams[reg]
+    if reg_idx is not None:
+        rec.cams[reg_idx] = cams
+    else:
+        rec.cams[reg] = cams[reg]
     rec.pts_d[pts_ids] = pts
     mean = point_mean(err_d, first)
     rec.has_d[pts_ids[mean > max_err]] = False

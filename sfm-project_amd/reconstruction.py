@@ -442,9 +442,10 @@ class BAProblem:
                           self.pt_ptr, self.cam_ptr, self.cam_obs, loss_s=loss_s,
                           n_slot=self._slots())
 
-    def solve(self, lin, lam, max_iter=100, tol=1e-10, poll=8):
+    def solve(self, lin, lam, max_iter=100, tol=1e-10, poll=8, poll_first=0):
         return self._call(self.ctx.ba_solve, lin, self.cam_idx, self.pt_idx, self.pt_ptr,
-                          self.cam_ptr, self.cam_obs, lam, max_iter=max_iter, tol=tol, poll=poll)
+                          self.cam_ptr, self.cam_obs, lam, max_iter=max_iter, tol=tol, poll=poll,
+                          poll_first=poll_first)
 
     def solve_sharded(self, lin, lam, allreduce, max_iter=100, tol=1e-10, **kw):
         return self._call(self.ctx.ba_solve_sharded, lin, self.cam_idx, self.pt_idx, self.pt_ptr,
@@ -650,20 +651,48 @@ def _gather_rows(t, counts, group):
     return torch.cat([g[r, :counts[r]] for r in range(world)]).contiguous()
 
 
+# CG convergence polls after the first one (at the previous LM step's iteration count): with
+# the hint the solve polls once where it expects to be done, and then often, instead of every 8
+# iterations (a poll is a host round trip; an iteration past convergence two empty launches)
+POLL_AFTER_HINT = 4
+
+
 def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
     """bundle_adjust's Levenberg-Marquardt iterations (the step rule in its docstring); one host
-    read of 7 scalars per step.  Returns (cams, pts, history)."""
+    read of 7 scalars per step, and the solve's convergence poll placed at the previous step's
+    CG iteration count (SFM_BA_POLL_HINT=0: every 8).  Returns (cams, pts, history)."""
+    import os
     import torch
     lam, nu = lam0, 2.0
     hist = []
     old = float(cost(cams_d, pts_d).item())
     lin = linearize(cams_d, pts_d)
+    hint = 0
+    use_hint = os.environ.get("SFM_BA_POLL_HINT", "1") != "0"
+    # speculative linearisation: the next step's J^T J at the trial point is enqueued before the
+    # host waits for this step's 7 scalars, so the GPU works through the host's round trip (a
+    # rejected or final step wastes it)
+    spec = os.environ.get("SFM_BA_SPEC", "1") != "0"
+    buf = ev = None
     for _ in range(max_iter):
-        dc, dp, sinfo = solve(lin, lam)
+        dc, dp, sinfo = solve(lin, lam, hint)
         c2, p2 = upd.update(cams_d, dc, pts_d, dp)
         new_t = cost(c2, p2)
-        vals = torch.cat([sinfo, new_t]).cpu().numpy()      # the one host sync of the step
+        vals_d = torch.cat([sinfo, new_t])
+        nxt = None
+        if spec:
+            if buf is None:
+                buf = torch.empty(vals_d.numel(), dtype=vals_d.dtype, pin_memory=True)
+                ev = torch.cuda.Event()
+            buf.copy_(vals_d, non_blocking=True)
+            ev.record()
+            nxt = linearize(c2, p2)
+            ev.synchronize()                                 # the one host wait of the step
+            vals = buf.numpy()
+        else:
+            vals = vals_d.cpu().numpy()                      # the one host sync of the step
         it, gd, q, new = int(vals[0]), float(vals[2]), float(vals[3]), float(vals[5])
+        hint = it if use_hint else 0
         pred = -(gd + 0.5 * q)
         if new < old and pred > 0:
             rho = (old - new) / pred
@@ -675,7 +704,7 @@ def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
             old = new
             if done:
                 break
-            lin = linearize(cams_d, pts_d)
+            lin = nxt if nxt is not None else linearize(cams_d, pts_d)
         else:
             lam *= nu
             nu *= 2.0
@@ -918,12 +947,16 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             allreduce(t)
         return t
 
-    def solve(lin, lam):
+    def solve(lin, lam, first=0):
+        # first: where to poll the CG's convergence first (the previous solve's iteration count;
+        # then every POLL_AFTER_HINT), instead of at every multiple of 8
+        poll = POLL_AFTER_HINT if first > 0 else 8
         if full is not None:
-            return full.solve(lin, lam, max_cg, cg_tol)
+            return full.solve(lin, lam, max_cg, cg_tol, poll=poll, poll_first=first)
         if allreduce is None:
-            return prob.solve(lin, lam, max_cg, cg_tol)
-        return prob.solve_sharded(lin, lam, allreduce, max_iter=max_cg, tol=cg_tol)
+            return prob.solve(lin, lam, max_cg, cg_tol, poll=poll, poll_first=first)
+        return prob.solve_sharded(lin, lam, allreduce, max_iter=max_cg, tol=cg_tol, poll=poll,
+                                  poll_first=first)
     upd = full if full is not None else prob
     if info is not None:
         torch.cuda.synchronize(prob.dev)

@@ -41,7 +41,7 @@ class MatchParams(C.Structure):
 
 class BaSolveParams(C.Structure):
     _fields_ = [("lam", C.c_double), ("tol", C.c_double), ("max_iter", C.c_int32),
-                ("poll", C.c_int32)]
+                ("poll", C.c_int32), ("poll_first", C.c_int32)]
 
 
 class RegisterParams(C.Structure):
@@ -509,11 +509,11 @@ class Context:
         return pts, stats
 
     def ba_solve(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, max_iter=100,
-                 tol=1e-10, out=None, poll=8):
+                 tol=1e-10, out=None, poll=8, poll_first=0):
         """Damped Schur-complement PCG step from the ba_jtj blocks `lin`; returns
         (dc [n_cam,8], dp [n_pt,3], info [5] f64 device tensor).  poll: convergence poll period
-        in CG iterations (one host sync each; <= 0 = none, fully asynchronous / graph-capturable),
-        see include/sfmcore.h."""
+        in CG iterations (one host sync each; <= 0 = none, fully asynchronous / graph-capturable);
+        poll_first > 0: the first poll at that iteration; see include/sfmcore.h."""
         torch = self.torch
         U = lin["U"]
         dev = U.device
@@ -525,7 +525,8 @@ class Context:
                    torch.empty(5, dtype=f64, device=dev))
         dc, dp, info = out
         # C ABI: poll 0 = every SFM_BA_POLL_DEFAULT, < 0 = never; here poll <= 0 = never
-        prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll) if poll > 0 else -1)
+        prm = BaSolveParams(float(lam), float(tol), int(max_iter), int(poll) if poll > 0 else -1,
+                            max(int(poll_first), 0))
         self._bind_stream()
         _check(self.lib.sfm_ba_solve(self.handle, nc, npt, no, _ptr(cam_idx), _ptr(pt_idx),
                                      _ptr(pt_ptr), _ptr(cam_ptr), _ptr(cam_obs), _ptr(U),
@@ -536,14 +537,15 @@ class Context:
 
     def ba_solve_sharded(self, lin, cam_idx, pt_idx, pt_ptr, cam_ptr, cam_obs, lam, allreduce,
                          max_iter=100, tol=1e-10, out=None, poll=8, graph=False, chunks=None,
-                         schur=None):
+                         schur=None, poll_first=0):
         """ba_solve on this rank's point shard (lin: ba_jtj of the shard with U / gc already
         all-reduced), driving sfm_ba_solve_stage: allreduce(t) sums the f64 device tensor t over
         all ranks in place, ordered on the current stream (reconstruction.make_allreduce).
         graph: replay the CG windows between polls as one HIP graph captured on the first
         window after k = 0 (needs allreduce.graph_safe, i.e. RCCL; the capture costs about as much
         as the launches it saves within one solve, profiles/r03/ba_sharded_ab.txt, so it is off
-        by default).  Returns (dc, dp, info) like ba_solve."""
+        by default).  poll_first > 0: the first poll at that iteration (ba_solve).  Returns
+        (dc, dp, info) like ba_solve."""
         torch = self.torch
         U = lin["U"]
         dev = U.device
@@ -605,6 +607,9 @@ class Context:
         graph = (graph and not ns and getattr(allreduce, "graph_safe", False) and every > 0
                  and every % 2 == 0 and nc <= BA_FINISH_VEC_MAX_CAM)
         win = every if every > 0 else max(max_iter, 1)
+        # the first window ends at poll_first (then every `win`: the windows after it start at
+        # k = poll_first + m·win, one parity when win is even, so the graph replay holds)
+        win0 = int(poll_first) if every > 0 and poll_first > 0 else win
         g = None
         k = 0
         while k < max_iter:
@@ -612,7 +617,7 @@ class Context:
                 stage(BA_STAGE_POLL)   # the same decision on every rank (replicated state)
                 if done.value:
                     break
-            n = min(win, max_iter - k)
+            n = min(win0 if k == 0 else win, max_iter - k)
             if graph and k > 0 and n == win:
                 if g is None:
                     g = torch.cuda.CUDAGraph()

@@ -34,7 +34,7 @@ def host_gpu(fn, reps=20):
     return {"host_us": host * 1e6, "gpu_us": e0.elapsed_time(e1) / reps * 1e3}
 
 
-def local_problem(n_cam, n_pt, seed=0):
+def local_problem(n_cam, n_pt, seed=0, sorted_pts=False):
     """make_ba_problem's cameras, but each point seen by 4 cameras adjacent on a ring (cfg5's
     views see their grid neighbours, so the reduced camera system stays sparse)."""
     base = synth.make_ba_problem(n_cam, 8, obs_per_pt=4, seed=seed)
@@ -42,6 +42,8 @@ def local_problem(n_cam, n_pt, seed=0):
     cams_true, pp = base["cams"], base["pp"]
     pts_true = rng.uniform(-2.0, 2.0, size=(n_pt, 3))
     b = rng.integers(0, n_cam, n_pt)
+    if sorted_pts:   # points in the order of their first camera (tracks in image order)
+        b = np.sort(b)
     cam_idx = np.sort((b[:, None] + np.arange(4)[None, :]) % n_cam, 1).reshape(-1).astype(np.int32)
     pt_idx = np.repeat(np.arange(n_pt, dtype=np.int32), 4)
     uv = np.empty((cam_idx.size, 2))

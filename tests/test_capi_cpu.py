@@ -42,7 +42,8 @@ def test_library_targets_gfx950_only():
 
 def test_version_and_errors_without_device():
     lib = sfmcore.load_library()
-    assert lib.sfm_version() == 4   # 2: poll 0 = every 8; 3: BA chunk mode; 4: explicit Schur
+    assert lib.sfm_version() == 5   # 2: poll 0 = every 8; 3: BA chunk mode; 4: explicit Schur;
+    # 5: sfm_ba_solve_params.poll_first
     prm = sfmcore.MatchParams(0, 1, 4, 5, -1)
     rc = lib.sfm_match_batch(None, None, None, 0, 0, 128, None, 1, C.byref(prm), None, None, None)
     assert rc == -1

@@ -10,6 +10,11 @@ import re
 import sys
 
 
+def short(name):
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return re.sub(r"[(<].*", "", n)[-48:]
+
+
 def main():
     path = sys.argv[1]
     rx = re.compile(sys.argv[2]) if len(sys.argv) > 2 else None
@@ -30,11 +35,11 @@ def main():
     for (s0, e0, n0), (s1, e1, n1) in zip(rows, rows[1:]):
         g = s1 - e0
         if g > 2000:
-            k = re.sub(r"\(.*", "", n0).replace("void ", "").replace("(anonymous namespace)::", "")[-48:]
+            k = short(n0)
             gaps[k][0] += 1
             gaps[k][1] += g / 1e3
     for s, e, n in rows:
-        k = re.sub(r"\(.*", "", n).replace("void ", "").replace("(anonymous namespace)::", "")[-48:]
+        k = short(n)
         kt[k][0] += 1
         kt[k][1] += (e - s) / 1e3
     print(f"kernels {len(rows)}  span {span / 1e6:.3f} ms  busy {busy / 1e6:.3f} ms  "
