@@ -722,46 +722,11 @@ __global__ __launch_bounds__(CC) void bas_pcg_camera(
     }
 }
 
-// Thread per (camera, component): α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera
-// r·z (slot (k+1)&1) and r·r (slot (k+1)&1).  A breakdown (p·q <= 0) stops the iteration.
-// One camera component of the CG vector update (thread gi = 8 c + i; the 8 components of a camera
-// are 8 consecutive lanes): x += α p; r -= α q; z = M r; the camera's r·z and r·r into slot
-// (k+1)&1 (rr = 0 on a breakdown).
-__device__ __forceinline__ void pcg_vec_component(int gi, int k, int n_cam, const double* __restrict__ Mc,
-                                                  double* __restrict__ x, double* __restrict__ r,
-                                                  double* __restrict__ z, const double* __restrict__ pv,
-                                                  const double* __restrict__ q, double alpha,
-                                                  bool breakdown, double* __restrict__ rzc,
-                                                  double* __restrict__ rrc) {
-    const int c = gi >> 3, i = gi & 7;
-    const bool valid = c < n_cam;
-    const int s1 = (k + 1) & 1;
-    double ri = 0.0;
-    if (valid) {
-        const size_t kk = 8 * (size_t)c + i;
-        x[kk] += alpha * pv[kk];
-        ri = r[kk] - alpha * q[kk];
-        r[kk] = ri;
-    }
-    double zi = 0.0;
-    const double* M = Mc + 64 * (size_t)(valid ? c : 0) + 8 * i;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) zi += M[j] * __shfl(ri, (threadIdx.x & ~7) + j, 64);
-    double rz = ri * zi, rr = ri * ri;
-    rz += __shfl_down(rz, 4, 8); rr += __shfl_down(rr, 4, 8);
-    rz += __shfl_down(rz, 2, 8); rr += __shfl_down(rr, 2, 8);
-    rz += __shfl_down(rz, 1, 8); rr += __shfl_down(rr, 1, 8);
-    if (valid) {
-        z[8 * (size_t)c + i] = zi;
-        if (i == 0) {
-            rzc[(size_t)s1 * n_cam + c] = rz;
-            rrc[(size_t)s1 * n_cam + c] = breakdown ? 0.0 : rr;
-        }
-    }
-}
-
-// Thread per (camera, component): α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera
-// r·z (slot (k+1)&1) and r·r (slot (k+1)&1).  A breakdown (p·q <= 0) stops the iteration.
+// Thread per (camera, component) gi = 8 c + i (a camera's 8 components are 8 consecutive lanes):
+// α = rz_k / Σ p·q; x += α p; r -= α q; z = M r; per-camera r·z and r·r into slot (k+1)&1 (rr = 0
+// on a breakdown).  A breakdown (p·q <= 0) stops the iteration.  The component's x, p, r, q and
+// its row of M are loaded before canon_sum's barriers (they do not depend on α), so their latency
+// overlaps the reduction's (round 6: the kernel is a chain of dependent global round trips).
 __global__ __launch_bounds__(256) void bas_pcg_vec(
     int k, int n_cam, const double* __restrict__ Mc, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, const double* __restrict__ pv,
@@ -782,10 +747,40 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
         }
         return;
     }
+    const size_t kk = 8 * (size_t)(valid ? c : 0) + i;
+    double xv = 0.0, pvv = 0.0, rv = 0.0, qv = 0.0, m[8];
+    if (valid) {
+        xv = x[kk];
+        pvv = pv[kk];
+        rv = r[kk];
+        qv = q[kk];
+    }
+    const double* M = Mc + 64 * (size_t)(valid ? c : 0) + 8 * i;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = M[j];
     const double pqs = canon_sum(pq, n_cam, red4);
     const bool breakdown = !(pqs > 0.0);
     const double alpha = breakdown ? 0.0 : rz_k / pqs;
-    pcg_vec_component(gi, k, n_cam, Mc, x, r, z, pv, q, alpha, breakdown, rzc, rrc);
+    double ri = 0.0;
+    if (valid) {
+        x[kk] = xv + alpha * pvv;
+        ri = rv - alpha * qv;
+        r[kk] = ri;
+    }
+    double zi = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zi += m[j] * __shfl(ri, (threadIdx.x & ~7) + j, 64);
+    double rz = ri * zi, rr = ri * ri;
+    rz += __shfl_down(rz, 4, 8); rr += __shfl_down(rr, 4, 8);
+    rz += __shfl_down(rz, 2, 8); rr += __shfl_down(rr, 2, 8);
+    rz += __shfl_down(rz, 1, 8); rr += __shfl_down(rr, 1, 8);
+    if (valid) {
+        z[kk] = zi;
+        if (i == 0) {
+            rzc[(size_t)s1 * n_cam + c] = rz;
+            rrc[(size_t)s1 * n_cam + c] = breakdown ? 0.0 : rr;
+        }
+    }
     if (gi == 0) st->iter = k + 1;
     publish_next(k, n_cam, rzc, rrc, tol, st, gridDim.x, red4);
 }
@@ -889,10 +884,36 @@ __device__ __forceinline__ void schur_spmv_row(int c, int lane, int k, int n_cam
     const int g = lane >> 3, r = lane & 7;
     const int e0 = row_ptr[c], e1 = row_ptr[c + 1];
     double s = 0.0;
-    for (int e = e0 + g; e < e1; e += 8) {
+    // the lane group's entries two at a time: both entries' index loads, then both blocks' and
+    // neighbours' loads, are in flight together (a row's entry chain is row_ent -> slot_cam ->
+    // T / z / p: three dependent global round trips per entry otherwise)
+    int e = e0 + g;
+    for (; e + 8 < e1; e += 16) {
+        const int ent0 = row_ent[e], ent1 = row_ent[e + 8];
+        const int slot0 = ent0 >> 1, tr0 = ent0 & 1, slot1 = ent1 >> 1, tr1 = ent1 & 1;
+        const int j0 = slot_cam[2 * slot0 + (tr0 ? 0 : 1)];   // the other camera of the block
+        const int j1 = slot_cam[2 * slot1 + (tr1 ? 0 : 1)];
+        const double* Tb0 = T + 64 * (size_t)slot0;
+        const double* Tb1 = T + 64 * (size_t)slot1;
+        double t0[8], t1[8], z0[8], z1[8], o0[8], o1[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            t0[m] = tr0 ? Tb0[8 * m + r] : Tb0[8 * r + m];
+            t1[m] = tr1 ? Tb1[8 * m + r] : Tb1[8 * r + m];
+            z0[m] = z[8 * (size_t)j0 + m];
+            o0[m] = pold[8 * (size_t)j0 + m];
+            z1[m] = z[8 * (size_t)j1 + m];
+            o1[m] = pold[8 * (size_t)j1 + m];
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) s += t0[m] * (z0[m] + beta * o0[m]);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) s += t1[m] * (z1[m] + beta * o1[m]);
+    }
+    if (e < e1) {
         const int ent = row_ent[e];
         const int slot = ent >> 1, tr = ent & 1;
-        const int j = slot_cam[2 * slot + (tr ? 0 : 1)];   // the other camera of the block
+        const int j = slot_cam[2 * slot + (tr ? 0 : 1)];
         const double* Tb = T + 64 * (size_t)slot;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
