@@ -772,6 +772,7 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
             allreduce = make_allreduce(group, device=device)
             rank, world = dist.get_rank(group), dist.get_world_size(group)
     mode = "single"
+    deferred_rule = False
     lo, hi = 0, n_pt
     full = None
     tensors = isinstance(pt_idx, torch.Tensor)
@@ -825,18 +826,25 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                 m = torch.bincount(pt_idx.long(), minlength=n_pt)
                 pairs = float((m * (m - 1) // 2).sum())
                 likely_schur = schur_mode() == "1" or pairs <= SCHUR_INST_PER_OBS * max(n_obs_all, 1)
-            if world == 1 or likely_schur:
-                mode = "sharded"
-                if info is not None and world > 1:
-                    info["rule"] = {"explicit_schur_candidate": True}
-            else:
+            def rule():
                 # the chunked sharded CG all-reduces nchunk camera-vector partials per iteration
                 # (ADVICE r5): probe and price that payload, not one camera vector
                 lat, bw = probe_collectives(allreduce, n_cam * max(nchunk, 1), device, group)
-                mode, terms = pcg_rule(len(pt_idx), n_pt, n_cam, world, lat, bw)
+                m_, terms = pcg_rule(n_obs_all, n_pt, n_cam, world, lat, bw)
                 terms["allreduce_doubles"] = 8 * n_cam * max(nchunk, 1)
                 if info is not None:
                     info["rule"] = terms
+                return m_
+            if world == 1 or likely_schur:
+                mode = "sharded"
+                # the pair count alone made the explicit system the candidate: if schur_rule's
+                # other tests reject it below, pcg_rule decides the branch then
+                deferred_rule = world > 1
+                if info is not None and world > 1:
+                    info["rule"] = {"explicit_schur_candidate": True}
+            else:
+                mode = rule()
+        whole = (cam_idx, pt_idx, uv)   # the whole problem, for a replicated branch decided late
         if mode == "replicated":
             # the whole problem for the solve (every rank), the shard for the linearisation
             full = BAProblem(pp, cam_idx, pt_idx, uv, n_cam, n_pt, device, chunks=nchunk or None)
@@ -893,6 +901,14 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
                 info["schur_terms"] = {"n_inst": n_inst_tot, "n_seg": n_seg_tot,
                                        "n_slot": sp.n_slot, "n_obs": n_obs_tot}
                 info["schur_s"] = time.perf_counter() - t_s   # structure + rule (ends in a sync)
+    if deferred_rule and not use_schur:
+        mode = rule()
+        if mode == "replicated":
+            full = BAProblem(pp, *whole, n_cam, n_pt, device, chunks=nchunk or None)
+            counts_pt = [cuts[r + 1] - cuts[r] for r in range(world)]
+            counts_obs = [ocuts[r + 1] - ocuts[r] for r in range(world)]
+        if info is not None:
+            info.update(pcg=mode, rule=dict(info["rule"], explicit_schur_rejected=True))
     if info is not None:
         info["schur"] = use_schur
         torch.cuda.synchronize(prob.dev)

@@ -33,16 +33,18 @@ def main():
     fixed = R.gauge_mask(prob["cams"], ref=0, fix_intrinsics=True)
     pcg = sys.argv[3] if len(sys.argv) > 3 else "sharded"
     repeat = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-    branches = []
+    branches, deferred = [], []
     for _ in range(repeat):   # sequential auto-mode calls probe / cache consistently
         binfo = {}
         cams, pts, hist = R.bundle_adjust(*args, loss_s=2.0, max_iter=30, fixed=fixed,
                                           shard=True, pcg=pcg, info=binfo)
         branches.append(binfo["pcg"])
+        rule = binfo.get("rule")
+        deferred.append(bool(isinstance(rule, dict) and rule.get("explicit_schur_rejected")))
     dc, dp, info, lo, hi = shard_solve(prob, rank, world, R.make_allreduce())
     np.savez(f"{out}.rank{rank}.npz", cams=cams, pts=pts, hist=np.array(hist, np.float64),
              dc=dc, dp=dp, info=info, lo=lo, hi=hi, pcg=np.array(binfo["pcg"]),
-             branches=np.array(branches),
+             branches=np.array(branches), deferred=np.array(deferred),
              nchunk_adj=np.array(binfo.get("chunks_adjusted", {}).get("nchunk", -1)))
     dist.barrier()
     dist.destroy_process_group()

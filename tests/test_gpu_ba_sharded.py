@@ -290,10 +290,14 @@ def test_ba_auto_mode_repeated_on_three_ranks(tmp_path, monkeypatch, schur):
     collective probe's cache key is the same on every rank (backend, group, device, path, n_cam),
     so every rank hits or misses it together and takes the same branch; the ranks agree bit for
     bit and every call gives the same result.  schur "0" keeps the explicit Schur candidate out of
-    the branch decision (so the probe runs); "auto" lets its pair count pick the sharded branch."""
+    the branch decision (so the probe runs); "auto" lets its pair count make the explicit system
+    the candidate, and since schur_rule then rejects it (random visibility: 6 products per
+    (chunk, camera pair) group, fewer than 16) pcg_rule decides the branch after all,
+    on every rank alike."""
     monkeypatch.setenv("SFM_BA_SCHUR", schur)
     d = _run_ranks(tmp_path, 3, "std", "auto", "3")
     for k in (1, 2):
-        for key in ("cams", "pts", "hist", "branches"):
+        for key in ("cams", "pts", "hist", "branches", "deferred"):
             np.testing.assert_array_equal(d[0][key], d[k][key])
     assert len(set(d[0]["branches"].tolist())) == 1
+    assert bool(d[0]["deferred"].all()) == (schur == "auto")
