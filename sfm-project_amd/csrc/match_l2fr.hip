@@ -142,6 +142,66 @@ __global__ void l2fr_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
 // Block 0 also cuts order_f into recovery ranges: runs of at most REC_R consecutive entries with
 // the same train image, rng[r] = (first entry, length), *n_rng of them, and their pairs (rinfo).
 constexpr int REC_R = 4;  // pairs (sharing their train image) per recovery block
+
+// The forward scan's UNITS (block unit_blk of l2fr_order_kernel): the pairs grouped by query image
+// pairs[p][0], UNIT of them per unit (the query fragments are loaded once for all, and each next
+// pair's first train chunk is staged under the previous pair's last one); an image's leftover
+// pairs make one shorter unit.  uinfo[UNIT u] = (p, a, b, n_kp[a] | n_kp[b] << 16), uinfo[UNIT u + j]
+// = (p_j, b_j, n_kp[b_j], 0) for j > 0, p_j = -1 past the unit's pairs; the full units first (by
+// query image), then the shorter ones, so the scan's last dispatched blocks are the short ones.
+// *n_units = their count.  Which pairs share a unit follows the atomic slot order: it moves no
+// result (each pair's records are its own).
+#ifndef L2FR_UNIT
+#define L2FR_UNIT 2
+#endif
+constexpr int UNIT = L2FR_UNIT;
+__device__ void build_units(const int32_t* __restrict__ pairs, int n_pairs, int n_img,
+                            const int32_t* __restrict__ n_kp, int4* __restrict__ uinfo,
+                            int32_t* __restrict__ n_units, int* lds) {
+    int* cur = lds;                  // [n_img] counts, then slot cursors
+    int* fu = lds + n_img;           // [n_img + 1] full units before image i
+    int* ru = lds + 2 * n_img + 1;   // [n_img + 1] short units before image i
+    __shared__ int ftot;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < n_img; i += 1024) cur[i] = 0;
+    __syncthreads();
+    // a pair without queries or trains emits nothing (as its one-pair block exits at once): it
+    // joins no unit, so every unit record has rows on both sides
+    auto live = [&](int a, int b) { return n_kp[a] > 0 && n_kp[b] > 0; };
+    for (int p = tid; p < n_pairs; p += 1024)
+        if (live(pairs[2 * p], pairs[2 * p + 1])) atomicAdd(&cur[pairs[2 * p]], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int f = 0, r = 0;
+        for (int i = 0; i < n_img; ++i) {
+            const int c = cur[i];
+            fu[i] = f;
+            ru[i] = r;
+            f += c / UNIT;
+            r += (c % UNIT) != 0;
+            cur[i] = 0;
+        }
+        fu[n_img] = f;
+        ru[n_img] = r;
+        ftot = f;
+        *n_units = f + r;
+    }
+    __syncthreads();
+    // the short units' records start as padding (p = -1); their real pairs overwrite them below
+    for (int t = tid; t < ru[n_img] * UNIT; t += 1024) uinfo[(size_t)ftot * UNIT + t] = make_int4(-1, 0, 0, 0);
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += 1024) {
+        const int a = pairs[2 * p], b = pairs[2 * p + 1];
+        if (!live(a, b)) continue;
+        const int k = atomicAdd(&cur[a], 1);
+        const int nf = UNIT * (fu[a + 1] - fu[a]);
+        const int u = k < nf ? fu[a] + k / UNIT : ftot + ru[a];
+        const int jj = k < nf ? k % UNIT : k - nf;
+        uinfo[(size_t)u * UNIT + jj] = jj ? make_int4(p, b, n_kp[b], 0)
+                                          : make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
+    }
+}
+
 __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restrict__ pairs,
                                                           int n_pairs, int n_img,
                                                           int32_t* __restrict__ order_f,
@@ -150,8 +210,14 @@ __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restr
                                                           int32_t* __restrict__ n_rng,
                                                           const int32_t* __restrict__ n_kp,
                                                           int4* __restrict__ rinfo,
-                                                          int4* __restrict__ sinfo_f) {
+                                                          int4* __restrict__ sinfo_f, int unit_blk,
+                                                          int4* __restrict__ uinfo,
+                                                          int32_t* __restrict__ n_units) {
     extern __shared__ int hist[];
+    if ((int)blockIdx.x == unit_blk) {
+        build_units(pairs, n_pairs, n_img, n_kp, uinfo, n_units, hist);
+        return;
+    }
     const int tid = threadIdx.x, col = blockIdx.x == 0 ? 1 : 0;
     int32_t* order = blockIdx.x == 0 ? order_f : order_r;
     for (int i = tid; i < n_img; i += 1024) hist[i] = 0;
@@ -257,34 +323,58 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
     const int32_t* __restrict__ cinit, const uint8_t* __restrict__ zero_row,
     const int32_t* __restrict__ pairs, int n_qblk, const int32_t* __restrict__ pair_order,
     const int4* __restrict__ sinfo, int n_blk, const int4* __restrict__ qlist,
-    const int32_t* __restrict__ qcount, int4* __restrict__ out, FwdCls fc) {
+    const int32_t* __restrict__ qcount, int4* __restrict__ out, FwdCls fc,
+    const int32_t* __restrict__ n_units) {
     __shared__ __attribute__((aligned(16))) unsigned char lds0[CHUNK * D + CHUNK * 4];
     __shared__ __attribute__((aligned(16))) unsigned char lds1[CHUNK * D + CHUNK * 4];
 
-    // XCD-aware block order: workgroups go round-robin over the 8 XCDs (blockIdx % 8); XCD x owns
-    // the x-th contiguous run of ppx pairs of pair_order (pairs sharing the streamed image are
-    // adjacent, so its L2 serves them) and runs all their query block 0s first, then block 1s
-    // (in the reverse scan most block 1s are empty and exit at once, after the real work).
-    const int ppx = (int)(gridDim.x >> 3) / n_qblk;
-    const int l = (int)(blockIdx.x >> 3);
-    const int pos = (int)(blockIdx.x & 7) * ppx + l % ppx, qb = l / ppx;
-    if (pos >= n_blk) return;  // block-uniform, before any barrier
-    int p, qi, ti, nq, nb;
-    if (REV) {
-        p = pair_order[pos];
-        qi = pairs[2 * p + 1];
-        ti = pairs[2 * p];
-        nq = qcount[p];
-        nb = n_kp[ti];
-    } else {  // one record (order kernel): pair, query image, train image, both counts
-        const int4 u = sinfo[pos];
-        // all four fields before the early exit: one s_load_dwordx4, not two dependent loads
+    int p, qi, ti, nq, nb, qb;
+    int p2 = -1, ti2 = 0, nb2 = 0;   // unit mode: the unit's next pair (same query image)
+    int pos = 0, kk = 0;             // unit mode: the unit, the record of the next pair
+    if (!REV && n_units) {
+        // Unit mode (build_units): a block takes one unit of up to two pairs; units go round-robin
+        // over the 8 XCDs (pos = 8 j + blockIdx % 8), all units' query block 0 first, then block
+        // 1, the single-pair units last in each pass.  The grid is sized for one pair per unit:
+        // the blocks past the units exit at once.
+        const int nu = *n_units;
+        const int u8 = (nu + 7) >> 3;
+        const int l = (int)(blockIdx.x >> 3);
+        qb = u8 > 0 ? l / u8 : n_qblk;
+        pos = (l - qb * u8) * 8 + (int)(blockIdx.x & 7);
+        if (qb >= n_qblk || pos >= nu) return;  // block-uniform, before any barrier
+        const int4 u = sinfo[(size_t)UNIT * pos];
         asm volatile("" : : "s"(u.x), "s"(u.y), "s"(u.z), "s"(u.w));
         p = u.x;
         qi = u.y;
         ti = u.z;
         nq = u.w & 0xFFFF;
-        nb = u.w >> 16;
+        nb = u.w >> 16;   // > 0: build_units places only pairs with rows on both sides
+    } else {
+        // XCD-aware block order: workgroups go round-robin over the 8 XCDs (blockIdx % 8); XCD x
+        // owns the x-th contiguous run of ppx pairs of pair_order (pairs sharing the streamed image
+        // are adjacent, so its L2 serves them) and runs all their query block 0s first, then block
+        // 1s (in the reverse scan most block 1s are empty and exit at once, after the real work).
+        const int ppx = (int)(gridDim.x >> 3) / n_qblk;
+        const int l = (int)(blockIdx.x >> 3);
+        const int pos = (int)(blockIdx.x & 7) * ppx + l % ppx;
+        qb = l / ppx;
+        if (pos >= n_blk) return;  // block-uniform, before any barrier
+        if (REV) {
+            p = pair_order[pos];
+            qi = pairs[2 * p + 1];
+            ti = pairs[2 * p];
+            nq = qcount[p];
+            nb = n_kp[ti];
+        } else {  // one record (order kernel): pair, query image, train image, both counts
+            const int4 u = sinfo[pos];
+            // all four fields before the early exit: one s_load_dwordx4, not two dependent loads
+            asm volatile("" : : "s"(u.x), "s"(u.y), "s"(u.z), "s"(u.w));
+            p = u.x;
+            qi = u.y;
+            ti = u.z;
+            nq = u.w & 0xFFFF;
+            nb = u.w >> 16;
+        }
     }
     if (qb * QB >= nq || nb <= 0) return;  // block-uniform
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
@@ -292,23 +382,43 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
 
     const uint8_t* db = desc + (size_t)ti * k_max * D;
     const int32_t* cib = cinit + (size_t)ti * k_pad;
-    const int n_chunk = (nb + CHUNK - 1) / CHUNK;
+    int n_chunk = (nb + CHUNK - 1) / CHUNK;
+    const uint8_t* db2 = desc;
+    const int32_t* cib2 = cinit;
+    // unit mode: the unit's pair after record kk (p2 = -1: none)
+    auto find_next = [&]() {
+        p2 = -1;
+        if (REV || !n_units || ++kk >= UNIT) return;
+        const int4 v = sinfo[(size_t)UNIT * pos + kk];
+        p2 = v.x;
+        ti2 = v.y;
+        nb2 = v.z;
+        db2 = desc + (size_t)ti2 * k_max * D;
+        cib2 = cinit + (size_t)ti2 * k_pad;
+    };
+    find_next();
 
-    auto stage = [&](int ch, unsigned char* dst) {
+    // chunk ch of train image (sdb, scib, snb rows) into the LDS stage dst
+    auto stage = [&](const uint8_t* sdb, const int32_t* scib, int snb, int ch, unsigned char* dst) {
 #pragma unroll
         for (int i = 0; i < PIECES; ++i) {
             const int piece = wave * PIECES + i;
             const int row = piece * RPP + lane / SLOTS;
             const int slot = (lane % SLOTS) ^ swz(row);
             const int j = ch * CHUNK + row;
-            const uint8_t* src = (j < nb) ? db + (size_t)j * D + slot * 16 : zero_row + slot * 16;
+            const uint8_t* src = (j < snb) ? sdb + (size_t)j * D + slot * 16 : zero_row + slot * 16;
             __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + piece * 1024), 16, 0, 0);
         }
         if (tid < CHUNK / 4) {  // the chunk's accumulator init: whole waves 0 (.. 1)
-            const int32_t* src = cib + ch * CHUNK + tid * 4;
+            const int32_t* src = scib + ch * CHUNK + tid * 4;
             __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + CHUNK * D + wave * 1024),
                                              16, 0, 0);
         }
+    };
+    // the next stage after chunk ch: this pair's next chunk, or the unit's second pair's first
+    auto stage_next = [&](int ch, unsigned char* dst) {
+        if (ch + 1 < n_chunk) stage(db, cib, nb, ch + 1, dst);
+        else if (p2 >= 0) stage(db2, cib2, nb2, 0, dst);
     };
 
     const int qbase = qb * QB + wave * QT * 32;
@@ -348,10 +458,8 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
         tb[c] = INT_MIN; ts[c] = INT_MIN; t1[c] = 0;
     }
     v4i acc[QS][2];
-    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
-#ifndef L2FR_ABL_NOSTAGE
-        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
-#endif
+    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) __attribute__((always_inline)) {
+        stage_next(ch, nxt);
         const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
         if (active) {
             const int* Ci = (const int*)(cur + CHUNK * D);
@@ -440,10 +548,8 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
         }
     };
 
-    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) {
-#ifndef L2FR_ABL_NOSTAGE
-        if (ch + 1 < n_chunk) stage(ch + 1, nxt);
-#endif
+    auto process = [&](int ch, const unsigned char* cur, unsigned char* nxt) __attribute__((always_inline)) {
+        stage_next(ch, nxt);
         const int nt = min(NT, (nb - ch * CHUNK + 31) >> 5);
         if (active) {
             const int* Ci = (const int*)(cur + CHUNK * D);
@@ -494,28 +600,8 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
     };
 #endif
 
-    if (n_chunk > 0) stage(0, lds0);
-    __syncthreads();
-    L2FR_STAMP(1, __builtin_amdgcn_s_memrealtime());
-    L2FR_STAMP(2, __builtin_amdgcn_s_memtime());
-#ifdef L2FR_PRIO  // static priority for the second-dispatched half (MI355X_MICROARCH.md, item 4)
-    if (wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef L2FR_ABL_NOSTAGE  // ablation: every chunk reads chunk 0's stage, no barriers in the loop
-    for (int ch = 0; ch < n_chunk; ++ch) process(ch, lds0, lds1);
-#else
-    for (int ch = 0; ch < n_chunk; ch += 2) {
-        process(ch, lds0, lds1);
-        __syncthreads();
-        if (ch < 16) L2FR_STAMP(3 + ch, __builtin_amdgcn_s_memrealtime());
-        if (ch + 1 < n_chunk) process(ch + 1, lds1, lds0);
-        __syncthreads();
-        if (ch + 1 < 16) L2FR_STAMP(4 + ch, __builtin_amdgcn_s_memrealtime());
-    }
-#endif
-    L2FR_STAMP(19, __builtin_amdgcn_s_memtime());
-    L2FR_STAMP(20, __builtin_amdgcn_s_memrealtime());
-    if (active) {
+    // the pair's records: top-2 of the lane halves / quarters, then emit
+    auto epilogue = [&]() {
 #if L2FR_MFMA16
 #pragma unroll
         for (int c = 0; c < QS; ++c) {
@@ -530,6 +616,7 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
             }
             const int e = qbase + c * 16 + r16;
             if (g4 == 0 && e < nq) emit(e, e1, e2, t);
+            tb[c] = INT_MIN; ts[c] = INT_MIN; t1[c] = 0;
         }
 #else
 #pragma unroll
@@ -542,8 +629,47 @@ __global__ __launch_bounds__(SCAN_THREADS, SCAN_MIN_WAVES) void l2fr_scan_kernel
             const int t = tb[c] > P1 ? t1[c] : (P1 > tb[c] ? PT : min(t1[c], PT));
             const int e = qbase + c * 32 + r32;
             if (h == 0 && e < nq) emit(e, e1, e2, t);
+            tb[c] = INT_MIN; ts[c] = INT_MIN; t1[c] = 0;   // a unit's second pair starts afresh
         }
 #endif
+    };
+
+    if (n_chunk > 0) stage(db, cib, nb, 0, lds0);
+    __syncthreads();
+    L2FR_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    L2FR_STAMP(2, __builtin_amdgcn_s_memtime());
+    // the chunks of the unit's pairs in turn through the two LDS stages (g: the stage parity over
+    // the whole unit); a pair's records leave after its last chunk, the next pair's first chunk
+    // already staged
+    // one pair's chunks two at a time, from stage s0 (the other one s1): static LDS addresses
+    auto run_pair = [&](unsigned char* s0, unsigned char* s1) __attribute__((always_inline)) {
+        for (int ch = 0; ch < n_chunk; ch += 2) {
+            process(ch, s0, s1);
+            __syncthreads();
+            if (ch < 16) L2FR_STAMP(3 + ch, __builtin_amdgcn_s_memrealtime());
+            if (ch + 1 < n_chunk) process(ch + 1, s1, s0);
+            __syncthreads();
+            if (ch + 1 < 16) L2FR_STAMP(4 + ch, __builtin_amdgcn_s_memrealtime());
+        }
+    };
+    int g = 0;   // the stage that holds the pair's first chunk
+    for (;;) {
+        if (g & 1)
+            run_pair(lds1, lds0);
+        else
+            run_pair(lds0, lds1);
+        g += n_chunk;
+        L2FR_STAMP(19, __builtin_amdgcn_s_memtime());
+        L2FR_STAMP(20, __builtin_amdgcn_s_memrealtime());
+        if (active) epilogue();
+        if (p2 < 0) break;
+        p = p2;
+        ti = ti2;
+        nb = nb2;
+        db = db2;
+        cib = cib2;
+        n_chunk = (nb + CHUNK - 1) / CHUNK;
+        find_next();
     }
 #ifdef L2FR_CLOCK
     L2FR_STAMP(21, __builtin_amdgcn_s_memrealtime());
@@ -1104,8 +1230,9 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     const size_t rngb = sfm::align_up(sizeof(int2) * (size_t)n_rng_max, 256);
     const size_t rinfob = sizeof(int4) * (size_t)n_rng_max * REC_R;
     const size_t sinfob = sfm::align_up(sizeof(int4) * (size_t)n_pairs, 256);
+    const size_t uinfob = sfm::align_up(UNIT * sizeof(int4) * (size_t)n_pairs, 256);
     char* ws = (char*)sfm::workspace(ctx, 256 + 2 * tab + 3 * recb + cntb + descb + 2 * ordb + clsb +
-                                              256 + rngb + rinfob + sinfob);
+                                              256 + rngb + rinfob + 256 + sinfob + uinfob + 256);
     if (!ws) return SFM_ERR_NOMEM;
     char* w = ws;
     uint8_t* zero_row = (uint8_t*)w; w += 256;
@@ -1123,6 +1250,14 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     int2* rng = (int2*)w; w += rngb;
     int4* rinfo = (int4*)w; w += rinfob;
     int4* sinfo_f = (int4*)sfm::align_up((size_t)w, 256);
+    int4* uinfo = (int4*)((char*)sinfo_f + sinfob);
+    int32_t* n_units = (int32_t*)((char*)uinfo + uinfob);
+    // the forward scan by units of two pairs sharing their query image (build_units;
+    // SFM_L2FR_UNITS=0: one pair per block, XCD-contiguous runs by train image)
+    static const bool units = [] {
+        const char* e = getenv("SFM_L2FR_UNITS");
+        return !(e && e[0] == '0');
+    }();
     const int ppx = (n_pairs + 7) / 8;  // pairs per XCD run (scan kernel block order)
     const int n_blk = n_pairs;
     const int grid = 8 * ppx * n_qblk;
@@ -1133,18 +1268,19 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     SFM_HIP_CHECK(hipGetLastError());
     const int32_t* sord_f = ord_f;
     const int32_t* sord_r = ord_r;
-    hipLaunchKernelGGL(l2fr_order_kernel, dim3(mutual ? 2 : 1), dim3(1024),
-                       2 * sizeof(int) * (size_t)n_img, st, pairs, n_pairs, n_img, ord_f, ord_r, rng,
-                       n_rng, n_kp, rinfo, sinfo_f);
+    const int unit_blk = units ? (mutual ? 2 : 1) : -1;
+    hipLaunchKernelGGL(l2fr_order_kernel, dim3((mutual ? 2 : 1) + (units ? 1 : 0)), dim3(1024),
+                       (3 * (size_t)n_img + 2) * sizeof(int), st, pairs, n_pairs, n_img, ord_f, ord_r,
+                       rng, n_rng, n_kp, rinfo, sinfo_f, unit_blk, uinfo, n_units);
     SFM_HIP_CHECK(hipGetLastError());
     // qst (per-query status of the recovery) shares the reverse scan's output buffer: it is
     // consumed by the compaction before the reverse scan writes there.
     int4* qst = rev;
     const FwdCls fc{norm, prm->ratio_num, prm->ratio_den, (long long)prm->max_dist, qst, cls};
     hipLaunchKernelGGL(l2fr_scan_kernel<false>, dim3(grid), dim3(SCAN_THREADS), 0, st, desc_i8, n_kp, k_max,
-                       k_pad, cinit, zero_row, pairs, n_qblk, sord_f, (const int4*)sinfo_f, n_blk,
-                       (const int4*)nullptr,
-                       (const int32_t*)nullptr, fwd, fc);
+                       k_pad, cinit, zero_row, pairs, n_qblk, sord_f,
+                       (const int4*)(units ? uinfo : sinfo_f), n_blk, (const int4*)nullptr,
+                       (const int32_t*)nullptr, fwd, fc, (const int32_t*)(units ? n_units : nullptr));
     SFM_HIP_CHECK(hipGetLastError());
     const char* dbg = getenv("SFM_L2FR_DEBUG");
     const int dmode = dbg ? atoi(dbg) : 0;
@@ -1179,7 +1315,8 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
         hipLaunchKernelGGL(l2fr_scan_kernel<true>, dim3(grid), dim3(SCAN_THREADS), 0, st, desc_i8, n_kp,
                            k_max, k_pad, cinit, zero_row, pairs, n_qblk, sord_r,
                            (const int4*)nullptr, n_blk,
-                           (const int4*)surv, (const int32_t*)scount, rev, fc);
+                           (const int4*)surv, (const int32_t*)scount, rev, fc,
+                           (const int32_t*)nullptr);
         SFM_HIP_CHECK(hipGetLastError());
     }
     if (dmode == 3) {
