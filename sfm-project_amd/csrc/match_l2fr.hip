@@ -1254,10 +1254,13 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     int32_t* n_units = (int32_t*)((char*)uinfo + uinfob);
     // the forward scan by units of two pairs sharing their query image (build_units;
     // SFM_L2FR_UNITS=0: one pair per block, XCD-contiguous runs by train image)
-    static const bool units = [] {
+    static const bool units_env = [] {
         const char* e = getenv("SFM_L2FR_UNITS");
         return !(e && e[0] == '0');
     }();
+    // build_units keeps 3 n_img + 2 ints in LDS (64 KB per block): beyond ~5 400 images the
+    // one-pair blocks
+    const bool units = units_env && (3 * (size_t)n_img + 2) * sizeof(int) <= 65536;
     const int ppx = (n_pairs + 7) / 8;  // pairs per XCD run (scan kernel block order)
     const int n_blk = n_pairs;
     const int grid = 8 * ppx * n_qblk;
@@ -1270,7 +1273,8 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     const int32_t* sord_r = ord_r;
     const int unit_blk = units ? (mutual ? 2 : 1) : -1;
     hipLaunchKernelGGL(l2fr_order_kernel, dim3((mutual ? 2 : 1) + (units ? 1 : 0)), dim3(1024),
-                       (3 * (size_t)n_img + 2) * sizeof(int), st, pairs, n_pairs, n_img, ord_f, ord_r,
+                       ((units ? 3 : 2) * (size_t)n_img + 2) * sizeof(int), st, pairs, n_pairs, n_img,
+                       ord_f, ord_r,
                        rng, n_rng, n_kp, rinfo, sinfo_f, unit_blk, uinfo, n_units);
     SFM_HIP_CHECK(hipGetLastError());
     // qst (per-query status of the recovery) shares the reverse scan's output buffer: it is
