@@ -70,13 +70,30 @@ __device__ __forceinline__ void block_sum(double (&a)[N], double (*red)[N], doub
 constexpr int LONG_OBS = 64;
 constexpr int LONG_BLOCKS = 64;  // extra point-pass blocks (4 waves each) that take the long points
 
+__device__ __forceinline__ void soa_one(int e, int n_obs, const int32_t* __restrict__ cam_obs,
+                                        const int32_t* __restrict__ pt_idx,
+                                        const double* __restrict__ W, double* __restrict__ Wp,
+                                        int32_t* __restrict__ ptc);
+
+// Blocks [0, pblk): a point each thread (V_d⁻¹, V_d⁻¹ g_p, the long-track list); blocks from pblk
+// on: bas_soa's work for observation e (one launch for both, they are independent).
 __global__ __launch_bounds__(256) void bas_point_setup(int n_pt, const int32_t* __restrict__ pt_ptr,
                                                        const double* __restrict__ V,
                                                        const double* __restrict__ gp, double lam,
                                                        double* __restrict__ Vinv,
                                                        double* __restrict__ vg,
                                                        int32_t* __restrict__ long_list,
-                                                       int32_t* __restrict__ long_cnt) {
+                                                       int32_t* __restrict__ long_cnt, int pblk,
+                                                       int n_obs, const int32_t* __restrict__ cam_obs,
+                                                       const int32_t* __restrict__ pt_idx,
+                                                       const double* __restrict__ W,
+                                                       double* __restrict__ Wp,
+                                                       int32_t* __restrict__ ptc) {
+    if ((int)blockIdx.x >= pblk) {
+        const int e = ((int)blockIdx.x - pblk) * blockDim.x + threadIdx.x;
+        if (e < n_obs) soa_one(e, n_obs, cam_obs, pt_idx, W, Wp, ptc);
+        return;
+    }
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pt) return;
     if (pt_ptr[p + 1] - pt_ptr[p] > LONG_OBS)  // order of the list is irrelevant (points independent)
@@ -111,12 +128,10 @@ __global__ __launch_bounds__(256) void bas_point_setup(int n_pt, const int32_t* 
 // instead of 192-B rows per lane; ptc = pt_idx in camera-major order (cam_obs) for the camera
 // setup.  The camera side never needs W again after the setup: the point pass hands it
 // u_o = W_o t_p (bas_pcg_point).
-__global__ __launch_bounds__(256) void bas_soa(int n_obs, const int32_t* __restrict__ cam_obs,
-                                               const int32_t* __restrict__ pt_idx,
-                                               const double* __restrict__ W,
-                                               double* __restrict__ Wp, int32_t* __restrict__ ptc) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n_obs) return;
+__device__ __forceinline__ void soa_one(int e, int n_obs, const int32_t* __restrict__ cam_obs,
+                                        const int32_t* __restrict__ pt_idx,
+                                        const double* __restrict__ W, double* __restrict__ Wp,
+                                        int32_t* __restrict__ ptc) {
     const size_t n = (size_t)n_obs;
     if (Wp) {   // nullptr: the explicit Schur solve (no CG point pass; backsub reads W row-major)
         const double2* a = (const double2*)(W + 24 * (size_t)e);
@@ -144,7 +159,7 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ pv,
     double* __restrict__ rz_c, double* __restrict__ bb_c, int32_t* __restrict__ bad, int phase,
     double* __restrict__ comm, const int32_t* __restrict__ cb, int nck, int ntot,
-    double* __restrict__ Scc) {
+    double* __restrict__ Scc, double* __restrict__ pv2) {
     constexpr int N = 44;
     __shared__ double red[4][N];
     __shared__ double tot[N];
@@ -302,6 +317,8 @@ __global__ __launch_bounds__(CT) void bas_camera_setup(
         z[8 * (size_t)c + tid] = sz;
         pv[8 * (size_t)c + tid] = 0.0;  // p_{-1}: p_0 = z_0 + 0 * p_{-1}
     }
+    // the explicit system's p in its two parity slots, zeroed (p_{-1} = 0; was a memset per solve)
+    if (pv2 && tid < 16) pv2[(size_t)(tid >> 3) * 8 * n_cam + 8 * (size_t)c + (tid & 7)] = 0.0;
     __syncthreads();
     if (tid == 0) {
         double rz = 0.0, bb = 0.0;
@@ -845,11 +862,38 @@ __global__ __launch_bounds__(256) void bas_schur_build(
 
 // T = per slot, the canonical chunk tree over its group partials (parts [n_group][64]; chunks
 // without a group are 0 leaves — the dense [n_total][n_slot] tree's bits).  Thread per element.
+// The CG's iteration-0 scalars from the camera set-up's partials (one block of 256).
+__device__ void pcg_init_body(int n_cam, const double* __restrict__ rzc,
+                              const double* __restrict__ bb_c, double tol,
+                              PcgState* __restrict__ st) {
+    __shared__ double red4[12];
+    const double bb = canon_sum(bb_c, n_cam, red4);
+    const Scalars sc = pcg_scalars(0, n_cam, rzc, bb_c, bb, tol, red4);
+    if (threadIdx.x == 0) {
+        st->bb = bb;
+        st->rz = sc.rz;
+        st->beta = sc.beta;
+        st->rr = bb;
+        st->iter = 0;
+        st->done = sc.done ? 1 : 0;
+        st->cnt = 0u;
+    }
+}
+
+// Block tblk (one past the tree's blocks) runs bas_pcg_init's work: the camera set-up that wrote
+// its partials finished before this launch, so the explicit solve needs no launch of its own for it.
 __global__ __launch_bounds__(256) void bas_schur_tree(int n_slot, const int32_t* __restrict__ sg_ptr,
                                                       const int32_t* __restrict__ sg,
                                                       const int32_t* __restrict__ gk,
                                                       const double* __restrict__ parts,
-                                                      double* __restrict__ out) {
+                                                      double* __restrict__ out, int tblk, int n_cam,
+                                                      const double* __restrict__ rzc,
+                                                      const double* __restrict__ bb_c, double tol,
+                                                      PcgState* __restrict__ st) {
+    if ((int)blockIdx.x == tblk) {
+        pcg_init_body(n_cam, rzc, bb_c, tol, st);
+        return;
+    }
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (long long)n_slot * 64) return;
     const int s = (int)(i >> 6), e = (int)(i & 63);
@@ -1074,18 +1118,7 @@ __global__ __launch_bounds__(FV) void bas_pcg_finish_vec(
 __global__ __launch_bounds__(256) void bas_pcg_init(int n_cam, const double* __restrict__ rzc,
                                                     const double* __restrict__ bb_c, double tol,
                                                     PcgState* __restrict__ st) {
-    __shared__ double red4[12];
-    const double bb = canon_sum(bb_c, n_cam, red4);
-    const Scalars sc = pcg_scalars(0, n_cam, rzc, bb_c, bb, tol, red4);
-    if (threadIdx.x == 0) {
-        st->bb = bb;
-        st->rz = sc.rz;
-        st->beta = sc.beta;
-        st->rr = bb;
-        st->iter = 0;
-        st->done = sc.done ? 1 : 0;
-        st->cnt = 0u;
-    }
+    pcg_init_body(n_cam, rzc, bb_c, tol, st);
 }
 
 // Fixed-order sum over a 1024-thread block (16 waves); returns the total to every thread.
@@ -1257,12 +1290,10 @@ __global__ __launch_bounds__(256) void bas_backsub_ck(sfm::ChunkOff cpt, int n_o
 // Chunk mode, one wave: chunk k's model terms = its BPB block partials (one per lane, xor tree);
 // exp: this rank's chunks to out[k][2] (the exchange form); else the canonical tree -> out[0..2).
 // gathered (ntot > 0, in = the gathered [ntot][2]): out[0..2) = the tree of in.
-__global__ __launch_bounds__(64) void bas_mchunk(int nck, int exp, int ntot,
-                                                 const double* __restrict__ mpart,
-                                                 const double* __restrict__ in,
-                                                 double* __restrict__ out) {
-    const int lane = threadIdx.x;
-    double a[16], b[16];
+__device__ __forceinline__ void mchunk_terms(int lane, int nck, int ntot,
+                                             const double* __restrict__ mpart,
+                                             const double* __restrict__ in, double (&a)[16],
+                                             double (&b)[16]) {
     if (ntot > 0) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
@@ -1287,13 +1318,32 @@ __global__ __launch_bounds__(64) void bas_mchunk(int nck, int exp, int ntot,
             b[k] = v;
         }
     }
+}
+
+// The non-export form's tree by one wave (lane < 64): out[0..2) from lane 0.
+__device__ __forceinline__ void mchunk_tree(int lane, int nck, int ntot,
+                                            const double* __restrict__ mpart,
+                                            const double* __restrict__ in, double* out) {
+    double a[16], b[16];
+    mchunk_terms(lane, nck, ntot, mpart, in, a, b);
     if (lane != 0) return;
-    if (exp) {
-        for (int k = 0; k < nck; ++k) { out[2 * k] = a[k]; out[2 * k + 1] = b[k]; }
-        return;
-    }
     out[0] = sfm::chunk_tree16(a);
     out[1] = sfm::chunk_tree16(b);
+}
+
+__global__ __launch_bounds__(64) void bas_mchunk(int nck, int exp, int ntot,
+                                                 const double* __restrict__ mpart,
+                                                 const double* __restrict__ in,
+                                                 double* __restrict__ out) {
+    const int lane = threadIdx.x;
+    if (!exp) {
+        mchunk_tree(lane, nck, ntot, mpart, in, out);
+        return;
+    }
+    double a[16], b[16];
+    mchunk_terms(lane, nck, ntot, mpart, in, a, b);
+    if (lane != 0) return;
+    for (int k = 0; k < nck; ++k) { out[2 * k] = a[k]; out[2 * k + 1] = b[k]; }
 }
 
 // Sharded solve, one block: this rank's point-block partials of bas_backsub summed into
@@ -1310,6 +1360,9 @@ __global__ __launch_bounds__(1024) void bas_mpart_total(int n_pblk, const double
 
 // One block: camera terms (g_c·δc, δcᵀ U δc) + the point-block partials -> info.
 //   info = {iterations, |r|/|b|, gᵀδ, δᵀ JᵀJ δ, preconditioner fallback (0/1)}
+// Chunk mode (nck > 0 or ntot > 0): the back-substitution's model partials are the chunk tree of
+// bas_mchunk's non-export form — formed here by wave 0 (the same code, the same bits) and taken by
+// thread 0 where it took the separate kernel's total, one launch fewer per solve.
 __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const double* __restrict__ U,
                                                   const double* __restrict__ gc,
                                                   const double* __restrict__ dc,
@@ -1317,9 +1370,12 @@ __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const d
                                                   const double* __restrict__ rrc,
                                                   const PcgState* __restrict__ st,
                                                   const int32_t* __restrict__ bad,
-                                                  double* __restrict__ info) {
+                                                  double* __restrict__ info, int nck, int ntot,
+                                                  const double* __restrict__ min) {
     __shared__ double red[16];
+    __shared__ double mt[2];
     const int tid = threadIdx.x;
+    if ((nck > 0 || ntot > 0) && tid < 64) mchunk_tree(tid, nck, ntot, mpart, min, mt);
     double a = 0.0, b = 0.0;
     for (int c = tid; c < n_cam; c += 1024) {
         const double* Uc = U + 64 * (size_t)c;
@@ -1333,7 +1389,12 @@ __global__ __launch_bounds__(1024) void bas_model(int n_cam, int n_pblk, const d
             a += gc[8 * (size_t)c + i] * d[i];
         }
     }
-    for (int k = tid; k < n_pblk; k += 1024) { a += mpart[2 * (size_t)k]; b += mpart[2 * (size_t)k + 1]; }
+    if (nck > 0 || ntot > 0) {
+        __syncthreads();
+        if (tid == 0) { a += mt[0]; b += mt[1]; }
+    } else {
+        for (int k = tid; k < n_pblk; k += 1024) { a += mpart[2 * (size_t)k]; b += mpart[2 * (size_t)k + 1]; }
+    }
     const double ga = block_sum1024(a, red);
     const double qb = block_sum1024(b, red);
     const int it = st->iter;
@@ -1438,25 +1499,23 @@ static int solve_setup(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, in
                        const double* gc, const double* gp, double lam, double* dc, int phase,
                        double* comm, bool soa = true) {
     SFM_HIP_CHECK(hipMemsetAsync(w.bad, 0, 2 * sizeof(int32_t), st));  // bad flag, long count
-    if (n_pt > 0) {
-        hipLaunchKernelGGL(bas_point_setup, dim3(w.pblk), dim3(256), 0, st, n_pt, pt_ptr, V, gp,
-                           lam, w.Vinv, w.vg, w.long_list, w.long_cnt);
-        SFM_HIP_CHECK(hipGetLastError());
-    }
-    if (n_obs > 0) {
-        hipLaunchKernelGGL(bas_soa, dim3((n_obs + 255) / 256), dim3(256), 0, st, n_obs, cam_obs,
-                           pt_idx, W, soa ? w.Wp : nullptr, w.ptc);
+    // the point set-up and the SoA copy / camera-major point ids (bas_soa's work) in one launch
+    const int pb = n_pt > 0 ? w.pblk : 0, ob = n_obs > 0 ? (n_obs + 255) / 256 : 0;
+    if (pb + ob > 0) {
+        hipLaunchKernelGGL(bas_point_setup, dim3(pb + ob), dim3(256), 0, st, n_pt, pt_ptr, V, gp,
+                           lam, w.Vinv, w.vg, w.long_list, w.long_cnt, pb, n_obs, cam_obs, pt_idx,
+                           W, soa ? w.Wp : nullptr, w.ptc);
         SFM_HIP_CHECK(hipGetLastError());
     }
     hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
                        w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z, w.pv,
-                       w.rzc, w.rrc, w.bad, phase, comm, ck.cb, ck.nck, ck.ntot, w.Scc);
+                       w.rzc, w.rrc, w.bad, phase, comm, ck.cb, ck.nck, ck.ntot, w.Scc, w.pv2);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
 
-// Back-substitution + the model terms (chunk mode: chunk-aligned blocks, combined by the tree into
-// mtot, or exported to comm[k][2] when exp).  Returns the (n_pblk, mpart) pair bas_model reads.
+// Back-substitution + the model terms (chunk mode: chunk-aligned blocks, combined by bas_model's
+// chunk tree, or exported to comm[k][2] when exp).  Returns the (n_pblk, mpart) pair bas_model reads.
 static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, int32_t n_pt,
                          int32_t n_obs, const int32_t* pt_ptr, const int32_t* cam_idx,
                          const double* V, const double* gp, const double* dc, double* dp, bool exp,
@@ -1472,9 +1531,11 @@ static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, 
                        W ? 24LL : 1LL, W ? 1LL : (long long)n_obs, pt_ptr, cam_idx, W ? W : w.Wp,
                        V, w.Vinv, w.vg, gp, dc, dp, w.mpart);
     SFM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bas_mchunk, dim3(1), dim3(64), 0, st, ck.nck, exp ? 1 : 0, 0, w.mpart,
-                       (const double*)nullptr, exp ? comm : w.mtot);
-    SFM_HIP_CHECK(hipGetLastError());
+    if (exp) {   // the non-export tree is formed by bas_model
+        hipLaunchKernelGGL(bas_mchunk, dim3(1), dim3(64), 0, st, ck.nck, 1, 0, w.mpart,
+                           (const double*)nullptr, comm);
+        SFM_HIP_CHECK(hipGetLastError());
+    }
     return SFM_OK;
 }
 
@@ -1490,15 +1551,17 @@ static int schur_build(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, con
     return SFM_OK;
 }
 
-// Explicit S: T from the whole problem's group partials (slot trees) and the zeroed p_{-1} slot.
+// Explicit S: T from the whole problem's group partials (slot trees; p's parity slots are zeroed by
+// bas_camera_setup).
 static int schur_finish(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, int32_t n_cam,
-                        const double* parts) {
+                        const double* parts, double tol) {
     const long long n = (long long)ctx->ba_nslot * 64;
-    hipLaunchKernelGGL(bas_schur_tree, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                       ctx->ba_nslot, ctx->ba_sg_ptr, ctx->ba_sg, ctx->ba_gk, parts, w.T);
+    const int tblk = (int)((n + 255) / 256);
+    hipLaunchKernelGGL(bas_schur_tree, dim3((unsigned)tblk + 1), dim3(256), 0, st, ctx->ba_nslot,
+                       ctx->ba_sg_ptr, ctx->ba_sg, ctx->ba_gk, parts, w.T, tblk, n_cam, w.rzc, w.rrc,
+                       tol, w.state);
     SFM_HIP_CHECK(hipGetLastError());
-    SFM_HIP_CHECK(hipMemsetAsync(w.pv2, 0, sizeof(double) * 16 * (size_t)n_cam, st));
-    return SFM_OK;
+    return SFM_OK;   // p's parity slots: zeroed by bas_camera_setup
 }
 
 // One explicit CG iteration: the S product, then the vector update (p_k in parity slot k & 1).
@@ -1569,9 +1632,10 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
     if (rc != SFM_OK) return rc;
     if (ex) {
         if (schur_build(ctx, st, w, pt_idx, W, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
-        if (schur_finish(ctx, st, w, n_cam, w.Tpart) != SFM_OK) return SFM_ERR_HIP;
+        if (schur_finish(ctx, st, w, n_cam, w.Tpart, tol) != SFM_OK) return SFM_ERR_HIP;   // + init
+    } else {
+        hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
     }
-    hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
     SFM_HIP_CHECK(hipGetLastError());
     // 0 (the zero-initialised struct) = every 8 iterations, the library default; < 0 = never
     // (no host synchronisation: fully asynchronous, capturable in a hip graph).  A stream under
@@ -1628,7 +1692,8 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, int32_t n_cam, int32_t n_pt, int32_t n
                       ex ? W : nullptr) != SFM_OK)
         return SFM_ERR_HIP;
     hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, ck.cb ? 1 : w.gblk, U, gc, dc,
-                       ck.cb ? w.mtot : w.mpart, w.rrc, w.state, w.bad, info);
+                       (const double*)w.mpart, w.rrc, w.state, w.bad, info, ck.cb ? ck.nck : 0, 0,
+                       (const double*)nullptr);
     SFM_HIP_CHECK(hipGetLastError());
     return SFM_OK;
 }
@@ -1674,11 +1739,15 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
     case SFM_BA_STAGE_SETUP_FINISH:
         hipLaunchKernelGGL(bas_camera_setup, dim3(n_cam), dim3(CT), 0, st, n_cam, n_obs, cam_ptr,
                            w.ptc, cam_obs, U, W, w.Vinv, w.vg, gc, lam, w.Ud, w.Mc, dc, w.r, w.z,
-                           w.pv, w.rzc, w.rrc, w.bad, 2, comm, ck.cb, ck.nck, ck.ntot, w.Scc);
+                           w.pv, w.rzc, w.rrc, w.bad, 2, comm, ck.cb, ck.nck, ck.ntot, w.Scc, w.pv2);
         SFM_HIP_CHECK(hipGetLastError());
-        if (ex && schur_finish(ctx, st, w, n_cam, comm + (size_t)ck.ntot * 44 * n_cam) != SFM_OK)
-            return SFM_ERR_HIP;
-        hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol, w.state);
+        if (ex) {   // the tree launch also forms the CG's iteration-0 scalars
+            if (schur_finish(ctx, st, w, n_cam, comm + (size_t)ck.ntot * 44 * n_cam, tol) != SFM_OK)
+                return SFM_ERR_HIP;
+        } else {
+            hipLaunchKernelGGL(bas_pcg_init, dim3(1), dim3(256), 0, st, n_cam, w.rzc, w.rrc, tol,
+                               w.state);
+        }
         break;
     case SFM_BA_STAGE_ITER:  // -> comm[0, 8 n_cam)
         if (ex) {   // S is replicated: the whole iteration locally, nothing to exchange
@@ -1721,13 +1790,10 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
         hipLaunchKernelGGL(bas_mpart_total, dim3(1), dim3(1024), 0, st, w.gblk, w.mpart, comm);
         break;
     case SFM_BA_STAGE_MODEL:
-        if (ck.cb) {   // the gathered [n_total][2] model partials: the canonical tree
-            hipLaunchKernelGGL(bas_mchunk, dim3(1), dim3(64), 0, st, ck.nck, 0, ck.ntot,
-                               (const double*)nullptr, comm, w.mtot);
-            SFM_HIP_CHECK(hipGetLastError());
-        }
+        // chunk mode: the gathered [n_total][2] model partials' canonical tree, inside bas_model
         hipLaunchKernelGGL(bas_model, dim3(1), dim3(1024), 0, st, n_cam, 1, U, gc, dc,
-                           ck.cb ? w.mtot : comm, w.rrc, w.state, w.bad, info);
+                           (const double*)comm, w.rrc, w.state, w.bad, info, ck.cb ? ck.nck : 0,
+                           ck.cb ? ck.ntot : 0, (const double*)comm);
         break;
     case SFM_BA_STAGE_POLL:
         return solve_poll(ctx, st, w, done);
@@ -1744,21 +1810,23 @@ extern "C" int sfm_ba_solve_stage(sfm_ctx* ctx, int32_t stage, int32_t k, int32_
 // zeroed.  The Schur system then decouples them with right-hand side 0, so δ = 0 for them exactly
 // and the LM model terms (gᵀδ, δᵀJᵀJδ) do not see them.  Mirrors oracle/ba_lm.py fix_params().
 namespace {
-__global__ __launch_bounds__(256) void bas_fix_cam(int n_cam, const uint8_t* __restrict__ fixed,
-                                                   double* __restrict__ U,
-                                                   double* __restrict__ gc) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (camera, i, j)
-    if (g >= n_cam * 64) return;
-    const int c = g >> 6, i = (g >> 3) & 7, j = g & 7;
-    const bool fi = fixed[8 * (size_t)c + i] != 0, fj = fixed[8 * (size_t)c + j] != 0;
-    if (fi || fj) U[g] = (i == j) ? 1.0 : 0.0;
-    if (j == 0 && fi) gc[8 * (size_t)c + i] = 0.0;
-}
-
-__global__ __launch_bounds__(256) void bas_fix_obs(int n_obs, const int32_t* __restrict__ cam_idx,
-                                                   const uint8_t* __restrict__ fixed,
-                                                   double* __restrict__ W) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (observation, row i of W_o)
+// One launch for both halves (blocks [0, ncb): (camera, i, j) of U and g_c; the rest (observation,
+// row i of W_o)): a held parameter's U row / column become the identity's, its g_c entry and W rows 0.
+__global__ __launch_bounds__(256) void bas_fix(int n_cam, int ncb, int n_obs,
+                                               const int32_t* __restrict__ cam_idx,
+                                               const uint8_t* __restrict__ fixed,
+                                               double* __restrict__ U, double* __restrict__ gc,
+                                               double* __restrict__ W) {
+    if ((int)blockIdx.x < ncb) {
+        const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (camera, i, j)
+        if (g >= n_cam * 64) return;
+        const int c = g >> 6, i = (g >> 3) & 7, j = g & 7;
+        const bool fi = fixed[8 * (size_t)c + i] != 0, fj = fixed[8 * (size_t)c + j] != 0;
+        if (fi || fj) U[g] = (i == j) ? 1.0 : 0.0;
+        if (j == 0 && fi) gc[8 * (size_t)c + i] = 0.0;
+        return;
+    }
+    const int g = ((int)blockIdx.x - ncb) * blockDim.x + threadIdx.x;  // (observation, row i)
     if (g >= n_obs * 8) return;
     const int o = g >> 3, i = g & 7;
     if (fixed[8 * (size_t)cam_idx[o] + i]) {
@@ -1778,14 +1846,10 @@ extern "C" int sfm_ba_fix_params(sfm_ctx* ctx, int32_t n_cam, int32_t n_obs,
                 "sfm_ba_fix_params: NULL array");
     SFM_HIP_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    hipLaunchKernelGGL(bas_fix_cam, dim3((64 * n_cam + 255) / 256), dim3(256), 0, st, n_cam,
-                       fixed, U, gc);
+    const int ncb = (64 * n_cam + 255) / 256, nob = n_obs > 0 ? (8 * n_obs + 255) / 256 : 0;
+    hipLaunchKernelGGL(bas_fix, dim3(ncb + nob), dim3(256), 0, st, n_cam, ncb, n_obs, cam_idx,
+                       fixed, U, gc, W);
     SFM_HIP_CHECK(hipGetLastError());
-    if (n_obs > 0) {
-        hipLaunchKernelGGL(bas_fix_obs, dim3((8 * n_obs + 255) / 256), dim3(256), 0, st, n_obs,
-                           cam_idx, fixed, W);
-        SFM_HIP_CHECK(hipGetLastError());
-    }
     return SFM_OK;
 }
 
