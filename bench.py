@@ -729,6 +729,7 @@ def cfg5_run(n_img, k, n_pts, steps, warmup, world, rank, local, pcg):
                        for k in ("select_s", "entry_wait_s", "setup_s", "problem_s", "schur_s", "lm_s",
                                  "post_s", "s")},
         "lm_steps": int(sum(b["lm_steps"] for b in rec.ba_log)),
+        "lm_rejected": int(sum(b.get("lm_rejected", 0) for b in rec.ba_log)),
         "cg_iters": int(sum(b["cg_iters"] for b in rec.ba_log)),
         "pcg_branches": sorted({b["pcg"] for b in rec.ba_log}),
         "shard_ba": world > 1, "n_gpus": world,

@@ -455,6 +455,7 @@ def _bundle(rec, intr, loss_s, ba_iter, max_err, device, shard_ba=False, group=N
     err_d = info.pop("err")   # device, at the returned parameters (bundle_adjust reproj_err)
     rec.ba_log.append(dict(info, n_cam=int(rec.registered.sum()), n_pt=int(pts_ids.numel()),
                            n_obs=n_use, lm_steps=len(hist),
+                           lm_rejected=int(sum(1 for h in hist if not h[2])),
                            cg_iters=int(sum(h[3] for h in hist))))
     reg = rec.registered
     if reg_idx is not None:

@@ -672,6 +672,8 @@ def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
     # speculative linearisation: the next step's J^T J at the trial point is enqueued before the
     # host waits for this step's 7 scalars, so the GPU works through the host's round trip (a
     # rejected or final step wastes it)
+    # (cfg5: 0 of 160 steps rejected, so only the 17 final steps waste it; skipping it where the
+    # previous decrease was already small measured slower — profiles/r06/ba_study/s25, s26)
     spec = os.environ.get("SFM_BA_SPEC", "1") != "0"
     buf = ev = None
     for _ in range(max_iter):
