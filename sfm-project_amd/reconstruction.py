@@ -660,7 +660,9 @@ POLL_AFTER_HINT = 4
 def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
     """bundle_adjust's Levenberg-Marquardt iterations (the step rule in its docstring); one host
     read of 7 scalars per step, and the solve's convergence poll placed at the previous step's
-    CG iteration count (SFM_BA_POLL_HINT=0: every 8).  Returns (cams, pts, history)."""
+    CG iteration count (SFM_BA_POLL_HINT=0: every 8).  Returns (cams, pts, history, the
+    linearisation at the returned parameters when the loop converged with one at hand, else
+    None)."""
     import os
     import torch
     lam, nu = lam0, 2.0
@@ -676,6 +678,7 @@ def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
     # previous decrease was already small measured slower — profiles/r06/ba_study/s25, s26)
     spec = os.environ.get("SFM_BA_SPEC", "1") != "0"
     buf = ev = None
+    final_lin = None
     for _ in range(max_iter):
         dc, dp, sinfo = solve(lin, lam, hint)
         c2, p2 = upd.update(cams_d, dc, pts_d, dp)
@@ -705,6 +708,7 @@ def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
             done = old - new <= ftol * old
             old = new
             if done:
+                final_lin = nxt   # the speculative K3 sits at the returned parameters
                 break
             lin = nxt if nxt is not None else linearize(cams_d, pts_d)
         else:
@@ -713,7 +717,7 @@ def _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0, max_iter, ftol):
             hist.append((old, lam, False, it))
             if lam > 1e16:
                 break
-    return cams_d, pts_d, hist
+    return cams_d, pts_d, hist, final_lin
 
 
 def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_iter: int = 50,
@@ -984,12 +988,15 @@ def bundle_adjust(cams, pp, pts, cam_idx, pt_idx, uv, loss_s: float = 0.0, max_i
     bound = (prob.bind() if full is None and os.environ.get("SFM_BA_BIND", "1") != "0"
              else contextlib.nullcontext())
     with bound:
-        cams_d, pts_d, hist = _lm_loop(cams_d, pts_d, cost, linearize, solve, upd, lam0,
-                                       max_iter, ftol)
+        cams_d, pts_d, hist, final_lin = _lm_loop(cams_d, pts_d, cost, linearize, solve, upd,
+                                                  lam0, max_iter, ftol)
     if info is not None:
         info["lm_s"] = time.perf_counter() - t_lm   # the loop ends in a host sync (the last step)
     if reproj_err and info is not None:
-        r = prob.linearize(cams_d, shard_of(pts_d), loss_s)["res"]
+        # the residuals at the returned parameters: the LM's last speculative K3 when the loop
+        # ended on convergence (the same call on the same parameters), else one more K3
+        r = (final_lin["res"] if final_lin is not None
+             else prob.linearize(cams_d, shard_of(pts_d), loss_s)["res"])
         e = torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1])
         if allreduce is None:
             if prob.order is not None:   # BAProblem regrouped the observations by point
