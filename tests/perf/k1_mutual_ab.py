@@ -3,7 +3,8 @@ the two exact implementations — the mutual kernel (SFM_L2_PATH=mutual, the dis
 for this rule) and the forward/recovery/reverse ratio path (SFM_L2_PATH=fr) — interleaved in one
 process on a cfg4 shard (the 1/8 shard rank 3 gets at N = 8: ~15.6 k pairs of the 500 x 4096
 scene), with their outputs compared bit for bit on every pair.
-python tests/perf/k1_mutual_ab.py  (SHARD=r/n, ROUNDS override)"""
+python tests/perf/k1_mutual_ab.py  (SHARD=r/n, ROUNDS, N_IMG, K override; cfg3: N_IMG=50 K=2048
+SHARD=0/1)"""
 import json
 import os
 import sys
@@ -22,8 +23,9 @@ import synth
 def main():
     r, n = (int(x) for x in os.environ.get("SHARD", "3/8").split("/"))
     rounds = int(os.environ.get("ROUNDS", "3"))
-    s = synth.make_scene(500, 4096, seed=0)
-    pairs = synth.unordered_pairs(500)
+    n_img, k = int(os.environ.get("N_IMG", "500")), int(os.environ.get("K", "4096"))
+    s = synth.make_scene(n_img, k, seed=0)
+    pairs = synth.unordered_pairs(n_img)
     lo, hi = match_graph.shard_range(pairs, r, n, s["n_kp"])
     pairs = pairs[lo:hi]
     ctx = sfmcore.context(0)
@@ -52,7 +54,7 @@ def main():
         for p in range(len(pairs)):
             c = cm[p]
             same &= bool((mm[p, :c] == mf[p, :c]).all() and (dm[p, :c] == df[p, :c]).all())
-    res = {"shard": f"{r}/{n}", "pairs": int(len(pairs)), "k": 4096,
+    res = {"shard": f"{r}/{n}", "pairs": int(len(pairs)), "n_img": n_img, "k": k,
            "ms_mutual": times["mutual"], "ms_fr": times["fr"],
            "tops_mutual": ops / (min(times["mutual"]) * 1e-3) / 1e12,
            "tops_fr": ops / (min(times["fr"]) * 1e-3) / 1e12,
