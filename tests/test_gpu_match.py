@@ -73,6 +73,15 @@ def test_l2_ragged_and_edges(ctx):
     pairs = np.array([[a, b] for a in range(n_img) for b in range(n_img) if a != b], np.int32)
     for xc, ratio in [(1, (4, 5)), (0, None), (2, None), (1, None)]:
         _check_pairs(ctx, desc, n_kp, pairs, cross_check=xc, ratio=ratio)
+    # the ratio path (scan units: pairs of an image without descriptors join no unit), ratio only
+    # and mutual + ratio through it
+    import os
+    os.environ["SFM_L2_PATH"] = "fr"
+    try:
+        for xc in (0, 1):
+            _check_pairs(ctx, desc, n_kp, pairs, cross_check=xc, ratio=(4, 5))
+    finally:
+        os.environ.pop("SFM_L2_PATH", None)
 
 
 def test_l2_extreme_values(ctx):
