@@ -105,12 +105,11 @@ __device__ __forceinline__ int dot128(const uint4* x, const uint4* y) {
 
 // Per descriptor: the i8 row x ^ 0x80, A = |x'|^2 and the scan's accumulator init -ceil(A/2)
 // (PAD_INIT for the padding rows up to k_pad).
-__global__ void l2fr_prep_kernel(const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
-                                 int k_max, int k_pad, int32_t* __restrict__ norm,
-                                 int32_t* __restrict__ cinit, uint8_t* __restrict__ zero_row,
-                                 uint4* __restrict__ desc_i8) {
-    const int img = blockIdx.y;
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void prep_one(int img, int j, const uint8_t* __restrict__ desc,
+                                         const int32_t* __restrict__ n_kp, int k_max, int k_pad,
+                                         int32_t* __restrict__ norm, int32_t* __restrict__ cinit,
+                                         uint8_t* __restrict__ zero_row,
+                                         uint4* __restrict__ desc_i8) {
     if (img == 0 && j < D) zero_row[j] = 0;
     if (j >= k_pad) return;
     int nv = 0;
@@ -120,16 +119,14 @@ __global__ void l2fr_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
 #pragma unroll
         for (int q = 0; q < SLOTS; ++q) {
             const uint4 v = p[q];
-            o8[q] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u,
-                               v.w ^ 0x80808080u);
-            const unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int x = (int)((w[e] >> (8 * b)) & 0xFF) - 128;
-                    nv += x * x;
-                }
+            const uint4 x = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u,
+                                       v.w ^ 0x80808080u);
+            o8[q] = x;
+            // |x'|^2 of the signed bytes x' = x - 128, four at a time (exact integer sums)
+            nv = __builtin_amdgcn_sdot4((int)x.x, (int)x.x, nv, false);
+            nv = __builtin_amdgcn_sdot4((int)x.y, (int)x.y, nv, false);
+            nv = __builtin_amdgcn_sdot4((int)x.z, (int)x.z, nv, false);
+            nv = __builtin_amdgcn_sdot4((int)x.w, (int)x.w, nv, false);
         }
     }
     const size_t o = (size_t)img * k_pad + j;
@@ -143,7 +140,7 @@ __global__ void l2fr_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
 // the same train image, rng[r] = (first entry, length), *n_rng of them, and their pairs (rinfo).
 constexpr int REC_R = 4;  // pairs (sharing their train image) per recovery block
 
-// The forward scan's UNITS (block unit_blk of l2fr_order_kernel): the pairs grouped by query image
+// The forward scan's UNITS (order block unit_blk of l2fr_setup_kernel): the pairs grouped by query image
 // pairs[p][0], UNIT of them per unit (the query fragments are loaded once for all, and each next
 // pair's first train chunk is staged under the previous pair's last one); an image's leftover
 // pairs make one shorter unit.  uinfo[UNIT u] = (p, a, b, n_kp[a] | n_kp[b] << 16), uinfo[UNIT u + j]
@@ -202,24 +199,18 @@ __device__ void build_units(const int32_t* __restrict__ pairs, int n_pairs, int 
     }
 }
 
-__global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restrict__ pairs,
-                                                          int n_pairs, int n_img,
-                                                          int32_t* __restrict__ order_f,
-                                                          int32_t* __restrict__ order_r,
-                                                          int2* __restrict__ rng,
-                                                          int32_t* __restrict__ n_rng,
-                                                          const int32_t* __restrict__ n_kp,
-                                                          int4* __restrict__ rinfo,
-                                                          int4* __restrict__ sinfo_f, int unit_blk,
-                                                          int4* __restrict__ uinfo,
-                                                          int32_t* __restrict__ n_units) {
-    extern __shared__ int hist[];
-    if ((int)blockIdx.x == unit_blk) {
+__device__ void order_block(int ob, const int32_t* __restrict__ pairs, int n_pairs, int n_img,
+                            int32_t* __restrict__ order_f, int32_t* __restrict__ order_r,
+                            int2* __restrict__ rng, int32_t* __restrict__ n_rng,
+                            const int32_t* __restrict__ n_kp, int4* __restrict__ rinfo,
+                            int4* __restrict__ sinfo_f, int unit_blk, int4* __restrict__ uinfo,
+                            int32_t* __restrict__ n_units, int* hist) {
+    if (ob == unit_blk) {
         build_units(pairs, n_pairs, n_img, n_kp, uinfo, n_units, hist);
         return;
     }
-    const int tid = threadIdx.x, col = blockIdx.x == 0 ? 1 : 0;
-    int32_t* order = blockIdx.x == 0 ? order_f : order_r;
+    const int tid = threadIdx.x, col = ob == 0 ? 1 : 0;
+    int32_t* order = ob == 0 ? order_f : order_r;
     for (int i = tid; i < n_img; i += 1024) hist[i] = 0;
     __syncthreads();
     for (int p = tid; p < n_pairs; p += 1024) atomicAdd(&hist[pairs[2 * p + col]], 1);
@@ -234,10 +225,10 @@ __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restr
             hist[i] = off;
             off += c;
         }
-        if (blockIdx.x == 0) *n_rng = nr;
+        if (ob == 0) *n_rng = nr;
     }
     __syncthreads();
-    if (blockIdx.x == 0)
+    if (ob == 0)
         for (int i = tid; i < n_img; i += 1024) {
             const int c = (i + 1 < n_img ? hist[i + 1] : n_pairs) - hist[i];
             for (int k = 0; k < c; k += REC_R)
@@ -251,9 +242,9 @@ __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restr
         order[slot] = p;
         // block 0: the forward scan's per-slot pair record, so its blocks start after ONE
         // dependent load instead of the pair_order -> pairs -> n_kp chain
-        if (blockIdx.x == 0) sinfo_f[slot] = make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
+        if (ob == 0) sinfo_f[slot] = make_int4(p, a, b, n_kp[a] | (n_kp[b] << 16));
     }
-    if (blockIdx.x != 0) return;
+    if (ob != 0) return;
     // the recovery ranges' pairs: rinfo[r][e] = (p, a, b, n_kp[a] | n_kp[b] << 16), p = -1 past
     // the range's length (order_f and rng come from this block: visible after the barrier)
     __threadfence_block();
@@ -271,6 +262,31 @@ __global__ __launch_bounds__(1024) void l2fr_order_kernel(const int32_t* __restr
             rinfo[(size_t)r * REC_R + e] = v;
         }
     }
+}
+
+// The ratio path's set-up in ONE launch of 1024-thread blocks: blocks [0, n_prep) convert the
+// descriptors (prep_one: the i8 rows, |x'|^2, the scan's accumulator init; bpi blocks per image),
+// the n_order blocks after them sort the pairs (order_block), concurrently with the conversion —
+// the two are independent, and the order blocks' latency-bound serial prefix no longer waits its
+// own launch (round 6: prep 10.4 + order 9.0 us as two launches at cfg2).
+__global__ __launch_bounds__(1024) void l2fr_setup_kernel(
+    int n_prep, int bpi, const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp,
+    int k_max, int k_pad, int32_t* __restrict__ norm, int32_t* __restrict__ cinit,
+    uint8_t* __restrict__ zero_row, uint4* __restrict__ desc_i8, const int32_t* __restrict__ pairs,
+    int n_pairs, int n_img, int32_t* __restrict__ order_f, int32_t* __restrict__ order_r,
+    int2* __restrict__ rng, int32_t* __restrict__ n_rng, int4* __restrict__ rinfo,
+    int4* __restrict__ sinfo_f, int unit_blk, int4* __restrict__ uinfo,
+    int32_t* __restrict__ n_units) {
+    extern __shared__ int hist[];
+    const int b = (int)blockIdx.x;
+    if (b < n_prep) {
+        const int img = b / bpi;
+        prep_one(img, (b - img * bpi) * 1024 + (int)threadIdx.x, desc, n_kp, k_max, k_pad, norm,
+                 cinit, zero_row, desc_i8);
+        return;
+    }
+    order_block(b - n_prep, pairs, n_pairs, n_img, order_f, order_r, rng, n_rng, n_kp, rinfo,
+                sinfo_f, unit_blk, uinfo, n_units, hist);
 }
 
 // Ratio bounds of one forward record: DROP (cannot pass even at the favourable ends of the d1, d2
@@ -1266,16 +1282,15 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
     const int grid = 8 * ppx * n_qblk;
     const bool mutual = prm->cross_check == SFM_XC_MUTUAL;
 
-    hipLaunchKernelGGL(l2fr_prep_kernel, dim3(k_pad / 256, n_img), dim3(256), 0, st, desc, n_kp,
-                       k_max, k_pad, norm, cinit, zero_row, (uint4*)desc_i8);
-    SFM_HIP_CHECK(hipGetLastError());
     const int32_t* sord_f = ord_f;
     const int32_t* sord_r = ord_r;
     const int unit_blk = units ? (mutual ? 2 : 1) : -1;
-    hipLaunchKernelGGL(l2fr_order_kernel, dim3((mutual ? 2 : 1) + (units ? 1 : 0)), dim3(1024),
-                       ((units ? 3 : 2) * (size_t)n_img + 2) * sizeof(int), st, pairs, n_pairs, n_img,
-                       ord_f, ord_r,
-                       rng, n_rng, n_kp, rinfo, sinfo_f, unit_blk, uinfo, n_units);
+    const int bpi = (k_pad + 1023) / 1024, n_prep = bpi * n_img;
+    hipLaunchKernelGGL(l2fr_setup_kernel, dim3(n_prep + (mutual ? 2 : 1) + (units ? 1 : 0)),
+                       dim3(1024), ((units ? 3 : 2) * (size_t)n_img + 2) * sizeof(int), st, n_prep,
+                       bpi, desc, n_kp, k_max, k_pad, norm, cinit, zero_row, (uint4*)desc_i8, pairs,
+                       n_pairs, n_img, ord_f, ord_r, rng, n_rng, rinfo, sinfo_f, unit_blk, uinfo,
+                       n_units);
     SFM_HIP_CHECK(hipGetLastError());
     // qst (per-query status of the recovery) shares the reverse scan's output buffer: it is
     // consumed by the compaction before the reverse scan writes there.

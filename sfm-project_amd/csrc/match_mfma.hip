@@ -179,17 +179,15 @@ __global__ void mfma_prep_kernel(const uint8_t* __restrict__ desc, const int32_t
         if (METRIC == SFM_METRIC_L2) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                uint4 v = p[q];
-                o8[q] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u, v.z ^ 0x80808080u,
-                                   v.w ^ 0x80808080u);
-                unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        int x = (int)((w[e] >> (8 * b)) & 0xFF) - 128;
-                        nv += x * x;
-                    }
+                const uint4 v = p[q];
+                const uint4 x = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u,
+                                           v.z ^ 0x80808080u, v.w ^ 0x80808080u);
+                o8[q] = x;
+                // |x'|^2 of the signed bytes x' = x - 128, four at a time (exact integer sums)
+                nv = __builtin_amdgcn_sdot4((int)x.x, (int)x.x, nv, false);
+                nv = __builtin_amdgcn_sdot4((int)x.y, (int)x.y, nv, false);
+                nv = __builtin_amdgcn_sdot4((int)x.z, (int)x.z, nv, false);
+                nv = __builtin_amdgcn_sdot4((int)x.w, (int)x.w, nv, false);
             }
         } else {
             // bit b of byte k (OpenCV's bit order is irrelevant: the distance counts all bits)
