@@ -1082,15 +1082,24 @@ __global__ __launch_bounds__(256) void l2fr_compact_kernel(
     const uint8_t* __restrict__ desc, const int32_t* __restrict__ n_kp, int k_max, int k_pad,
     const int32_t* __restrict__ norm, const int32_t* __restrict__ pairs,
     const int4* __restrict__ qst, int rnum, int rden, long long max_dist,
-    int4* __restrict__ surv, int32_t* __restrict__ scount) {
+    int4* __restrict__ surv, int32_t* __restrict__ scount, int32_t* __restrict__ out_count,
+    int32_t* __restrict__ out_match, int32_t* __restrict__ out_dist) {
     __shared__ Top2 red[256];
     __shared__ int slow[256];
     __shared__ int nslow, wsum[8];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int a = pairs[2 * p], b = pairs[2 * p + 1];
     const int na = n_kp[a], nb = n_kp[b];
+    // out_count != nullptr (the ratio rule without cross check): the survivors ARE the output —
+    // the final kernel's copy of them in the same order, written here instead of surv
+    const bool direct = out_count != nullptr;
+    int32_t* om = direct ? out_match + (size_t)p * k_max * 2 : nullptr;
+    int32_t* od = direct ? out_dist + (size_t)p * k_max : nullptr;
     if (na <= 0 || nb <= 0) {
-        if (tid == 0) scount[p] = 0;
+        if (tid == 0) {
+            if (direct) out_count[p] = 0;
+            else scount[p] = 0;
+        }
         return;
     }
     const int4* qs = qst + (size_t)p * k_pad;
@@ -1118,9 +1127,15 @@ __global__ __launch_bounds__(256) void l2fr_compact_kernel(
             }
         }
         const bool keep = r.x == ST_PASS;
-        base = compact_rec(keep, make_int4(q, r.y, r.z, 0), base, wsum, sv);
+        if (direct)
+            base = sfm::compact256(keep, q, r.y, r.z, base, wsum, om, od);
+        else
+            base = compact_rec(keep, make_int4(q, r.y, r.z, 0), base, wsum, sv);
     }
-    if (tid == 0) scount[p] = base;
+    if (tid == 0) {
+        if (direct) out_count[p] = base;
+        else scount[p] = base;
+    }
 }
 
 // Mutual decision from the reverse scan + ordered output (block of 256 per pair).
@@ -1320,10 +1335,14 @@ int sfm_match_l2fr_launch(sfm_ctx* ctx, const uint8_t* desc, const int32_t* n_kp
                        (long long)prm->max_dist, qst);
 #endif
     SFM_HIP_CHECK(hipGetLastError());
+    // the ratio rule alone: the compaction writes the output itself (no final kernel)
+    const bool direct = !mutual && dmode == 0;
     hipLaunchKernelGGL(l2fr_compact_kernel, dim3(n_pairs), dim3(256), 0, st, desc_i8, n_kp, k_max,
                        k_pad, norm, pairs, (const int4*)qst, prm->ratio_num, prm->ratio_den,
-                       (long long)prm->max_dist, surv, scount);
+                       (long long)prm->max_dist, surv, scount, direct ? out_count : nullptr,
+                       out_match, out_dist);
     SFM_HIP_CHECK(hipGetLastError());
+    if (direct) return SFM_OK;
     if (dmode == 2) {
         hipLaunchKernelGGL(l2fr_dump_kernel, dim3(n_pairs), dim3(256), 0, st, n_kp, pairs, k_max,
                            k_pad, (const int4*)surv, (const int32_t*)scount, out_count, out_match,
