@@ -372,3 +372,27 @@ def test_explicit_schur_sharded_world1_bit_identical():
         dist.destroy_process_group()
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("schur", [False, True])
+def test_poll_first_and_look_ahead_give_the_same_bits(schur):
+    """sfm_version 5 (round 6): where the solve polls its convergence flag — the first poll at
+    `poll_first`, then every `poll`, each read after look-ahead iterations — moves no result: the
+    iterations enqueued past convergence are empty.  The implicit CG and the explicit reduced
+    camera system (chunk mode + sfm_ba_set_schur), against the every-8 default, bit for bit."""
+    import torch
+    prob = synth.make_ba_problem(10, 300, obs_per_pt=4, seed=23, perturb=2e-3)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()
+    cams, pts = T(prob["cams"]), T(prob["pts"])
+    args = (prob["pp"], prob["cam_idx"], prob["pt_idx"], prob["uv"], len(prob["cams"]),
+            len(prob["pts"]))
+    P = R.BAProblem(*args, chunks=R.ba_chunk_count() if schur else None)
+    if schur:
+        P.set_schur()
+    lin = P.linearize(cams, pts)
+    ref = [t.clone() for t in P.solve(lin, 1e-3, max_iter=60, tol=1e-6, poll=8)]
+    assert 0 < ref[2][0].item() < 60   # converged before the cap: polls decide where it stops
+    for poll, first in ((4, 1), (4, 3), (1, 0), (8, 100), (3, 7)):
+        out = P.solve(lin, 1e-3, max_iter=60, tol=1e-6, poll=poll, poll_first=first)
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b), (poll, first)
