@@ -829,8 +829,12 @@ def ba_rooflines(pp, cams, pts, cam_idx, pt_idx, uv, device, reps=20, cg=32):
         sne = timed(lambda: Pe.solve(lin, 1e-3, max_iter=cg, tol=0.0, poll=-1), max(reps // 4, 2))
         build_ms = s0e - s0z            # T's products (bas_schur_build), once per solve
         tb = sp.n_inst * (192 + 192 + 72)
+        gsz = (sp.seg[3] - sp.seg[2]).cpu().numpy()   # products per (chunk, slot) group
         explicit = {"rule": R.schur_rule(sp.n_inst, sp.n_seg, sp.n_slot, n_obs),
                     "n_inst": sp.n_inst, "n_slot": sp.n_slot, "n_seg": sp.n_seg,
+                    "group_products": {"mean": float(gsz.mean()), "p50": float(np.median(gsz)),
+                                       "p99": float(np.percentile(gsz, 99)),
+                                       "max": int(gsz.max())} if len(gsz) else None,
                     "setup_backsub_ms": s0e,
                     "schur_build": {"ms": build_ms, "bytes": tb,
                                     "achieved_GBs": tb / (build_ms * 1e-3) / 1e9 if build_ms > 0 else None,

@@ -812,7 +812,9 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
 // they are fetched once.  32 accumulators per lane, then the recursive-halving sum over the lanes
 // of the same h: lane 2j + h ends holding element 32 h + j and stores it.  (Two waves per group,
 // each half the rows for every instance, fetched W_b and V_d⁻¹ twice: 0.22 ms at cfg5's final
-// model; 1 / 4 / 8 waves per group 0.25 / 0.31 / 0.57.)
+// model; 1 / 4 / 8 waves per group 0.25 / 0.31 / 0.57.  The inst -> pt_idx chain run one and two
+// instances ahead, 3 waves per SIMD: 0.27 - 0.29; the wave's 32 records staged in LDS by whole
+// 16-byte pieces first: 0.31; this form 0.19 — profiles/r06/ba_study/t6_t7_schur_build_variants.txt.)
 __global__ __launch_bounds__(256) void bas_schur_build(
     int n_seg, int n_inst, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ inst, const int32_t* __restrict__ pt_idx,
