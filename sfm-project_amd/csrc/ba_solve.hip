@@ -806,56 +806,117 @@ __global__ __launch_bounds__(256) void bas_pcg_vec(
 //
 // T_slot = Σ over the slot's camera-pair instances (a, b) of Y_a W_bᵀ, Y_a = W_a V_d⁻¹ (the point of
 // a), so the off-diagonal Schur blocks are S_ij = -T_ij; the diagonal blocks S_cc come from
-// bas_camera_setup.  One wave per (chunk, slot) group, a lane PAIR per instance: lane 2j + h takes
-// rows 4h .. 4h + 3 of the 8x8 block for instances j, j + 32, ... of the group (an order that
-// depends only on the group) — the pair reads the same W_b and V_d⁻¹ in one wave instruction, so
-// they are fetched once.  32 accumulators per lane, then the recursive-halving sum over the lanes
-// of the same h: lane 2j + h ends holding element 32 h + j and stores it.  (Two waves per group,
-// each half the rows for every instance, fetched W_b and V_d⁻¹ twice: 0.22 ms at cfg5's final
-// model; 1 / 4 / 8 waves per group 0.25 / 0.31 / 0.57.  The inst -> pt_idx chain run one and two
-// instances ahead, 3 waves per SIMD: 0.27 - 0.29; the wave's 32 records staged in LDS by whole
-// 16-byte pieces first: 0.31; this form 0.19 — profiles/r06/ba_study/t6_t7_schur_build_variants.txt.)
-__global__ __launch_bounds__(256) void bas_schur_build(
+// bas_camera_setup.  One wave (one workgroup) per (chunk, slot) group, a lane PAIR per instance:
+// lane 2j + h takes rows 4h .. 4h + 3 of the 8x8 block for instances j, j + 32, ... of the group (an
+// order that depends only on the group).  The wave's 32 instances' W_a, W_b (16-byte pieces, 12 per
+// record: whole cache lines per load instruction) and V_d⁻¹ (dwords, 18 per record) are staged
+// into LDS by global_load_lds, double-buffered: batch t + 1's records arrive while batch t is
+// multiplied from LDS (no staging VGPRs); the index chain inst -> pt_idx runs ahead (a, b two
+// batches, p one).  32 accumulators per lane, then the recursive-halving sum over the lanes of the
+// same h: lane 2j + h ends holding element 32 h + j and stores it.  At cfg5's final model
+// 0.175 - 0.181 ms per solve against 0.19 for direct loads by each lane pair (16 B of 32 different
+// records per instruction); 1 / 2 / 4 / 8 waves per group with direct loads 0.25 / 0.22 / 0.31 /
+// 0.57, the chain pipelined without staging 0.27 - 0.29, LDS staging through VGPRs 0.31 (its load
+// latency exposed), W_b and V_d⁻¹ staged with W_a in registers (half the LDS, 8 waves per CU
+// instead of 5) 0.183 — profiles/r06/ba_study/t6_t7_schur_build_variants.txt, t9_*, t10_*.  Same
+// bits in every form.
+typedef __attribute__((address_space(3))) void tb_lds_void;
+typedef const __attribute__((address_space(1))) void tb_gbl_void;
+__global__ __launch_bounds__(64) void bas_schur_build(
     int n_seg, int n_inst, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ inst, const int32_t* __restrict__ pt_idx,
     const double* __restrict__ W, const double* __restrict__ Vinv, double* __restrict__ Tpart) {
-    const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (s >= n_seg) return;   // wave-uniform
+    constexpr int WB = 32 * 12 * 16, VB = 32 * 18 * 4, BUF = 2 * WB + VB;   // bytes per buffer
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * BUF];
+    const int s = blockIdx.x, lane = threadIdx.x;
     const int h = lane & 1, j = lane >> 1;
     const int i0 = seg[2 * n_seg + s], i1 = seg[3 * n_seg + s];
+    const unsigned char* Wb8 = (const unsigned char*)W;
+    const unsigned char* Vb8 = (const unsigned char*)Vinv;
+    // every lane issues every piece (lanes past the batch read record 0: valid memory, never
+    // used), so no load sits in a branch and the compiler's vmcnt counts stay exact
+    auto stage = [&](int a, int b, int p, unsigned char* buf) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int q = lane + 64 * k, rec = q / 12, off = q - 12 * rec;
+            const int ar = __shfl(a, rec), br = __shfl(b, rec);
+            __builtin_amdgcn_global_load_lds((tb_gbl_void*)(Wb8 + 192 * (size_t)ar + 16 * off),
+                                             (tb_lds_void*)(buf + 1024 * k), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((tb_gbl_void*)(Wb8 + 192 * (size_t)br + 16 * off),
+                                             (tb_lds_void*)(buf + WB + 1024 * k), 16, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int d = lane + 64 * k, rec = d / 18, off = d - 18 * rec;
+            const int pr = __shfl(p, rec);
+            __builtin_amdgcn_global_load_lds((tb_gbl_void*)(Vb8 + 72 * (size_t)pr + 4 * off),
+                                             (tb_lds_void*)(buf + 2 * WB + 256 * k), 4, 0, 0);
+        }
+    };
+    auto ab = [&](int base, int& a, int& b) {   // batch `base`'s instance of this lane (< 32)
+        a = 0; b = 0;
+        if (lane < 32 && base + lane < i1) { a = inst[base + lane]; b = inst[n_inst + base + lane]; }
+    };
     double acc[32];
 #pragma unroll
     for (int t = 0; t < 32; ++t) acc[t] = 0.0;
-    for (int i = i0 + j; i < i1; i += 32) {
-        const int a = inst[i], b = inst[n_inst + i];
-        const int p = pt_idx[a];
-        double wa[12], wb[24], vi[9];
-        const double2* Wa = (const double2*)(W + 24 * (size_t)a + 12 * h);   // rows 4h .. 4h + 3
-        const double2* Wb = (const double2*)(W + 24 * (size_t)b);
+    if (i0 < i1) {
+        int a0, b0, a1, b1, a2, b2;
+        ab(i0, a0, b0);
+        const int p0 = pt_idx[a0];
+        stage(a0, b0, p0, lds);
+        ab(i0 + 32, a1, b1);
+        int p1 = pt_idx[a1];
+        ab(i0 + 64, a2, b2);
+        __syncthreads();
+        int t = 0;
+        for (int base = i0; base < i1; base += 32, ++t) {
+            const unsigned char* cur = lds + (t & 1) * BUF;
+            unsigned char* nxt = lds + ((t + 1) & 1) * BUF;
+            const int nb = min(32, i1 - base);
+            const int jj = min(j, 31);
+            double wa[12], wb[24], vi[9];
+            {
+                const double2* sWa = (const double2*)cur;
+                const double2* sWb = (const double2*)(cur + WB);
+                const double* sV = (const double*)(cur + 2 * WB);
 #pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            const double2 u = Wa[t];
-            wa[2 * t] = u.x; wa[2 * t + 1] = u.y;
+                for (int u = 0; u < 6; ++u) {
+                    const double2 x = sWa[12 * jj + 6 * h + u];
+                    wa[2 * u] = x.x; wa[2 * u + 1] = x.y;
+                }
+#pragma unroll
+                for (int u = 0; u < 12; ++u) {
+                    const double2 x = sWb[12 * jj + u];
+                    wb[2 * u] = x.x; wb[2 * u + 1] = x.y;
+                }
+#pragma unroll
+                for (int u = 0; u < 9; ++u) vi[u] = sV[9 * jj + u];
+            }
+            // the next batch's records into the other buffer (its readers passed the last
+            // barrier), the index chain one step on: they arrive while this batch is multiplied
+            int p2 = 0, a3 = 0, b3 = 0;
+            if (base + 32 < i1) {
+                stage(a1, b1, p1, nxt);
+                p2 = pt_idx[a2];
+                ab(base + 96, a3, b3);
+            }
+            if (j < nb) {
+                double y[12];
+#pragma unroll
+                for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c)
+                        y[3 * i2 + c] = wa[3 * i2] * vi[c] + wa[3 * i2 + 1] * vi[3 + c] + wa[3 * i2 + 2] * vi[6 + c];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 8; ++c)
+                        acc[8 * r + c] += y[3 * r] * wb[3 * c] + y[3 * r + 1] * wb[3 * c + 1] + y[3 * r + 2] * wb[3 * c + 2];
+            }
+            __syncthreads();   // the next batch has landed; this buffer may be refilled
+            a1 = a2; b1 = b2; p1 = p2; a2 = a3; b2 = b3;
         }
-#pragma unroll
-        for (int t = 0; t < 12; ++t) {
-            const double2 v = Wb[t];
-            wb[2 * t] = v.x; wb[2 * t + 1] = v.y;
-        }
-        const double* Vi = Vinv + 9 * (size_t)p;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) vi[t] = Vi[t];
-        double y[12];   // rows 4h .. 4h + 3 of W_a V_d⁻¹, bas_camera_setup's expression
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2)
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-                y[3 * i2 + c] = wa[3 * i2] * vi[c] + wa[3 * i2 + 1] * vi[3 + c] + wa[3 * i2 + 2] * vi[6 + c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                acc[8 * r + c] += y[3 * r] * wb[3 * c] + y[3 * r + 1] * wb[3 * c + 1] + y[3 * r + 2] * wb[3 * c + 2];
     }
     int idx;
     if (sfm::wave_halving_sum_strided<32, 2>(acc, lane, idx))
@@ -1541,13 +1602,12 @@ static int solve_backsub(hipStream_t st, const SolveWs& w, const ChunkArgs& ck, 
     return SFM_OK;
 }
 
-// Explicit S: this problem's group partials of T ([n_seg][64], one wave pair per group) into out.
+// Explicit S: this problem's group partials of T ([n_seg][64], one wave per group) into out.
 static int schur_build(const sfm_ctx* ctx, hipStream_t st, const SolveWs& w, const int32_t* pt_idx,
                        const double* W, double* out) {
     if (ctx->ba_nseg > 0) {
-        hipLaunchKernelGGL(bas_schur_build, dim3((ctx->ba_nseg + 3) / 4), dim3(256), 0,
-                           st, ctx->ba_nseg, ctx->ba_ninst, ctx->ba_seg, ctx->ba_inst, pt_idx, W,
-                           w.Vinv, out);
+        hipLaunchKernelGGL(bas_schur_build, dim3(ctx->ba_nseg), dim3(64), 0, st, ctx->ba_nseg,
+                           ctx->ba_ninst, ctx->ba_seg, ctx->ba_inst, pt_idx, W, w.Vinv, out);
         SFM_HIP_CHECK(hipGetLastError());
     }
     return SFM_OK;
